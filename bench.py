@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Headline benchmark: finger-routed successor lookups with hop counts on a
+2^24-peer Chord ring (BASELINE.json metric, config C4 per GPU).
+
+One step = one cx_route launch over this rank's batch of keys resident in HBM
+(the converged m=128 finger table, ring and Eytzinger copy are built before the
+timed region).  Weak scaling: every rank holds a replica of the ring and routes
+its own slice of the global key stream (keys[q] = splitmix(seed, q), src[q] =
+q mod N), so the data path has no collective; the barrier and the max-over-ranks
+timing are the only cross-rank traffic.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "p2p-dhts_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import chordx  # noqa: E402
+
+SEED_RING = 0x5EED0005
+SEED_KEYS = 0x5EED0006
+HBM_PEAK = 8.0e12  # B/s per MI355X (MI355X_MICROARCH.md, HBM3E spec)
+# Algorithmic bytes of one routed lookup: 25 B streamed
+# (16 key + 4 src + 4 owner + 1 hops) + 64 B source-peer record (first
+# StoredLocally) + 128 B per hop (finger granule + ring granule).
+BYTES_STREAM = 25
+BYTES_SRC = 64
+BYTES_HOP = 128
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--peers-log2", type=int, default=24)
+    ap.add_argument("--keys-log2", type=int, default=25, help="keys per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="target wall time of the CPU-oracle baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_route.json"))
+    return ap.parse_args()
+
+
+def dist_init(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
+    """Literal restatement (oracle/chord_oracle.c or_route: linear 128-entry
+    InBetween scan per hop, StoredLocally, ForwardRequest substitution) timed on
+    this host's cores over a bounded sample of the same key stream; also checks
+    the GPU's owner/hops on that sample."""
+    import oracle as O
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    ring_np = ring.ids()
+    P = O.Peers(ring_np, F_host)
+    cal = 2048
+    t0 = time.perf_counter()
+    O.route(P, src_np[:cal], keys_np[:cal], threads=threads)
+    per = (time.perf_counter() - t0) / cal
+    q = int(min(len(keys_np), max(cal, budget_s / max(per, 1e-9))))
+    t0 = time.perf_counter()
+    wo, wh, ws = O.route(P, src_np[:q], keys_np[:q], threads=threads)
+    dt = time.perf_counter() - t0
+    ok = bool((wo == gpu_owner[:q]).all() and (wh == gpu_hops[:q]).all() and (ws == 0).all())
+    return {"value": q / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
+            "sample": f"first {q} keys of the rank-0 stream (of {len(keys_np)}), "
+                      f"{dt:.1f} s wall, oracle/chord_oracle.c or_route",
+            "parity_on_sample": ok}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_init(args)
+    dev = torch.device(f"cuda:{local}")
+    N = 1 << args.peers_log2
+    Q = 1 << args.keys_log2
+
+    # ---- setup (untimed): ring, Eytzinger copy, converged finger table ----
+    ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(ids, SEED_RING)
+    t0 = time.perf_counter()
+    ring = chordx.Ring(ids, device=local)
+    torch.cuda.synchronize(dev)
+    t_ring = time.perf_counter() - t0
+    del ids
+    t0 = time.perf_counter()
+    ring.build_fingers()
+    ring.sync()
+    t_fing = time.perf_counter() - t0
+    keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(keys, SEED_KEYS, offset=rank * Q)
+    gq = torch.arange(rank * Q, (rank + 1) * Q, device=dev, dtype=torch.int64)
+    src = (gq % ring.n).to(torch.int32)
+    del gq
+    owner = torch.empty(Q, dtype=torch.int32, device=dev)
+    hops = torch.empty(Q, dtype=torch.uint8, device=dev)
+    status = torch.empty(Q, dtype=torch.uint8, device=dev)
+    out = (owner, hops, status)
+
+    # ---- warmup ----
+    for _ in range(args.warmup):
+        ring.route(src, keys, out=out)
+    torch.cuda.synchronize(dev)
+
+    # ---- timed: exactly K steps, barrier + sync on both sides ----
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        ring.route(src, keys, out=out)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt_max = max_over_ranks(dt, world, dev)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one cx_route launch per step
+
+    # ---- results ----
+    bad = int((status != 0).sum().item())
+    sum_hops = int(hops.to(torch.int64).sum().item())
+    algo_bytes = Q * (BYTES_STREAM + BYTES_SRC) + BYTES_HOP * sum_hops
+    achieved = algo_bytes / (kern_ms * 1e-3)
+    # exact-successor rate on the same keys (row a5, C2 kernel at C4 size)
+    succ_out = torch.empty(Q, dtype=torch.int32, device=dev)
+    ring.successor(keys, out=succ_out)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(3):
+        ring.successor(keys, out=succ_out)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    succ_ms = e0.elapsed_time(e1) / 3
+    owner_eq = bool((succ_out == owner).all().item())
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
+        F_host[:] = ring.fingers_device().cpu().numpy().view(np.uint32)
+        cs = min(Q, 1 << 21)
+        cpu = cpu_baseline(ring, F_host, keys[:cs].cpu().numpy().view(np.uint64),
+                           src[:cs].cpu().numpy().view(np.uint32),
+                           owner[:cs].cpu().numpy().view(np.uint32),
+                           hops[:cs].cpu().numpy(), args.cpu_seconds)
+        del F_host
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("peers") == N and tj.get("keys") == Q:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        total = world * Q * args.steps
+        line = {
+            "metric": "successor lookups/sec (whole node) + % HBM roofline, 2^24-peer ring, "
+                      "1/2/4/8 GPUs",
+            "value": total / dt_max,
+            "unit": "lookups/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u128",
+            "data": "synthetic",
+            "config": {"workload": "C4 finger-routed lookups with hop counts (per GPU): "
+                                   f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step, "
+                                   "src = q mod N, splitmix seeds 0x5EED0005/0x5EED0006",
+                       "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
+                       "parallelism": f"replicated ring, keys sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "kernel": "k_route_conv", "kernel_ms": kern_ms,
+                         "algo_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu,
+            "mean_hops": sum_hops / Q,
+            "bad_status": bad,
+            "route_owner_equals_successor": owner_eq,
+            "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
+            "setup_s": {"ring_sort": t_ring, "fingers_build": t_fing},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+/*
+ * chordx.h -- C ABI of the MI355X batched Chord/DHash lookup engine.
+ *
+ * Drop-in boundary for the lookup hot path of Patrick-McKeever/P2P-DHTs.
+ * The reference has no FFI layer: the path sits behind C++ class interfaces
+ * (FingerTable<PeerType>, ChordKey::InBetween, AbstractChordPeer::GetSuccessor /
+ * GetNSuccessors, DHashPeer::RunGlobalMaintenance).  Each entry point below
+ * names the reference interface it replaces (file:line under /root/reference).
+ * INTEGRATION.md shows the binding a ChordPeer/DHashPeer maintainer would add.
+ *
+ * Conventions
+ *  - 128-bit ring values are cx_u128 {lo, hi}: value = hi * 2^64 + lo
+ *    (ChordKey = GenericKey<16,32>, key.h:355, ring size 16^32 = 2^128).
+ *  - Peers are named by their index in the sorted ring (cx_ring_ids maps
+ *    index -> ID); the reference names them by RemotePeer (id, ip, port).
+ *  - Every call returns CX_OK (0) or a CX_E_* code; cx_last_error() gives a
+ *    thread-local message.  Error texts reuse the reference's runtime_error
+ *    messages where one exists ("Lookup failed", "Insufficient succs in list
+ *    to complete request.", ...).
+ *  - memkind CX_MEM_HOST: caller buffers are host memory; the engine stages
+ *    them.  CX_MEM_DEVICE: caller buffers are device pointers on the ring's
+ *    device and the call is asynchronous on the ring's stream (cx_ring_sync).
+ *  - A ring handle is immutable once built (fingers/state uploads excepted,
+ *    which are exclusive writes like the reference's WriteLock'ed
+ *    FingerTable edits, finger_table.h:91-168).  Const queries from several
+ *    host threads are safe if each thread uses its own handle stream.
+ *  - No compute path exists on the host: without a HIP device every compute
+ *    call fails with CX_E_HIP.
+ */
+#ifndef CHORDX_H
+#define CHORDX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CHORDX_VERSION 1
+#define CX_FINGERS 128u          /* ChordKey::BinaryLen(), key.h:152-155; finger_table.h:44 */
+#define CX_NONE 0xFFFFFFFFu      /* "no peer" index */
+#define CX_HOP_CAP 255u          /* max forwards recorded per lookup (uint8 hops) */
+#define CX_MAX_NSUCC 16          /* n-successor list cap (uint16 misplaced mask) */
+
+typedef struct { uint64_t lo, hi; } cx_u128;
+typedef struct { uint64_t w[4]; } cx_u256; /* little-endian limbs, raw uint256_t values */
+typedef struct cx_ring cx_ring;
+
+enum cx_err {
+    CX_OK = 0,
+    CX_E_INVALID = 1,      /* bad argument */
+    CX_E_NOT_FOUND = 2,    /* "ChordKey not found" (finger_table.h:129) */
+    CX_E_LOOKUP_FAILED = 3,/* "Lookup failed" (chord_peer.cpp:206, dhash_peer.cpp:524) */
+    CX_E_INSUFFICIENT = 4, /* "Insufficient succs in list to complete request." (dhash_peer.cpp:110) */
+    CX_E_HIP = 5,          /* HIP runtime failure or no device */
+    CX_E_RCCL = 6,
+    CX_E_NOMEM = 7,
+    CX_E_STATE = 8         /* operation needs state not built yet (e.g. fingers) */
+};
+
+enum cx_memkind { CX_MEM_HOST = 0, CX_MEM_DEVICE = 1 };
+
+/* Per-query status of cx_route. */
+enum cx_qstatus { CX_Q_OK = 0, CX_Q_HOPCAP = 1, CX_Q_BADPEER = 2 /* src or finger entry >= ring size */ };
+
+/* ---- library --------------------------------------------------------- */
+int cx_version(void);
+const char *cx_last_error(void);
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int cx_device_count(int *count);
+
+/* ---- ring lifecycle (a13) ---------------------------------------------
+ * Replaces the converged RemotePeerList/successor ring that Join/Stabilize/
+ * UpdateSuccList build over RPC (abstract_chord_peer.cpp:83-117,460-562;
+ * remote_peer_list.cpp:31-84): LSD radix sort of the IDs on the GPU, equal
+ * IDs dropped (remote_peer_list.cpp:56-58).  n >= 1. */
+int cx_ring_create(const cx_u128 *ids, size_t n, int memkind, int device, cx_ring **out);
+int cx_ring_destroy(cx_ring *ring);
+int cx_ring_size(const cx_ring *ring, size_t *n);
+/* Sorted unique IDs (index -> ID map), n entries. */
+int cx_ring_ids(const cx_ring *ring, cx_u128 *out, int memkind);
+/* Device pointer to the ring's sorted IDs (n x 16 B, read-only). */
+int cx_ring_ids_device(const cx_ring *ring, const cx_u128 **ids);
+/* Use the caller's hipStream_t (NULL = the handle's own stream). */
+int cx_ring_set_stream(cx_ring *ring, void *hip_stream);
+int cx_ring_sync(const cx_ring *ring);
+
+/* ---- a5/a7: exact successor --------------------------------------------
+ * owner[i] = index of the peer whose StoredLocally(keys[i]) holds in the
+ * converged ring (abstract_chord_peer.cpp:720-725, min_key = pred+1,
+ * chord_peer.cpp:275): the first ID >= key, wrapping to 0.  Eytzinger search
+ * with the top levels staged in LDS. */
+int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *owner,
+                 int memkind);
+
+/* ---- a4/a6: fingers ----------------------------------------------------
+ * Converged PopulateFingerTable (abstract_chord_peer.cpp:564-613): row p,
+ * entry i = succ(GetNthRange(i).first) = succ(id_p + 2^i mod 2^128)
+ * (finger_table.h:177-188).  The table stays on the device for cx_route;
+ * fingers_out (n x 128 uint32, may be NULL) receives a copy. */
+int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind);
+/* Hand-edited / churned finger table (EditNthFinger, AdjustFingers,
+ * ReplaceDeadPeer: finger_table.h:137-168), n x 128 peer indices.  Switches
+ * cx_route to the literal ForwardRequest walk. */
+int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind);
+/* Device pointer to the n x 128 finger table (NULL until built/uploaded). */
+int cx_fingers_device(const cx_ring *ring, const uint32_t **fingers);
+/* Per-peer min_key_ and predecessor_ (CX_NONE = predecessor not alive),
+ * as white-box tests set them (chord_test.cpp:18-90).  Either may be NULL
+ * (= converged value: pred+1 / ring[p-1]).  Switches cx_route to the literal
+ * walk. */
+int cx_peer_state_upload(cx_ring *ring, const cx_u128 *min_keys, const uint32_t *preds,
+                         int memkind);
+
+/* ---- a7-a9: finger-routed lookup with hop counts -------------------------
+ * GetSuccessor(key) issued at peer src[i] (abstract_chord_peer.cpp:318-330),
+ * forwarded hop by hop through ChordPeer::ForwardRequest (chord_peer.cpp:
+ * 185-211): FingerTable::Lookup's first matching finger (finger_table.h:
+ * 115-130), self -> live predecessor substitution.  hops[i] = GET_SUCC
+ * requests sent (0 if src stores the key).  status[i] = CX_Q_HOPCAP (owner =
+ * CX_NONE) if the walk exceeds CX_HOP_CAP forwards.  status may be NULL.
+ * Needs fingers (cx_fingers_build or cx_fingers_upload). */
+int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
+             uint32_t *owner, uint8_t *hops, uint8_t *status, int memkind);
+
+/* ---- a10/a11: n-successor replica lists -----------------------------------
+ * GetNSuccessors(key, n) (abstract_chord_peer.cpp:345-373) as used for DHash
+ * fragment placement (dhash_peer.cpp:103-129): lists[i*n + j] = j-th
+ * successor, count[i] = min(n, ring size), unused slots CX_NONE.  1 <= n <= 16. */
+int cx_nsucc(const cx_ring *ring, const cx_u128 *keys, size_t q, int n, uint32_t *lists,
+             uint8_t *count, int memkind);
+/* DHashPeer::Create's precondition (dhash_peer.cpp:109-112): CX_E_INSUFFICIENT
+ * when the ring has fewer than m peers (every key then gets < m successors). */
+int cx_dhash_check(const cx_ring *ring, int n, int m);
+
+/* ---- a12: churn + global-maintenance misplaced scan ------------------------
+ * Batched join/leave: new ring = (old minus leaves) + joins, sorted, equal IDs
+ * dropped (a join equal to a surviving ID is rejected).  Leaves not in the ring
+ * are ignored.  old_to_new[p] = new index of old peer p or CX_NONE if it left
+ * (may be NULL).  All buffers in memkind. */
+int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_u128 *leaves,
+             size_t nl, int memkind, cx_ring **new_ring, uint32_t *old_to_new);
+/* DHashPeer::RunGlobalMaintenance (dhash_peer.cpp:298-348) after churn, per
+ * key.  Holders = the key's old n-window (DHashPeer::Create placed fragment j
+ * on old list rank j), survivors mapped by old_to_new.  Outputs (q x n unless
+ * noted): new_lists = new n-successor lists; count[q]; mask[q] bit j = old
+ * holder j is misplaced (survived, not in its new list, dhash_peer.cpp:
+ * 322-328); target[j] = rank in new_lists of the successor holder j's
+ * CREATE_KEY goes to (first successor lacking the key, holders processed in
+ * rank order), 0xFF if none (every successor already holds it).
+ * old_to_new is in memkind and may come from cx_churn. */
+int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_t *old_to_new,
+                 const cx_u128 *keys, size_t q, int n, uint32_t *new_lists, uint8_t *count,
+                 uint16_t *mask, uint8_t *target, int memkind);
+/* Same scan with explicit holders (q x nh ring indices, CX_NONE = empty), e.g.
+ * keys inserted straight into a non-owner's db (dhash_test.cpp:123-149).
+ * target is q x nh.  nh <= 16. */
+int cx_misplaced_holders(const cx_ring *ring, const cx_u128 *keys, size_t q,
+                         const uint32_t *holders, int nh, int n, uint32_t *new_lists,
+                         uint8_t *count, uint16_t *mask, uint8_t *target, int memkind);
+
+/* ---- a2: clockwise interval test ----------------------------------------
+ * ChordKey::InBetween(lb, ub, inclusive) (key.h:103-131) on raw uint256
+ * operands (its raw-bound compare and equal-bound point test included),
+ * batched on the GPU: out[i] = 0/1. */
+int cx_in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,
+                  int inclusive, uint8_t *out, int memkind);
+
+/* ---- synthetic inputs (bench / tests) --------------------------------------
+ * out[i] = {splitmix64(seed, 2(offset+i)), splitmix64(seed, 2(offset+i)+1)}
+ * written on the device (SURVEY 8d generator). */
+int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t offset,
+                     int device, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHORDX_H */

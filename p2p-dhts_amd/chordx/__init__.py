@@ -1,0 +1,16 @@
+"""chordx -- MI355X batched Chord/DHash lookup engine (Python face of libchordx).
+
+The engine is a C-ABI shared library (include/chordx.h) over hand-written
+gfx950 HIP kernels (p2p-dhts_amd/csrc/).  This package binds it with ctypes and
+mirrors the reference's lookup-path interface (see ring.py).
+"""
+from ._lib import (CX_FINGERS, CX_HOP_CAP, CX_MAX_NSUCC, CX_NONE, CX_Q_BADPEER, CX_Q_HOPCAP,
+                   CX_Q_OK, ChordError, device_count, lib)
+from .key import ChordKey
+from .ring import Ring, fill_splitmix, in_between
+
+__all__ = [
+    "Ring", "ChordKey", "ChordError", "in_between", "fill_splitmix", "device_count", "lib",
+    "CX_FINGERS", "CX_NONE", "CX_HOP_CAP", "CX_MAX_NSUCC", "CX_Q_OK", "CX_Q_HOPCAP",
+    "CX_Q_BADPEER",
+]

@@ -1,0 +1,109 @@
+"""ctypes binding of libchordx.so (include/chordx.h).
+
+The shared library is built in-tree by `make -C p2p-dhts_amd/csrc` (or
+__graft_entry__.build()).  Loading it needs no GPU; every compute entry point
+fails with CX_E_HIP when no HIP device is visible -- there is no host fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libchordx.so")
+
+CX_OK = 0
+CX_E_INVALID = 1
+CX_E_NOT_FOUND = 2
+CX_E_LOOKUP_FAILED = 3
+CX_E_INSUFFICIENT = 4
+CX_E_HIP = 5
+CX_E_RCCL = 6
+CX_E_NOMEM = 7
+CX_E_STATE = 8
+
+CX_MEM_HOST = 0
+CX_MEM_DEVICE = 1
+
+CX_FINGERS = 128
+CX_NONE = 0xFFFFFFFF
+CX_HOP_CAP = 255
+CX_MAX_NSUCC = 16
+CX_Q_OK, CX_Q_HOPCAP, CX_Q_BADPEER = 0, 1, 2
+
+# Every symbol include/chordx.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "cx_version", "cx_last_error", "cx_device_count",
+    "cx_ring_create", "cx_ring_destroy", "cx_ring_size", "cx_ring_ids",
+    "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_sync",
+    "cx_successor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
+    "cx_peer_state_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
+    "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
+    "cx_fill_splitmix",
+)
+
+
+class ChordError(RuntimeError):
+    """A CX_E_* failure; .code is the cx_err value."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ChordError(CX_E_HIP, f"{LIB_PATH} is missing: build it with "
+                                   "`make -C p2p-dhts_amd/csrc` (no host fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "cx_version": ([], i),
+        "cx_last_error": ([], ctypes.c_char_p),
+        "cx_device_count": ([ctypes.POINTER(ctypes.c_int)], i),
+        "cx_ring_create": ([vp, sz, i, i, pp], i),
+        "cx_ring_destroy": ([vp], i),
+        "cx_ring_size": ([vp, ctypes.POINTER(ctypes.c_size_t)], i),
+        "cx_ring_ids": ([vp, vp, i], i),
+        "cx_ring_ids_device": ([vp, pp], i),
+        "cx_ring_set_stream": ([vp, vp], i),
+        "cx_ring_sync": ([vp], i),
+        "cx_successor": ([vp, vp, sz, vp, i], i),
+        "cx_fingers_build": ([vp, vp, i], i),
+        "cx_fingers_upload": ([vp, vp, i], i),
+        "cx_fingers_device": ([vp, pp], i),
+        "cx_peer_state_upload": ([vp, vp, vp, i], i),
+        "cx_route": ([vp, vp, vp, sz, vp, vp, vp, i], i),
+        "cx_nsucc": ([vp, vp, sz, i, vp, vp, i], i),
+        "cx_dhash_check": ([vp, i, i], i),
+        "cx_churn": ([vp, vp, sz, vp, sz, i, pp, vp], i),
+        "cx_misplaced": ([vp, vp, vp, vp, sz, i, vp, vp, vp, vp, i], i),
+        "cx_misplaced_holders": ([vp, vp, sz, vp, i, i, vp, vp, vp, vp, i], i),
+        "cx_in_between": ([vp, vp, vp, sz, i, vp, i], i),
+        "cx_fill_splitmix": ([vp, sz, u64, u64, i, vp], i),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != CX_OK:
+        msg = lib().cx_last_error()
+        raise ChordError(rc, msg.decode() if msg else f"chordx error {rc}")
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    check(lib().cx_device_count(ctypes.byref(c)))
+    return c.value

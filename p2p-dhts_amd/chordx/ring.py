@@ -1,0 +1,277 @@
+"""Ring handle: the batched replacement for a converged Chord ring of peers.
+
+Mirrors what a ChordPeer/DHashPeer exposes on the lookup path
+(abstract_chord_peer.h:113-160, finger_table.h:30-288, dhash_peer.h:54-81),
+batched over keys and source peers:
+
+  ChordPeer API (reference)                      Ring method
+  ---------------------------------------------  -----------------------------
+  converged successor ring (Join/Stabilize)      Ring(ids)  (GPU radix sort)
+  StoredLocally / owner of a key                 successor(keys)
+  PopulateFingerTable (converged)                build_fingers()
+  EditNthFinger / AdjustFingers (hand edits)     upload_fingers(F)
+  min_key_ / predecessor_ (white-box state)      upload_peer_state(...)
+  GetSuccessor(key) from peer src (+ hops)       route(src, keys)
+  GetNSuccessors(key, n)                         nsucc(keys, n)
+  batched Join/Leave                             churn(joins, leaves)
+  RunGlobalMaintenance misplaced check           misplaced(...), misplaced_holders(...)
+  ChordKey::InBetween                            in_between(...)
+
+Buffers: numpy arrays are host memory (staged by the library); torch CUDA
+tensors are device memory, and the call is ordered on torch's current stream.
+128-bit values are (q, 2) arrays of uint64 (numpy) / int64 (torch):
+column 0 = low 64 bits, column 1 = high 64 bits.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+try:  # torch is optional plumbing (device memory, streams)
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def _is_dev(x) -> bool:
+    return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
+
+
+def _keys_np(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1, 2))
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if _is_dev(a):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Ring:
+    """Sorted, de-duplicated ring of 128-bit peer IDs on one GPU."""
+
+    def __init__(self, ids, device: int = 0, _handle=None):
+        self._h = None
+        if _handle is not None:
+            self._h = _handle
+        else:
+            h = ctypes.c_void_p()
+            if _is_dev(ids):
+                ids = ids.contiguous()
+                assert ids.dim() == 2 and ids.shape[1] == 2 and ids.element_size() == 8
+                device = ids.device.index or 0
+                # the build runs on the handle's own stream: order it after torch's
+                torch.cuda.current_stream(device).synchronize()
+                L.check(L.lib().cx_ring_create(_ptr(ids), ids.shape[0], L.CX_MEM_DEVICE, device,
+                                               ctypes.byref(h)))
+            else:
+                ids = _keys_np(ids)
+                L.check(L.lib().cx_ring_create(_ptr(ids), len(ids), L.CX_MEM_HOST, device,
+                                               ctypes.byref(h)))
+            self._h = h
+        self.device = device
+        n = ctypes.c_size_t()
+        L.check(L.lib().cx_ring_size(self._h, ctypes.byref(n)))
+        self.n = n.value
+
+    # ---- lifecycle -------------------------------------------------------
+    def close(self):
+        if self._h is not None:
+            L.lib().cx_ring_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.n
+
+    def _mem(self, *arrays) -> int:
+        dev = [_is_dev(a) for a in arrays if a is not None]
+        if dev and all(dev):
+            # order the library's work on torch's current stream
+            L.check(L.lib().cx_ring_set_stream(
+                self._h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+            return L.CX_MEM_DEVICE
+        if any(dev):
+            raise TypeError("mix of device tensors and host arrays")
+        L.check(L.lib().cx_ring_set_stream(self._h, None))
+        return L.CX_MEM_HOST
+
+    def _empty(self, like, shape, np_dtype, th_dtype):
+        if _is_dev(like):
+            return torch.empty(shape, dtype=th_dtype, device=like.device)
+        return np.empty(shape, dtype=np_dtype)
+
+    @staticmethod
+    def _prep_keys(keys):
+        if _is_dev(keys):
+            return keys.contiguous().view(-1, 2)
+        return _keys_np(keys)
+
+    @staticmethod
+    def _prep_u32(a):
+        if _is_dev(a):
+            return a.contiguous()
+        return np.ascontiguousarray(a, dtype=np.uint32)
+
+    def ids(self) -> np.ndarray:
+        out = np.empty((self.n, 2), dtype=np.uint64)
+        L.check(L.lib().cx_ring_ids(self._h, _ptr(out), L.CX_MEM_HOST))
+        return out
+
+    def ids_device(self):
+        """Zero-copy view of the ring's sorted IDs as a torch int64 (n, 2) tensor."""
+        p = ctypes.c_void_p()
+        L.check(L.lib().cx_ring_ids_device(self._h, ctypes.byref(p)))
+        return _wrap_device(p.value, (self.n, 2), torch.int64, self.device, self)
+
+    def sync(self):
+        L.check(L.lib().cx_ring_sync(self._h))
+
+    # ---- a5/a7 -----------------------------------------------------------
+    def successor(self, keys, out=None):
+        keys = self._prep_keys(keys)
+        q = keys.shape[0]
+        owner = out if out is not None else self._empty(keys, (q,), np.uint32, torch and torch.int32)
+        mk = self._mem(keys, owner)
+        L.check(L.lib().cx_successor(self._h, _ptr(keys), q, _ptr(owner), mk))
+        return owner
+
+    # ---- a4/a6 -----------------------------------------------------------
+    def build_fingers(self, copy_out: bool = False):
+        """Converged PopulateFingerTable; returns the n x 128 table if copy_out."""
+        if copy_out:
+            F = np.empty((self.n, L.CX_FINGERS), dtype=np.uint32)
+            L.check(L.lib().cx_fingers_build(self._h, _ptr(F), L.CX_MEM_HOST))
+            return F
+        L.check(L.lib().cx_fingers_build(self._h, None, L.CX_MEM_HOST))
+        return None
+
+    def upload_fingers(self, F):
+        F = self._prep_u32(F)
+        assert tuple(F.shape) == (self.n, L.CX_FINGERS)
+        mk = self._mem(F)
+        L.check(L.lib().cx_fingers_upload(self._h, _ptr(F), mk))
+
+    def upload_peer_state(self, min_keys=None, preds=None):
+        mk_arr = None if min_keys is None else self._prep_keys(min_keys)
+        pr = None if preds is None else self._prep_u32(preds)
+        mk = self._mem(*(a for a in (mk_arr, pr) if a is not None)) if (mk_arr is not None or pr is not None) else L.CX_MEM_HOST
+        L.check(L.lib().cx_peer_state_upload(self._h, _ptr(mk_arr), _ptr(pr), mk))
+
+    def fingers_device(self):
+        p = ctypes.c_void_p()
+        L.check(L.lib().cx_fingers_device(self._h, ctypes.byref(p)))
+        if not p.value:
+            return None
+        return _wrap_device(p.value, (self.n, L.CX_FINGERS), torch.int32, self.device, self)
+
+    # ---- a7-a9 -----------------------------------------------------------
+    def route(self, src, keys, out=None):
+        """GetSuccessor(key) issued at peer src: (owner, hops, status)."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src)
+        q = keys.shape[0]
+        if out is None:
+            owner = self._empty(keys, (q,), np.uint32, torch and torch.int32)
+            hops = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+            status = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        else:
+            owner, hops, status = out
+        mk = self._mem(keys, src, owner, hops)
+        L.check(L.lib().cx_route(self._h, _ptr(src), _ptr(keys), q, _ptr(owner), _ptr(hops),
+                                 _ptr(status), mk))
+        return owner, hops, status
+
+    # ---- a10/a11 ---------------------------------------------------------
+    def nsucc(self, keys, n: int):
+        keys = self._prep_keys(keys)
+        q = keys.shape[0]
+        lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
+        count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        mk = self._mem(keys, lists)
+        L.check(L.lib().cx_nsucc(self._h, _ptr(keys), q, n, _ptr(lists), _ptr(count), mk))
+        return lists, count
+
+    def dhash_check(self, n: int = 14, m: int = 10):
+        L.check(L.lib().cx_dhash_check(self._h, n, m))
+
+    # ---- a12 -------------------------------------------------------------
+    def churn(self, joins, leaves):
+        joins, leaves = self._prep_keys(joins), self._prep_keys(leaves)
+        o2n = self._empty(joins, (self.n,), np.uint32, torch and torch.int32)
+        mk = self._mem(joins, leaves, o2n)
+        h = ctypes.c_void_p()
+        L.check(L.lib().cx_churn(self._h, _ptr(joins), joins.shape[0], _ptr(leaves),
+                                 leaves.shape[0], mk, ctypes.byref(h), _ptr(o2n)))
+        return Ring(None, self.device, _handle=h), o2n
+
+    def misplaced(self, new_ring: "Ring", old_to_new, keys, n: int):
+        keys = self._prep_keys(keys)
+        o2n = self._prep_u32(old_to_new)
+        q = keys.shape[0]
+        lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
+        count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        mask = self._empty(keys, (q,), np.uint16, torch and torch.int16)
+        target = self._empty(keys, (q, n), np.uint8, torch and torch.uint8)
+        mk = new_ring._mem(keys, o2n, lists)
+        L.check(L.lib().cx_misplaced(self._h, new_ring._h, _ptr(o2n), _ptr(keys), q, n,
+                                     _ptr(lists), _ptr(count), _ptr(mask), _ptr(target), mk))
+        return lists, count, mask, target
+
+    def misplaced_holders(self, keys, holders, n: int):
+        keys = self._prep_keys(keys)
+        holders = self._prep_u32(holders)
+        q, nh = holders.shape
+        lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
+        count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        mask = self._empty(keys, (q,), np.uint16, torch and torch.int16)
+        target = self._empty(keys, (q, nh), np.uint8, torch and torch.uint8)
+        mk = self._mem(keys, holders, lists)
+        L.check(L.lib().cx_misplaced_holders(self._h, _ptr(keys), q, _ptr(holders), nh, n,
+                                             _ptr(lists), _ptr(count), _ptr(mask),
+                                             _ptr(target), mk))
+        return lists, count, mask, target
+
+
+def in_between(v, lb, ub, inclusive: bool = True) -> np.ndarray:
+    """Batched ChordKey::InBetween on raw uint256 operands ((q, 4) uint64 each)."""
+    v, lb, ub = (np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1, 4))
+                 for a in (v, lb, ub))
+    out = np.empty(len(v), dtype=np.uint8)
+    L.check(L.lib().cx_in_between(_ptr(v), _ptr(lb), _ptr(ub), len(v), int(inclusive),
+                                  _ptr(out), L.CX_MEM_HOST))
+    return out
+
+
+def fill_splitmix(out, seed: int, offset: int = 0):
+    """Synthetic uniform 128-bit keys written on the device into `out` ((q, 2) int64)."""
+    assert _is_dev(out) and out.dim() == 2 and out.shape[1] == 2
+    L.check(L.lib().cx_fill_splitmix(_ptr(out), out.shape[0], seed, offset,
+                                     out.device.index or 0,
+                                     ctypes.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)))
+    return out
+
+
+class _DevArray:
+    """__cuda_array_interface__ shim so torch can view engine-owned memory."""
+
+    def __init__(self, ptr, shape, typestr, owner):
+        self._owner = owner
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr,
+                                         "data": (ptr, True), "version": 2, "strides": None}
+
+
+def _wrap_device(ptr, shape, dtype, device, owner):
+    typestr = {torch.int64: "<i8", torch.int32: "<i4"}[dtype]
+    with torch.cuda.device(device):
+        return torch.as_tensor(_DevArray(ptr, shape, typestr, owner), device=f"cuda:{device}")

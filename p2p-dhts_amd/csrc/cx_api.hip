@@ -1,0 +1,636 @@
+// cx_api.hip -- C ABI of libchordx (include/chordx.h): ring handles, staging
+// of host buffers, argument validation and error reporting.  All compute runs
+// in the gfx950 kernels of cx_kernels.hip; there is no host compute path.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cx_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define CX_HIP(expr)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(CX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+#define CX_CHECK(cond, code, msg)                                                         \
+    do {                                                                                  \
+        if (!(cond)) return fail((code), (msg));                                          \
+    } while (0)
+
+// RAII device allocation.
+struct DBuf {
+    void *p = nullptr;
+    ~DBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t bytes) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        return hipMalloc(&p, bytes ? bytes : 16);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+    void *release() {
+        void *r = p;
+        p = nullptr;
+        return r;
+    }
+};
+
+}  // namespace
+
+struct cx_ring {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    size_t n = 0;
+    cell128 *d_ring = nullptr;     // sorted unique IDs [n]
+    cell128 *d_eyt = nullptr;      // Eytzinger copy [n+1]
+    uint32_t *d_fingers = nullptr; // [n][128]
+    bool fingers_converged = false;
+    cell128 *d_min_keys = nullptr; // optional per-peer min_key_
+    uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
+    uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
+
+    EytView eyt() const {
+        EytView v;
+        v.E = d_eyt;
+        v.n = (uint32_t)n;
+        v.h = 63 - __builtin_clzll((unsigned long long)n);
+        return v;
+    }
+    bool literal() const { return !fingers_converged || d_min_keys || d_preds; }
+};
+
+namespace {
+
+int use_device(const cx_ring *r) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == r->device) return CX_OK;
+    CX_HIP(hipSetDevice(r->device));
+    return CX_OK;
+}
+
+// Makes `count` elements of a caller buffer available on the device.
+template <class T>
+int stage_in(const T *src, size_t count, int memkind, DBuf &tmp, const T **dev, hipStream_t s) {
+    if (count == 0) {
+        *dev = src;
+        return CX_OK;
+    }
+    CX_CHECK(src != nullptr, CX_E_INVALID, "null input buffer");
+    if (memkind == CX_MEM_DEVICE) {
+        *dev = src;
+        return CX_OK;
+    }
+    CX_CHECK(memkind == CX_MEM_HOST, CX_E_INVALID, "bad memkind");
+    CX_HIP(tmp.alloc(count * sizeof(T)));
+    CX_HIP(hipMemcpyAsync(tmp.p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+    *dev = tmp.as<T>();
+    return CX_OK;
+}
+
+template <class T>
+int stage_out(T *dst, size_t count, int memkind, DBuf &tmp, T **dev) {
+    if (count == 0) {
+        *dev = dst;
+        return CX_OK;
+    }
+    CX_CHECK(dst != nullptr, CX_E_INVALID, "null output buffer");
+    if (memkind == CX_MEM_DEVICE) {
+        *dev = dst;
+        return CX_OK;
+    }
+    CX_CHECK(memkind == CX_MEM_HOST, CX_E_INVALID, "bad memkind");
+    CX_HIP(tmp.alloc(count * sizeof(T)));
+    *dev = tmp.as<T>();
+    return CX_OK;
+}
+
+template <class T>
+int finish_out(T *dst, const T *dev, size_t count, int memkind, hipStream_t s) {
+    if (memkind == CX_MEM_HOST && count) {
+        CX_HIP(hipMemcpyAsync(dst, dev, count * sizeof(T), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+    }
+    return CX_OK;
+}
+
+int sync_if_host(int memkind, hipStream_t s) {
+    if (memkind == CX_MEM_HOST) CX_HIP(hipStreamSynchronize(s));
+    return CX_OK;
+}
+
+int alloc_ring(int device, cx_ring **out) {
+    cx_ring *r = new cx_ring();
+    r->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete r;
+        return fail(CX_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    r->stream = r->own_stream;
+    e = hipMalloc(&r->d_scratch, 64);
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(r->own_stream);
+        delete r;
+        return fail(CX_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    *out = r;
+    return CX_OK;
+}
+
+void free_ring(cx_ring *r) {
+    if (!r) return;
+    (void)hipSetDevice(r->device);
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    (void)hipFree(r->d_ring);
+    (void)hipFree(r->d_eyt);
+    (void)hipFree(r->d_fingers);
+    (void)hipFree(r->d_min_keys);
+    (void)hipFree(r->d_preds);
+    (void)hipFree(r->d_scratch);
+    if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
+    delete r;
+}
+
+}  // namespace
+
+// ===========================================================================
+// ABI
+// ===========================================================================
+extern "C" {
+
+int cx_version(void) { return CHORDX_VERSION; }
+
+const char *cx_last_error(void) { return g_err.c_str(); }
+
+int cx_device_count(int *count) {
+    CX_CHECK(count != nullptr, CX_E_INVALID, "null count");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return CX_OK;
+}
+
+int cx_ring_create(const cx_u128 *ids, size_t n, int memkind, int device, cx_ring **out) {
+    CX_CHECK(out != nullptr, CX_E_INVALID, "null out");
+    *out = nullptr;
+    CX_CHECK(n >= 1, CX_E_INVALID, "a ring needs at least one peer");
+    CX_CHECK(n < (size_t)CX_TAG_JOIN, CX_E_INVALID, "ring larger than 2^31 peers");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    CX_CHECK(device >= 0 && device < ndev, CX_E_INVALID, "bad device ordinal");
+    CX_HIP(hipSetDevice(device));
+    cx_ring *r = nullptr;
+    int rc = alloc_ring(device, &r);
+    if (rc) return rc;
+    hipStream_t s = r->stream;
+    DBuf k0, k1, t0, t1, stage;
+    auto bail = [&](int code) {
+        free_ring(r);
+        return code;
+    };
+    if (k0.alloc(n * sizeof(cell128)) != hipSuccess || k1.alloc(n * sizeof(cell128)) ||
+        t0.alloc(n * sizeof(uint32_t)) || t1.alloc(n * sizeof(uint32_t)))
+        return bail(fail(CX_E_NOMEM, "hipMalloc failed for ring build"));
+    const hipMemcpyKind kind =
+        memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (memkind != CX_MEM_DEVICE && memkind != CX_MEM_HOST)
+        return bail(fail(CX_E_INVALID, "bad memkind"));
+    if (!ids) return bail(fail(CX_E_INVALID, "null ids"));
+    if (hipMemcpyAsync(k0.p, ids, n * sizeof(cell128), kind, s) != hipSuccess)
+        return bail(fail(CX_E_HIP, "copying ids failed"));
+    if (cxk::iota(t0.as<uint32_t>(), n, 0, s) != hipSuccess)
+        return bail(fail(CX_E_HIP, "iota launch failed"));
+    rc = [&]() -> int {
+        DBuf ws, pos, ring;
+        const size_t sw = cxk::sort_workspace_words(n), cw = cxk::scan_workspace_words(n);
+        CX_HIP(ws.alloc((sw > cw ? sw : cw) * sizeof(uint32_t)));
+        CX_HIP(pos.alloc(n * sizeof(uint32_t)));
+        CX_HIP(cxk::radix_sort(k0.as<cell128>(), t0.as<uint32_t>(), k1.as<cell128>(),
+                               t1.as<uint32_t>(), n, ws.as<uint32_t>(), s));
+        CX_HIP(ring.alloc(n * sizeof(cell128)));
+        CX_HIP(cxk::unique_sorted(k0.as<cell128>(), t0.as<uint32_t>(), n, pos.as<uint32_t>(),
+                                  ws.as<uint32_t>(), ring.as<cell128>(), nullptr,
+                                  r->d_scratch, s));
+        uint32_t m = 0;
+        CX_HIP(hipMemcpyAsync(&m, r->d_scratch, sizeof(m), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        CX_CHECK(m >= 1 && m <= n, CX_E_HIP, "ring build produced an invalid size");
+        r->n = m;
+        r->d_ring = ring.as<cell128>();
+        ring.release();
+        DBuf E;
+        CX_HIP(E.alloc((m + 1) * sizeof(cell128)));
+        CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
+        r->d_eyt = E.as<cell128>();
+        E.release();
+        CX_HIP(hipStreamSynchronize(s));
+        return CX_OK;
+    }();
+    if (rc) return bail(rc);
+    *out = r;
+    return CX_OK;
+}
+
+int cx_ring_destroy(cx_ring *ring) {
+    free_ring(ring);
+    return CX_OK;
+}
+
+int cx_ring_size(const cx_ring *ring, size_t *n) {
+    CX_CHECK(ring && n, CX_E_INVALID, "null argument");
+    *n = ring->n;
+    return CX_OK;
+}
+
+int cx_ring_ids(const cx_ring *ring, cx_u128 *out, int memkind) {
+    CX_CHECK(ring && out, CX_E_INVALID, "null argument");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    const hipMemcpyKind kind =
+        memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    CX_HIP(hipMemcpyAsync(out, ring->d_ring, ring->n * sizeof(cell128), kind, ring->stream));
+    return sync_if_host(memkind, ring->stream);
+}
+
+int cx_ring_ids_device(const cx_ring *ring, const cx_u128 **ids) {
+    CX_CHECK(ring && ids, CX_E_INVALID, "null argument");
+    *ids = reinterpret_cast<const cx_u128 *>(ring->d_ring);
+    return CX_OK;
+}
+
+int cx_ring_set_stream(cx_ring *ring, void *hip_stream) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    ring->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ring->own_stream;
+    return CX_OK;
+}
+
+int cx_ring_sync(const cx_ring *ring) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    CX_HIP(hipStreamSynchronize(ring->stream));
+    return CX_OK;
+}
+
+int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *owner,
+                 int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    DBuf tk, to;
+    const cx_u128 *dk;
+    uint32_t *dout;
+    if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(owner, q, memkind, to, &dout))) return rc;
+    CX_HIP(cxk::successor(ring->eyt(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    return finish_out(owner, dout, q, memkind, s);
+}
+
+int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    const size_t cnt = ring->n * CX_FINGERS;
+    if (!ring->d_fingers) {
+        hipError_t e = hipMalloc(&ring->d_fingers, cnt * sizeof(uint32_t));
+        if (e != hipSuccess) {
+            ring->d_fingers = nullptr;
+            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
+        }
+    }
+    CX_HIP(cxk::fingers_build(ring->eyt(), ring->d_ring, ring->d_fingers, s));
+    ring->fingers_converged = true;
+    if (fingers_out) {
+        const hipMemcpyKind kind =
+            memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        CX_HIP(hipMemcpyAsync(fingers_out, ring->d_fingers, cnt * sizeof(uint32_t), kind, s));
+    }
+    return sync_if_host(memkind, s);
+}
+
+int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
+    CX_CHECK(ring && fingers, CX_E_INVALID, "null argument");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    const size_t cnt = ring->n * CX_FINGERS;
+    if (!ring->d_fingers) {
+        hipError_t e = hipMalloc(&ring->d_fingers, cnt * sizeof(uint32_t));
+        if (e != hipSuccess) {
+            ring->d_fingers = nullptr;
+            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
+        }
+    }
+    const hipMemcpyKind kind =
+        memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    CX_HIP(hipMemcpyAsync(ring->d_fingers, fingers, cnt * sizeof(uint32_t), kind, s));
+    CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
+    CX_HIP(cxk::check_indices(ring->d_fingers, cnt, (uint32_t)ring->n, false, ring->d_scratch,
+                              s));
+    uint32_t bad = 0;
+    CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    ring->fingers_converged = false;
+    CX_CHECK(!bad, CX_E_INVALID, "finger entry is not a ring index");
+    return CX_OK;
+}
+
+int cx_fingers_device(const cx_ring *ring, const uint32_t **fingers) {
+    CX_CHECK(ring && fingers, CX_E_INVALID, "null argument");
+    *fingers = ring->d_fingers;
+    return CX_OK;
+}
+
+int cx_peer_state_upload(cx_ring *ring, const cx_u128 *min_keys, const uint32_t *preds,
+                         int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    const hipMemcpyKind kind =
+        memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    (void)hipFree(ring->d_min_keys);
+    (void)hipFree(ring->d_preds);
+    ring->d_min_keys = nullptr;
+    ring->d_preds = nullptr;
+    if (min_keys) {
+        CX_HIP(hipMalloc(&ring->d_min_keys, ring->n * sizeof(cell128)));
+        CX_HIP(hipMemcpyAsync(ring->d_min_keys, min_keys, ring->n * sizeof(cell128), kind, s));
+    }
+    if (preds) {
+        CX_HIP(hipMalloc(&ring->d_preds, ring->n * sizeof(uint32_t)));
+        CX_HIP(hipMemcpyAsync(ring->d_preds, preds, ring->n * sizeof(uint32_t), kind, s));
+        CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
+        CX_HIP(cxk::check_indices(ring->d_preds, ring->n, (uint32_t)ring->n, true,
+                                  ring->d_scratch, s));
+        uint32_t bad = 0;
+        CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        CX_CHECK(!bad, CX_E_INVALID, "predecessor is neither a ring index nor CX_NONE");
+    }
+    return sync_if_host(memkind, s);
+}
+
+int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
+             uint32_t *owner, uint8_t *hops, uint8_t *status, int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ring->d_fingers != nullptr, CX_E_STATE,
+             "finger table not built (cx_fingers_build / cx_fingers_upload)");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    DBuf ts, tk, to, th, tst;
+    const uint32_t *dsrc;
+    const cx_u128 *dk;
+    uint32_t *dow;
+    uint8_t *dh, *dst = nullptr;
+    if ((rc = stage_in(src, q, memkind, ts, &dsrc, s))) return rc;
+    if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
+    if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
+    if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
+    CX_HIP(cxk::route(ring->d_ring, ring->n, ring->d_fingers, ring->d_min_keys, ring->d_preds,
+                      ring->literal(), dsrc, reinterpret_cast<const cell128 *>(dk), q, dow, dh,
+                      dst, s));
+    if (memkind == CX_MEM_HOST && q) {
+        CX_HIP(hipMemcpyAsync(owner, dow, q * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(hops, dh, q, hipMemcpyDeviceToHost, s));
+        if (status) CX_HIP(hipMemcpyAsync(status, dst, q, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+    }
+    return CX_OK;
+}
+
+int cx_nsucc(const cx_ring *ring, const cx_u128 *keys, size_t q, int n, uint32_t *lists,
+             uint8_t *count, int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(n >= 1 && n <= CX_MAX_NSUCC, CX_E_INVALID, "n must be in [1, 16]");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    DBuf tk, tl, tc;
+    const cx_u128 *dk;
+    uint32_t *dl;
+    uint8_t *dc;
+    if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(lists, q * (size_t)n, memkind, tl, &dl))) return rc;
+    if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
+    CX_HIP(cxk::nsucc(ring->eyt(), reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, s));
+    if (memkind == CX_MEM_HOST && q) {
+        CX_HIP(hipMemcpyAsync(lists, dl, q * (size_t)n * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(count, dc, q, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+    }
+    return CX_OK;
+}
+
+int cx_dhash_check(const cx_ring *ring, int n, int m) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(n >= 1 && m >= 1, CX_E_INVALID, "n and m must be positive");
+    const size_t got = ring->n < (size_t)n ? ring->n : (size_t)n;
+    if (got < (size_t)m)
+        return fail(CX_E_INSUFFICIENT, "Insufficient succs in list to complete request.");
+    return CX_OK;
+}
+
+int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_u128 *leaves,
+             size_t nl, int memkind, cx_ring **new_ring, uint32_t *old_to_new) {
+    CX_CHECK(old_ring && new_ring, CX_E_INVALID, "null argument");
+    *new_ring = nullptr;
+    int rc = use_device(old_ring);
+    if (rc) return rc;
+    const size_t n_old = old_ring->n;
+    CX_CHECK(n_old + nj < (size_t)CX_TAG_JOIN, CX_E_INVALID, "ring larger than 2^31 peers");
+    cx_ring *r = nullptr;
+    if ((rc = alloc_ring(old_ring->device, &r))) return rc;
+    hipStream_t s = r->stream;
+    // order the new handle's work after anything pending on the old one
+    rc = [&]() -> int {
+        CX_HIP(hipStreamSynchronize(old_ring->stream));
+        DBuf tj, tl, gone, k0, k1, t0, t1, ws, pos, o2n, ringbuf;
+        const cx_u128 *dj, *dl;
+        int e;
+        if ((e = stage_in(joins, nj, memkind, tj, &dj, s))) return e;
+        if ((e = stage_in(leaves, nl, memkind, tl, &dl, s))) return e;
+        CX_HIP(gone.alloc(n_old));
+        CX_HIP(hipMemsetAsync(gone.p, 0, n_old, s));
+        CX_HIP(cxk::mark_leaves(old_ring->eyt(), old_ring->d_ring,
+                                reinterpret_cast<const cell128 *>(dl), nl, gone.as<uint8_t>(), s));
+        const size_t cap = n_old + nj;
+        CX_HIP(k0.alloc(cap * sizeof(cell128)));
+        CX_HIP(k1.alloc(cap * sizeof(cell128)));
+        CX_HIP(t0.alloc(cap * sizeof(uint32_t)));
+        CX_HIP(t1.alloc(cap * sizeof(uint32_t)));
+        CX_HIP(pos.alloc(cap * sizeof(uint32_t)));
+        const size_t sw = cxk::sort_workspace_words(cap), cw = cxk::scan_workspace_words(cap);
+        CX_HIP(ws.alloc((sw > cw ? sw : cw) * sizeof(uint32_t)));
+        CX_HIP(cxk::compact_survivors(old_ring->d_ring, gone.as<uint8_t>(), n_old,
+                                      pos.as<uint32_t>(), ws.as<uint32_t>(), k0.as<cell128>(),
+                                      t0.as<uint32_t>(), r->d_scratch, s));
+        uint32_t ns = 0;
+        CX_HIP(hipMemcpyAsync(&ns, r->d_scratch, sizeof(ns), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        const size_t total = ns + nj;
+        CX_CHECK(total >= 1, CX_E_INVALID, "churn would leave an empty ring");
+        CX_HIP(cxk::copy_tagged(reinterpret_cast<const cell128 *>(dj), nj, CX_TAG_JOIN,
+                                k0.as<cell128>() + ns, t0.as<uint32_t>() + ns, s));
+        CX_HIP(cxk::radix_sort(k0.as<cell128>(), t0.as<uint32_t>(), k1.as<cell128>(),
+                               t1.as<uint32_t>(), total, ws.as<uint32_t>(), s));
+        CX_HIP(o2n.alloc(n_old * sizeof(uint32_t)));
+        CX_HIP(cxk::fill_u32(o2n.as<uint32_t>(), n_old, CX_NONE, s));
+        CX_HIP(ringbuf.alloc(total * sizeof(cell128)));
+        CX_HIP(cxk::unique_sorted(k0.as<cell128>(), t0.as<uint32_t>(), total,
+                                  pos.as<uint32_t>(), ws.as<uint32_t>(),
+                                  ringbuf.as<cell128>(), o2n.as<uint32_t>(), r->d_scratch, s));
+        uint32_t m = 0;
+        CX_HIP(hipMemcpyAsync(&m, r->d_scratch, sizeof(m), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        CX_CHECK(m >= 1 && m <= total, CX_E_HIP, "churn produced an invalid ring size");
+        r->n = m;
+        r->d_ring = ringbuf.as<cell128>();
+        ringbuf.release();
+        DBuf E;
+        CX_HIP(E.alloc((m + 1) * sizeof(cell128)));
+        CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
+        r->d_eyt = E.as<cell128>();
+        E.release();
+        if (old_to_new) {
+            const hipMemcpyKind kind =
+                memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+            CX_HIP(hipMemcpyAsync(old_to_new, o2n.p, n_old * sizeof(uint32_t), kind, s));
+        }
+        CX_HIP(hipStreamSynchronize(s));
+        return CX_OK;
+    }();
+    if (rc) {
+        free_ring(r);
+        return rc;
+    }
+    *new_ring = r;
+    return CX_OK;
+}
+
+int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_t *old_to_new,
+                 const cx_u128 *keys, size_t q, int n, uint32_t *new_lists, uint8_t *count,
+                 uint16_t *mask, uint8_t *target, int memkind) {
+    CX_CHECK(old_ring && new_ring, CX_E_INVALID, "null ring");
+    CX_CHECK(old_ring->device == new_ring->device, CX_E_INVALID, "rings on different devices");
+    CX_CHECK(n >= 1 && n <= CX_MAX_NSUCC, CX_E_INVALID, "n must be in [1, 16]");
+    int rc = use_device(new_ring);
+    if (rc) return rc;
+    hipStream_t s = new_ring->stream;
+    DBuf to2n, tk, tl, tc, tm, tt;
+    const uint32_t *d_o2n;
+    const cx_u128 *dk;
+    uint32_t *dl;
+    uint8_t *dc, *dt;
+    uint16_t *dm;
+    if ((rc = stage_in(old_to_new, old_ring->n, memkind, to2n, &d_o2n, s))) return rc;
+    if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl))) return rc;
+    if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
+    if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
+    if ((rc = stage_out(target, q * (size_t)n, memkind, tt, &dt))) return rc;
+    CX_HIP(cxk::misplaced_churn(old_ring->eyt(), new_ring->eyt(), d_o2n,
+                                reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, dm, dt, s));
+    if (memkind == CX_MEM_HOST && q) {
+        CX_HIP(hipMemcpyAsync(new_lists, dl, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(count, dc, q, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(mask, dm, q * 2, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(target, dt, q * (size_t)n, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+    }
+    return CX_OK;
+}
+
+int cx_misplaced_holders(const cx_ring *ring, const cx_u128 *keys, size_t q,
+                         const uint32_t *holders, int nh, int n, uint32_t *new_lists,
+                         uint8_t *count, uint16_t *mask, uint8_t *target, int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(n >= 1 && n <= CX_MAX_NSUCC, CX_E_INVALID, "n must be in [1, 16]");
+    CX_CHECK(nh >= 1 && nh <= CX_MAX_NSUCC, CX_E_INVALID, "nh must be in [1, 16]");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    DBuf th, tk, tl, tc, tm, tt;
+    const uint32_t *dh;
+    const cx_u128 *dk;
+    uint32_t *dl;
+    uint8_t *dc, *dt;
+    uint16_t *dm;
+    if ((rc = stage_in(holders, q * (size_t)nh, memkind, th, &dh, s))) return rc;
+    if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl))) return rc;
+    if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
+    if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
+    if ((rc = stage_out(target, q * (size_t)nh, memkind, tt, &dt))) return rc;
+    CX_HIP(cxk::misplaced_holders(ring->eyt(), dh, nh, reinterpret_cast<const cell128 *>(dk), q,
+                                  n, dl, dc, dm, dt, s));
+    if (memkind == CX_MEM_HOST && q) {
+        CX_HIP(hipMemcpyAsync(new_lists, dl, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(count, dc, q, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(mask, dm, q * 2, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(target, dt, q * (size_t)nh, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+    }
+    return CX_OK;
+}
+
+int cx_in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,
+                  int inclusive, uint8_t *out, int memkind) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    hipStream_t s = nullptr;  // default stream of the current device
+    DBuf tv, tl, tu, to;
+    const cx_u256 *dv, *dl, *du;
+    uint8_t *dout;
+    int rc;
+    if ((rc = stage_in(v, q, memkind, tv, &dv, s))) return rc;
+    if ((rc = stage_in(lb, q, memkind, tl, &dl, s))) return rc;
+    if ((rc = stage_in(ub, q, memkind, tu, &du, s))) return rc;
+    if ((rc = stage_out(out, q, memkind, to, &dout))) return rc;
+    CX_HIP(cxk::in_between(dv, dl, du, q, inclusive, dout, s));
+    if (memkind == CX_MEM_HOST && q) {
+        CX_HIP(hipMemcpyAsync(out, dout, q, hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+    }
+    return CX_OK;
+}
+
+int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t offset,
+                     int device, void *hip_stream) {
+    CX_CHECK(out_device || count == 0, CX_E_INVALID, "null output");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    CX_HIP(hipSetDevice(device));
+    CX_HIP(cxk::fill_splitmix(reinterpret_cast<cell128 *>(out_device), count, seed, offset,
+                              static_cast<hipStream_t>(hip_stream)));
+    return CX_OK;
+}
+
+}  // extern "C"

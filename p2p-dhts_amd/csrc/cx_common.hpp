@@ -1,0 +1,123 @@
+// cx_common.hpp -- shared device/host definitions for the chordx HIP engine.
+//
+// Ring values are unsigned 128-bit (ChordKey = GenericKey<16,32>, key.h:355).
+// In HBM a value is one 16-byte cell {lo, hi} (cx_u128); in registers it is an
+// unsigned __int128, which hipcc lowers to 64-bit VALU pairs on gfx950.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/chordx.h"
+
+typedef unsigned __int128 u128;
+
+struct alignas(16) cell128 {
+    uint64_t lo, hi;
+};
+static_assert(sizeof(cell128) == 16, "cell128 must be 16 B");
+static_assert(sizeof(cx_u128) == 16, "cx_u128 must be 16 B");
+
+__host__ __device__ __forceinline__ u128 to_u128(cell128 c) {
+    return ((u128)c.hi << 64) | c.lo;
+}
+__host__ __device__ __forceinline__ cell128 to_cell(u128 v) {
+    cell128 c;
+    c.lo = (uint64_t)v;
+    c.hi = (uint64_t)(v >> 64);
+    return c;
+}
+
+// One 16-byte load (global_load_dwordx4) of a ring cell.
+__device__ __forceinline__ u128 ld128(const cell128 *p) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);
+    return ((u128)(((uint64_t)v.w << 32) | v.z) << 64) | (((uint64_t)v.y << 32) | v.x);
+}
+__device__ __forceinline__ void st128(cell128 *p, u128 x) {
+    uint4 v;
+    v.x = (uint32_t)x;
+    v.y = (uint32_t)(x >> 32);
+    v.z = (uint32_t)(x >> 64);
+    v.w = (uint32_t)(x >> 96);
+    *reinterpret_cast<uint4 *>(p) = v;
+}
+
+// floor(log2(d)) for d != 0: the finger index FingerTable::Lookup's first-match
+// scan selects (finger ranges [id+2^i, id+2^(i+1)-1] partition (id, id-1],
+// finger_table.h:177-188).
+__device__ __forceinline__ int msb128(u128 d) {
+    const uint64_t hi = (uint64_t)(d >> 64);
+    const uint64_t lo = (uint64_t)d;
+    return hi ? 127 - __clzll((long long)hi) : 63 - __clzll((long long)lo);
+}
+
+// Counter-based synthetic generator of SURVEY 8(d).
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t ctr) {
+    uint64_t z = seed + (ctr + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// Eytzinger (BFS) layout of the sorted ring.  Node k (1-based) of a heap-shaped
+// tree with n nodes; tree height h = floor(log2 n).  The first `lds_levels`
+// levels are staged in LDS by every search workgroup.
+// ---------------------------------------------------------------------------
+struct EytView {
+    const cell128 *E;   // E[1..n]
+    uint32_t n;
+    int h;              // floor(log2 n)
+};
+
+// Number of nodes in the subtree rooted at j (depth dj), 0 if j > n.
+__host__ __device__ __forceinline__ uint32_t eyt_subtree(uint64_t j, int dj, uint32_t n, int h) {
+    if (j > n) return 0;
+    const int t = h - dj;                    // levels below j down to level h
+    const uint32_t full = (1u << t) - 1u;    // complete levels dj .. h-1
+    const uint64_t first_last = j << t;      // leftmost level-h node under j
+    uint64_t last = 0;
+    if ((uint64_t)n >= first_last) {
+        last = (uint64_t)n - first_last + 1;
+        if (last > (1ull << t)) last = 1ull << t;
+    }
+    return full + (uint32_t)last;
+}
+
+#define CX_LDS_LEVELS 12                     // 4095 nodes x 16 B = 64 KiB of LDS
+#define CX_LDS_NODES ((1u << CX_LDS_LEVELS) - 1u)
+
+// Sorted index of succ(x) (first id >= x, wrapping to 0).  `lds` holds nodes
+// 1..min(n, CX_LDS_NODES) at lds[k-1].  Tracks the count of ids < x along the
+// descent: going right past node k passes its left subtree and k itself.
+__device__ __forceinline__ uint32_t eyt_successor(const EytView &ev, const u128 *lds, u128 x) {
+    uint64_t k = 1;
+    uint32_t less = 0;
+    int d = 0;
+    const uint32_t n = ev.n;
+    while (k <= n) {
+        const u128 e = (k <= CX_LDS_NODES) ? lds[k - 1] : ld128(ev.E + k);
+        const bool lt = e < x;
+        if (lt) less += eyt_subtree(2 * k, d + 1, n, ev.h) + 1u;
+        k = 2 * k + (lt ? 1 : 0);
+        ++d;
+    }
+    return less == n ? 0u : less;
+}
+
+__device__ __forceinline__ void eyt_stage_lds(const EytView &ev, u128 *lds) {
+    const uint32_t m = ev.n < CX_LDS_NODES ? ev.n : CX_LDS_NODES;
+    for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) lds[k] = ld128(ev.E + 1 + k);
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch helpers.
+// ---------------------------------------------------------------------------
+static inline unsigned cx_grid(size_t work, unsigned block, unsigned cap = 8192) {
+    size_t g = (work + block - 1) / block;
+    if (g == 0) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}

@@ -1,0 +1,794 @@
+// cx_kernels.hip -- gfx950 kernels of the chordx engine and their launchers.
+//
+// Every kernel is HBM/latency bound integer work: no MFMA.  Layout
+// in HBM: ring IDs as 16-B cells (AoS, one dwordx4 per ID), finger table as
+// row-major uint32 [peer][128], Eytzinger copy of the ring for searches.
+#include "cx_kernels.hpp"
+
+namespace cxk {
+
+// ===========================================================================
+// Device-wide exclusive scan of uint32 (radix offsets, compaction indices).
+// ===========================================================================
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of one value per thread; returns the block total
+// through *total.  Block = SCAN_BLOCK threads (4 waves).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *total) {
+    __shared__ uint32_t wsum[SCAN_BLOCK / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_BLOCK / 64; ++w) {
+        wbase += (w < wave) ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + inc - v;
+}
+
+// In-place exclusive scan inside each SCAN_TILE tile; tile totals -> sums.
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(uint32_t *data, size_t n,
+                                                           uint32_t *sums) {
+    __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];  // +1 pad per 32 words
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const int li = j * SCAN_BLOCK + t;
+        const size_t gi = base + li;
+        tile[li + (li >> 5)] = gi < n ? data[gi] : 0u;
+    }
+    __syncthreads();
+    // thread t owns elements [t*ITEMS, t*ITEMS + ITEMS)
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const int li = t * SCAN_ITEMS + j;
+        run += tile[li + (li >> 5)];
+    }
+    uint32_t total;
+    const uint32_t off = block_excl_scan(run, &total);
+    run = off;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const int li = t * SCAN_ITEMS + j;
+        const uint32_t v = tile[li + (li >> 5)];
+        tile[li + (li >> 5)] = run;
+        run += v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const int li = j * SCAN_BLOCK + t;
+        const size_t gi = base + li;
+        if (gi < n) data[gi] = tile[li + (li >> 5)];
+    }
+    if (t == 0 && sums) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_add(uint32_t *data, size_t n,
+                                                         const uint32_t *sums) {
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    const uint32_t add = sums[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        const size_t gi = base + j * SCAN_BLOCK + threadIdx.x;
+        if (gi < n) data[gi] += add;
+    }
+}
+
+size_t scan_workspace_words(size_t n) {
+    size_t words = 0;
+    while (n > (size_t)SCAN_TILE) {
+        n = (n + SCAN_TILE - 1) / SCAN_TILE;
+        words += n;
+    }
+    return words + 1;
+}
+
+hipError_t exclusive_scan(uint32_t *data, size_t n, uint32_t *ws, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (tiles == 1) {
+        k_scan_tiles<<<1, SCAN_BLOCK, 0, s>>>(data, n, nullptr);
+        return hipGetLastError();
+    }
+    uint32_t *sums = ws;
+    k_scan_tiles<<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(data, n, sums);
+    hipError_t e = exclusive_scan(sums, tiles, ws + tiles, s);
+    if (e != hipSuccess) return e;
+    k_scan_add<<<(unsigned)tiles, SCAN_BLOCK, 0, s>>>(data, n, sums);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// LSD radix sort of (128-bit key, uint32 tag): 16 stable passes of 8 bits.
+// Pass = histogram per 4096-element tile -> exclusive scan over [digit][tile]
+// -> stable scatter (wave match via 8 ballots + cross-wave prefix in LDS).
+// ===========================================================================
+constexpr int RS_BLOCK = 256;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_BLOCK * RS_ITEMS;
+
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const cell128 *keys, size_t n, int shift,
+                                                      uint32_t *hist, uint32_t ntiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const size_t i = base + j * RS_BLOCK + threadIdx.x;
+        if (i < n) {
+            const uint32_t d = (uint32_t)(ld128(keys + i) >> shift) & 0xFFu;
+            atomicAdd(&h[d], 1u);
+        }
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const cell128 *kin, const uint32_t *tin,
+                                                         cell128 *kout, uint32_t *tout, size_t n,
+                                                         int shift, const uint32_t *offs,
+                                                         uint32_t ntiles) {
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wcnt[RS_BLOCK / 64][256];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    base[t] = offs[(size_t)t * ntiles + blockIdx.x];
+    const size_t tile0 = (size_t)blockIdx.x * RS_TILE;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const size_t i = tile0 + (size_t)j * RS_BLOCK + t;
+        const bool valid = i < n;
+        u128 key = 0;
+        uint32_t tag = 0, d = 0;
+        if (valid) {
+            key = ld128(kin + i);
+            tag = tin[i];
+            d = (uint32_t)(key >> shift) & 0xFFu;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wcnt[wave][lane + 64 * r] = 0;
+        __syncthreads();
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lt_mask);
+        if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = 0;
+            for (int w = 0; w < wave; ++w) pre += wcnt[w][d];
+            const uint32_t pos = base[d] + pre + rank;
+            st128(kout + pos, key);
+            tout[pos] = tag;
+        }
+        __syncthreads();
+        uint32_t add = 0;
+#pragma unroll
+        for (int w = 0; w < RS_BLOCK / 64; ++w) add += wcnt[w][t];
+        base[t] += add;
+        __syncthreads();  // every wave has read wcnt before the next slot zeroes it
+    }
+}
+
+size_t sort_workspace_words(size_t n) {
+    const size_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+    return 256 * ntiles + scan_workspace_words(256 * ntiles);
+}
+
+// Sorts (keys, tags) by key, stable.  Ping-pongs between (k0,t0) and (k1,t1);
+// 16 passes leave the result in (k0, t0).
+hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
+                      uint32_t *ws, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    uint32_t *hist = ws;
+    uint32_t *scan_ws = ws + (size_t)256 * ntiles;
+    for (int pass = 0; pass < 16; ++pass) {
+        const int shift = 8 * pass;
+        cell128 *ki = (pass & 1) ? k1 : k0, *ko = (pass & 1) ? k0 : k1;
+        uint32_t *ti = (pass & 1) ? t1 : t0, *to = (pass & 1) ? t0 : t1;
+        k_rs_hist<<<ntiles, RS_BLOCK, 0, s>>>(ki, n, shift, hist, ntiles);
+        hipError_t e = exclusive_scan(hist, (size_t)256 * ntiles, scan_ws, s);
+        if (e != hipSuccess) return e;
+        k_rs_scatter<<<ntiles, RS_BLOCK, 0, s>>>(ki, ti, ko, to, n, shift, hist, ntiles);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// ===========================================================================
+// Dedupe / compaction (equal IDs rejected, remote_peer_list.cpp:56-58).
+// ===========================================================================
+__global__ void k_flag_unique(const cell128 *keys, size_t n, uint32_t *flag) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        flag[i] = (i == 0 || ld128(keys + i) != ld128(keys + i - 1)) ? 1u : 0u;
+}
+
+// pos = exclusive scan of flags.  Keeps flagged keys; a kept tag < CX_TAG_JOIN
+// (an old peer index) gets old_to_new[tag] = new position.
+__global__ void k_compact_unique(const cell128 *keys, const uint32_t *tags, size_t n,
+                                 const uint32_t *pos, cell128 *out, uint32_t *old_to_new) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const bool keep = (i == 0 || ld128(keys + i) != ld128(keys + i - 1));
+        if (!keep) continue;
+        const uint32_t p = pos[i];
+        st128(out + p, ld128(keys + i));
+        if (old_to_new && tags[i] < CX_TAG_JOIN) old_to_new[tags[i]] = p;
+    }
+}
+
+__global__ void k_iota(uint32_t *t, size_t n, uint32_t base) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        t[i] = base + (uint32_t)i;
+}
+
+__global__ void k_fill_u32(uint32_t *t, size_t n, uint32_t v) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        t[i] = v;
+}
+
+__global__ void k_count_last(const uint32_t *pos, const cell128 *keys, size_t n, uint32_t *out) {
+    // unique count = pos[n-1] + flag[n-1]
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const bool keep = (n == 1) || ld128(keys + n - 1) != ld128(keys + n - 2);
+        *out = pos[n - 1] + (keep ? 1u : 0u);
+    }
+}
+
+hipError_t unique_sorted(const cell128 *keys, const uint32_t *tags, size_t n, uint32_t *pos,
+                         uint32_t *scan_ws, cell128 *out, uint32_t *old_to_new,
+                         uint32_t *d_count, hipStream_t s) {
+    const unsigned g = cx_grid(n, 256);
+    k_flag_unique<<<g, 256, 0, s>>>(keys, n, pos);
+    hipError_t e = exclusive_scan(pos, n, scan_ws, s);
+    if (e != hipSuccess) return e;
+    k_count_last<<<1, 64, 0, s>>>(pos, keys, n, d_count);
+    k_compact_unique<<<g, 256, 0, s>>>(keys, tags, n, pos, out, old_to_new);
+    return hipGetLastError();
+}
+
+// Survivor compaction for churn: keep[p] = !gone[p].
+__global__ void k_keep_flags(const uint8_t *gone, size_t n, uint32_t *flag) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        flag[i] = gone[i] ? 0u : 1u;
+}
+__global__ void k_compact_survivors(const cell128 *ring, const uint8_t *gone, size_t n,
+                                    const uint32_t *pos, cell128 *out_keys, uint32_t *out_tags) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        if (gone[i]) continue;
+        const uint32_t p = pos[i];
+        st128(out_keys + p, ld128(ring + i));
+        out_tags[p] = (uint32_t)i;
+    }
+}
+__global__ void k_count_survivors(const uint32_t *pos, const uint8_t *gone, size_t n,
+                                  uint32_t *out) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *out = pos[n - 1] + (gone[n - 1] ? 0u : 1u);
+}
+
+hipError_t compact_survivors(const cell128 *ring, const uint8_t *gone, size_t n, uint32_t *pos,
+                             uint32_t *scan_ws, cell128 *out_keys, uint32_t *out_tags,
+                             uint32_t *d_count, hipStream_t s) {
+    const unsigned g = cx_grid(n, 256);
+    k_keep_flags<<<g, 256, 0, s>>>(gone, n, pos);
+    hipError_t e = exclusive_scan(pos, n, scan_ws, s);
+    if (e != hipSuccess) return e;
+    k_count_survivors<<<1, 64, 0, s>>>(pos, gone, n, d_count);
+    k_compact_survivors<<<g, 256, 0, s>>>(ring, gone, n, pos, out_keys, out_tags);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// Eytzinger build: E[k] = sorted[inorder rank of node k].
+// ===========================================================================
+__device__ __forceinline__ uint32_t eyt_rank(uint64_t k, uint32_t n, int h) {
+    const int depth = 63 - __clzll((long long)k);
+    uint64_t node = 1;
+    uint32_t r = 0;
+    for (int b = depth - 1, d = 0; b >= 0; --b, ++d) {
+        if ((k >> b) & 1ull) {
+            r += eyt_subtree(2 * node, d + 1, n, h) + 1u;
+            node = 2 * node + 1;
+        } else {
+            node = 2 * node;
+        }
+    }
+    return r + eyt_subtree(2 * k, depth + 1, n, h);
+}
+
+__global__ void k_eyt_build(const cell128 *sorted, uint32_t n, int h, cell128 *E) {
+    for (size_t k = 1 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; k <= n;
+         k += (size_t)gridDim.x * blockDim.x)
+        st128(E + k, ld128(sorted + eyt_rank(k, n, h)));
+}
+
+hipError_t eyt_build(const cell128 *sorted, size_t n, cell128 *E, hipStream_t s) {
+    const int h = 63 - __builtin_clzll((unsigned long long)n);
+    k_eyt_build<<<cx_grid(n, 256), 256, 0, s>>>(sorted, (uint32_t)n, h, E);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// a5/a7: exact successor.  One lane per query; top CX_LDS_LEVELS of the
+// Eytzinger tree in LDS (64 KiB), the rest gathered from HBM/L2.
+// ===========================================================================
+constexpr int SUCC_BLOCK = 1024;
+
+__global__ __launch_bounds__(SUCC_BLOCK) void k_successor(EytView ev, const cell128 *keys,
+                                                          size_t q, uint32_t *owner) {
+    __shared__ u128 lds[CX_LDS_NODES];
+    eyt_stage_lds(ev, lds);
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x)
+        owner[i] = eyt_successor(ev, lds, ld128(keys + i));
+}
+
+hipError_t successor(const EytView &ev, const cell128 *keys, size_t q, uint32_t *owner,
+                     hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_successor<<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, keys, q, owner);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// a6: converged finger table.  Lane (p, i): succ(id_p + 2^i).  When 2^i is no
+// larger than the gap to the next peer the answer is p+1 without a search.
+// ===========================================================================
+__global__ __launch_bounds__(SUCC_BLOCK) void k_fingers(EytView ev, const cell128 *ring,
+                                                        uint32_t *F) {
+    __shared__ u128 lds[CX_LDS_NODES];
+    eyt_stage_lds(ev, lds);
+    const uint32_t n = ev.n;
+    const size_t total = (size_t)n * CX_FINGERS;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t p = (uint32_t)(t >> 7);
+        const int i = (int)(t & 127);
+        uint32_t f = 0;
+        if (n > 1) {
+            const u128 idp = ld128(ring + p);
+            const uint32_t nx = (p + 1 == n) ? 0u : p + 1;
+            const u128 gap = ld128(ring + nx) - idp;  // clockwise distance to next peer
+            const u128 step = (u128)1 << i;
+            f = (step <= gap) ? nx : eyt_successor(ev, lds, idp + step);
+        }
+        F[t] = f;
+    }
+}
+
+hipError_t fingers_build(const EytView &ev, const cell128 *ring, uint32_t *F, hipStream_t s) {
+    const size_t total = (size_t)ev.n * CX_FINGERS;
+    k_fingers<<<cx_grid(total, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, ring, F);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// a7-a9: routed lookup, converged table.
+// StoredLocally(src) = key in (ring[src-1], ring[src]] (min_key = pred + 1).
+// Each hop: i = msb(key - id_cur) (= FingerTable::Lookup's first match),
+// nxt = F[cur][i].  Because nxt = succ(id_cur + 2^i) and key - id_cur >= 2^i,
+// StoredLocally(nxt) <=> key - id_cur <= id_nxt - id_cur: the hop needs only
+// the finger and the next peer's ID (no predecessor gather).  The self ->
+// predecessor substitution of ForwardRequest (chord_peer.cpp:195-197) cannot
+// trigger on a converged table ("route").
+// ===========================================================================
+constexpr int ROUTE_BLOCK = 256;
+
+__global__ __launch_bounds__(ROUTE_BLOCK) void k_route_conv(const cell128 *ring, uint32_t n,
+                                                            const uint32_t *F,
+                                                            const uint32_t *src,
+                                                            const cell128 *keys, size_t q,
+                                                            uint32_t *owner, uint8_t *hops,
+                                                            uint8_t *status) {
+    for (size_t qi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; qi < q;
+         qi += (size_t)gridDim.x * blockDim.x) {
+        const u128 key = ld128(keys + qi);
+        uint32_t cur = src[qi];
+        uint32_t own = cur, h = 0;
+        uint8_t st = CX_Q_OK;
+        if (cur >= n) {
+            own = CX_NONE;
+            st = CX_Q_BADPEER;
+        } else if (n > 1) {
+            u128 idc = ld128(ring + cur);
+            const u128 idp = ld128(ring + (cur == 0 ? n - 1 : cur - 1));
+            const bool local = (key - idp - 1) <= (idc - idp - 1);
+            if (!local) {
+                for (;;) {
+                    const u128 d = key - idc;
+                    const int i = msb128(d);
+                    const uint32_t nxt = F[(size_t)cur * CX_FINGERS + i];
+                    if (nxt >= n) {  // corrupt table: never gather out of bounds
+                        own = CX_NONE;
+                        st = CX_Q_BADPEER;
+                        break;
+                    }
+                    const u128 idn = ld128(ring + nxt);
+                    ++h;
+                    if (d <= idn - idc) {
+                        own = nxt;
+                        break;
+                    }
+                    if (h == CX_HOP_CAP) {
+                        own = CX_NONE;
+                        st = CX_Q_HOPCAP;
+                        break;
+                    }
+                    cur = nxt;
+                    idc = idn;
+                }
+            }
+        }
+        owner[qi] = own;
+        hops[qi] = (uint8_t)h;
+        if (status) status[qi] = st;
+    }
+}
+
+// Literal walk for hand-edited tables / peer state: StoredLocally with the
+// peer's own min_key_ (InBetween(min_key, id, true), key.h:103-131 on
+// canonical operands), first-match finger, self -> predecessor substitution.
+__device__ __forceinline__ bool in_between128(u128 v, u128 lb, u128 ub) {
+    if (lb == ub) return v == ub;
+    if (lb < ub) return lb <= v && v <= ub;
+    return !(ub < v && v < lb);
+}
+
+__global__ __launch_bounds__(ROUTE_BLOCK) void k_route_literal(
+    const cell128 *ring, uint32_t n, const uint32_t *F, const cell128 *min_keys,
+    const uint32_t *preds, const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
+    uint8_t *hops, uint8_t *status) {
+    for (size_t qi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; qi < q;
+         qi += (size_t)gridDim.x * blockDim.x) {
+        const u128 key = ld128(keys + qi);
+        uint32_t cur = src[qi], h = 0, own = CX_NONE;
+        uint8_t st = CX_Q_OK;
+        for (;;) {
+            if (cur >= n) {
+                st = CX_Q_BADPEER;
+                own = CX_NONE;
+                break;
+            }
+            const u128 id = ld128(ring + cur);
+            const uint32_t pdef = (n == 1) ? CX_NONE : (cur == 0 ? n - 1 : cur - 1);
+            const u128 mk = min_keys ? ld128(min_keys + cur)
+                                     : ld128(ring + (n == 1 ? cur : pdef)) + 1;
+            if (in_between128(key, mk, id)) {
+                own = cur;
+                break;
+            }
+            const int i = msb128(key - id);  // key != id here (id is always local)
+            uint32_t nxt = F[(size_t)cur * CX_FINGERS + i];
+            const uint32_t pr = preds ? preds[cur] : pdef;
+            if (nxt == cur && pr != CX_NONE) nxt = pr;
+            if (h == CX_HOP_CAP) {
+                st = CX_Q_HOPCAP;
+                own = CX_NONE;
+                break;
+            }
+            ++h;
+            cur = nxt;
+        }
+        owner[qi] = own;
+        hops[qi] = (uint8_t)h;
+        if (status) status[qi] = st;
+    }
+}
+
+hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
+                 const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
+                 size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const unsigned g = cx_grid(q, ROUTE_BLOCK, 1u << 20);
+    if (literal)
+        k_route_literal<<<g, ROUTE_BLOCK, 0, s>>>(ring, (uint32_t)n, F, min_keys, preds, src,
+                                                  keys, q, owner, hops, status);
+    else
+        k_route_conv<<<g, ROUTE_BLOCK, 0, s>>>(ring, (uint32_t)n, F, src, keys, q, owner, hops,
+                                               status);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// a10/a11: n-successor windows.
+// ===========================================================================
+__global__ __launch_bounds__(SUCC_BLOCK) void k_nsucc(EytView ev, const cell128 *keys, size_t q,
+                                                      int nlist, uint32_t *lists,
+                                                      uint8_t *count) {
+    __shared__ u128 lds[CX_LDS_NODES];
+    eyt_stage_lds(ev, lds);
+    const uint32_t n = ev.n;
+    const int nn = (uint32_t)nlist < n ? nlist : (int)n;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s0 = eyt_successor(ev, lds, ld128(keys + i));
+        uint32_t *l = lists + i * (size_t)nlist;
+        for (int j = 0; j < nlist; ++j) {
+            uint32_t v = s0 + (uint32_t)j;
+            if (v >= n) v -= n;
+            l[j] = j < nn ? v : CX_NONE;
+        }
+        count[i] = (uint8_t)nn;
+    }
+}
+
+hipError_t nsucc(const EytView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
+                 uint8_t *count, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_nsucc<<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, keys, q, n, lists, count);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// a12: churn support + misplaced scan.
+// ===========================================================================
+__global__ __launch_bounds__(SUCC_BLOCK) void k_mark_leaves(EytView ev, const cell128 *ring,
+                                                            const cell128 *leaves, size_t nl,
+                                                            uint8_t *gone) {
+    __shared__ u128 lds[CX_LDS_NODES];
+    eyt_stage_lds(ev, lds);
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nl;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const u128 x = ld128(leaves + i);
+        const uint32_t s0 = eyt_successor(ev, lds, x);
+        if (ld128(ring + s0) == x) gone[s0] = 1;
+    }
+}
+
+hipError_t mark_leaves(const EytView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
+                       uint8_t *gone, hipStream_t s) {
+    if (nl == 0) return hipSuccess;
+    k_mark_leaves<<<cx_grid(nl, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, ring, leaves, nl,
+                                                                      gone);
+    return hipGetLastError();
+}
+
+__global__ void k_copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 *dk,
+                              uint32_t *dt) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        st128(dk + i, ld128(src + i));
+        dt[i] = tag_base + (uint32_t)i;
+    }
+}
+
+hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 *dk,
+                       uint32_t *dt, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_copy_tagged<<<cx_grid(n, 256), 256, 0, s>>>(src, n, tag_base, dk, dt);
+    return hipGetLastError();
+}
+
+// Misplaced scan core.  Holder ranks j in order; `has` = 16-bit mask of new-list
+// ranks already holding the key; membership of a holder in the new window is
+// (holder - s_new) mod n_new < nn.
+template <bool CHURN>
+__global__ __launch_bounds__(512) void k_misplaced(EytView ev_new, EytView ev_old,
+                                                   const uint32_t *old_to_new,
+                                                   const uint32_t *holders, int nh,
+                                                   const cell128 *keys, size_t q, int nlist,
+                                                   uint32_t *new_lists, uint8_t *count,
+                                                   uint16_t *mask, uint8_t *target) {
+    __shared__ u128 lds_new[CX_LDS_NODES];
+    __shared__ u128 lds_old[CHURN ? CX_LDS_NODES : 1];
+    eyt_stage_lds(ev_new, lds_new);
+    if (CHURN) eyt_stage_lds(ev_old, lds_old);
+    const uint32_t n_new = ev_new.n;
+    const int nn = (uint32_t)nlist < n_new ? nlist : (int)n_new;
+    const uint32_t n_old = CHURN ? ev_old.n : 0;
+    const int no = CHURN ? ((uint32_t)nlist < n_old ? nlist : (int)n_old) : nh;
+    const int nslots = CHURN ? nlist : nh;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const u128 key = ld128(keys + i);
+        const uint32_t sn = eyt_successor(ev_new, lds_new, key);
+        uint32_t so = 0;
+        if (CHURN) so = eyt_successor(ev_old, lds_old, key);
+        uint32_t *l = new_lists + i * (size_t)nlist;
+        for (int j = 0; j < nlist; ++j) {
+            uint32_t v = sn + (uint32_t)j;
+            if (v >= n_new) v -= n_new;
+            l[j] = j < nn ? v : CX_NONE;
+        }
+        count[i] = (uint8_t)nn;
+        // pass 1: which new-list ranks already hold the key
+        uint32_t has = 0;
+        for (int j = 0; j < no; ++j) {
+            uint32_t hj;
+            if (CHURN) {
+                uint32_t o = so + (uint32_t)j;
+                if (o >= n_old) o -= n_old;
+                hj = old_to_new[o];
+            } else {
+                hj = holders[i * (size_t)nh + j];
+            }
+            if (hj >= n_new) continue;  // CX_NONE (empty / departed) or invalid
+            uint32_t r = hj >= sn ? hj - sn : hj + n_new - sn;
+            if (r < (uint32_t)nn) has |= 1u << r;
+        }
+        // pass 2: misplaced holders in rank order take the first lacking rank
+        uint32_t m = 0;
+        const uint32_t full = (nn >= 32) ? 0xFFFFFFFFu : ((1u << nn) - 1u);
+        uint8_t *tg = target + i * (size_t)nslots;
+        for (int j = 0; j < nslots; ++j) {
+            uint8_t t = 0xFF;
+            if (j < no) {
+                uint32_t hj;
+                if (CHURN) {
+                    uint32_t o = so + (uint32_t)j;
+                    if (o >= n_old) o -= n_old;
+                    hj = old_to_new[o];
+                } else {
+                    hj = holders[i * (size_t)nh + j];
+                }
+                if (hj < n_new) {
+                    const uint32_t r = hj >= sn ? hj - sn : hj + n_new - sn;
+                    if (r >= (uint32_t)nn) {
+                        m |= 1u << j;
+                        const uint32_t free_ranks = ~has & full;
+                        if (free_ranks) {
+                            const int rr = __builtin_ctz(free_ranks);
+                            has |= 1u << rr;
+                            t = (uint8_t)rr;
+                        }
+                    }
+                }
+            }
+            tg[j] = t;
+        }
+        mask[i] = (uint16_t)m;
+    }
+}
+
+hipError_t misplaced_churn(const EytView &ev_old, const EytView &ev_new,
+                           const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
+                           uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
+                           hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_misplaced<true><<<cx_grid(q, 512, 256), 512, 0, s>>>(ev_new, ev_old, old_to_new, nullptr,
+                                                          0, keys, q, n, lists, count, mask,
+                                                          target);
+    return hipGetLastError();
+}
+
+hipError_t misplaced_holders(const EytView &ev, const uint32_t *holders, int nh,
+                             const cell128 *keys, size_t q, int n, uint32_t *lists,
+                             uint8_t *count, uint16_t *mask, uint8_t *target, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_misplaced<false><<<cx_grid(q, 512, 512), 512, 0, s>>>(ev, ev, nullptr, holders, nh, keys, q,
+                                                           n, lists, count, mask, target);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// a2: InBetween on raw uint256 operands (key.h:103-131).
+// ===========================================================================
+struct u256v {
+    uint64_t w[4];
+};
+__device__ __forceinline__ int cmp256(const u256v &a, const u256v &b) {
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        if (a.w[i] < b.w[i]) return -1;
+        if (a.w[i] > b.w[i]) return 1;
+    }
+    return 0;
+}
+__global__ void k_in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,
+                             int inclusive, uint8_t *out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x) {
+        u256v V, L, U;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            V.w[j] = v[i].w[j];
+            L.w[j] = lb[i].w[j];
+            U.w[j] = ub[i].w[j];
+        }
+        bool r;
+        if (cmp256(L, U) == 0) {
+            r = cmp256(V, U) == 0;
+        } else {
+            u256v ml = {{L.w[0], L.w[1], 0, 0}}, mu = {{U.w[0], U.w[1], 0, 0}},
+                  mv = {{V.w[0], V.w[1], 0, 0}};
+            if (cmp256(L, U) < 0)
+                r = inclusive ? (cmp256(ml, mv) <= 0 && cmp256(mv, U) <= 0)
+                              : (cmp256(ml, mv) < 0 && cmp256(mv, U) < 0);
+            else
+                r = inclusive ? !(cmp256(mu, mv) < 0 && cmp256(mv, ml) < 0)
+                              : !(cmp256(mu, mv) <= 0 && cmp256(mv, ml) <= 0);
+        }
+        out[i] = r ? 1 : 0;
+    }
+}
+
+hipError_t in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,
+                      int inclusive, uint8_t *out, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_in_between<<<cx_grid(q, 256), 256, 0, s>>>(v, lb, ub, q, inclusive, out);
+    return hipGetLastError();
+}
+
+// ===========================================================================
+// Synthetic keys.
+// ===========================================================================
+__global__ void k_splitmix(cell128 *out, size_t count, uint64_t seed, uint64_t offset) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t c = offset + i;
+        cell128 v;
+        v.lo = splitmix64(seed, 2 * c);
+        v.hi = splitmix64(seed, 2 * c + 1);
+        out[i] = v;
+    }
+}
+
+hipError_t fill_splitmix(cell128 *out, size_t count, uint64_t seed, uint64_t offset,
+                         hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    k_splitmix<<<cx_grid(count, 256), 256, 0, s>>>(out, count, seed, offset);
+    return hipGetLastError();
+}
+
+hipError_t iota(uint32_t *t, size_t n, uint32_t base, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_iota<<<cx_grid(n, 256), 256, 0, s>>>(t, n, base);
+    return hipGetLastError();
+}
+
+hipError_t fill_u32(uint32_t *t, size_t n, uint32_t v, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_fill_u32<<<cx_grid(n, 256), 256, 0, s>>>(t, n, v);
+    return hipGetLastError();
+}
+
+// Validation of caller-supplied peer indices (finger uploads, preds):
+// *d_bad = 1 if any entry is >= limit (CX_NONE allowed when allow_none).
+__global__ void k_check_indices(const uint32_t *idx, size_t count, uint32_t limit,
+                                int allow_none, uint32_t *bad) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t v = idx[i];
+        if (v >= limit && !(allow_none && v == CX_NONE)) atomicOr(bad, 1u);
+    }
+}
+
+hipError_t check_indices(const uint32_t *idx, size_t count, uint32_t limit, bool allow_none,
+                         uint32_t *d_bad, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    k_check_indices<<<cx_grid(count, 256), 256, 0, s>>>(idx, count, limit, allow_none ? 1 : 0,
+                                                        d_bad);
+    return hipGetLastError();
+}
+
+}  // namespace cxk

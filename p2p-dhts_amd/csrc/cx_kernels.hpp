@@ -1,0 +1,54 @@
+// cx_kernels.hpp -- launchers of the gfx950 kernels (internal to libchordx).
+#pragma once
+
+#include "cx_common.hpp"
+
+// Tags >= CX_TAG_JOIN mark joining peers during a churn sort; smaller tags
+// are old ring indices.
+#define CX_TAG_JOIN 0x80000000u
+
+namespace cxk {
+
+size_t scan_workspace_words(size_t n);
+hipError_t exclusive_scan(uint32_t *data, size_t n, uint32_t *ws, hipStream_t s);
+
+size_t sort_workspace_words(size_t n);
+hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
+                      uint32_t *ws, hipStream_t s);
+hipError_t unique_sorted(const cell128 *keys, const uint32_t *tags, size_t n, uint32_t *pos,
+                         uint32_t *scan_ws, cell128 *out, uint32_t *old_to_new,
+                         uint32_t *d_count, hipStream_t s);
+hipError_t compact_survivors(const cell128 *ring, const uint8_t *gone, size_t n, uint32_t *pos,
+                             uint32_t *scan_ws, cell128 *out_keys, uint32_t *out_tags,
+                             uint32_t *d_count, hipStream_t s);
+hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 *dk,
+                       uint32_t *dt, hipStream_t s);
+hipError_t iota(uint32_t *t, size_t n, uint32_t base, hipStream_t s);
+hipError_t fill_u32(uint32_t *t, size_t n, uint32_t v, hipStream_t s);
+
+hipError_t eyt_build(const cell128 *sorted, size_t n, cell128 *E, hipStream_t s);
+hipError_t successor(const EytView &ev, const cell128 *keys, size_t q, uint32_t *owner,
+                     hipStream_t s);
+hipError_t fingers_build(const EytView &ev, const cell128 *ring, uint32_t *F, hipStream_t s);
+hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
+                 const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
+                 size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t nsucc(const EytView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
+                 uint8_t *count, hipStream_t s);
+hipError_t mark_leaves(const EytView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
+                       uint8_t *gone, hipStream_t s);
+hipError_t misplaced_churn(const EytView &ev_old, const EytView &ev_new,
+                           const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
+                           uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
+                           hipStream_t s);
+hipError_t misplaced_holders(const EytView &ev, const uint32_t *holders, int nh,
+                             const cell128 *keys, size_t q, int n, uint32_t *lists,
+                             uint8_t *count, uint16_t *mask, uint8_t *target, hipStream_t s);
+hipError_t in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,
+                      int inclusive, uint8_t *out, hipStream_t s);
+hipError_t fill_splitmix(cell128 *out, size_t count, uint64_t seed, uint64_t offset,
+                         hipStream_t s);
+hipError_t check_indices(const uint32_t *idx, size_t count, uint32_t limit, bool allow_none,
+                         uint32_t *d_bad, hipStream_t s);
+
+}  // namespace cxk

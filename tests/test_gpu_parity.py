@@ -1,0 +1,322 @@
+"""Parity of the HIP engine (through the C ABI) against the CPU oracle.
+
+Bit-exact integer comparisons throughout: owner indices, hop counts, finger
+tables, replica lists, misplaced masks and transfer targets.  Sizes are chosen
+so the oracle finishes in seconds; full BASELINE sizes are covered by
+size-independent properties (test_gpu_fullsize.py).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+H = lambda s: int(s, 16)  # noqa: E731
+MAX = (1 << 128) - 1
+
+
+@pytest.fixture(scope="module")
+def cx():
+    import chordx
+    if chordx.device_count() == 0:
+        pytest.fail("gpu test without a HIP device")
+    return chordx
+
+
+def edge_ring(O, n, seed):
+    """Random IDs plus the ring's edge values and adjacent pairs."""
+    base = O.ints_from_keys(O.splitmix_keys(seed, n))
+    extra = [0, 1, MAX, MAX - 1, base[0] + 1, base[1] - 1, 1 << 127, (1 << 127) - 1]
+    return O.keys_from_ints([v % (1 << 128) for v in base + extra])
+
+
+def edge_keys(O, ring, seed, q):
+    ids = O.ints_from_keys(ring)
+    vals = O.ints_from_keys(O.splitmix_keys(seed, q))
+    for v in ids[:64]:
+        vals += [v, (v + 1) % (1 << 128), (v - 1) % (1 << 128)]
+    vals += [0, 1, MAX, MAX - 1]
+    return O.keys_from_ints(vals)
+
+
+# ---------------------------------------------------------------- a13 ring build
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 1000, 4097, 70000])
+def test_ring_build(cx, O, n):
+    ids = O.splitmix_keys(1000 + n, n)
+    if n > 3:  # duplicates must be dropped (remote_peer_list.cpp:56-58)
+        ids = np.concatenate([ids, ids[: n // 3], O.keys_from_ints([0, MAX, 0])])
+    ring = cx.Ring(ids)
+    want = O.ring_build(ids)
+    assert ring.n == len(want)
+    assert (ring.ids() == want).all()
+
+
+def test_ring_build_equal_high_bits(cx, O):
+    """Keys that differ only in low bits / only in high bits (radix passes)."""
+    v = [(7 << 100) + i for i in range(300)] + [(i << 120) for i in range(200)] + [5] * 10
+    ids = O.keys_from_ints(v)
+    assert (cx.Ring(ids).ids() == O.ring_build(ids)).all()
+
+
+# ---------------------------------------------------------------- a5/a7 successor
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 1000, 4095, 4096, 70000])
+def test_successor(cx, O, n):
+    ids = edge_ring(O, n, 77 + n)
+    ring = cx.Ring(ids)
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, 5 + n, 20000)
+    got = ring.successor(keys)
+    assert (got == O.successor(want_ring, keys)).all()
+
+
+def test_successor_c2(cx, O):
+    """Config C2: 2^16-peer ring, 2^20 uniform keys (seeds of SURVEY 8d)."""
+    ids = O.splitmix_keys(0x5EED0001, 1 << 16)
+    keys = O.splitmix_keys(0x5EED0002, 1 << 20)
+    ring = cx.Ring(ids)
+    assert (ring.successor(keys) == O.successor(O.ring_build(ids), keys)).all()
+
+
+# ---------------------------------------------------------------- a6 fingers
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 5000])
+def test_fingers(cx, O, n):
+    ids = edge_ring(O, n, 300 + n)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    assert (F == O.fingers(O.ring_build(ids))).all()
+
+
+def test_fingers_c2_ring(cx, O):
+    ids = O.splitmix_keys(0x5EED0001, 1 << 16)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    assert (F == O.fingers(O.ring_build(ids))).all()
+
+
+# ---------------------------------------------------------------- a7-a9 route
+def test_route_c1_golden(cx, O, c1truth):
+    """Config C1 ground truth (8 peers, key0..key999 from every peer)."""
+    ids = O.keys_from_ints([O.uuid5_key(p) for p in c1truth["peers"]])
+    ring = cx.Ring(ids)
+    assert [format(v, "x") for v in O.ints_from_keys(ring.ids())] == c1truth["ring"]
+    ring.build_fingers()
+    kv = O.keys_from_ints([O.uuid5_key(k) for k in c1truth["keys"]])
+    src = np.repeat(np.arange(8, dtype=np.uint32), len(kv))
+    owner, hops, status = ring.route(src, np.tile(kv, (8, 1)))
+    assert owner.tolist() == c1truth["owner"]
+    assert hops.tolist() == c1truth["hops"]
+    assert (status == 0).all()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 9, 1000, 20000])
+def test_route_converged(cx, O, n):
+    ids = edge_ring(O, n, 900 + n)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, 31 + n, 30000)
+    rng = np.random.default_rng(n)
+    src = rng.integers(0, len(want_ring), len(keys)).astype(np.uint32)
+    owner, hops, status = ring.route(src, keys)
+    P = O.Peers(want_ring, F)
+    wo, wh, ws = O.route(P, src, keys)
+    assert (owner == wo).all() and (hops == wh).all() and (status == ws).all()
+    assert (owner == O.successor(want_ring, keys)).all()
+
+
+def test_route_from_predecessor(cx, O, refvec):
+    """ChordGetSucc.FromPredecessor: all fingers of the source point at itself."""
+    g = refvec["get_succ"]["from_predecessor"]
+    ids = O.keys_from_ints([H(x) for x in g["peers"]])
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
+    s = names.index(g["src"])
+    F[s, :] = s
+    ring.upload_fingers(F)
+    owner, hops, status = ring.route(np.array([s], np.uint32), O.keys_from_ints([H(g["key"])]))
+    assert owner[0] == (s - 1) % 2 and hops[0] == 1 and status[0] == 0
+
+
+def test_route_local_key_custom_min_key(cx, O, refvec):
+    g = refvec["get_succ"]["local_key"]
+    ring = cx.Ring(O.keys_from_ints([H(g["peer"])]))
+    ring.build_fingers()
+    ring.upload_peer_state(min_keys=O.keys_from_ints([H(g["min_key"])]))
+    owner, hops, status = ring.route(np.array([0], np.uint32), O.keys_from_ints([H(g["key"])]))
+    assert owner[0] == 0 and hops[0] == 0 and status[0] == 0
+
+
+def test_route_from_finger_table(cx, O, refvec):
+    g = refvec["get_succ"]["from_finger_table"]
+    ring = cx.Ring(O.keys_from_ints([H(x) for x in g["peers"]]))
+    ring.build_fingers()
+    names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
+    owner, hops, _ = ring.route(np.array([names.index(g["src"])], np.uint32),
+                                O.keys_from_ints([H(g["key"])]))
+    assert names[owner[0]] == g["expected"] and hops[0] == 1
+
+
+def test_route_literal_random_edits(cx, O):
+    """Hand-edited fingers + custom preds/min_keys: literal ForwardRequest walk,
+    including hop-cap (self-loops with no live predecessor)."""
+    rng = np.random.default_rng(42)
+    ids = O.splitmix_keys(4242, 300)
+    ring = cx.Ring(ids)
+    want_ring = O.ring_build(ids)
+    n = len(want_ring)
+    F = ring.build_fingers(copy_out=True)
+    rows = rng.integers(0, n, 60)
+    F[rows, rng.integers(0, 128, 60)] = rng.integers(0, n, 60).astype(np.uint32)
+    F[rows[:10], :] = rows[:10, None].astype(np.uint32)  # self-pointing rows
+    preds = ((np.arange(n) - 1) % n).astype(np.uint32)
+    preds[rows[:5]] = 0xFFFFFFFF  # dead predecessor -> livelock -> hop cap
+    mk = O.keys_from_ints([(v + 1) % (1 << 128) for v in O.ints_from_keys(want_ring[preds % n])])
+    ring.upload_fingers(F)
+    ring.upload_peer_state(min_keys=mk, preds=preds)
+    keys = O.splitmix_keys(4343, 40000)
+    src = rng.integers(0, n, len(keys)).astype(np.uint32)
+    src[:2000] = rows[rng.integers(0, 10, 2000)]
+    owner, hops, status = ring.route(src, keys)
+    wo, wh, ws = O.route(O.Peers(want_ring, F, min_keys=mk, preds=preds), src, keys)
+    assert (owner == wo).all() and (hops == wh).all() and (status == ws).all()
+    assert (status == 1).any()
+
+
+def test_route_bad_src_is_flagged(cx, O):
+    ring = cx.Ring(O.splitmix_keys(3, 50))
+    ring.build_fingers()
+    owner, hops, status = ring.route(np.array([0, 49, 50, 0xFFFFFFFF], np.uint32),
+                                     O.splitmix_keys(4, 4))
+    assert status.tolist()[2:] == [2, 2] and owner.tolist()[2:] == [0xFFFFFFFF] * 2
+
+
+def test_fingers_upload_rejects_bad_index(cx, O):
+    ring = cx.Ring(O.splitmix_keys(3, 50))
+    F = ring.build_fingers(copy_out=True)
+    F[3, 4] = 50
+    with pytest.raises(cx.ChordError):
+        ring.upload_fingers(F)
+
+
+# ---------------------------------------------------------------- a10/a11 DHash
+@pytest.mark.parametrize("n_ring", [1, 2, 13, 14, 15, 28, 3000])
+def test_nsucc(cx, O, n_ring):
+    ids = O.splitmix_keys(50 + n_ring, n_ring)
+    ring = cx.Ring(ids)
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, 51, 5000)
+    lists, count = ring.nsucc(keys, 14)
+    P = O.Peers(want_ring, O.fingers(want_ring))
+    wl, wc = O.nsucc(P, keys, 14)
+    assert (lists == wl).all() and (count == wc).all()
+
+
+def test_dhash_insufficient(cx, O):
+    ring = cx.Ring(O.splitmix_keys(1, 9))
+    with pytest.raises(cx.ChordError) as e:
+        ring.dhash_check(14, 10)
+    assert "Insufficient succs" in str(e.value)
+    cx.Ring(O.splitmix_keys(1, 10)).dhash_check(14, 10)
+
+
+# ---------------------------------------------------------------- a12 churn
+@pytest.mark.parametrize("n_old,nj,nl", [(1, 1, 0), (5, 0, 2), (60, 3, 4), (20000, 200, 200)])
+def test_churn_and_misplaced(cx, O, n_old, nj, nl):
+    ids = O.splitmix_keys(7000 + n_old, n_old)
+    old = cx.Ring(ids)
+    want_old = O.ring_build(ids)
+    rng = np.random.default_rng(n_old)
+    joins = O.splitmix_keys(7100 + n_old, nj)
+    if nj > 2:
+        joins[1] = want_old[0]  # duplicate of a survivor: rejected
+    leave_idx = rng.choice(len(want_old), nl, replace=False)
+    leaves = np.concatenate([want_old[leave_idx], O.splitmix_keys(9, 1)])  # + unknown ID
+    new, o2n = old.churn(joins, leaves)
+    want_new, want_o2n = O.churn(want_old, joins, leaves)
+    assert (new.ids() == want_new).all() and (o2n == want_o2n).all()
+    keys = edge_keys(O, want_new, 77, 20000)
+    for n in (2, 14):
+        lists, count, mask, target = old.misplaced(new, o2n, keys, n)
+        wl, wc, wm, wt = O.misplaced(want_old, want_new, want_o2n, keys, n)
+        assert (lists == wl).all() and (count == wc).all()
+        assert (mask == wm).all() and (target == wt).all()
+
+
+def test_global_maintenance_fixture(cx, O, refvec):
+    g = refvec["global_maintenance"]
+    ring = cx.Ring(O.keys_from_ints([H(x) for x in g["peers"]]))
+    names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
+    keys = O.keys_from_ints([H(k) for k in g["keys"]])
+    holders = np.full((len(keys), 1), names.index(g["holder"]), np.uint32)
+    lists, count, mask, target = ring.misplaced_holders(keys, holders, g["n"])
+    assert (mask == 1).all()
+    assert all(names[lists[q, target[q, 0]]] == g["expected_target"] for q in range(len(keys)))
+
+
+def test_misplaced_holders_random(cx, O):
+    ids = O.splitmix_keys(31337, 500)
+    ring = cx.Ring(ids)
+    want = O.ring_build(ids)
+    rng = np.random.default_rng(5)
+    keys = O.splitmix_keys(31338, 5000)
+    holders = rng.integers(0, 500, (5000, 6)).astype(np.uint32)
+    holders[rng.random((5000, 6)) < 0.2] = 0xFFFFFFFF
+    s = O.successor(want, keys)
+    holders[:, 0] = s  # make some holders correct
+    got = ring.misplaced_holders(keys, holders, 4)
+    exp = O.misplaced_holders(want, keys, holders, 4)
+    for a, b in zip(got, exp):
+        assert (a == b).all()
+
+
+# ---------------------------------------------------------------- a2 InBetween
+def test_in_between_gpu(cx, O, refvec):
+    def u256(v):
+        return [(v >> (64 * j)) & 0xFFFFFFFFFFFFFFFF for j in range(4)]
+
+    cases = [(H(r["v"]), H(r["lb"]), H(r["ub"]), r["incl"], r["expect"])
+             for r in refvec["in_between"]]
+    rng = np.random.default_rng(9)
+    special = [0, 1, MAX, 1 << 128, (1 << 128) + 1, (1 << 256) - 1, 1 << 127]
+    vals = special + [int.from_bytes(rng.bytes(16), "big") for _ in range(8)]
+    for v in vals:
+        for lb in vals:
+            for ub in vals:
+                cases.append((v, lb, ub, True, None))
+                cases.append((v, lb, ub, False, None))
+    for inc in (True, False):
+        sel = [c for c in cases if c[3] == inc]
+        V = np.array([u256(c[0]) for c in sel], np.uint64)
+        L = np.array([u256(c[1]) for c in sel], np.uint64)
+        U = np.array([u256(c[2]) for c in sel], np.uint64)
+        got = cx.in_between(V, L, U, inc)
+        for c, g in zip(sel, got):
+            want = O.in_between(c[0], c[1], c[2], inc)
+            assert bool(g) == want
+            if c[4] is not None:
+                assert want == c[4]
+    from chordx import ChordKey
+    assert not ChordKey("f4ee136cb4059b2883450e7e93698be").in_between(
+        H("633bd46b5c515992a5ce553d0680bec9"), H("f4ee136cb4059b2883450e7e93698bd"))
+
+
+# ---------------------------------------------------------------- device buffers
+def test_device_memkind_matches_host(cx, O):
+    import torch
+    ids = O.splitmix_keys(0x5EED0003, 1 << 14)
+    ring = cx.Ring(ids)
+    ring.build_fingers()
+    q = 1 << 16
+    keys_d = torch.empty((q, 2), dtype=torch.int64, device="cuda:0")
+    cx.fill_splitmix(keys_d, 0x5EED0004)
+    keys_h = O.splitmix_keys(0x5EED0004, q)
+    assert (keys_d.cpu().numpy().view(np.uint64) == keys_h).all()
+    src_d = (torch.arange(q, device="cuda:0", dtype=torch.int32) % ring.n)
+    od, hd, sd = ring.route(src_d, keys_d)
+    oh, hh, sh = ring.route(src_d.cpu().numpy().astype(np.uint32), keys_h)
+    torch.cuda.synchronize()
+    assert (od.cpu().numpy().view(np.uint32) == oh).all()
+    assert (hd.cpu().numpy() == hh).all()
+    ow = ring.successor(keys_d)
+    torch.cuda.synchronize()
+    assert (ow.cpu().numpy().view(np.uint32) == O.successor(O.ring_build(ids), keys_h)).all()
