@@ -82,8 +82,10 @@ int cx_ring_size(const cx_ring *ring, size_t *n);
 int cx_ring_ids(const cx_ring *ring, cx_u128 *out, int memkind);
 /* Device pointer to the ring's sorted IDs (n x 16 B, read-only). */
 int cx_ring_ids_device(const cx_ring *ring, const cx_u128 **ids);
-/* Use the caller's hipStream_t (NULL = the handle's own stream). */
+/* Enqueue the handle's work on the caller's hipStream_t (NULL = the device's
+ * null stream); cx_ring_use_own_stream restores the handle's private stream. */
 int cx_ring_set_stream(cx_ring *ring, void *hip_stream);
+int cx_ring_use_own_stream(cx_ring *ring);
 int cx_ring_sync(const cx_ring *ring);
 
 /* ---- a5/a7: exact successor --------------------------------------------

@@ -35,7 +35,7 @@ CX_Q_OK, CX_Q_HOPCAP, CX_Q_BADPEER = 0, 1, 2
 EXPORTS = (
     "cx_version", "cx_last_error", "cx_device_count",
     "cx_ring_create", "cx_ring_destroy", "cx_ring_size", "cx_ring_ids",
-    "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_sync",
+    "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_use_own_stream", "cx_ring_sync",
     "cx_successor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
     "cx_peer_state_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
@@ -74,6 +74,7 @@ def lib() -> ctypes.CDLL:
         "cx_ring_ids": ([vp, vp, i], i),
         "cx_ring_ids_device": ([vp, pp], i),
         "cx_ring_set_stream": ([vp, vp], i),
+        "cx_ring_use_own_stream": ([vp], i),
         "cx_ring_sync": ([vp], i),
         "cx_successor": ([vp, vp, sz, vp, i], i),
         "cx_fingers_build": ([vp, vp, i], i),

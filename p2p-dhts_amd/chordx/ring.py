@@ -103,7 +103,7 @@ class Ring:
             return L.CX_MEM_DEVICE
         if any(dev):
             raise TypeError("mix of device tensors and host arrays")
-        L.check(L.lib().cx_ring_set_stream(self._h, None))
+        L.check(L.lib().cx_ring_use_own_stream(self._h))
         return L.CX_MEM_HOST
 
     def _empty(self, like, shape, np_dtype, th_dtype):
@@ -174,6 +174,12 @@ class Ring:
         if not p.value:
             return None
         return _wrap_device(p.value, (self.n, L.CX_FINGERS), torch.int32, self.device, self)
+
+    def set_route_variant(self, v: int):
+        """Internal A/B switch: 0 = finger + ring gather per hop, 1 = route table."""
+        f = L.lib().cxi_set_route_variant
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.check(f(self._h, v))
 
     # ---- a7-a9 -----------------------------------------------------------
     def route(self, src, keys, out=None):
@@ -268,7 +274,7 @@ class _DevArray:
     def __init__(self, ptr, shape, typestr, owner):
         self._owner = owner
         self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr,
-                                         "data": (ptr, True), "version": 2, "strides": None}
+                                         "data": (ptr, False), "version": 2, "strides": None}
 
 
 def _wrap_device(ptr, shape, dtype, device, owner):

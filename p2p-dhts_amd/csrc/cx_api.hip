@@ -64,6 +64,10 @@ struct cx_ring {
     cell128 *d_eyt = nullptr;      // Eytzinger copy [n+1]
     uint32_t *d_fingers = nullptr; // [n][128]
     bool fingers_converged = false;
+    RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
+    cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
+    int rt_l0 = 128, rt_R = 0;
+    int route_variant = 1;         // 0: finger+ring gathers, 1: route table + wave queue
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
@@ -163,6 +167,8 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_ring);
     (void)hipFree(r->d_eyt);
     (void)hipFree(r->d_fingers);
+    (void)hipFree(r->d_rt);
+    (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
     (void)hipFree(r->d_scratch);
@@ -280,7 +286,13 @@ int cx_ring_ids_device(const cx_ring *ring, const cx_u128 **ids) {
 
 int cx_ring_set_stream(cx_ring *ring, void *hip_stream) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    ring->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ring->own_stream;
+    ring->stream = static_cast<hipStream_t>(hip_stream);
+    return CX_OK;
+}
+
+int cx_ring_use_own_stream(cx_ring *ring) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    ring->stream = ring->own_stream;
     return CX_OK;
 }
 
@@ -322,6 +334,29 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     }
     CX_HIP(cxk::fingers_build(ring->eyt(), ring->d_ring, ring->d_fingers, s));
     ring->fingers_converged = true;
+    // route table: levels [l0, 128) with l0 = 128 - R, R = ceil(log2 n) + 8
+    // rounded up to 8 (levels below it are almost always "next peer")
+    if (!ring->d_rt) {
+        int lg = 0;
+        while (((size_t)1 << lg) < ring->n) ++lg;
+        int R = ((lg + 8 + 7) / 8) * 8;
+        if (R < 16) R = 16;
+        if (R > 128) R = 128;
+        const size_t bytes = ring->n * (size_t)R * sizeof(RtEntry);
+        if (hipMalloc(&ring->d_rt, bytes) != hipSuccess) {
+            ring->d_rt = nullptr;  // not enough HBM: route falls back to variant 0
+        } else if (hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess) {
+            (void)hipFree(ring->d_rt);
+            ring->d_rt = nullptr;
+            ring->d_ring_ext = nullptr;
+        } else {
+            ring->rt_R = R;
+            ring->rt_l0 = 128 - R;
+        }
+    }
+    if (ring->d_rt)
+        CX_HIP(cxk::rt_build(ring->d_fingers, ring->d_ring, ring->n, ring->rt_l0, ring->rt_R,
+                             ring->d_rt, ring->d_ring_ext, s));
     if (fingers_out) {
         const hipMemcpyKind kind =
             memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -411,9 +446,14 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
     if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
     if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
-    CX_HIP(cxk::route(ring->d_ring, ring->n, ring->d_fingers, ring->d_min_keys, ring->d_preds,
-                      ring->literal(), dsrc, reinterpret_cast<const cell128 *>(dk), q, dow, dh,
-                      dst, s));
+    if (!ring->literal() && ring->route_variant == 1 && ring->d_rt)
+        CX_HIP(cxk::route_rt(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_rt, ring->rt_l0,
+                             ring->rt_R, ring->d_fingers, dsrc,
+                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
+    else
+        CX_HIP(cxk::route(ring->d_ring, ring->n, ring->d_fingers, ring->d_min_keys,
+                          ring->d_preds, ring->literal(), dsrc,
+                          reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(owner, dow, q * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         CX_HIP(hipMemcpyAsync(hops, dh, q, hipMemcpyDeviceToHost, s));
@@ -630,6 +670,15 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
     CX_HIP(hipSetDevice(device));
     CX_HIP(cxk::fill_splitmix(reinterpret_cast<cell128 *>(out_device), count, seed, offset,
                               static_cast<hipStream_t>(hip_stream)));
+    return CX_OK;
+}
+
+// ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
+// and parity tests.  0 = finger + ring gathers per hop, 1 = route table.
+int cxi_set_route_variant(cx_ring *ring, int variant) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    ring->route_variant = variant;
     return CX_OK;
 }
 

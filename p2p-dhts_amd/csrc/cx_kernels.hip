@@ -505,6 +505,200 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route_literal(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Route table: the finger levels [l0, 128) of every peer with the successor's
+// ID stored beside its index, as the reference's Finger{lower, upper,
+// successor_} carries the successor RemotePeer (finger_table.h:20-28).  One
+// hop = one 32-byte gather.  ring_ext[0] = ring[n-1], ring_ext[1+p] = ring[p],
+// so (predecessor, self) of peer p is the contiguous pair ring_ext[p..p+1].
+// ---------------------------------------------------------------------------
+__global__ void k_rt_build(const uint32_t *F, const cell128 *ring, uint32_t n, int l0, int R,
+                           RtEntry *rt) {
+    const size_t total = (size_t)n * R;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        const size_t p = t / (unsigned)R;
+        const int j = (int)(t - p * (unsigned)R);
+        const uint32_t f = F[p * CX_FINGERS + l0 + j];
+        const u128 id = ld128(ring + f);
+        RtEntry e;
+        e.lo = (uint64_t)id;
+        e.hi = (uint64_t)(id >> 64);
+        e.idx = f;
+        e.pad0 = e.pad1 = e.pad2 = 0;
+        rt[t] = e;
+    }
+}
+
+__global__ void k_ring_ext(const cell128 *ring, uint32_t n, cell128 *ext) {
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t <= n;
+         t += (size_t)gridDim.x * blockDim.x)
+        st128(ext + t, ld128(ring + (t == 0 ? n - 1 : t - 1)));
+}
+
+hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
+                    cell128 *ring_ext, hipStream_t s) {
+    k_rt_build<<<cx_grid(n * (size_t)R, 256), 256, 0, s>>>(F, ring, (uint32_t)n, l0, R, rt);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_ring_ext<<<cx_grid(n + 1, 256), 256, 0, s>>>(ring, (uint32_t)n, ring_ext);
+    return hipGetLastError();
+}
+
+// Converged walk over the route table.  Each wave owns a contiguous chunk of
+// queries and a scalar queue head; a lane that finishes takes the next index
+// (ballot + mbcnt), so lanes never idle behind the wave's longest walk.  Every
+// loop iteration is ONE dependent load round per lane: either the (pred, self)
+// pair of a new source peer or the route-table entry of the current hop.  The
+// (key, src) of a lane's next query are prefetched while it walks.
+constexpr int RT_BLOCK = 256;
+
+__global__ __launch_bounds__(RT_BLOCK) void k_route_rt(
+    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const RtEntry *rt, int l0, int R,
+    const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
+    uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    const int lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t base = wave * chunk;
+    if (base >= q) return;  // wave-uniform
+    const size_t end = (base + chunk < q) ? base + chunk : q;
+    size_t head = base + 64;  // wave-uniform queue head (after the first 64)
+
+    // current query
+    size_t qi = base + lane;
+    bool live = qi < end;
+    u128 key = 0, idc = 0;
+    uint32_t cur = 0, h = 0;
+    bool init = true;
+    if (live) {
+        key = ld128(keys + qi);
+        cur = src[qi];
+    }
+    // prefetched next query of this lane
+    size_t pq = 0;
+    bool plive = false;
+    u128 pkey = 0;
+    uint32_t psrc = 0;
+    {
+        const uint64_t want = __ballot(live);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+        if (live) {
+            pq = head + rank;
+            plive = pq < end;
+            if (plive) {
+                pkey = ld128(keys + pq);
+                psrc = src[pq];
+            }
+        }
+        head += (size_t)__popcll(want);
+    }
+
+    while (__ballot(live) != 0) {
+        // ---- one load round ----
+        u128 a = 0, b = 0, d = 0;
+        uint32_t nxt = 0;
+        if (live) {
+            if (init) {
+                if (cur < n) {
+                    a = ld128(ring_ext + cur);      // predecessor id
+                    b = ld128(ring_ext + cur + 1);  // own id
+                }
+            } else {
+                d = key - idc;
+                const int i = msb128(d);
+                if (i >= l0) {
+                    const RtEntry *e = rt + (size_t)cur * (unsigned)R + (i - l0);
+                    a = ld128(reinterpret_cast<const cell128 *>(e));
+                    nxt = e->idx;
+                } else {  // rare: level below the route table
+                    nxt = F[(size_t)cur * CX_FINGERS + i];
+                    a = ld128(ring + nxt);
+                }
+            }
+        }
+        // ---- process ----
+        bool fin = false;
+        uint32_t own = CX_NONE;
+        uint8_t st = CX_Q_OK;
+        if (live) {
+            if (init) {
+                if (cur >= n) {
+                    fin = true;
+                    st = CX_Q_BADPEER;
+                    h = 0;
+                } else if (n == 1 || (key - a - 1) <= (b - a - 1)) {
+                    fin = true;  // StoredLocally at the source: 0 hops
+                    own = cur;
+                    h = 0;
+                } else {
+                    idc = b;
+                    init = false;
+                    h = 0;
+                }
+            } else {
+                ++h;
+                if (d <= a - idc) {  // StoredLocally(nxt)
+                    fin = true;
+                    own = nxt;
+                } else if (h == CX_HOP_CAP) {
+                    fin = true;
+                    st = CX_Q_HOPCAP;
+                } else {
+                    cur = nxt;
+                    idc = a;
+                }
+            }
+            if (fin) {
+                owner[qi] = own;
+                hops[qi] = (uint8_t)h;
+                if (status) status[qi] = st;
+            }
+        }
+        // ---- refill: finished lanes start their prefetched query ----
+        const uint64_t m = __ballot(fin);
+        if (m) {
+            const uint64_t want = __ballot(fin && plive);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+            if (fin) {
+                qi = pq;
+                live = plive;
+                key = pkey;
+                cur = psrc;
+                init = true;
+                h = 0;
+                if (plive) {
+                    pq = head + rank;
+                    plive = pq < end;
+                    if (plive) {
+                        pkey = ld128(keys + pq);
+                        psrc = src[pq];
+                    }
+                }
+            }
+            head += (size_t)__popcll(want);
+        }
+    }
+}
+
+hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, const RtEntry *rt,
+                    int l0, int R, const uint32_t *F, const uint32_t *src, const cell128 *keys,
+                    size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    // ~16 queries per lane: waves enough to fill 256 CUs x 8 waves/SIMD x 4
+    const size_t max_waves = 256 * 32;
+    size_t waves = (q + 1023) / 1024;
+    if (waves > max_waves) waves = max_waves;
+    if (waves == 0) waves = 1;
+    const size_t chunk = (q + waves - 1) / waves;
+    waves = (q + chunk - 1) / chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
+    k_route_rt<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n, rt, l0, R, F, src, keys, q,
+                                           chunk, owner, hops, status);
+    return hipGetLastError();
+}
+
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
                  size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {

@@ -7,6 +7,14 @@
 // are old ring indices.
 #define CX_TAG_JOIN 0x80000000u
 
+// Route-table entry: successor id + index of one finger (32-B aligned so one
+// hop is a single gather inside one 64-B granule).
+struct alignas(32) RtEntry {
+    uint64_t lo, hi;
+    uint32_t idx, pad0, pad1, pad2;
+};
+static_assert(sizeof(RtEntry) == 32, "RtEntry is 32 B");
+
 namespace cxk {
 
 size_t scan_workspace_words(size_t n);
@@ -33,6 +41,11 @@ hipError_t fingers_build(const EytView &ev, const cell128 *ring, uint32_t *F, hi
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
                  size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
+                    cell128 *ring_ext, hipStream_t s);
+hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, const RtEntry *rt,
+                    int l0, int R, const uint32_t *F, const uint32_t *src, const cell128 *keys,
+                    size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t nsucc(const EytView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const EytView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
