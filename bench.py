@@ -175,16 +175,18 @@ def main():
     torch.cuda.synchronize(dev)
     succ_ms = e0.elapsed_time(e1) / 3
     owner_eq = bool((succ_out == owner).all().item())
-    # A/B: the finger+ring-gather route kernel (variant 0) on the same batch
-    ring.set_route_variant(0)
-    ring.route(src, keys, out=out)
-    e0.record(stream)
-    for _ in range(3):
+    # A/B: the other route kernels on the same batch (bit-identical results)
+    variant_ms = {}
+    for v in (0, 1, 2):
+        ring.set_route_variant(v)
         ring.route(src, keys, out=out)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    v0_ms = e0.elapsed_time(e1) / 3
-    ring.set_route_variant(1)
+        e0.record(stream)
+        for _ in range(3):
+            ring.route(src, keys, out=out)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        variant_ms[v] = e0.elapsed_time(e1) / 3
+    ring.set_route_variant(2)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -227,14 +229,14 @@ def main():
                        "parallelism": f"replicated ring, keys sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "kernel": "k_route_rt", "kernel_ms": kern_ms,
+                         "kernel": "k_route_pk", "kernel_ms": kern_ms,
                          "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             "mean_hops": sum_hops / Q,
             "bad_status": bad,
             "route_owner_equals_successor": owner_eq,
             "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
-            "route_variant0_kernel_ms": v0_ms,
+            "route_variant_kernel_ms": variant_ms,
             "setup_s": {"ring_sort": t_ring, "fingers_build": t_fing},
         }
         print(json.dumps(line), flush=True)

@@ -67,7 +67,9 @@ struct cx_ring {
     RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
-    int route_variant = 1;         // 0: finger+ring gathers, 1: route table + wave queue
+    uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variant 2)
+    int pk_ib = 1;                 // index bits of a packed finger
+    int route_variant = 2;         // 0: finger+ring gathers, 1: route table, 2: packed table
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
@@ -168,6 +170,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_eyt);
     (void)hipFree(r->d_fingers);
     (void)hipFree(r->d_rt);
+    (void)hipFree(r->d_pk);
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
@@ -357,6 +360,16 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     if (ring->d_rt)
         CX_HIP(cxk::rt_build(ring->d_fingers, ring->d_ring, ring->n, ring->rt_l0, ring->rt_R,
                              ring->d_rt, ring->d_ring_ext, s));
+    if (ring->d_rt && !ring->d_pk) {
+        int ib = 1;
+        while (((size_t)1 << ib) < ring->n) ++ib;
+        ring->pk_ib = ib;
+        if (hipMalloc(&ring->d_pk, ring->n * (size_t)ring->rt_R * 16) != hipSuccess)
+            ring->d_pk = nullptr;  // not enough HBM: variant 2 unavailable
+    }
+    if (ring->d_pk)
+        CX_HIP(cxk::pk_build(ring->d_fingers, ring->d_ring, ring->n, ring->rt_l0, ring->rt_R,
+                             ring->pk_ib, ring->d_pk, s));
     if (fingers_out) {
         const hipMemcpyKind kind =
             memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -446,7 +459,11 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
     if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
     if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
-    if (!ring->literal() && ring->route_variant == 1 && ring->d_rt)
+    if (!ring->literal() && ring->route_variant == 2 && ring->d_pk)
+        CX_HIP(cxk::route_pk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
+                             ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
+                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
+    else if (!ring->literal() && ring->route_variant == 1 && ring->d_rt)
         CX_HIP(cxk::route_rt(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_rt, ring->rt_l0,
                              ring->rt_R, ring->d_fingers, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
@@ -674,10 +691,11 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
 }
 
 // ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
-// and parity tests.  0 = finger + ring gathers per hop, 1 = route table.
+// and parity tests.  0 = finger + ring gathers per hop, 1 = route table,
+// 2 = packed route table with one-level lookahead (default).
 int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
     ring->route_variant = variant;
     return CX_OK;
 }

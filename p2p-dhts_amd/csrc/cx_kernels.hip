@@ -699,6 +699,296 @@ hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Packed route table (variant 2).  A finger is packed into 8 bytes:
+//   pk = (id >> S) << ib | idx,   ib = ceil(log2 n) index bits, S = 64 + ib,
+// i.e. the exact peer index plus the top 64 - ib bits of its ID, so the ID is
+// known to lie in [T << S, (T << S) + 2^S - 1].  Entry (p, i), 16 B:
+//   .x = pk(finger(p, i)) = pk(nxt),  .y = pk(finger(nxt, i - 1))
+// The second half makes a hop whose level drops by exactly one free (no
+// gather).  Every decision of the walk (finger level, StoredLocally) is taken
+// on these ID intervals; if an interval straddles the decision the lane
+// fetches the exact IDs (ring[cur], ring[nxt]) and decides exactly, so
+// results are bit-exact for any ring (adversarial rings just run slower).
+// ---------------------------------------------------------------------------
+__global__ void k_pk_build(const uint32_t *F, const cell128 *ring, uint32_t n, int l0, int R,
+                           int ib, uint2 *pk_unused, uint64_t *rt) {
+    const size_t total = (size_t)n * R;
+    const int S = 64 + ib;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        const size_t p = t / (unsigned)R;
+        const int i = l0 + (int)(t - p * (unsigned)R);
+        const uint32_t f = F[p * CX_FINGERS + i];
+        const uint64_t a = ((uint64_t)(ld128(ring + f) >> S) << ib) | f;
+        uint64_t b = ~0ull;
+        if (i >= 1) {
+            const uint32_t g = F[(size_t)f * CX_FINGERS + i - 1];
+            b = ((uint64_t)(ld128(ring + g) >> S) << ib) | g;
+        }
+        rt[2 * t] = a;
+        rt[2 * t + 1] = b;
+    }
+}
+
+hipError_t pk_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
+                    uint64_t *rt, hipStream_t s) {
+    k_pk_build<<<cx_grid(n * (size_t)R, 256), 256, 0, s>>>(F, ring, (uint32_t)n, l0, R, ib,
+                                                           nullptr, rt);
+    return hipGetLastError();
+}
+
+// Level of the next hop, FingerTable::Lookup's first match = msb(key - id),
+// for id in [lo, lo + w]:  -1 if the interval does not decide it.
+__device__ __forceinline__ int level_iv(u128 key, u128 lo, u128 w) {
+    const u128 a = key - lo;          // = key - id_min
+    if (a <= w) return -1;            // key inside the interval (or d could be 0)
+    const u128 b = a - w;             // = key - id_max  (> 0)
+    const int i = msb128(a);
+    return msb128(b) == i ? i : -1;
+}
+
+// StoredLocally(nxt) for the hop cur -> nxt: key in (id_cur, id_nxt].
+// 1 = stored at nxt, 0 = not, -1 = undecided by the intervals.
+__device__ __forceinline__ int term_iv(u128 key, u128 clo, u128 cw, u128 nlo, u128 nw) {
+    const u128 a = key - clo;         // dk in [a - cw, a]   (a > cw: checked by level_iv)
+    const u128 b = nlo - clo;         // dn in [b - cw, b + nw]
+    if (b < cw) return -1;            // id_nxt may precede id_cur's interval end
+    if (b + nw < b) return -1;        // wraps past 2^128
+    if (a <= b - cw) return 1;        // dk_max <= dn_min
+    if (a - cw > b + nw) return 0;    // dk_min > dn_max
+    return -1;
+}
+
+enum { M_INIT = 0, M_HOP = 1, M_FIXC = 2, M_FIXT = 3 };
+
+__global__ __launch_bounds__(RT_BLOCK) void k_route_pk(
+    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const uint4 *rt, int l0, int R,
+    int ib, const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
+    uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    const int lane = threadIdx.x & 63;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t base = wave * chunk;
+    if (base >= q) return;
+    const size_t end = (base + chunk < q) ? base + chunk : q;
+    size_t head = base + 64;
+    const int S = 64 + ib;
+    const uint64_t imask = (1ull << ib) - 1;
+    const u128 W = ((u128)1 << S) - 1;  // width of a packed ID interval
+
+    size_t qi = base + lane;
+    bool live = qi < end;
+    u128 key = 0, clo = 0, cw = 0;      // id(cur) in [clo, clo + cw]
+    uint32_t cur = 0, h = 0, pn = 0;
+    int mode = M_INIT, lvl = 0, la_lvl = -2;
+    uint64_t la = 0;
+    if (live) {
+        key = ld128(keys + qi);
+        cur = src[qi];
+    }
+    size_t pq = 0;
+    bool plive = false;
+    u128 pkey = 0;
+    uint32_t psrc = 0;
+    {
+        const uint64_t want = __ballot(live);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+        if (live) {
+            pq = head + rank;
+            plive = pq < end;
+            if (plive) {
+                pkey = ld128(keys + pq);
+                psrc = src[pq];
+            }
+        }
+        head += (size_t)__popcll(want);
+    }
+
+    while (__ballot(live) != 0) {
+        // ---------------- memory: one load round ----------------
+        u128 xa = 0, xb = 0;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        if (live) {
+            if (mode == M_INIT) {
+                if (cur < n) {
+                    xa = ld128(ring_ext + cur);
+                    xb = ld128(ring_ext + cur + 1);
+                }
+            } else if (mode == M_HOP) {
+                e = rt[(size_t)cur * (unsigned)R + (lvl - l0)];
+            } else if (mode == M_FIXC) {
+                xa = ld128(ring + cur);
+            } else {
+                xa = ld128(ring + cur);
+                xb = ld128(ring + pn);
+            }
+        }
+        // ---------------- compute ----------------
+        bool fin = false, plan = false;
+        uint32_t own = CX_NONE;
+        uint8_t st = CX_Q_OK;
+        if (live) {
+            if (mode == M_INIT) {
+                h = 0;
+                la_lvl = -2;
+                if (cur >= n) {
+                    fin = true;
+                    st = CX_Q_BADPEER;
+                } else if (n == 1 || (key - xa - 1) <= (xb - xa - 1)) {
+                    fin = true;
+                    own = cur;
+                } else {
+                    clo = xb;
+                    cw = 0;
+                    plan = true;
+                }
+            } else if (mode == M_FIXC) {
+                clo = xa;
+                cw = 0;
+                plan = true;
+            } else if (mode == M_FIXT) {
+                // exact StoredLocally(pn) for the pending hop cur -> pn
+                if (key - xa <= xb - xa) {
+                    fin = true;
+                    own = pn;
+                } else if (h == CX_HOP_CAP) {
+                    fin = true;
+                    st = CX_Q_HOPCAP;
+                } else {
+                    cur = pn;
+                    clo = xb;
+                    cw = 0;
+                    plan = true;
+                }
+            } else {  // M_HOP: entry (cur, lvl) arrived
+                const uint64_t m0 = ((uint64_t)e.y << 32) | e.x;
+                la = ((uint64_t)e.w << 32) | e.z;
+                la_lvl = lvl - 1;
+                const uint32_t nxt = (uint32_t)(m0 & imask);
+                const u128 nlo = (u128)(m0 >> ib) << S;
+                ++h;
+                const int t = term_iv(key, clo, cw, nlo, W);
+                if (t == 1) {
+                    fin = true;
+                    own = nxt;
+                } else if (t < 0) {
+                    mode = M_FIXT;
+                    pn = nxt;
+                } else if (h == CX_HOP_CAP) {
+                    fin = true;
+                    st = CX_Q_HOPCAP;
+                } else {
+                    cur = nxt;
+                    clo = nlo;
+                    cw = W;
+                    plan = true;
+                }
+            }
+            // ---------------- plan the next load (free hops inline) ----------------
+            while (plan) {
+                plan = false;
+                const int i = level_iv(key, clo, cw);
+                if (i < 0) {
+                    mode = M_FIXC;  // id(cur) needed exactly
+                } else if (i == la_lvl) {
+                    // free hop: finger(cur, i) came with the previous entry
+                    la_lvl = -2;
+                    const uint32_t nxt = (uint32_t)(la & imask);
+                    const u128 nlo = (u128)(la >> ib) << S;
+                    ++h;
+                    const int t = term_iv(key, clo, cw, nlo, W);
+                    if (t == 1) {
+                        fin = true;
+                        own = nxt;
+                    } else if (t < 0) {
+                        mode = M_FIXT;
+                        pn = nxt;
+                    } else if (h == CX_HOP_CAP) {
+                        fin = true;
+                        st = CX_Q_HOPCAP;
+                    } else {
+                        cur = nxt;
+                        clo = nlo;
+                        cw = W;
+                        plan = true;
+                    }
+                } else if (i >= l0) {
+                    mode = M_HOP;
+                    lvl = i;
+                    la_lvl = -2;
+                } else {
+                    // rare: level below the table -> exact finger + exact ids
+                    la_lvl = -2;
+                    const uint32_t nxt = F[(size_t)cur * CX_FINGERS + i];
+                    const u128 idn = ld128(ring + nxt);
+                    const u128 idc = cw ? ld128(ring + cur) : clo;
+                    ++h;
+                    if (key - idc <= idn - idc) {
+                        fin = true;
+                        own = nxt;
+                    } else if (h == CX_HOP_CAP) {
+                        fin = true;
+                        st = CX_Q_HOPCAP;
+                    } else {
+                        cur = nxt;
+                        clo = idn;
+                        cw = 0;
+                        plan = true;
+                    }
+                }
+            }
+            if (fin) {
+                owner[qi] = own;
+                hops[qi] = (uint8_t)h;
+                if (status) status[qi] = st;
+            }
+        }
+        // ---------------- refill ----------------
+        const uint64_t m = __ballot(fin);
+        if (m) {
+            const uint64_t want = __ballot(fin && plive);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+            if (fin) {
+                qi = pq;
+                live = plive;
+                key = pkey;
+                cur = psrc;
+                mode = M_INIT;
+                h = 0;
+                if (plive) {
+                    pq = head + rank;
+                    plive = pq < end;
+                    if (plive) {
+                        pkey = ld128(keys + pq);
+                        psrc = src[pq];
+                    }
+                }
+            }
+            head += (size_t)__popcll(want);
+        }
+    }
+}
+
+hipError_t route_pk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
+                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
+                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                    uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const size_t max_waves = 256 * 32;
+    size_t waves = (q + 1023) / 1024;
+    if (waves > max_waves) waves = max_waves;
+    if (waves == 0) waves = 1;
+    const size_t chunk = (q + waves - 1) / waves;
+    waves = (q + chunk - 1) / chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
+    k_route_pk<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n,
+                                           reinterpret_cast<const uint4 *>(rt), l0, R, ib, F, src,
+                                           keys, q, chunk, owner, hops, status);
+    return hipGetLastError();
+}
+
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
                  size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {

@@ -46,6 +46,12 @@ hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, in
 hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, const RtEntry *rt,
                     int l0, int R, const uint32_t *F, const uint32_t *src, const cell128 *keys,
                     size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t pk_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
+                    uint64_t *rt, hipStream_t s);
+hipError_t route_pk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
+                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
+                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                    uint8_t *status, hipStream_t s);
 hipError_t nsucc(const EytView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const EytView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,

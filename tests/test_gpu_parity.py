@@ -95,7 +95,7 @@ def test_fingers_c2_ring(cx, O):
 
 
 # ---------------------------------------------------------------- a7-a9 route
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_route_c1_golden(cx, O, c1truth, variant):
     """Config C1 ground truth (8 peers, key0..key999 from every peer)."""
     ids = O.keys_from_ints([O.uuid5_key(p) for p in c1truth["peers"]])
@@ -111,7 +111,7 @@ def test_route_c1_golden(cx, O, c1truth, variant):
     assert (status == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("n", [1, 2, 3, 9, 1000, 20000])
 def test_route_converged(cx, O, n, variant):
     ids = edge_ring(O, n, 900 + n)
@@ -162,6 +162,41 @@ def test_route_from_finger_table(cx, O, refvec):
     assert names[owner[0]] == g["expected"] and hops[0] == 1
 
 
+def clustered_ring(O, n, seed, spread_bits):
+    """IDs packed within 2^spread_bits of a few centres: every packed-ID
+    interval straddles decisions, forcing the exact-ID fallbacks of variant 2."""
+    rng = np.random.default_rng(seed)
+    centres = [int.from_bytes(rng.bytes(16), "big") for _ in range(4)] + [MAX - 5, 3]
+    vals = []
+    for j in range(n):
+        c = centres[j % len(centres)]
+        off = int.from_bytes(rng.bytes(16), "big") >> (128 - spread_bits)
+        vals.append((c + off) % (1 << 128))
+    return O.keys_from_ints(vals)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("spread", [8, 40, 90, 100])
+def test_route_clustered_rings(cx, O, variant, spread):
+    ids = clustered_ring(O, 3000, spread, spread)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    ring.set_route_variant(variant)
+    want_ring = O.ring_build(ids)
+    ints = O.ints_from_keys(want_ring)
+    rng = np.random.default_rng(spread)
+    # keys right next to peer IDs + random keys + keys inside the clusters
+    kv = [(ints[j] + int(rng.integers(-3, 4))) % (1 << 128) for j in rng.integers(0, len(ints), 6000)]
+    kv += O.ints_from_keys(O.splitmix_keys(spread, 6000))
+    kv += [(ints[j] + (int.from_bytes(rng.bytes(16), "big") >> (128 - spread))) % (1 << 128)
+           for j in rng.integers(0, len(ints), 6000)]
+    keys = O.keys_from_ints(kv)
+    src = rng.integers(0, len(ints), len(keys)).astype(np.uint32)
+    owner, hops, status = ring.route(src, keys)
+    wo, wh, ws = O.route(O.Peers(want_ring, F), src, keys)
+    assert (owner == wo).all() and (hops == wh).all() and (status == ws).all()
+
+
 def test_route_literal_random_edits(cx, O):
     """Hand-edited fingers + custom preds/min_keys: literal ForwardRequest walk,
     including hop-cap (self-loops with no live predecessor)."""
@@ -188,7 +223,7 @@ def test_route_literal_random_edits(cx, O):
     assert (status == 1).any()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_route_bad_src_is_flagged(cx, O, variant):
     ring = cx.Ring(O.splitmix_keys(3, 50))
     ring.build_fingers()
