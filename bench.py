@@ -31,6 +31,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import chordx  # noqa: E402
+from chordx import dist  # noqa: E402
 
 SEED_RING = 0x5EED0005
 SEED_KEYS = 0x5EED0006
@@ -55,32 +56,6 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_route.json"))
     return ap.parse_args()
-
-
-def dist_init(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(0)
-    return world, rank, local
-
-
-def barrier(world):
-    if world > 1:
-        torch.distributed.barrier()
-
-
-def max_over_ranks(x: float, world: int, dev) -> float:
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    return float(t.item())
 
 
 def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
@@ -110,8 +85,10 @@ def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
 
 def main():
     args = parse()
-    world, rank, local = dist_init(args)
+    world, rank, local = dist.env_rank()
+    torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+    dist.init("nccl", dev)
     N = 1 << args.peers_log2
     Q = 1 << args.keys_log2
 
@@ -128,8 +105,9 @@ def main():
     ring.sync()
     t_fing = time.perf_counter() - t0
     keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
-    chordx.fill_splitmix(keys, SEED_KEYS, offset=rank * Q)
-    gq = torch.arange(rank * Q, (rank + 1) * Q, device=dev, dtype=torch.int64)
+    q0, q1 = dist.shard(rank, Q)
+    chordx.fill_splitmix(keys, SEED_KEYS, offset=q0)
+    gq = torch.arange(q0, q1, device=dev, dtype=torch.int64)
     src = (gq % ring.n).to(torch.int32)
     del gq
     owner = torch.empty(Q, dtype=torch.int32, device=dev)
@@ -145,7 +123,7 @@ def main():
     # ---- timed: exactly K steps, barrier + sync on both sides ----
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world)
+    dist.barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -153,13 +131,13 @@ def main():
         ring.route(src, keys, out=out)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    barrier(world)
+    dist.barrier(world)
     dt = time.perf_counter() - t0
-    dt_max = max_over_ranks(dt, world, dev)
+    dt_max = dist.max_over_ranks(dt, world, dev)
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # one cx_route launch per step
 
     # ---- results ----
-    bad = int((status != 0).sum().item())
+    bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
     sum_hops = int(hops.to(torch.int64).sum().item())
     algo_bytes = Q * (BYTES_STREAM + BYTES_SRC) + BYTES_HOP * sum_hops
     achieved = algo_bytes / (kern_ms * 1e-3)

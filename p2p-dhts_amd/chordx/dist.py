@@ -1,0 +1,55 @@
+"""Multi-GPU plumbing for the replicated-ring, key-sharded lookup path.
+
+The lookup path shards by query: every rank holds a replica of the ring (and
+its finger/route tables) and routes its own contiguous slice of the global key
+stream.  No collective touches the data path; the only cross-rank traffic is
+the start/stop barrier and the max-over-ranks timing reduction.  With the
+"nccl" backend torch.distributed runs RCCL over xGMI; tests use "gloo" on CPU.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as tdist
+
+
+def env_rank():
+    """(world, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str, device=None):
+    world, rank, local = env_rank()
+    if world > 1 and not tdist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
+        tdist.init_process_group(backend, **kw)
+    return world, rank, local
+
+
+def shard(rank: int, per_rank: int):
+    """Global key-stream range [begin, end) routed by `rank` (weak scaling)."""
+    return rank * per_rank, (rank + 1) * per_rank
+
+
+def barrier(world: int):
+    if world > 1:
+        tdist.barrier()
+
+
+def max_over_ranks(x: float, world: int, device=None) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: int, world: int, device=None) -> int:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.int64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+    return int(t.item())

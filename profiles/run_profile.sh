@@ -10,9 +10,9 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu > "$OUT/bench_trace.log" 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex "k_route|k_successor" \
+timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex "k_route|k_successor|k_fingers|k_nsucc" \
   -d "$OUT/pmc_fetch" -o run --output-format csv \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu > "$OUT/bench_fetch.log" 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --kernel-include-regex "k_route|k_successor" \
+timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --kernel-include-regex "k_route|k_successor|k_fingers|k_nsucc" \
   -d "$OUT/pmc_write" -o run --output-format csv \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu > "$OUT/bench_write.log" 2>&1

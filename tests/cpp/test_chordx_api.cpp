@@ -1,0 +1,142 @@
+// test_chordx_api.cpp -- the reference's gtest cases for the lookup path,
+// re-expressed against include/chordx.hpp (runs on the GPU; driven by
+// tests/test_cpp_api.py).  Fixture values come from tests/golden/
+// reference_vectors.json (test/test_json/** and test/key_test.cc data).
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/chordx.hpp"
+
+static int failures = 0;
+#define EXPECT_TRUE(c) do { if (!(c)) { ++failures; std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); } } while (0)
+#define EXPECT_FALSE(c) EXPECT_TRUE(!(c))
+#define EXPECT_EQ(a, b) EXPECT_TRUE((a) == (b))
+#define TEST(suite, name) static void suite##_##name()
+#define RUN(suite, name) do { suite##_##name(); std::printf("[ RUN ] %s.%s\n", #suite, #name); } while (0)
+
+using chordx::Key;
+using chordx::Ring;
+
+TEST(KeyInBetweenTest, ExclusiveNoModulo) {
+    EXPECT_TRUE(Key(0, 75).InBetween(Key(0, 0), Key(0, 99), false));
+    EXPECT_FALSE(Key(0, 99).InBetween(Key(0, 0), Key(0, 99), false));
+}
+TEST(KeyInBetweenTest, ExclusiveWithModulo) {
+    EXPECT_TRUE(Key(0, 1).InBetween(Key(0, 75), Key(0, 25), false));
+    EXPECT_FALSE(Key(0, 25).InBetween(Key(0, 75), Key(0, 25), false));
+}
+TEST(KeyInBetweenTest, InclusiveNoModulo) {
+    EXPECT_TRUE(Key(0, 75).InBetween(Key(0, 0), Key(0, 99), true));
+    EXPECT_TRUE(Key(0, 99).InBetween(Key(0, 0), Key(0, 99), true));
+}
+TEST(KeyInBetweenTest, InclusiveWithModulo) {
+    EXPECT_TRUE(Key(0, 1).InBetween(Key(0, 75), Key(0, 25), true));
+    EXPECT_TRUE(Key(0, 25).InBetween(Key(0, 75), Key(0, 25), true));
+}
+TEST(KeyInBetweenTest, DifferingLengths) {
+    Key key = Key::FromHex("f4ee136cb4059b2883450e7e93698be"),
+        lb = Key::FromHex("633bd46b5c515992a5ce553d0680bec9"),
+        ub = Key::FromHex("f4ee136cb4059b2883450e7e93698bd");
+    EXPECT_FALSE(key.InBetween(lb, ub, true));
+    EXPECT_EQ(key.Str(), std::string("f4ee136cb4059b2883450e7e93698be"));
+}
+
+TEST(ChordIntegration, Join) {
+    const char *peers[] = {
+        "36a22c462b875f71b5bad53d1909761d",
+        "633bd46b5c515992a5ce553d0680bec8",
+        "94227b6ddb5a5ee68a4b8c7627640f5d",
+        "ad8bf45ee3435094b624b513fdb21c1d",
+        "b9c49b7b7a18545e924cf36f8b9d3afd",
+        "e2a708de118a51bf948e9320eeac848c"};
+    struct { const char *key, *owner; } kv[] = {
+        {"ed7e9a11fb0b56d58fe3aab83e01dff2", "36a22c462b875f71b5bad53d1909761d"},
+        {"f02f9a33a1325add82c9f2935627fde8", "36a22c462b875f71b5bad53d1909761d"},
+        {"ad40ad8bebe5093bd9ea7a252b372b0", "36a22c462b875f71b5bad53d1909761d"},
+        {"21c6b801af4458738a829ee4726f14c0", "36a22c462b875f71b5bad53d1909761d"},
+        {"4d1f65d6a4af5419a51f6406aa23a2bf", "633bd46b5c515992a5ce553d0680bec8"},
+        {"8f218246f4e35dc7b60419ff9fcbce73", "94227b6ddb5a5ee68a4b8c7627640f5d"},
+        {"a81fd109d24757e39fcb2fb9ab345672", "ad8bf45ee3435094b624b513fdb21c1d"},
+        {"a8f274ce76875f48b20ff0fa1d9e3941", "ad8bf45ee3435094b624b513fdb21c1d"},
+        {"da9c4c9382605ae289c62a51f14a7949", "e2a708de118a51bf948e9320eeac848c"},
+        {"db8d652ed2e7541ea8034f2603232d64", "e2a708de118a51bf948e9320eeac848c"}};
+    std::vector<Key> ids;
+    for (const char *p : peers) ids.push_back(Key::FromHex(p));
+    Ring ring(ids);
+    ring.PopulateFingerTable();
+    std::vector<Key> all = ring.Ids();
+    const uint32_t src = ring.IndexOf(ids[0]);  // keys are created from peers[0]
+    for (const auto &e : kv) {
+        chordx::Lookup l = ring.GetSuccessor(src, Key::FromHex(e.key));
+        EXPECT_EQ(all[l.owner].Str(), std::string(e.owner));
+        EXPECT_EQ(all[ring.Owner(Key::FromHex(e.key))].Str(), std::string(e.owner));
+    }
+}
+
+TEST(ChordGetSucc, FromFingerTable) {
+    Ring ring({Key::FromHex("62a0959bff135ad296fbdc29252d927a"), Key::FromHex("5c22f4050c375657b05b35732eef0130")});
+    ring.PopulateFingerTable();
+    chordx::Lookup l = ring.GetSuccessor(ring.IndexOf(Key::FromHex("62a0959bff135ad296fbdc29252d927a")),
+                                         Key::FromHex("62a0959bff135ad296fbdc29252d927b"));
+    EXPECT_EQ(ring.Ids()[l.owner].Str(), std::string("5c22f4050c375657b05b35732eef0130"));
+    EXPECT_EQ(l.hops, 1);
+}
+
+TEST(ChordGetSucc, FromPredecessor) {
+    Ring ring({Key::FromHex("61b23792c54457c5ac5b7a95b35722db"), Key::FromHex("f56febc96cfa5a6f8469b933a76dd0e0")});
+    std::vector<uint32_t> F = ring.FingerTable();
+    const uint32_t s = ring.IndexOf(Key::FromHex("61b23792c54457c5ac5b7a95b35722db"));
+    for (unsigned i = 0; i < CX_FINGERS; ++i) F[s * CX_FINGERS + i] = s;  // AdjustFingers(self)
+    ring.EditFingers(F);
+    chordx::Lookup l = ring.GetSuccessor(s, Key::FromHex("61b23792c54457c5ac5b7a95b35722dc"));
+    EXPECT_EQ(l.owner, 1 - s);  // the predecessor
+    EXPECT_EQ(l.hops, 1);
+}
+
+TEST(ChordGetSucc, Failing) {
+    // every finger points at the peer itself and it has no live predecessor:
+    // the reference livelocks / throws; chordx reports "Lookup failed"
+    Ring ring({Key::FromHex("62a0959bff135ad296fbdc29252d927a"), Key::FromHex("5c22f4050c375657b05b35732eef0130")});
+    std::vector<uint32_t> F = ring.FingerTable();
+    for (unsigned i = 0; i < CX_FINGERS; ++i) F[i] = 0;
+    ring.EditFingers(F);
+    std::vector<uint32_t> preds = {CX_NONE, 0};
+    ring.SetPeerState(nullptr, &preds);
+    bool threw = false;
+    try {
+        ring.GetSuccessor(0, Key(ring.Ids()[1].value()));
+    } catch (const chordx::Error &e) {
+        threw = std::string(e.what()) == "Lookup failed";
+    }
+    EXPECT_TRUE(threw);
+}
+
+TEST(DHashPeer, InsufficientSuccs) {
+    std::vector<Key> ids;
+    for (int i = 0; i < 9; ++i) ids.push_back(Key(0x1000ull * i, 7));
+    Ring ring(ids);
+    bool threw = false;
+    try {
+        ring.CheckReplicas(14, 10);
+    } catch (const chordx::Error &e) {
+        threw = std::string(e.what()).find("Insufficient succs") == 0;
+    }
+    EXPECT_TRUE(threw);
+    EXPECT_EQ(ring.GetNSuccessors(Key(0, 5), 14).size(), 9u);
+}
+
+int main() {
+    RUN(KeyInBetweenTest, ExclusiveNoModulo);
+    RUN(KeyInBetweenTest, ExclusiveWithModulo);
+    RUN(KeyInBetweenTest, InclusiveNoModulo);
+    RUN(KeyInBetweenTest, InclusiveWithModulo);
+    RUN(KeyInBetweenTest, DifferingLengths);
+    RUN(ChordIntegration, Join);
+    RUN(ChordGetSucc, FromFingerTable);
+    RUN(ChordGetSucc, FromPredecessor);
+    RUN(ChordGetSucc, Failing);
+    RUN(DHashPeer, InsufficientSuccs);
+    std::printf(failures ? "FAILED (%d)\n" : "PASSED\n", failures);
+    return failures ? 1 : 0;
+}
