@@ -181,7 +181,7 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("peers") == N and tj.get("keys") == Q:
+        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == "k_route_pk":
             traffic = tj.get("hbm_bytes_per_launch")
 
     if rank == 0:
