@@ -69,7 +69,7 @@ struct cx_ring {
     int rt_l0 = 128, rt_R = 0;
     uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variant 2)
     int pk_ib = 1;                 // index bits of a packed finger
-    int route_variant = 2;         // 0: finger+ring gathers, 1: route table, 2: packed table
+    int route_variant = 3;         // 0: finger+ring gathers, 1: route table, 2: packed table, 3: 2 + staging
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
@@ -459,7 +459,11 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
     if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
     if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
-    if (!ring->literal() && ring->route_variant == 2 && ring->d_pk)
+    if (!ring->literal() && ring->route_variant == 3 && ring->d_pk)
+        CX_HIP(cxk::route_pk3(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
+                              ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
+                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
+    else if (!ring->literal() && ring->route_variant == 2 && ring->d_pk)
         CX_HIP(cxk::route_pk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
                              ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
@@ -692,10 +696,11 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
 
 // ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
 // and parity tests.  0 = finger + ring gathers per hop, 1 = route table,
-// 2 = packed route table with one-level lookahead (default).
+// 2 = packed route table with one-level lookahead, 3 = 2 + staged results and
+// prefetched source pairs.
 int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
+    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0..3");
     ring->route_variant = variant;
     return CX_OK;
 }

@@ -989,6 +989,288 @@ hipError_t route_pk(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Variant 3: variant 2's packed walk plus
+//  * result staging: a finished query's (owner, hops, status) goes to a
+//    per-wave LDS window; 64 consecutive results are flushed as coalesced
+//    stores (one 256-B owner store, two 64-B byte stores) instead of three
+//    scattered stores per query.  The wave's queue never hands out an index
+//    beyond flushed + RES_WIN, so every in-flight query has a window slot.
+//  * a two-slot pipeline per lane: slot B prefetches the next query's key,
+//    src and (pred, self) pair while slot A walks, so a new query starts
+//    walking in the iteration its predecessor finishes (no init round).
+// ---------------------------------------------------------------------------
+constexpr int RES_WIN = 512;
+enum { A_NONE = 0, A_HOP = 1, A_FIXC = 2, A_FIXT = 3 };
+enum { B_EMPTY = 0, B_KS = 1, B_PAIR = 2 };
+
+struct PkCtx {
+    const cell128 *ring;
+    const uint32_t *F;
+    uint32_t n;
+    int l0, ib, S;
+    uint64_t imask;
+    u128 W;
+};
+
+// Plan the next step from cur (free hops and below-table hops run inline).
+// Returns: 0 = needs a load (mode set), 1 = finished (own/st set).
+__device__ __forceinline__ int pk_plan(const PkCtx &c, u128 key, u128 &clo, bool &cex,
+                                       uint32_t &cur, uint32_t &h, uint32_t &pn, int &mode,
+                                       int &lvl, int &la_lvl, uint64_t la, uint32_t &own,
+                                       uint8_t &st) {
+    for (;;) {
+        const u128 cw = cex ? (u128)0 : c.W;
+        const int i = level_iv(key, clo, cw);
+        if (i < 0) {
+            mode = A_FIXC;
+            return 0;
+        }
+        if (i == la_lvl) {
+            la_lvl = -2;
+            const uint32_t nxt = (uint32_t)(la & c.imask);
+            const u128 nlo = (u128)(la >> c.ib) << c.S;
+            ++h;
+            const int t = term_iv(key, clo, cw, nlo, c.W);
+            if (t == 1) {
+                own = nxt;
+                return 1;
+            }
+            if (t < 0) {
+                mode = A_FIXT;
+                pn = nxt;
+                return 0;
+            }
+            if (h == CX_HOP_CAP) {
+                own = CX_NONE;
+                st = CX_Q_HOPCAP;
+                return 1;
+            }
+            cur = nxt;
+            clo = nlo;
+            cex = false;
+            continue;
+        }
+        if (i >= c.l0) {
+            mode = A_HOP;
+            lvl = i;
+            la_lvl = -2;
+            return 0;
+        }
+        // rare: below the table -> exact finger + exact ids
+        la_lvl = -2;
+        const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
+        const u128 idn = ld128(c.ring + nxt);
+        const u128 idc = cex ? clo : ld128(c.ring + cur);
+        ++h;
+        if (key - idc <= idn - idc) {
+            own = nxt;
+            return 1;
+        }
+        if (h == CX_HOP_CAP) {
+            own = CX_NONE;
+            st = CX_Q_HOPCAP;
+            return 1;
+        }
+        cur = nxt;
+        clo = idn;
+        cex = true;
+    }
+}
+
+__device__ __forceinline__ uint64_t pack_res(uint32_t own, uint32_t h, uint8_t st) {
+    return (1ull << 63) | ((uint64_t)st << 40) | ((uint64_t)(h & 0xFF) << 32) | own;
+}
+
+__global__ __launch_bounds__(RT_BLOCK) void k_route_pk3(
+    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const uint4 *rt, int l0, int R,
+    int ib, const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
+    uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    __shared__ uint64_t res_all[RT_BLOCK / 64][RES_WIN];
+    const int lane = threadIdx.x & 63;
+    uint64_t *res = res_all[threadIdx.x >> 6];
+    for (int j = lane; j < RES_WIN; j += 64) res[j] = 0;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t base = wave * chunk;
+    if (base >= q) return;  // wave-uniform
+    const size_t end = (base + chunk < q) ? base + chunk : q;
+    PkCtx c;
+    c.ring = ring;
+    c.F = F;
+    c.n = n;
+    c.l0 = l0;
+    c.ib = ib;
+    c.S = 64 + ib;
+    c.imask = (1ull << ib) - 1;
+    c.W = ((u128)1 << c.S) - 1;
+    size_t head = base, flushed = base;
+
+    // slot A (walking query)
+    int mode = A_NONE, lvl = 0, la_lvl = -2;
+    size_t qi = 0;
+    u128 key = 0, clo = 0;
+    bool cex = true;
+    uint32_t cur = 0, h = 0, pn = 0;
+    uint64_t la = 0;
+    // slot B (prefetched query)
+    int bst = B_EMPTY;
+    size_t pq = 0;
+    u128 pkey = 0, pa = 0, pb = 0;
+    uint32_t psrc = 0;
+
+    for (;;) {
+        // ---- refill slot B from the wave's queue (window-limited) ----
+        {
+            const size_t lim = (end < flushed + RES_WIN) ? end : flushed + RES_WIN;
+            const size_t avail = lim > head ? lim - head : 0;
+            const uint64_t want = __ballot(bst == B_EMPTY);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+            if (bst == B_EMPTY && rank < avail) {
+                pq = head + rank;
+                pkey = ld128(keys + pq);
+                psrc = src[pq];
+                bst = B_KS;
+            }
+            const size_t took = (size_t)__popcll(want);
+            head += took < avail ? took : avail;
+        }
+        // exit when nothing is in flight and the queue is drained (while work
+        // remains, an all-idle wave always has window room: every result below
+        // head is complete, so the previous flush advanced `flushed`)
+        if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end) break;
+
+        // ---- memory: one round (slot A's load + slot B's pair) ----
+        u128 xa = 0, xb = 0;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        if (mode == A_HOP) {
+            e = rt[(size_t)cur * (unsigned)R + (lvl - l0)];
+        } else if (mode == A_FIXC) {
+            xa = ld128(ring + cur);
+        } else if (mode == A_FIXT) {
+            xa = ld128(ring + cur);
+            xb = ld128(ring + pn);
+        }
+        if (bst == B_KS) {
+            if (psrc < n) {
+                pa = ld128(ring_ext + psrc);
+                pb = ld128(ring_ext + psrc + 1);
+            }
+            bst = B_PAIR;
+        }
+
+        // ---- compute slot A ----
+        bool fin = false, plan = false;
+        uint32_t own = CX_NONE;
+        uint8_t st = CX_Q_OK;
+        if (mode == A_HOP) {
+            const uint64_t m0 = ((uint64_t)e.y << 32) | e.x;
+            la = ((uint64_t)e.w << 32) | e.z;
+            la_lvl = lvl - 1;
+            const uint32_t nxt = (uint32_t)(m0 & c.imask);
+            const u128 nlo = (u128)(m0 >> ib) << c.S;
+            ++h;
+            const int t = term_iv(key, clo, cex ? (u128)0 : c.W, nlo, c.W);
+            if (t == 1) {
+                fin = true;
+                own = nxt;
+            } else if (t < 0) {
+                mode = A_FIXT;
+                pn = nxt;
+            } else if (h == CX_HOP_CAP) {
+                fin = true;
+                st = CX_Q_HOPCAP;
+            } else {
+                cur = nxt;
+                clo = nlo;
+                cex = false;
+                plan = true;
+            }
+        } else if (mode == A_FIXC) {
+            clo = xa;
+            cex = true;
+            plan = true;
+        } else if (mode == A_FIXT) {
+            if (key - xa <= xb - xa) {
+                fin = true;
+                own = pn;
+            } else if (h == CX_HOP_CAP) {
+                fin = true;
+                st = CX_Q_HOPCAP;
+            } else {
+                cur = pn;
+                clo = xb;
+                cex = true;
+                plan = true;
+            }
+        }
+        if (plan) fin = pk_plan(c, key, clo, cex, cur, h, pn, mode, lvl, la_lvl, la, own, st) == 1;
+        if (fin) {
+            res[qi & (RES_WIN - 1)] = pack_res(own, h, st);
+            mode = A_NONE;
+        }
+        // ---- promote slot B into an idle slot A ----
+        if (mode == A_NONE && bst == B_PAIR) {
+            bst = B_EMPTY;
+            qi = pq;
+            key = pkey;
+            cur = psrc;
+            h = 0;
+            la_lvl = -2;
+            own = CX_NONE;
+            st = CX_Q_OK;
+            bool done = true;
+            if (cur >= n) {
+                st = CX_Q_BADPEER;
+            } else if (n == 1 || (key - pa - 1) <= (pb - pa - 1)) {
+                own = cur;  // StoredLocally at the source: 0 hops
+            } else {
+                clo = pb;
+                cex = true;
+                done = pk_plan(c, key, clo, cex, cur, h, pn, mode, lvl, la_lvl, la, own, st) == 1;
+            }
+            if (done) {
+                res[qi & (RES_WIN - 1)] = pack_res(own, h, st);
+                mode = A_NONE;
+            }
+        }
+
+        // ---- flush complete 64-result segments (coalesced) ----
+        for (int it = 0; it < 2; ++it) {
+            if (flushed >= end) break;
+            const size_t idx = flushed + lane;
+            const bool inr = idx < end;
+            const uint64_t v = inr ? res[idx & (RES_WIN - 1)] : 0ull;
+            if (__ballot(!inr || (v >> 63)) != ~0ull) break;
+            if (inr) {
+                owner[idx] = (uint32_t)v;
+                hops[idx] = (uint8_t)(v >> 32);
+                if (status) status[idx] = (uint8_t)(v >> 40);
+                res[idx & (RES_WIN - 1)] = 0;
+            }
+            flushed += 64;
+        }
+    }
+}
+
+hipError_t route_pk3(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
+                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
+                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                     uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const size_t max_waves = 256 * 32;
+    size_t waves = (q + 1023) / 1024;
+    if (waves > max_waves) waves = max_waves;
+    if (waves == 0) waves = 1;
+    const size_t chunk = (q + waves - 1) / waves;
+    waves = (q + chunk - 1) / chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
+    k_route_pk3<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n,
+                                            reinterpret_cast<const uint4 *>(rt), l0, R, ib, F,
+                                            src, keys, q, chunk, owner, hops, status);
+    return hipGetLastError();
+}
+
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
                  size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
