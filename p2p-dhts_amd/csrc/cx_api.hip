@@ -74,11 +74,23 @@ struct cx_ring {
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
 
+    uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
+    int dir_k = 1;
+    int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory
+
     EytView eyt() const {
         EytView v;
         v.E = d_eyt;
         v.n = (uint32_t)n;
         v.h = 63 - __builtin_clzll((unsigned long long)n);
+        return v;
+    }
+    SearchView sv() const {
+        SearchView v;
+        v.ev = eyt();
+        v.dir = (search_variant == 1) ? d_dir : nullptr;
+        v.k = dir_k;
+        v.ring = d_ring;
         return v;
     }
     bool literal() const { return !fingers_converged || d_min_keys || d_preds; }
@@ -168,6 +180,7 @@ void free_ring(cx_ring *r) {
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     (void)hipFree(r->d_ring);
     (void)hipFree(r->d_eyt);
+    (void)hipFree(r->d_dir);
     (void)hipFree(r->d_fingers);
     (void)hipFree(r->d_rt);
     (void)hipFree(r->d_pk);
@@ -177,6 +190,28 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_scratch);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
     delete r;
+}
+
+// Eytzinger copy + bucket directory of r->d_ring (r->n set).
+int build_search(cx_ring *r, hipStream_t s) {
+    const size_t m = r->n;
+    DBuf E;
+    CX_HIP(E.alloc((m + 1) * sizeof(cell128)));
+    CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
+    r->d_eyt = E.as<cell128>();
+    E.release();
+    int k = 1;
+    while (((size_t)1 << k) < m) ++k;
+    if (k > 28) k = 28;
+    r->dir_k = k;
+    DBuf lo, dir;
+    CX_HIP(lo.alloc((((size_t)1 << k) + 1) * sizeof(uint32_t)));
+    CX_HIP(dir.alloc(((size_t)1 << k) * sizeof(uint4)));
+    CX_HIP(cxk::dir_build(r->d_ring, m, k, lo.as<uint32_t>(), dir.as<uint4>(), s));
+    CX_HIP(hipStreamSynchronize(s));
+    r->d_dir = dir.as<uint4>();
+    dir.release();
+    return CX_OK;
 }
 
 }  // namespace
@@ -247,13 +282,7 @@ int cx_ring_create(const cx_u128 *ids, size_t n, int memkind, int device, cx_rin
         r->n = m;
         r->d_ring = ring.as<cell128>();
         ring.release();
-        DBuf E;
-        CX_HIP(E.alloc((m + 1) * sizeof(cell128)));
-        CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
-        r->d_eyt = E.as<cell128>();
-        E.release();
-        CX_HIP(hipStreamSynchronize(s));
-        return CX_OK;
+        return build_search(r, s);
     }();
     if (rc) return bail(rc);
     *out = r;
@@ -318,7 +347,7 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
     uint32_t *dout;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
     if ((rc = stage_out(owner, q, memkind, to, &dout))) return rc;
-    CX_HIP(cxk::successor(ring->eyt(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     return finish_out(owner, dout, q, memkind, s);
 }
 
@@ -335,7 +364,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
             return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
         }
     }
-    CX_HIP(cxk::fingers_build(ring->eyt(), ring->d_ring, ring->d_fingers, s));
+    CX_HIP(cxk::fingers_build(ring->sv(), ring->d_ring, ring->d_fingers, s));
     ring->fingers_converged = true;
     // route table: levels [l0, 128) with l0 = 128 - R, R = ceil(log2 n) + 8
     // rounded up to 8 (levels below it are almost always "next peer")
@@ -498,7 +527,7 @@ int cx_nsucc(const cx_ring *ring, const cx_u128 *keys, size_t q, int n, uint32_t
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
     if ((rc = stage_out(lists, q * (size_t)n, memkind, tl, &dl))) return rc;
     if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
-    CX_HIP(cxk::nsucc(ring->eyt(), reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, s));
+    CX_HIP(cxk::nsucc(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(lists, dl, q * (size_t)n * sizeof(uint32_t),
                               hipMemcpyDeviceToHost, s));
@@ -538,7 +567,7 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         if ((e = stage_in(leaves, nl, memkind, tl, &dl, s))) return e;
         CX_HIP(gone.alloc(n_old));
         CX_HIP(hipMemsetAsync(gone.p, 0, n_old, s));
-        CX_HIP(cxk::mark_leaves(old_ring->eyt(), old_ring->d_ring,
+        CX_HIP(cxk::mark_leaves(old_ring->sv(), old_ring->d_ring,
                                 reinterpret_cast<const cell128 *>(dl), nl, gone.as<uint8_t>(), s));
         const size_t cap = n_old + nj;
         CX_HIP(k0.alloc(cap * sizeof(cell128)));
@@ -573,11 +602,11 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         r->n = m;
         r->d_ring = ringbuf.as<cell128>();
         ringbuf.release();
-        DBuf E;
-        CX_HIP(E.alloc((m + 1) * sizeof(cell128)));
-        CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
-        r->d_eyt = E.as<cell128>();
-        E.release();
+        r->search_variant = old_ring->search_variant;
+        {
+            int e2 = build_search(r, s);
+            if (e2) return e2;
+        }
         if (old_to_new) {
             const hipMemcpyKind kind =
                 memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -615,7 +644,7 @@ int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_
     if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
     if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
     if ((rc = stage_out(target, q * (size_t)n, memkind, tt, &dt))) return rc;
-    CX_HIP(cxk::misplaced_churn(old_ring->eyt(), new_ring->eyt(), d_o2n,
+    CX_HIP(cxk::misplaced_churn(old_ring->sv(), new_ring->sv(), d_o2n,
                                 reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, dm, dt, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(new_lists, dl, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -648,7 +677,7 @@ int cx_misplaced_holders(const cx_ring *ring, const cx_u128 *keys, size_t q,
     if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
     if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
     if ((rc = stage_out(target, q * (size_t)nh, memkind, tt, &dt))) return rc;
-    CX_HIP(cxk::misplaced_holders(ring->eyt(), dh, nh, reinterpret_cast<const cell128 *>(dk), q,
+    CX_HIP(cxk::misplaced_holders(ring->sv(), dh, nh, reinterpret_cast<const cell128 *>(dk), q,
                                   n, dl, dc, dm, dt, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(new_lists, dl, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -702,6 +731,14 @@ int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0..3");
     ring->route_variant = variant;
+    return CX_OK;
+}
+
+// 0 = Eytzinger search with LDS-staged top levels, 1 = bucket directory (default).
+int cxi_set_search_variant(cx_ring *ring, int variant) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    ring->search_variant = variant;
     return CX_OK;
 }
 

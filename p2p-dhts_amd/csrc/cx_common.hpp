@@ -113,6 +113,69 @@ __device__ __forceinline__ void eyt_stage_lds(const EytView &ev, u128 *lds) {
 }
 
 // ---------------------------------------------------------------------------
+// Bucket directory of the ring (uniform hash IDs): k = ceil(log2 n) top bits
+// pick bucket b; entry b (16 B) = {lo, hi, frac}: [lo, hi) are the ring
+// indices whose IDs fall in bucket b (lo = first index >= b << (128-k)), frac
+// = the 64 ID bits of ring[lo] just below the bucket bits.  One gather answers
+// an empty bucket, a key below the bucket's first ID, or a one-entry bucket;
+// otherwise an exact binary search over the bucket's IDs finishes it.
+// ---------------------------------------------------------------------------
+struct SearchView {
+    EytView ev;          // Eytzinger copy (always built)
+    const uint4 *dir;    // [2^k] directory entries, or nullptr (use Eytzinger)
+    int k;
+    const cell128 *ring;
+};
+
+__device__ __forceinline__ uint32_t dir_successor(const SearchView &sv, u128 x) {
+    const uint32_t n = sv.ev.n;
+    const int k = sv.k;
+    const uint4 e = sv.dir[(size_t)(uint64_t)(x >> (128 - k))];
+    const uint32_t lo = e.x, hi = e.y;
+    uint32_t ans;
+    if (lo == hi) {
+        ans = hi;
+    } else {
+        const uint64_t frac = ((uint64_t)e.w << 32) | e.z;
+        const uint64_t xf = (uint64_t)(x >> (64 - k));  // ID bits [64-k, 128-k)
+        if (xf < frac) {
+            ans = lo;
+        } else if (xf > frac && hi - lo == 1) {
+            ans = hi;
+        } else {
+            uint32_t a = (xf > frac) ? lo + 1 : lo, z = hi;
+            while (a < z) {
+                const uint32_t m = a + (z - a) / 2;
+                if (ld128(sv.ring + m) < x) a = m + 1;
+                else z = m;
+            }
+            ans = a;
+        }
+    }
+    return ans == n ? 0u : ans;
+}
+
+// Compile-time choice of the successor search inside a kernel.
+template <bool DIR>
+struct Searcher;
+template <>
+struct Searcher<false> {
+    static constexpr unsigned LDS = CX_LDS_NODES;
+    __device__ static void stage(const SearchView &sv, u128 *lds) { eyt_stage_lds(sv.ev, lds); }
+    __device__ static uint32_t find(const SearchView &sv, const u128 *lds, u128 x) {
+        return eyt_successor(sv.ev, lds, x);
+    }
+};
+template <>
+struct Searcher<true> {
+    static constexpr unsigned LDS = 1;
+    __device__ static void stage(const SearchView &, u128 *) {}
+    __device__ static uint32_t find(const SearchView &sv, const u128 *, u128 x) {
+        return dir_successor(sv, x);
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Host-side launch helpers.
 // ---------------------------------------------------------------------------
 static inline unsigned cx_grid(size_t work, unsigned block, unsigned cap = 8192) {

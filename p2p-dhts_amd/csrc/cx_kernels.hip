@@ -344,19 +344,57 @@ hipError_t eyt_build(const cell128 *sorted, size_t n, cell128 *E, hipStream_t s)
 // ===========================================================================
 constexpr int SUCC_BLOCK = 1024;
 
-__global__ __launch_bounds__(SUCC_BLOCK) void k_successor(EytView ev, const cell128 *keys,
+template <bool DIR>
+__global__ __launch_bounds__(SUCC_BLOCK) void k_successor(SearchView sv, const cell128 *keys,
                                                           size_t q, uint32_t *owner) {
-    __shared__ u128 lds[CX_LDS_NODES];
-    eyt_stage_lds(ev, lds);
+    __shared__ u128 lds[Searcher<DIR>::LDS];
+    Searcher<DIR>::stage(sv, lds);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
          i += (size_t)gridDim.x * blockDim.x)
-        owner[i] = eyt_successor(ev, lds, ld128(keys + i));
+        owner[i] = Searcher<DIR>::find(sv, lds, ld128(keys + i));
 }
 
-hipError_t successor(const EytView &ev, const cell128 *keys, size_t q, uint32_t *owner,
+hipError_t successor(const SearchView &sv, const cell128 *keys, size_t q, uint32_t *owner,
                      hipStream_t s) {
     if (q == 0) return hipSuccess;
-    k_successor<<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, keys, q, owner);
+    if (sv.dir)
+        k_successor<true><<<cx_grid(q, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, keys, q, owner);
+    else
+        k_successor<false><<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, keys, q, owner);
+    return hipGetLastError();
+}
+
+// Directory build: lo[b] = first ring index whose ID is >= b << (128 - k).
+// Thread j fills the buckets (bucket(ring[j-1]), bucket(ring[j])]; thread n
+// fills the tail up to 2^k.
+__global__ void k_dir_lo(const cell128 *ring, uint32_t n, int k, uint32_t *lo) {
+    const size_t nb = (size_t)1 << k;
+    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j <= n;
+         j += (size_t)gridDim.x * blockDim.x) {
+        const long long pb = j == 0 ? -1 : (long long)(uint64_t)(ld128(ring + j - 1) >> (128 - k));
+        const long long cb = j == n ? (long long)nb : (long long)(uint64_t)(ld128(ring + j) >> (128 - k));
+        for (long long b = pb + 1; b <= cb; ++b) lo[b] = (uint32_t)j;
+    }
+}
+
+__global__ void k_dir_pack(const cell128 *ring, uint32_t n, int k, const uint32_t *lo,
+                           uint4 *dir) {
+    const size_t nb = (size_t)1 << k;
+    for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < nb;
+         b += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t a = lo[b], z = lo[b + 1];
+        uint64_t frac = 0;
+        if (a < z) frac = (uint64_t)(ld128(ring + a) >> (64 - k));
+        dir[b] = make_uint4(a, z, (uint32_t)frac, (uint32_t)(frac >> 32));
+    }
+}
+
+hipError_t dir_build(const cell128 *ring, size_t n, int k, uint32_t *lo_tmp, uint4 *dir,
+                     hipStream_t s) {
+    k_dir_lo<<<cx_grid(n + 1, 256), 256, 0, s>>>(ring, (uint32_t)n, k, lo_tmp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_dir_pack<<<cx_grid((size_t)1 << k, 256), 256, 0, s>>>(ring, (uint32_t)n, k, lo_tmp, dir);
     return hipGetLastError();
 }
 
@@ -364,11 +402,12 @@ hipError_t successor(const EytView &ev, const cell128 *keys, size_t q, uint32_t 
 // a6: converged finger table.  Lane (p, i): succ(id_p + 2^i).  When 2^i is no
 // larger than the gap to the next peer the answer is p+1 without a search.
 // ===========================================================================
-__global__ __launch_bounds__(SUCC_BLOCK) void k_fingers(EytView ev, const cell128 *ring,
+template <bool DIR>
+__global__ __launch_bounds__(SUCC_BLOCK) void k_fingers(SearchView sv, const cell128 *ring,
                                                         uint32_t *F) {
-    __shared__ u128 lds[CX_LDS_NODES];
-    eyt_stage_lds(ev, lds);
-    const uint32_t n = ev.n;
+    __shared__ u128 lds[Searcher<DIR>::LDS];
+    Searcher<DIR>::stage(sv, lds);
+    const uint32_t n = sv.ev.n;
     const size_t total = (size_t)n * CX_FINGERS;
     for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
          t += (size_t)gridDim.x * blockDim.x) {
@@ -380,15 +419,18 @@ __global__ __launch_bounds__(SUCC_BLOCK) void k_fingers(EytView ev, const cell12
             const uint32_t nx = (p + 1 == n) ? 0u : p + 1;
             const u128 gap = ld128(ring + nx) - idp;  // clockwise distance to next peer
             const u128 step = (u128)1 << i;
-            f = (step <= gap) ? nx : eyt_successor(ev, lds, idp + step);
+            f = (step <= gap) ? nx : Searcher<DIR>::find(sv, lds, idp + step);
         }
         F[t] = f;
     }
 }
 
-hipError_t fingers_build(const EytView &ev, const cell128 *ring, uint32_t *F, hipStream_t s) {
-    const size_t total = (size_t)ev.n * CX_FINGERS;
-    k_fingers<<<cx_grid(total, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, ring, F);
+hipError_t fingers_build(const SearchView &sv, const cell128 *ring, uint32_t *F, hipStream_t s) {
+    const size_t total = (size_t)sv.ev.n * CX_FINGERS;
+    if (sv.dir)
+        k_fingers<true><<<cx_grid(total, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, ring, F);
+    else
+        k_fingers<false><<<cx_grid(total, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, ring, F);
     return hipGetLastError();
 }
 
@@ -1288,16 +1330,17 @@ hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128
 // ===========================================================================
 // a10/a11: n-successor windows.
 // ===========================================================================
-__global__ __launch_bounds__(SUCC_BLOCK) void k_nsucc(EytView ev, const cell128 *keys, size_t q,
+template <bool DIR>
+__global__ __launch_bounds__(SUCC_BLOCK) void k_nsucc(SearchView sv, const cell128 *keys, size_t q,
                                                       int nlist, uint32_t *lists,
                                                       uint8_t *count) {
-    __shared__ u128 lds[CX_LDS_NODES];
-    eyt_stage_lds(ev, lds);
-    const uint32_t n = ev.n;
+    __shared__ u128 lds[Searcher<DIR>::LDS];
+    Searcher<DIR>::stage(sv, lds);
+    const uint32_t n = sv.ev.n;
     const int nn = (uint32_t)nlist < n ? nlist : (int)n;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
          i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t s0 = eyt_successor(ev, lds, ld128(keys + i));
+        const uint32_t s0 = Searcher<DIR>::find(sv, lds, ld128(keys + i));
         uint32_t *l = lists + i * (size_t)nlist;
         for (int j = 0; j < nlist; ++j) {
             uint32_t v = s0 + (uint32_t)j;
@@ -1308,34 +1351,44 @@ __global__ __launch_bounds__(SUCC_BLOCK) void k_nsucc(EytView ev, const cell128 
     }
 }
 
-hipError_t nsucc(const EytView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
+hipError_t nsucc(const SearchView &sv, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s) {
     if (q == 0) return hipSuccess;
-    k_nsucc<<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, keys, q, n, lists, count);
+    if (sv.dir)
+        k_nsucc<true><<<cx_grid(q, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, keys, q, n, lists,
+                                                                          count);
+    else
+        k_nsucc<false><<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, keys, q, n, lists,
+                                                                          count);
     return hipGetLastError();
 }
 
 // ===========================================================================
 // a12: churn support + misplaced scan.
 // ===========================================================================
-__global__ __launch_bounds__(SUCC_BLOCK) void k_mark_leaves(EytView ev, const cell128 *ring,
+template <bool DIR>
+__global__ __launch_bounds__(SUCC_BLOCK) void k_mark_leaves(SearchView sv, const cell128 *ring,
                                                             const cell128 *leaves, size_t nl,
                                                             uint8_t *gone) {
-    __shared__ u128 lds[CX_LDS_NODES];
-    eyt_stage_lds(ev, lds);
+    __shared__ u128 lds[Searcher<DIR>::LDS];
+    Searcher<DIR>::stage(sv, lds);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nl;
          i += (size_t)gridDim.x * blockDim.x) {
         const u128 x = ld128(leaves + i);
-        const uint32_t s0 = eyt_successor(ev, lds, x);
+        const uint32_t s0 = Searcher<DIR>::find(sv, lds, x);
         if (ld128(ring + s0) == x) gone[s0] = 1;
     }
 }
 
-hipError_t mark_leaves(const EytView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
-                       uint8_t *gone, hipStream_t s) {
+hipError_t mark_leaves(const SearchView &sv, const cell128 *ring, const cell128 *leaves,
+                       size_t nl, uint8_t *gone, hipStream_t s) {
     if (nl == 0) return hipSuccess;
-    k_mark_leaves<<<cx_grid(nl, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(ev, ring, leaves, nl,
-                                                                      gone);
+    if (sv.dir)
+        k_mark_leaves<true><<<cx_grid(nl, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, ring, leaves,
+                                                                                nl, gone);
+    else
+        k_mark_leaves<false><<<cx_grid(nl, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, ring, leaves,
+                                                                                 nl, gone);
     return hipGetLastError();
 }
 
@@ -1358,28 +1411,28 @@ hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 
 // Misplaced scan core.  Holder ranks j in order; `has` = 16-bit mask of new-list
 // ranks already holding the key; membership of a holder in the new window is
 // (holder - s_new) mod n_new < nn.
-template <bool CHURN>
-__global__ __launch_bounds__(512) void k_misplaced(EytView ev_new, EytView ev_old,
+template <bool CHURN, bool DIR>
+__global__ __launch_bounds__(512) void k_misplaced(SearchView sv_new, SearchView sv_old,
                                                    const uint32_t *old_to_new,
                                                    const uint32_t *holders, int nh,
                                                    const cell128 *keys, size_t q, int nlist,
                                                    uint32_t *new_lists, uint8_t *count,
                                                    uint16_t *mask, uint8_t *target) {
-    __shared__ u128 lds_new[CX_LDS_NODES];
-    __shared__ u128 lds_old[CHURN ? CX_LDS_NODES : 1];
-    eyt_stage_lds(ev_new, lds_new);
-    if (CHURN) eyt_stage_lds(ev_old, lds_old);
-    const uint32_t n_new = ev_new.n;
+    __shared__ u128 lds_new[Searcher<DIR>::LDS];
+    __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
+    Searcher<DIR>::stage(sv_new, lds_new);
+    if (CHURN) Searcher<DIR>::stage(sv_old, lds_old);
+    const uint32_t n_new = sv_new.ev.n;
     const int nn = (uint32_t)nlist < n_new ? nlist : (int)n_new;
-    const uint32_t n_old = CHURN ? ev_old.n : 0;
+    const uint32_t n_old = CHURN ? sv_old.ev.n : 0;
     const int no = CHURN ? ((uint32_t)nlist < n_old ? nlist : (int)n_old) : nh;
     const int nslots = CHURN ? nlist : nh;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
          i += (size_t)gridDim.x * blockDim.x) {
         const u128 key = ld128(keys + i);
-        const uint32_t sn = eyt_successor(ev_new, lds_new, key);
+        const uint32_t sn = Searcher<DIR>::find(sv_new, lds_new, key);
         uint32_t so = 0;
-        if (CHURN) so = eyt_successor(ev_old, lds_old, key);
+        if (CHURN) so = Searcher<DIR>::find(sv_old, lds_old, key);
         uint32_t *l = new_lists + i * (size_t)nlist;
         for (int j = 0; j < nlist; ++j) {
             uint32_t v = sn + (uint32_t)j;
@@ -1436,23 +1489,30 @@ __global__ __launch_bounds__(512) void k_misplaced(EytView ev_new, EytView ev_ol
     }
 }
 
-hipError_t misplaced_churn(const EytView &ev_old, const EytView &ev_new,
+hipError_t misplaced_churn(const SearchView &sv_old, const SearchView &sv_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
                            hipStream_t s) {
     if (q == 0) return hipSuccess;
-    k_misplaced<true><<<cx_grid(q, 512, 256), 512, 0, s>>>(ev_new, ev_old, old_to_new, nullptr,
-                                                          0, keys, q, n, lists, count, mask,
-                                                          target);
+    if (sv_new.dir && sv_old.dir)
+        k_misplaced<true, true><<<cx_grid(q, 512, 4096), 512, 0, s>>>(
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target);
+    else
+        k_misplaced<true, false><<<cx_grid(q, 512, 256), 512, 0, s>>>(
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target);
     return hipGetLastError();
 }
 
-hipError_t misplaced_holders(const EytView &ev, const uint32_t *holders, int nh,
+hipError_t misplaced_holders(const SearchView &sv, const uint32_t *holders, int nh,
                              const cell128 *keys, size_t q, int n, uint32_t *lists,
                              uint8_t *count, uint16_t *mask, uint8_t *target, hipStream_t s) {
     if (q == 0) return hipSuccess;
-    k_misplaced<false><<<cx_grid(q, 512, 512), 512, 0, s>>>(ev, ev, nullptr, holders, nh, keys, q,
-                                                           n, lists, count, mask, target);
+    if (sv.dir)
+        k_misplaced<false, true><<<cx_grid(q, 512, 4096), 512, 0, s>>>(
+            sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target);
+    else
+        k_misplaced<false, false><<<cx_grid(q, 512, 512), 512, 0, s>>>(
+            sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target);
     return hipGetLastError();
 }
 

@@ -35,9 +35,11 @@ hipError_t iota(uint32_t *t, size_t n, uint32_t base, hipStream_t s);
 hipError_t fill_u32(uint32_t *t, size_t n, uint32_t v, hipStream_t s);
 
 hipError_t eyt_build(const cell128 *sorted, size_t n, cell128 *E, hipStream_t s);
-hipError_t successor(const EytView &ev, const cell128 *keys, size_t q, uint32_t *owner,
+hipError_t dir_build(const cell128 *ring, size_t n, int k, uint32_t *lo_tmp, uint4 *dir,
                      hipStream_t s);
-hipError_t fingers_build(const EytView &ev, const cell128 *ring, uint32_t *F, hipStream_t s);
+hipError_t successor(const SearchView &ev, const cell128 *keys, size_t q, uint32_t *owner,
+                     hipStream_t s);
+hipError_t fingers_build(const SearchView &ev, const cell128 *ring, uint32_t *F, hipStream_t s);
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
                  size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
@@ -56,15 +58,15 @@ hipError_t route_pk3(const cell128 *ring_ext, const cell128 *ring, size_t n, con
                      int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
                      const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
                      uint8_t *status, hipStream_t s);
-hipError_t nsucc(const EytView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
+hipError_t nsucc(const SearchView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
-hipError_t mark_leaves(const EytView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
+hipError_t mark_leaves(const SearchView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
                        uint8_t *gone, hipStream_t s);
-hipError_t misplaced_churn(const EytView &ev_old, const EytView &ev_new,
+hipError_t misplaced_churn(const SearchView &ev_old, const SearchView &ev_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
                            hipStream_t s);
-hipError_t misplaced_holders(const EytView &ev, const uint32_t *holders, int nh,
+hipError_t misplaced_holders(const SearchView &ev, const uint32_t *holders, int nh,
                              const cell128 *keys, size_t q, int n, uint32_t *lists,
                              uint8_t *count, uint16_t *mask, uint8_t *target, hipStream_t s);
 hipError_t in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,

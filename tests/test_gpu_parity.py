@@ -60,29 +60,35 @@ def test_ring_build_equal_high_bits(cx, O):
 
 
 # ---------------------------------------------------------------- a5/a7 successor
+@pytest.mark.parametrize("search", [0, 1])
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 1000, 4095, 4096, 70000])
-def test_successor(cx, O, n):
+def test_successor(cx, O, n, search):
     ids = edge_ring(O, n, 77 + n)
     ring = cx.Ring(ids)
+    ring.set_search_variant(search)
     want_ring = O.ring_build(ids)
     keys = edge_keys(O, want_ring, 5 + n, 20000)
     got = ring.successor(keys)
     assert (got == O.successor(want_ring, keys)).all()
 
 
-def test_successor_c2(cx, O):
+@pytest.mark.parametrize("search", [0, 1])
+def test_successor_c2(cx, O, search):
     """Config C2: 2^16-peer ring, 2^20 uniform keys (seeds of SURVEY 8d)."""
     ids = O.splitmix_keys(0x5EED0001, 1 << 16)
     keys = O.splitmix_keys(0x5EED0002, 1 << 20)
     ring = cx.Ring(ids)
+    ring.set_search_variant(search)
     assert (ring.successor(keys) == O.successor(O.ring_build(ids), keys)).all()
 
 
 # ---------------------------------------------------------------- a6 fingers
+@pytest.mark.parametrize("search", [0, 1])
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 5000])
-def test_fingers(cx, O, n):
+def test_fingers(cx, O, n, search):
     ids = edge_ring(O, n, 300 + n)
     ring = cx.Ring(ids)
+    ring.set_search_variant(search)
     F = ring.build_fingers(copy_out=True)
     assert (F == O.fingers(O.ring_build(ids))).all()
 
@@ -175,6 +181,26 @@ def clustered_ring(O, n, seed, spread_bits):
     return O.keys_from_ints(vals)
 
 
+@pytest.mark.parametrize("search", [0, 1])
+@pytest.mark.parametrize("spread", [8, 40, 100])
+def test_successor_clustered_rings(cx, O, search, spread):
+    """Skewed rings: whole clusters inside one directory bucket (binary-search path)."""
+    ids = clustered_ring(O, 5000, spread, spread)
+    ring = cx.Ring(ids)
+    ring.set_search_variant(search)
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, spread, 20000)
+    ints = O.ints_from_keys(want_ring)
+    rng = np.random.default_rng(spread)
+    near = O.keys_from_ints([(ints[j] + int(rng.integers(-2, 3))) % (1 << 128)
+                             for j in rng.integers(0, len(ints), 20000)])
+    keys = np.concatenate([keys, near])
+    assert (ring.successor(keys) == O.successor(want_ring, keys)).all()
+    lists, count = ring.nsucc(keys, 14)
+    wl, wc = O.nsucc(O.Peers(want_ring, O.fingers(want_ring)), keys, 14)
+    assert (lists == wl).all() and (count == wc).all()
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("spread", [8, 40, 90, 100])
 def test_route_clustered_rings(cx, O, variant, spread):
@@ -242,10 +268,12 @@ def test_fingers_upload_rejects_bad_index(cx, O):
 
 
 # ---------------------------------------------------------------- a10/a11 DHash
+@pytest.mark.parametrize("search", [0, 1])
 @pytest.mark.parametrize("n_ring", [1, 2, 13, 14, 15, 28, 3000])
-def test_nsucc(cx, O, n_ring):
+def test_nsucc(cx, O, n_ring, search):
     ids = O.splitmix_keys(50 + n_ring, n_ring)
     ring = cx.Ring(ids)
+    ring.set_search_variant(search)
     want_ring = O.ring_build(ids)
     keys = edge_keys(O, want_ring, 51, 5000)
     lists, count = ring.nsucc(keys, 14)
@@ -263,10 +291,12 @@ def test_dhash_insufficient(cx, O):
 
 
 # ---------------------------------------------------------------- a12 churn
+@pytest.mark.parametrize("search", [0, 1])
 @pytest.mark.parametrize("n_old,nj,nl", [(1, 1, 0), (5, 0, 2), (60, 3, 4), (20000, 200, 200)])
-def test_churn_and_misplaced(cx, O, n_old, nj, nl):
+def test_churn_and_misplaced(cx, O, n_old, nj, nl, search):
     ids = O.splitmix_keys(7000 + n_old, n_old)
     old = cx.Ring(ids)
+    old.set_search_variant(search)
     want_old = O.ring_build(ids)
     rng = np.random.default_rng(n_old)
     joins = O.splitmix_keys(7100 + n_old, nj)
