@@ -169,6 +169,15 @@ int cx_misplaced_holders(const cx_ring *ring, const cx_u128 *keys, size_t q,
 int cx_in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t q,
                   int inclusive, uint8_t *out, int memkind);
 
+/* ---- a1: identifiers ------------------------------------------------------
+ * out[i] = UUIDv5(DNS namespace, name_i) read as a big-endian 128-bit integer:
+ * the ID a ChordPeer gets from "ip:port" (abstract_chord_peer.cpp:21) and a key
+ * gets from ChordKey(plaintext, hashed = false) (key.h:29-33,76-79).  Names
+ * are concatenated in `bytes`; name i = bytes[offsets[i] .. offsets[i+1]),
+ * offsets has count + 1 entries.  SHA-1 runs on the GPU (one lane per name). */
+int cx_uuid5_dns(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx_u128 *out,
+                 int memkind, int device);
+
 /* ---- synthetic inputs (bench / tests) --------------------------------------
  * out[i] = {splitmix64(seed, 2(offset+i)), splitmix64(seed, 2(offset+i)+1)}
  * written on the device (SURVEY 8d generator). */

@@ -7,10 +7,11 @@ mirrors the reference's lookup-path interface (see ring.py).
 from ._lib import (CX_FINGERS, CX_HOP_CAP, CX_MAX_NSUCC, CX_NONE, CX_Q_BADPEER, CX_Q_HOPCAP,
                    CX_Q_OK, ChordError, device_count, lib)
 from .key import ChordKey
-from .ring import Ring, fill_splitmix, in_between
+from .ring import Ring, fill_splitmix, in_between, uuid5_dns
 
 __all__ = [
-    "Ring", "ChordKey", "ChordError", "in_between", "fill_splitmix", "device_count", "lib",
+    "Ring", "ChordKey", "ChordError", "in_between", "fill_splitmix", "uuid5_dns", "device_count",
+    "lib",
     "CX_FINGERS", "CX_NONE", "CX_HOP_CAP", "CX_MAX_NSUCC", "CX_Q_OK", "CX_Q_HOPCAP",
     "CX_Q_BADPEER",
 ]

@@ -39,7 +39,7 @@ EXPORTS = (
     "cx_successor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
     "cx_peer_state_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
-    "cx_fill_splitmix",
+    "cx_uuid5_dns", "cx_fill_splitmix",
 )
 
 
@@ -88,6 +88,7 @@ def lib() -> ctypes.CDLL:
         "cx_misplaced": ([vp, vp, vp, vp, sz, i, vp, vp, vp, vp, i], i),
         "cx_misplaced_holders": ([vp, vp, sz, vp, i, i, vp, vp, vp, vp, i], i),
         "cx_in_between": ([vp, vp, vp, sz, i, vp, i], i),
+        "cx_uuid5_dns": ([vp, vp, sz, vp, i, i], i),
         "cx_fill_splitmix": ([vp, sz, u64, u64, i, vp], i),
     }
     for name, (args, res) in sig.items():

@@ -3,12 +3,11 @@
 GenericKey<16,32> (src/data_structures/key.h:56-281, ChordKey at key.h:355).
 Values are held as raw uint256 integers so the reference's non-canonical
 results survive (1 - 1 -> 2^128, 0 - 1 -> 2^256 - 1: key.h:242-250).
-`in_between` is answered by the engine's GPU kernel (cx_in_between), the same
-code that the batch API uses; this class only builds and formats values.
+`in_between` and plaintext hashing are answered by the engine's GPU kernels
+(cx_in_between, cx_uuid5_dns), the same code the batch API uses; this class
+only builds, formats and does the reference's scalar +/- on values.
 """
 from __future__ import annotations
-
-import uuid
 
 import numpy as np
 
@@ -26,9 +25,11 @@ class ChordKey:
         if isinstance(key, str):
             if hashed:  # uint256_t("0x" + key), key.h:73-75
                 self.value = int(key, 16) if key else 0
-            else:  # UUIDv5(DNS, plaintext) read big-endian, key.h:76-79
+            else:  # UUIDv5(DNS, plaintext) read big-endian, key.h:76-79 (GPU)
+                from .ring import uuid5_dns
                 self.plaintext = key
-                self.value = int.from_bytes(uuid.uuid5(uuid.NAMESPACE_DNS, key).bytes, "big")
+                lo, hi = (int(x) for x in uuid5_dns([key])[0])
+                self.value = lo | (hi << 64)
         else:
             self.value = int(key) % U256
 
@@ -89,6 +90,12 @@ class ChordKey:
             out[i, 0] = v & 0xFFFFFFFFFFFFFFFF
             out[i, 1] = v >> 64
         return out
+
+    @staticmethod
+    def array_plaintext(names) -> np.ndarray:
+        """(q, 2) uint64 IDs of plaintext names, hashed in one GPU batch."""
+        from .ring import uuid5_dns
+        return uuid5_dns(list(names))
 
     @staticmethod
     def from_array(a) -> list:

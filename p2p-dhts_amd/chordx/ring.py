@@ -265,6 +265,20 @@ def in_between(v, lb, ub, inclusive: bool = True) -> np.ndarray:
     return out
 
 
+def uuid5_dns(names, device: int = 0) -> np.ndarray:
+    """IDs of plaintext names (peer "ip:port" strings or keys), hashed on the GPU:
+    (q, 2) uint64 [lo, hi] = UUIDv5(DNS, name) big-endian (key.h:29-33,76-79)."""
+    enc = [n.encode() if isinstance(n, str) else bytes(n) for n in names]
+    offs = np.zeros(len(enc) + 1, dtype=np.uint64)
+    if enc:
+        offs[1:] = np.cumsum([len(b) for b in enc])
+    buf = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).copy()
+    out = np.empty((len(enc), 2), dtype=np.uint64)
+    L.check(L.lib().cx_uuid5_dns(_ptr(buf), _ptr(offs), len(enc), _ptr(out), L.CX_MEM_HOST,
+                                 device))
+    return out
+
+
 def fill_splitmix(out, seed: int, offset: int = 0):
     """Synthetic uniform 128-bit keys written on the device into `out` ((q, 2) int64)."""
     assert _is_dev(out) and out.dim() == 2 and out.shape[1] == 2

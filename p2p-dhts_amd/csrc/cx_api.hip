@@ -711,6 +711,37 @@ int cx_in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t
     return CX_OK;
 }
 
+int cx_uuid5_dns(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx_u128 *out,
+                 int memkind, int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    CX_CHECK(device >= 0 && device < ndev, CX_E_INVALID, "bad device ordinal");
+    if (count == 0) return CX_OK;
+    CX_CHECK(offsets != nullptr && out != nullptr, CX_E_INVALID, "null argument");
+    CX_HIP(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    DBuf to, tb, tout;
+    const uint64_t *doff;
+    const uint8_t *dbytes;
+    cx_u128 *dout;
+    int rc;
+    if ((rc = stage_in(offsets, count + 1, memkind, to, &doff, s))) return rc;
+    uint64_t nbytes = 0;
+    if (memkind == CX_MEM_HOST) {
+        nbytes = offsets[count];
+        CX_CHECK(offsets[0] == 0, CX_E_INVALID, "offsets[0] must be 0");
+        for (size_t i = 0; i < count; ++i)
+            CX_CHECK(offsets[i] <= offsets[i + 1], CX_E_INVALID, "offsets not ascending");
+    } else {
+        CX_HIP(hipMemcpy(&nbytes, offsets + count, sizeof(nbytes), hipMemcpyDeviceToHost));
+    }
+    if ((rc = stage_in(bytes, (size_t)nbytes, memkind, tb, &dbytes, s))) return rc;
+    if ((rc = stage_out(out, count, memkind, tout, &dout))) return rc;
+    CX_HIP(cxk::uuid5(dbytes, doff, count, reinterpret_cast<cell128 *>(dout), s));
+    return finish_out(out, dout, count, memkind, s);
+}
+
 int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t offset,
                      int device, void *hip_stream) {
     CX_CHECK(out_device || count == 0, CX_E_INVALID, "null output");

@@ -1598,6 +1598,78 @@ hipError_t fill_u32(uint32_t *t, size_t n, uint32_t v, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// a1: batched UUIDv5 (RFC 4122, DNS namespace) of plaintext names -- the
+// peer/key ID construction of GenerateSha1Hash (key.h:29-33) + uint256_t(uuid)
+// big-endian (key.h:77-78).  One lane per name; SHA-1 (FIPS 180-4) over
+// ns || name with a 16-word rolling schedule.
+// ===========================================================================
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
+
+__global__ void k_uuid5(const uint8_t *bytes, const uint64_t *offs, size_t count, cell128 *out) {
+    const uint8_t ns[16] = {0x6b, 0xa7, 0xb8, 0x10, 0x9d, 0xad, 0x11, 0xd1,
+                            0x80, 0xb4, 0x00, 0xc0, 0x4f, 0xd4, 0x30, 0xc8};
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t o = offs[i], len = offs[i + 1] - o;
+        const uint64_t total = 16 + len;
+        const uint64_t nblk = (total + 8) / 64 + 1;
+        const uint64_t bits = total * 8;
+        uint32_t h0 = 0x67452301u, h1 = 0xEFCDAB89u, h2 = 0x98BADCFEu, h3 = 0x10325476u,
+                 h4 = 0xC3D2E1F0u;
+        for (uint64_t blk = 0; blk < nblk; ++blk) {
+            uint32_t w[16];
+            for (int j = 0; j < 16; ++j) {
+                uint32_t v = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const uint64_t p = blk * 64 + (uint64_t)(j * 4 + b);
+                    uint32_t c;
+                    if (p < 16) c = ns[p];
+                    else if (p < total) c = bytes[o + p - 16];
+                    else if (p == total) c = 0x80;
+                    else if (blk == nblk - 1 && p >= nblk * 64 - 8)
+                        c = (uint32_t)(bits >> (8 * (nblk * 64 - 1 - p))) & 0xFF;
+                    else c = 0;
+                    v = (v << 8) | c;
+                }
+                w[j] = v;
+            }
+            uint32_t a = h0, b = h1, c = h2, d = h3, e = h4;
+#pragma unroll
+            for (int t = 0; t < 80; ++t) {
+                uint32_t wt;
+                if (t < 16) {
+                    wt = w[t];
+                } else {
+                    wt = rotl32(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+                    w[t & 15] = wt;
+                }
+                uint32_t f, k;
+                if (t < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
+                else if (t < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
+                else if (t < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8F1BBCDCu; }
+                else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+                const uint32_t tmp = rotl32(a, 5) + f + e + k + wt;
+                e = d; d = c; c = rotl32(b, 30); b = a; a = tmp;
+            }
+            h0 += a; h1 += b; h2 += c; h3 += d; h4 += e;
+        }
+        h1 = (h1 & 0xFFFF0FFFu) | 0x00005000u;  // version 5 (byte 6 high nibble)
+        h2 = (h2 & 0x3FFFFFFFu) | 0x80000000u;  // RFC 4122 variant (byte 8)
+        cell128 r;
+        r.hi = ((uint64_t)h0 << 32) | h1;
+        r.lo = ((uint64_t)h2 << 32) | h3;
+        out[i] = r;
+    }
+}
+
+hipError_t uuid5(const uint8_t *bytes, const uint64_t *offs, size_t count, cell128 *out,
+                 hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    k_uuid5<<<cx_grid(count, 256), 256, 0, s>>>(bytes, offs, count, out);
+    return hipGetLastError();
+}
+
 // Validation of caller-supplied peer indices (finger uploads, preds):
 // *d_bad = 1 if any entry is >= limit (CX_NONE allowed when allow_none).
 __global__ void k_check_indices(const uint32_t *idx, size_t count, uint32_t limit,

@@ -73,6 +73,8 @@ hipError_t in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, si
                       int inclusive, uint8_t *out, hipStream_t s);
 hipError_t fill_splitmix(cell128 *out, size_t count, uint64_t seed, uint64_t offset,
                          hipStream_t s);
+hipError_t uuid5(const uint8_t *bytes, const uint64_t *offs, size_t count, cell128 *out,
+                 hipStream_t s);
 hipError_t check_indices(const uint32_t *idx, size_t count, uint32_t limit, bool allow_none,
                          uint32_t *d_bad, hipStream_t s);
 

@@ -51,7 +51,7 @@ def test_no_host_fallback_without_gpu():
 def test_chordkey_host_values():
     """ChordKey mirror: construction/formatting/arithmetic (key.h:41-47,70-93,236-270)."""
     from chordx import ChordKey
-    k = ChordKey("127.0.0.1:5012", hashed=False)
+    k = ChordKey("091186395ae2562aaa1ff7f3513747e9")
     assert str(k) == "91186395ae2562aaa1ff7f3513747e9"  # no leading zero
     assert (ChordKey(1) - 1).value == 1 << 128
     assert (ChordKey(0) - 1).value == (1 << 256) - 1

@@ -393,3 +393,35 @@ def test_device_memkind_matches_host(cx, O):
     ow = ring.successor(keys_d)
     torch.cuda.synchronize()
     assert (ow.cpu().numpy().view(np.uint32) == O.successor(O.ring_build(ids), keys_h)).all()
+
+
+# ---------------------------------------------------------------- a1 IDs
+def test_uuid5_fixture_ids(cx, O, refvec):
+    """GPU SHA-1/UUIDv5 of the 103 fixture ip:port names and the Join key names."""
+    names = [r["name"] for r in refvec["id_hash"]]
+    got = cx.uuid5_dns(names)
+    assert [format(v, "x") for v in O.ints_from_keys(got)] == [r["id"] for r in refvec["id_hash"]]
+    jk = refvec["join_placement"]["keys"]
+    got = cx.uuid5_dns([k["plain"] for k in jk])
+    assert [format(v, "x") for v in O.ints_from_keys(got)] == [k["hash"] for k in jk]
+    from chordx import ChordKey
+    assert str(ChordKey("127.0.0.1:5012", hashed=False)) == "91186395ae2562aaa1ff7f3513747e9"
+
+
+def test_uuid5_lengths_and_bytes(cx, O):
+    """SHA-1 padding boundaries (1 vs 2 vs 3 blocks), empty names, arbitrary bytes."""
+    rng = np.random.default_rng(11)
+    names = [b""] + [bytes(rng.integers(0, 256, L, dtype=np.uint8)) for L in
+                     list(range(0, 140)) + [183, 184, 247, 248, 1000]]
+    names += [f"key{i}".encode() for i in range(2000)]
+    got = cx.uuid5_dns(names)
+    import uuid as U
+    want = [int.from_bytes(U.uuid5(U.NAMESPACE_DNS, n.decode("latin-1")).bytes, "big")
+            if all(c < 128 for c in n) else None for n in names]
+    for g, w, n in zip(O.ints_from_keys(got), want, names):
+        if w is not None:
+            assert g == w
+    # arbitrary (non-ASCII) bytes checked against the C oracle's SHA-1
+    for g, n in zip(O.ints_from_keys(got), names):
+        k = O.lib().or_uuid5_dns(n, len(n))
+        assert g == (k.lo | (k.hi << 64))
