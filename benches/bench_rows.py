@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Per-row measurements of the hot-path scope table at the
+BASELINE.json configs, one MI355X.  Prints one JSON object (profiles/<round>/rows.json).
+
+  C2  2^16-peer ring, 2^20 keys: exact successor (directory and Eytzinger)
+  C3  2^20-peer ring: m=128 finger build; 2^24 routed lookups with hops
+  C5  2^24-peer ring, 2^26 keys, n=14: replica lists; 1 % join + 1 % leave
+      churn; global-maintenance misplaced scan
+
+Kernel times are HIP events on the launch stream (torch's current stream, which
+the library enqueues on for device buffers); host-synchronous calls (ring
+build, churn) are wall-clock.  Inputs: splitmix seeds of SURVEY 8(d).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
+
+import torch  # noqa: E402
+
+import chordx  # noqa: E402
+
+HBM = 8.0e12
+
+
+def ev_time(fn, reps=3):
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps / 1e3
+
+
+def keys_dev(n, seed, offset=0):
+    k = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(k, seed, offset)
+    return k
+
+
+def main():
+    out = {"device": torch.cuda.get_device_name(0)}
+    # ---------------- C2 ----------------
+    ring = chordx.Ring(keys_dev(1 << 16, 0x5EED0001))
+    keys = keys_dev(1 << 20, 0x5EED0002)
+    res = {}
+    for v, name in ((1, "directory"), (0, "eytzinger")):
+        ring.set_search_variant(v)
+        t = ev_time(lambda: ring.successor(keys))
+        res[name] = {"s": t, "lookups_per_s": (1 << 20) / t,
+                     "algo_GBps": (1 << 20) * 20 / t / 1e9}
+    out["C2_exact_successor"] = res
+    del ring, keys
+
+    # ---------------- C3 ----------------
+    N3 = 1 << 20
+    ring = chordx.Ring(keys_dev(N3, 0x5EED0003))
+    t0 = time.perf_counter()
+    ring.build_fingers()
+    ring.sync()
+    tf = time.perf_counter() - t0
+    q = 1 << 24
+    keys = keys_dev(q, 0x5EED0004)
+    src = (torch.arange(q, device="cuda", dtype=torch.int64) % N3).to(torch.int32)
+    owner = torch.empty(q, dtype=torch.int32, device="cuda")
+    hops = torch.empty(q, dtype=torch.uint8, device="cuda")
+    status = torch.empty(q, dtype=torch.uint8, device="cuda")
+    tr = ev_time(lambda: ring.route(src, keys, out=(owner, hops, status)))
+    sh = int(hops.to(torch.int64).sum())
+    algo = q * (25 + 64) + 128 * sh
+    out["C3"] = {"fingers_build_s_wall": tf,
+                 "fingers_algo_GBps": N3 * 528 / tf / 1e9,
+                 "route_s": tr, "route_lookups_per_s": q / tr, "mean_hops": sh / q,
+                 "route_algo_frac_of_hbm": algo / tr / HBM,
+                 "bad_status": int((status != 0).sum())}
+    del ring, keys, src, owner, hops, status
+
+    # ---------------- C5 ----------------
+    N5, q5, n = 1 << 24, 1 << 26, 14
+    old = chordx.Ring(keys_dev(N5, 0x5EED0007))
+    keys = keys_dev(q5, 0x5EED0008)
+    lists = torch.empty((q5, n), dtype=torch.int32, device="cuda")
+    tl = ev_time(lambda: old.nsucc(keys, n), reps=2)
+    joins = keys_dev(N5 // 100, 0x5EED0009)
+    pick = keys_dev(N5 // 100, 0x5EED0009, offset=1 << 40)[:, 0].remainder(N5)
+    leaves = old.ids_device()[pick].contiguous()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    new, o2n = old.churn(joins, leaves)
+    torch.cuda.synchronize()
+    tc = time.perf_counter() - t0
+    tm = ev_time(lambda: old.misplaced(new, o2n, keys, n), reps=2)
+    lists, count, mask, target = old.misplaced(new, o2n, keys, n)
+    torch.cuda.synchronize()
+    out["C5"] = {"ring_old": N5, "ring_new": new.n, "keys": q5, "n": n,
+                 "nsucc_s": tl, "nsucc_keys_per_s": q5 / tl,
+                 "churn_s_wall": tc,
+                 "misplaced_s": tm, "misplaced_keys_per_s": q5 / tm,
+                 "misplaced_algo_GBps": q5 * 139 / tm / 1e9,
+                 "keys_with_misplaced_holder": int((mask != 0).sum()),
+                 "misplaced_pairs": int(sum(int(((mask.to(torch.int32) >> j) & 1).sum())
+                                            for j in range(n)))}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

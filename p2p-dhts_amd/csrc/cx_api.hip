@@ -67,6 +67,7 @@ struct cx_ring {
     RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
+    bool rt_valid = false;         // d_rt matches the current converged fingers
     uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variant 2)
     int pk_ib = 1;                 // index bits of a packed finger
     int route_variant = 3;         // 0: finger+ring gathers, 1: route table, 2: packed table, 3: 2 + staging
@@ -366,36 +367,26 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     }
     CX_HIP(cxk::fingers_build(ring->sv(), ring->d_ring, ring->d_fingers, s));
     ring->fingers_converged = true;
-    // route table: levels [l0, 128) with l0 = 128 - R, R = ceil(log2 n) + 8
-    // rounded up to 8 (levels below it are almost always "next peer")
-    if (!ring->d_rt) {
+    // route-table levels [l0, 128): l0 = 128 - R, R = ceil(log2 n) + 8 rounded up
+    // to 8 (levels below are almost always "next peer")
+    {
         int lg = 0;
         while (((size_t)1 << lg) < ring->n) ++lg;
         int R = ((lg + 8 + 7) / 8) * 8;
         if (R < 16) R = 16;
         if (R > 128) R = 128;
-        const size_t bytes = ring->n * (size_t)R * sizeof(RtEntry);
-        if (hipMalloc(&ring->d_rt, bytes) != hipSuccess) {
-            ring->d_rt = nullptr;  // not enough HBM: route falls back to variant 0
-        } else if (hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess) {
-            (void)hipFree(ring->d_rt);
-            ring->d_rt = nullptr;
-            ring->d_ring_ext = nullptr;
-        } else {
-            ring->rt_R = R;
-            ring->rt_l0 = 128 - R;
-        }
+        ring->rt_R = R;
+        ring->rt_l0 = 128 - R;
+        ring->pk_ib = lg < 1 ? 1 : lg;
     }
-    if (ring->d_rt)
-        CX_HIP(cxk::rt_build(ring->d_fingers, ring->d_ring, ring->n, ring->rt_l0, ring->rt_R,
-                             ring->d_rt, ring->d_ring_ext, s));
-    if (ring->d_rt && !ring->d_pk) {
-        int ib = 1;
-        while (((size_t)1 << ib) < ring->n) ++ib;
-        ring->pk_ib = ib;
-        if (hipMalloc(&ring->d_pk, ring->n * (size_t)ring->rt_R * 16) != hipSuccess)
-            ring->d_pk = nullptr;  // not enough HBM: variant 2 unavailable
-    }
+    ring->rt_valid = false;  // the 32-B table (variant 1) is rebuilt lazily
+    if (!ring->d_ring_ext &&
+        hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
+        ring->d_ring_ext = nullptr;
+    if (ring->d_ring_ext && !ring->d_pk &&
+        hipMalloc(&ring->d_pk, ring->n * (size_t)ring->rt_R * 16) != hipSuccess)
+        ring->d_pk = nullptr;  // not enough HBM: route falls back to variant 0
+    if (ring->d_ring_ext) CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
     if (ring->d_pk)
         CX_HIP(cxk::pk_build(ring->d_fingers, ring->d_ring, ring->n, ring->rt_l0, ring->rt_R,
                              ring->pk_ib, ring->d_pk, s));
@@ -488,6 +479,17 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
     if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
     if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
+    if (!ring->literal() && ring->route_variant == 1 && !ring->rt_valid) {
+        cx_ring *rw = const_cast<cx_ring *>(ring);  // lazily built A/B table
+        if (!rw->d_rt &&
+            hipMalloc(&rw->d_rt, rw->n * (size_t)rw->rt_R * sizeof(RtEntry)) != hipSuccess)
+            rw->d_rt = nullptr;
+        if (rw->d_rt) {
+            CX_HIP(cxk::rt_build(rw->d_fingers, rw->d_ring, rw->n, rw->rt_l0, rw->rt_R, rw->d_rt,
+                                 rw->d_ring_ext, s));
+            rw->rt_valid = true;
+        }
+    }
     if (!ring->literal() && ring->route_variant == 3 && ring->d_pk)
         CX_HIP(cxk::route_pk3(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
                               ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
@@ -496,7 +498,7 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
         CX_HIP(cxk::route_pk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
                              ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
-    else if (!ring->literal() && ring->route_variant == 1 && ring->d_rt)
+    else if (!ring->literal() && ring->route_variant == 1 && ring->rt_valid)
         CX_HIP(cxk::route_rt(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_rt, ring->rt_l0,
                              ring->rt_R, ring->d_fingers, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));

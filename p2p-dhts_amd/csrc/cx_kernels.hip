@@ -581,8 +581,10 @@ __global__ void k_ring_ext(const cell128 *ring, uint32_t n, cell128 *ext) {
 hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
                     cell128 *ring_ext, hipStream_t s) {
     k_rt_build<<<cx_grid(n * (size_t)R, 256), 256, 0, s>>>(F, ring, (uint32_t)n, l0, R, rt);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t ring_ext_build(const cell128 *ring, size_t n, cell128 *ring_ext, hipStream_t s) {
     k_ring_ext<<<cx_grid(n + 1, 256), 256, 0, s>>>(ring, (uint32_t)n, ring_ext);
     return hipGetLastError();
 }

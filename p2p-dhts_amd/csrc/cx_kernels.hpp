@@ -45,6 +45,7 @@ hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128
                  size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
                     cell128 *ring_ext, hipStream_t s);
+hipError_t ring_ext_build(const cell128 *ring, size_t n, cell128 *ring_ext, hipStream_t s);
 hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, const RtEntry *rt,
                     int l0, int R, const uint32_t *F, const uint32_t *src, const cell128 *keys,
                     size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
