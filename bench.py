@@ -180,7 +180,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
         F_host[:] = ring.fingers_device().cpu().numpy().view(np.uint32)
-        cs = min(Q, 1 << 21)
+        cs = Q  # the sample is sized by --cpu-seconds inside cpu_baseline
         cpu = cpu_baseline(ring, F_host, keys[:cs].cpu().numpy().view(np.uint64),
                            src[:cs].cpu().numpy().view(np.uint32),
                            owner[:cs].cpu().numpy().view(np.uint32),

@@ -1332,24 +1332,42 @@ hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128
 // ===========================================================================
 // a10/a11: n-successor windows.
 // ===========================================================================
+// Rows of `w` elements for keys [base, base + cnt) are staged in LDS by the
+// block and written as one contiguous, coalesced range.
+constexpr int ROW_BLOCK = 256;
+
+template <class T>
+__device__ __forceinline__ void flush_rows(const T *stage, T *out, size_t base, int cnt, int w) {
+    const int total = cnt * w;
+    T *dst = out + base * (size_t)w;
+    for (int t = threadIdx.x; t < total; t += blockDim.x) dst[t] = stage[t];
+}
+
 template <bool DIR>
-__global__ __launch_bounds__(SUCC_BLOCK) void k_nsucc(SearchView sv, const cell128 *keys, size_t q,
-                                                      int nlist, uint32_t *lists,
-                                                      uint8_t *count) {
+__global__ __launch_bounds__(ROW_BLOCK) void k_nsucc(SearchView sv, const cell128 *keys, size_t q,
+                                                     int nlist, uint32_t *lists, uint8_t *count) {
     __shared__ u128 lds[Searcher<DIR>::LDS];
+    __shared__ uint32_t stage[ROW_BLOCK * CX_MAX_NSUCC];
     Searcher<DIR>::stage(sv, lds);
     const uint32_t n = sv.ev.n;
     const int nn = (uint32_t)nlist < n ? nlist : (int)n;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t s0 = Searcher<DIR>::find(sv, lds, ld128(keys + i));
-        uint32_t *l = lists + i * (size_t)nlist;
-        for (int j = 0; j < nlist; ++j) {
-            uint32_t v = s0 + (uint32_t)j;
-            if (v >= n) v -= n;
-            l[j] = j < nn ? v : CX_NONE;
+    for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q;
+         base += (size_t)gridDim.x * ROW_BLOCK) {
+        const size_t i = base + threadIdx.x;
+        const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
+        if (i < q) {
+            const uint32_t s0 = Searcher<DIR>::find(sv, lds, ld128(keys + i));
+            uint32_t *l = stage + threadIdx.x * nlist;
+            for (int j = 0; j < nlist; ++j) {
+                uint32_t v = s0 + (uint32_t)j;
+                if (v >= n) v -= n;
+                l[j] = j < nn ? v : CX_NONE;
+            }
+            count[i] = (uint8_t)nn;
         }
-        count[i] = (uint8_t)nn;
+        __syncthreads();
+        flush_rows(stage, lists, base, cnt, nlist);
+        __syncthreads();
     }
 }
 
@@ -1357,11 +1375,11 @@ hipError_t nsucc(const SearchView &sv, const cell128 *keys, size_t q, int n, uin
                  uint8_t *count, hipStream_t s) {
     if (q == 0) return hipSuccess;
     if (sv.dir)
-        k_nsucc<true><<<cx_grid(q, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, keys, q, n, lists,
-                                                                          count);
+        k_nsucc<true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(sv, keys, q, n, lists,
+                                                                        count);
     else
-        k_nsucc<false><<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, keys, q, n, lists,
-                                                                          count);
+        k_nsucc<false><<<cx_grid(q, ROW_BLOCK, 512), ROW_BLOCK, 0, s>>>(sv, keys, q, n, lists,
+                                                                        count);
     return hipGetLastError();
 }
 
@@ -1410,18 +1428,21 @@ hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 
     return hipGetLastError();
 }
 
-// Misplaced scan core.  Holder ranks j in order; `has` = 16-bit mask of new-list
-// ranks already holding the key; membership of a holder in the new window is
-// (holder - s_new) mod n_new < nn.
+// Misplaced scan core.  Holder ranks j in order; `has` = mask of new-list ranks
+// already holding the key; membership of a holder in the new window is
+// (holder - s_new) mod n_new < nn.  Rows (new list, targets) are staged in LDS
+// per block of 256 consecutive keys and written coalesced.
 template <bool CHURN, bool DIR>
-__global__ __launch_bounds__(512) void k_misplaced(SearchView sv_new, SearchView sv_old,
-                                                   const uint32_t *old_to_new,
-                                                   const uint32_t *holders, int nh,
-                                                   const cell128 *keys, size_t q, int nlist,
-                                                   uint32_t *new_lists, uint8_t *count,
-                                                   uint16_t *mask, uint8_t *target) {
+__global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, SearchView sv_old,
+                                                         const uint32_t *old_to_new,
+                                                         const uint32_t *holders, int nh,
+                                                         const cell128 *keys, size_t q, int nlist,
+                                                         uint32_t *new_lists, uint8_t *count,
+                                                         uint16_t *mask, uint8_t *target) {
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
+    __shared__ uint32_t stage_l[ROW_BLOCK * CX_MAX_NSUCC];
+    __shared__ uint8_t stage_t[ROW_BLOCK * CX_MAX_NSUCC];
     Searcher<DIR>::stage(sv_new, lds_new);
     if (CHURN) Searcher<DIR>::stage(sv_old, lds_old);
     const uint32_t n_new = sv_new.ev.n;
@@ -1429,49 +1450,56 @@ __global__ __launch_bounds__(512) void k_misplaced(SearchView sv_new, SearchView
     const uint32_t n_old = CHURN ? sv_old.ev.n : 0;
     const int no = CHURN ? ((uint32_t)nlist < n_old ? nlist : (int)n_old) : nh;
     const int nslots = CHURN ? nlist : nh;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const u128 key = ld128(keys + i);
-        const uint32_t sn = Searcher<DIR>::find(sv_new, lds_new, key);
-        uint32_t so = 0;
-        if (CHURN) so = Searcher<DIR>::find(sv_old, lds_old, key);
-        uint32_t *l = new_lists + i * (size_t)nlist;
-        for (int j = 0; j < nlist; ++j) {
-            uint32_t v = sn + (uint32_t)j;
-            if (v >= n_new) v -= n_new;
-            l[j] = j < nn ? v : CX_NONE;
-        }
-        count[i] = (uint8_t)nn;
-        // pass 1: which new-list ranks already hold the key
-        uint32_t has = 0;
-        for (int j = 0; j < no; ++j) {
-            uint32_t hj;
-            if (CHURN) {
-                uint32_t o = so + (uint32_t)j;
-                if (o >= n_old) o -= n_old;
-                hj = old_to_new[o];
-            } else {
-                hj = holders[i * (size_t)nh + j];
+    const uint32_t full = (nn >= 32) ? 0xFFFFFFFFu : ((1u << nn) - 1u);
+    for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q;
+         base += (size_t)gridDim.x * ROW_BLOCK) {
+        const size_t i = base + threadIdx.x;
+        const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
+        if (i < q) {
+            const u128 key = ld128(keys + i);
+            const uint32_t sn = Searcher<DIR>::find(sv_new, lds_new, key);
+            uint32_t so = 0;
+            if (CHURN) so = Searcher<DIR>::find(sv_old, lds_old, key);
+            uint32_t *l = stage_l + threadIdx.x * nlist;
+            for (int j = 0; j < nlist; ++j) {
+                uint32_t v = sn + (uint32_t)j;
+                if (v >= n_new) v -= n_new;
+                l[j] = j < nn ? v : CX_NONE;
             }
-            if (hj >= n_new) continue;  // CX_NONE (empty / departed) or invalid
-            uint32_t r = hj >= sn ? hj - sn : hj + n_new - sn;
-            if (r < (uint32_t)nn) has |= 1u << r;
-        }
-        // pass 2: misplaced holders in rank order take the first lacking rank
-        uint32_t m = 0;
-        const uint32_t full = (nn >= 32) ? 0xFFFFFFFFu : ((1u << nn) - 1u);
-        uint8_t *tg = target + i * (size_t)nslots;
-        for (int j = 0; j < nslots; ++j) {
-            uint8_t t = 0xFF;
-            if (j < no) {
-                uint32_t hj;
-                if (CHURN) {
-                    uint32_t o = so + (uint32_t)j;
-                    if (o >= n_old) o -= n_old;
-                    hj = old_to_new[o];
-                } else {
-                    hj = holders[i * (size_t)nh + j];
+            count[i] = (uint8_t)nn;
+            // holders: old n-window mapped to the new ring, or the caller's list
+            uint32_t hv[CX_MAX_NSUCC];
+#pragma unroll
+            for (int j = 0; j < CX_MAX_NSUCC; ++j) {
+                uint32_t hj = CX_NONE;
+                if (j < no) {
+                    if (CHURN) {
+                        uint32_t o = so + (uint32_t)j;
+                        if (o >= n_old) o -= n_old;
+                        hj = old_to_new[o];
+                    } else {
+                        hj = holders[i * (size_t)nh + j];
+                    }
                 }
+                hv[j] = hj;
+            }
+            // pass 1: which new-list ranks already hold the key
+            uint32_t has = 0;
+#pragma unroll
+            for (int j = 0; j < CX_MAX_NSUCC; ++j) {
+                const uint32_t hj = hv[j];
+                if (hj >= n_new) continue;  // CX_NONE (empty / departed) or invalid
+                const uint32_t r = hj >= sn ? hj - sn : hj + n_new - sn;
+                if (r < (uint32_t)nn) has |= 1u << r;
+            }
+            // pass 2: misplaced holders in rank order take the first lacking rank
+            uint32_t m = 0;
+            uint8_t *tg = stage_t + threadIdx.x * nslots;
+#pragma unroll
+            for (int j = 0; j < CX_MAX_NSUCC; ++j) {
+                if (j >= nslots) break;
+                uint8_t t = 0xFF;
+                const uint32_t hj = hv[j];
                 if (hj < n_new) {
                     const uint32_t r = hj >= sn ? hj - sn : hj + n_new - sn;
                     if (r >= (uint32_t)nn) {
@@ -1484,10 +1512,14 @@ __global__ __launch_bounds__(512) void k_misplaced(SearchView sv_new, SearchView
                         }
                     }
                 }
+                tg[j] = t;
             }
-            tg[j] = t;
+            mask[i] = (uint16_t)m;
         }
-        mask[i] = (uint16_t)m;
+        __syncthreads();
+        flush_rows(stage_l, new_lists, base, cnt, nlist);
+        flush_rows(stage_t, target, base, cnt, nslots);
+        __syncthreads();
     }
 }
 
@@ -1497,10 +1529,10 @@ hipError_t misplaced_churn(const SearchView &sv_old, const SearchView &sv_new,
                            hipStream_t s) {
     if (q == 0) return hipSuccess;
     if (sv_new.dir && sv_old.dir)
-        k_misplaced<true, true><<<cx_grid(q, 512, 4096), 512, 0, s>>>(
+        k_misplaced<true, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
             sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target);
     else
-        k_misplaced<true, false><<<cx_grid(q, 512, 256), 512, 0, s>>>(
+        k_misplaced<true, false><<<cx_grid(q, ROW_BLOCK, 256), ROW_BLOCK, 0, s>>>(
             sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target);
     return hipGetLastError();
 }
@@ -1510,10 +1542,10 @@ hipError_t misplaced_holders(const SearchView &sv, const uint32_t *holders, int 
                              uint8_t *count, uint16_t *mask, uint8_t *target, hipStream_t s) {
     if (q == 0) return hipSuccess;
     if (sv.dir)
-        k_misplaced<false, true><<<cx_grid(q, 512, 4096), 512, 0, s>>>(
+        k_misplaced<false, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
             sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target);
     else
-        k_misplaced<false, false><<<cx_grid(q, 512, 512), 512, 0, s>>>(
+        k_misplaced<false, false><<<cx_grid(q, ROW_BLOCK, 512), ROW_BLOCK, 0, s>>>(
             sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target);
     return hipGetLastError();
 }
