@@ -165,7 +165,7 @@ def main():
     ring.set_search_variant(1)
     # A/B: the other route kernels on the same batch (bit-identical results)
     variant_ms = {}
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2, 3, 4):
         ring.set_route_variant(v)
         ring.route(src, keys, out=out)
         e0.record(stream)
@@ -174,7 +174,7 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize(dev)
         variant_ms[v] = e0.elapsed_time(e1) / 3
-    ring.set_route_variant(3)
+    ring.set_route_variant(4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -191,7 +191,7 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == "k_route_pk3":
+        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == "k_route_tree":
             traffic = tj.get("hbm_bytes_per_launch")
 
     if rank == 0:
@@ -217,7 +217,7 @@ def main():
                        "parallelism": f"replicated ring, keys sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "kernel": "k_route_pk3", "kernel_ms": kern_ms,
+                         "kernel": "k_route_tree", "kernel_ms": kern_ms,
                          "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             "mean_hops": sum_hops / Q,

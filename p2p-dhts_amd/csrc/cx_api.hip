@@ -68,9 +68,13 @@ struct cx_ring {
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
     bool rt_valid = false;         // d_rt matches the current converged fingers
-    uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variant 2)
+    uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variants 2, 3)
+    bool pk_valid = false;
+    uint64_t *d_tree = nullptr;    // lookahead-tree table [n][rt_R][8] (variant 4)
+    bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
-    int route_variant = 3;         // 0: finger+ring gathers, 1: route table, 2: packed table, 3: 2 + staging
+    int route_variant = 4;         // 0: finger+ring gathers, 1: route table, 2: packed table,
+                                   // 3: 2 + staging, 4: lookahead-tree table (default)
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
@@ -185,6 +189,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_fingers);
     (void)hipFree(r->d_rt);
     (void)hipFree(r->d_pk);
+    (void)hipFree(r->d_tree);
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
@@ -212,6 +217,33 @@ int build_search(cx_ring *r, hipStream_t s) {
     CX_HIP(hipStreamSynchronize(s));
     r->d_dir = dir.as<uint4>();
     dir.release();
+    return CX_OK;
+}
+
+// Builds (once per finger build) the table the selected route variant reads.
+// Without HBM for it the route falls back to variant 0 (finger + ring gathers).
+int ensure_route_table(cx_ring *r, hipStream_t s) {
+    if (!r->fingers_converged || !r->d_ring_ext) return CX_OK;
+    const size_t ent = r->n * (size_t)r->rt_R;
+    if (r->route_variant == 1 && !r->rt_valid) {
+        if (!r->d_rt && hipMalloc(&r->d_rt, ent * sizeof(RtEntry)) != hipSuccess) r->d_rt = nullptr;
+        if (r->d_rt) {
+            CX_HIP(cxk::rt_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->d_rt, r->d_ring_ext, s));
+            r->rt_valid = true;
+        }
+    } else if ((r->route_variant == 2 || r->route_variant == 3) && !r->pk_valid) {
+        if (!r->d_pk && hipMalloc(&r->d_pk, ent * 16) != hipSuccess) r->d_pk = nullptr;
+        if (r->d_pk) {
+            CX_HIP(cxk::pk_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_pk, s));
+            r->pk_valid = true;
+        }
+    } else if (r->route_variant == 4 && !r->tree_valid) {
+        if (!r->d_tree && hipMalloc(&r->d_tree, ent * 64) != hipSuccess) r->d_tree = nullptr;
+        if (r->d_tree) {
+            CX_HIP(cxk::tree_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_tree, s));
+            r->tree_valid = true;
+        }
+    }
     return CX_OK;
 }
 
@@ -379,17 +411,13 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
         ring->rt_l0 = 128 - R;
         ring->pk_ib = lg < 1 ? 1 : lg;
     }
-    ring->rt_valid = false;  // the 32-B table (variant 1) is rebuilt lazily
+    ring->rt_valid = ring->pk_valid = ring->tree_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
-    if (ring->d_ring_ext && !ring->d_pk &&
-        hipMalloc(&ring->d_pk, ring->n * (size_t)ring->rt_R * 16) != hipSuccess)
-        ring->d_pk = nullptr;  // not enough HBM: route falls back to variant 0
     if (ring->d_ring_ext) CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
-    if (ring->d_pk)
-        CX_HIP(cxk::pk_build(ring->d_fingers, ring->d_ring, ring->n, ring->rt_l0, ring->rt_R,
-                             ring->pk_ib, ring->d_pk, s));
+    // the default route kernel's table is built now (outside any timed query)
+    if (int rc2 = ensure_route_table(ring, s)) return rc2;
     if (fingers_out) {
         const hipMemcpyKind kind =
             memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -421,6 +449,7 @@ int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
     CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
     ring->fingers_converged = false;
+    ring->rt_valid = ring->pk_valid = ring->tree_valid = false;
     CX_CHECK(!bad, CX_E_INVALID, "finger entry is not a ring index");
     return CX_OK;
 }
@@ -479,26 +508,24 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
     if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
     if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
-    if (!ring->literal() && ring->route_variant == 1 && !ring->rt_valid) {
-        cx_ring *rw = const_cast<cx_ring *>(ring);  // lazily built A/B table
-        if (!rw->d_rt &&
-            hipMalloc(&rw->d_rt, rw->n * (size_t)rw->rt_R * sizeof(RtEntry)) != hipSuccess)
-            rw->d_rt = nullptr;
-        if (rw->d_rt) {
-            CX_HIP(cxk::rt_build(rw->d_fingers, rw->d_ring, rw->n, rw->rt_l0, rw->rt_R, rw->d_rt,
-                                 rw->d_ring_ext, s));
-            rw->rt_valid = true;
-        }
+    if (!ring->literal()) {
+        int e2 = ensure_route_table(const_cast<cx_ring *>(ring), s);
+        if (e2) return e2;
     }
-    if (!ring->literal() && ring->route_variant == 3 && ring->d_pk)
+    const int v = ring->literal() ? -1 : ring->route_variant;
+    if (v == 4 && ring->tree_valid)
+        CX_HIP(cxk::route_tree(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_tree, ring->rt_l0,
+                               ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
+                               reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
+    else if (v == 3 && ring->pk_valid)
         CX_HIP(cxk::route_pk3(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
                               ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
                               reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
-    else if (!ring->literal() && ring->route_variant == 2 && ring->d_pk)
+    else if (v == 2 && ring->pk_valid)
         CX_HIP(cxk::route_pk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
                              ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
-    else if (!ring->literal() && ring->route_variant == 1 && ring->rt_valid)
+    else if (v == 1 && ring->rt_valid)
         CX_HIP(cxk::route_rt(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_rt, ring->rt_l0,
                              ring->rt_R, ring->d_fingers, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
@@ -759,10 +786,10 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
 // ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
 // and parity tests.  0 = finger + ring gathers per hop, 1 = route table,
 // 2 = packed route table with one-level lookahead, 3 = 2 + staged results and
-// prefetched source pairs.
+// prefetched source pairs, 4 = lookahead-tree table (default).
 int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0..3");
+    CX_CHECK(variant >= 0 && variant <= 4, CX_E_INVALID, "variant must be 0..4");
     ring->route_variant = variant;
     return CX_OK;
 }

@@ -59,6 +59,12 @@ hipError_t route_pk3(const cell128 *ring_ext, const cell128 *ring, size_t n, con
                      int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
                      const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
                      uint8_t *status, hipStream_t s);
+hipError_t tree_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
+                      uint64_t *tree, hipStream_t s);
+hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
+                      const uint64_t *tree, int l0, int R, int ib, const uint32_t *F,
+                      const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
+                      uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t nsucc(const SearchView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const SearchView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,

@@ -78,6 +78,41 @@ __global__ __launch_bounds__(256) void k_chase(const uint4 *t, uint64_t slots, i
     if (r == 0x1234567) sink[0] = r;
 }
 
+// G lanes cooperate on one chain: each loads 16 B of a G*16-byte slot (one
+// wave instruction, adjacent addresses), lane 0's data picks the next slot.
+template <int G>
+__global__ __launch_bounds__(256) void k_chase_coop(const uint4 *t, uint64_t slots, int hops,
+                                                    uint64_t *sink) {
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const int sub = threadIdx.x & (G - 1);
+    uint64_t x = mix(tid / G + 777);
+    for (int h = 0; h < hops; ++h) {
+        const uint64_t slot = x % slots;
+        const uint4 a = t[slot * G + sub];
+        uint64_t v = ((uint64_t)a.y << 32 | a.x) ^ a.z;
+        v = __shfl(v, (threadIdx.x & 63) & ~(G - 1), 64);  // lane 0 of the group
+        x = mix(v + x);
+    }
+    if (x == 0x1234567) sink[0] = x;
+}
+
+template <int G>
+double run_coop(const uint4 *t, size_t bytes, int lanes, int hops, uint64_t *sink) {
+    const uint64_t slots = bytes / (16 * G);
+    const int blocks = lanes / 256;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    k_chase_coop<G><<<blocks, 256>>>(t, slots, 4, sink);
+    CK(hipEventRecord(a));
+    k_chase_coop<G><<<blocks, 256>>>(t, slots, hops, sink);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return (double)(lanes / G) * hops / (ms * 1e-3);  // chain steps (entries) per second
+}
+
 template <int WIDTH, int CHAINS>
 double run(const uint4 *t, size_t bytes, int lanes, int hops, uint64_t *sink) {
     const uint64_t slots = WIDTH == 4 ? bytes / 64 : (WIDTH >= 2 ? bytes / 32 : bytes / 16);
@@ -128,6 +163,13 @@ int main(int argc, char **argv) {
     row("64B", 1, 1024ull << 20, full, run<4, 1>(t, 1024ull << 20, full, 64, sink));
     row("16B", 1, 2ull << 20, full, run<1, 1>(t, 2ull << 20, full, 64, sink));
     row("16B", 1, 32ull << 20, full, run<1, 1>(t, 32ull << 20, full, 64, sink));
+    // cooperative wide entries: G lanes x 16 B = one entry
+    row("32B/2lanes", 1, big, full, run_coop<2>(t, big, full, 64, sink));
+    row("64B/4lanes", 1, big, full, run_coop<4>(t, big, full, 64, sink));
+    row("128B/8lanes", 1, big, full, run_coop<8>(t, big, full, 64, sink));
+    row("16B/1lane", 1, big, full, run_coop<1>(t, big, full, 64, sink));
+    row("32B/2lanes", 1, 8192ull << 20, full, run_coop<2>(t, 8192ull << 20, full, 64, sink));
+    row("64B/4lanes", 1, 8192ull << 20, full, run_coop<4>(t, 8192ull << 20, full, 64, sink));
     // lanes in flight
     for (int lanes : {full / 8, full / 4, full / 2}) row("16B", 1, big, lanes, run<1, 1>(t, big, lanes, 64, sink));
     // chains per lane (more MLP per lane)

@@ -41,6 +41,8 @@ def test_c3_routed_lookups(O, c3):
     o1, h1, s1 = ring.route(src, keys)
     ring.set_route_variant(0)
     o0, h0, s0 = ring.route(src, keys)
+    ring.set_route_variant(4)
+    o4, h4, s4 = ring.route(src, keys)
     ring.set_route_variant(3)
     o3, h3, s3 = ring.route(src, keys)
     ring.set_route_variant(2)
@@ -51,6 +53,7 @@ def test_c3_routed_lookups(O, c3):
     assert bool((o1 == succ).all()) and bool((o0 == o1).all()) and bool((h0 == h1).all())
     assert bool((o2 == o1).all()) and bool((h2 == h1).all())
     assert bool((o3 == o1).all()) and bool((h3 == h1).all()) and int((s3 != 0).sum()) == 0
+    assert bool((o4 == o1).all()) and bool((h4 == h1).all()) and int((s4 != 0).sum()) == 0
     mean = float(h1.double().mean())
     assert 9.0 < mean < 11.0  # ~log2(N)/2 for uniform rings
     # oracle literal walk on a sample, with the oracle's own finger table

@@ -101,7 +101,7 @@ def test_fingers_c2_ring(cx, O):
 
 
 # ---------------------------------------------------------------- a7-a9 route
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_route_c1_golden(cx, O, c1truth, variant):
     """Config C1 ground truth (8 peers, key0..key999 from every peer)."""
     ids = O.keys_from_ints([O.uuid5_key(p) for p in c1truth["peers"]])
@@ -117,7 +117,7 @@ def test_route_c1_golden(cx, O, c1truth, variant):
     assert (status == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("n", [1, 2, 3, 9, 1000, 20000])
 def test_route_converged(cx, O, n, variant):
     ids = edge_ring(O, n, 900 + n)
@@ -201,7 +201,7 @@ def test_successor_clustered_rings(cx, O, search, spread):
     assert (lists == wl).all() and (count == wc).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("spread", [8, 40, 90, 100])
 def test_route_clustered_rings(cx, O, variant, spread):
     ids = clustered_ring(O, 3000, spread, spread)
@@ -249,7 +249,7 @@ def test_route_literal_random_edits(cx, O):
     assert (status == 1).any()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_route_bad_src_is_flagged(cx, O, variant):
     ring = cx.Ring(O.splitmix_keys(3, 50))
     ring.build_fingers()
