@@ -36,6 +36,10 @@ from chordx import dist  # noqa: E402
 SEED_RING = 0x5EED0005
 SEED_KEYS = 0x5EED0006
 HBM_PEAK = 8.0e12  # B/s per MI355X (MI355X_MICROARCH.md, HBM3E spec)
+# Measured random-gather ceiling for 64-B entries loaded by 4 cooperating lanes
+# on an 8-16 GiB table (p2p-dhts_amd/csrc/tools/gather_probe.hip,
+# profiles/r01/gather_probe.json): the bound the walk actually runs against.
+GATHER_CEILING = 46.0e9  # dependent random 64-B requests / s
 # Algorithmic bytes of one routed lookup: 25 B streamed
 # (16 key + 4 src + 4 owner + 1 hops) + 64 B source-peer record (first
 # StoredLocally) + 128 B per hop (finger granule + ring granule).
@@ -187,12 +191,19 @@ def main():
                            hops[:cs].cpu().numpy(), args.cpu_seconds)
         del F_host
 
-    traffic = None
+    traffic = gather = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == "k_route_tree":
             traffic = tj.get("hbm_bytes_per_launch")
+            req = tj["fetch_bytes"] / 64 / (kern_ms * 1e-3)
+            gather = {"requests_per_s": req, "ceiling": GATHER_CEILING,
+                      "frac": req / GATHER_CEILING,
+                      "traffic_frac_of_hbm": traffic / (kern_ms * 1e-3) / HBM_PEAK,
+                      "note": "PMC FETCH_SIZE / 64 B per launch (profiles/traffic_route.json) "
+                              "over this run's kernel time, vs the measured dependent "
+                              "random-gather ceiling"}
 
     if rank == 0:
         total = world * Q * args.steps
@@ -220,6 +231,7 @@ def main():
                          "kernel": "k_route_tree", "kernel_ms": kern_ms,
                          "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
+            "gather_roofline": gather,
             "mean_hops": sum_hops / Q,
             "bad_status": bad,
             "route_owner_equals_successor": owner_eq,
