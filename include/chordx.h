@@ -184,6 +184,45 @@ int cx_uuid5_dns(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx
 int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t offset,
                      int device, void *hip_stream);
 
+/* ---- arc-sharded routing (multi-GPU layout 2) -------------------
+ * Each rank keeps the replicated sorted ring but the lookahead-tree rows of its
+ * own arc of peers only, arc g of G = [g n / G, (g+1) n / G).  A lookup walks
+ * on the rank that owns the row it needs next, as the reference's
+ * GET_SUCC request travels to the peer it is forwarded to
+ * (ChordPeer::ForwardRequest, chord_peer.cpp:293-325): one bulk-synchronous
+ * step per exchange, in-flight lookups travel between ranks as 32-B records.
+ * Owners, hops and statuses equal cx_route's on the replicated ring.
+ * All arc buffers are device memory (CX_MEM_DEVICE). */
+typedef struct cx_arc_rec {
+    uint64_t w0, w1; /* key (lookups) / owner | status << 32 (results) */
+    uint64_t qid;    /* origin rank << 40 | index at the origin */
+    uint32_t cur;    /* peer the lookup continues at / owner (results) */
+    uint32_t hk;     /* hops | kind << 8 */
+} cx_arc_rec;
+enum { CX_ARC_NEW = 0, CX_ARC_RESULT = 1, CX_ARC_WALK = 2, CX_ARC_NONE = 3 };
+#define CX_ARC_MAX_RANKS 64
+
+/* Builds the tree rows of peers [lo, hi) by successor searches on the ring
+ * (no full finger table).  Replaces this rank's share of the finger tables
+ * (FingerTable::AdjustFingers, finger_table.h:143-160). */
+int cx_arc_build(cx_ring *ring, uint32_t lo, uint32_t hi);
+
+/* Records of q lookups issued at peers src[i] by rank `rank` (kind NEW). */
+int cx_arc_seed(const cx_ring *ring, int rank, const uint32_t *src, const cx_u128 *keys,
+                size_t q, cx_arc_rec *out);
+
+/* One step on rank `rank`: every input record yields exactly one output record:
+ * WALK (continue at the rank owning cur's row), RESULT (for a remote origin)
+ * or NONE (result written to owner/hops/status at qid's index: results for
+ * this rank's lookups, and RESULT records coming home). */
+int cx_arc_step(const cx_ring *ring, int rank, const cx_arc_rec *in, size_t q, cx_arc_rec *out,
+                uint32_t *owner, uint8_t *hops, uint8_t *status);
+
+/* Groups WALK/RESULT records by destination rank into `send` (NONE dropped);
+ * counts[world] (host) receives the per-destination record counts. */
+int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t q,
+                  cx_arc_rec *send, uint64_t *counts);
+
 #ifdef __cplusplus
 }
 #endif

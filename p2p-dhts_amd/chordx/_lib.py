@@ -40,7 +40,11 @@ EXPORTS = (
     "cx_peer_state_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
     "cx_uuid5_dns", "cx_fill_splitmix",
+    "cx_arc_build", "cx_arc_seed", "cx_arc_step", "cx_arc_bucket",
 )
+
+CX_ARC_NEW, CX_ARC_RESULT, CX_ARC_WALK, CX_ARC_NONE = 0, 1, 2, 3
+CX_ARC_MAX_RANKS = 64
 
 
 class ChordError(RuntimeError):
@@ -90,6 +94,10 @@ def lib() -> ctypes.CDLL:
         "cx_in_between": ([vp, vp, vp, sz, i, vp, i], i),
         "cx_uuid5_dns": ([vp, vp, sz, vp, i, i], i),
         "cx_fill_splitmix": ([vp, sz, u64, u64, i, vp], i),
+        "cx_arc_build": ([vp, ctypes.c_uint32, ctypes.c_uint32], i),
+        "cx_arc_seed": ([vp, i, vp, vp, sz, vp], i),
+        "cx_arc_step": ([vp, i, vp, sz, vp, vp, vp, vp], i),
+        "cx_arc_bucket": ([vp, i, vp, sz, vp, vp], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -254,6 +254,45 @@ class Ring:
                                              _ptr(target), mk))
         return lists, count, mask, target
 
+    # ---- arc-sharded routing (chordx.arc drives the exchange) -------------
+    def arc_build(self, lo: int, hi: int):
+        """Tree rows of peers [lo, hi) (this rank's arc), cx_arc_build."""
+        L.check(L.lib().cx_arc_build(self._h, lo, hi))
+
+    def _arc_stream(self):
+        L.check(L.lib().cx_ring_set_stream(
+            self._h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+
+    def arc_seed(self, rank: int, src, keys):
+        """(q, 4) int64 device tensor of NEW records (32 B each)."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src)
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        out = torch.empty((q, 4), dtype=torch.int64, device=keys.device)
+        self._arc_stream()
+        L.check(L.lib().cx_arc_seed(self._h, rank, _ptr(src), _ptr(keys), q, _ptr(out)))
+        return out
+
+    def arc_step(self, rank: int, recs, owner, hops, status=None):
+        """One walk step over `recs`; returns the outcome records (same count)."""
+        q = recs.shape[0]
+        out = torch.empty_like(recs)
+        self._arc_stream()
+        L.check(L.lib().cx_arc_step(self._h, rank, _ptr(recs), q, _ptr(out), _ptr(owner),
+                                    _ptr(hops), _ptr(status)))
+        return out
+
+    def arc_bucket(self, world: int, recs):
+        """(send, counts): records grouped by destination rank, NONE dropped."""
+        q = recs.shape[0]
+        send = torch.empty_like(recs)
+        counts = np.zeros(world, dtype=np.uint64)
+        self._arc_stream()
+        L.check(L.lib().cx_arc_bucket(self._h, world, _ptr(recs), q, _ptr(send), _ptr(counts)))
+        return send[: int(counts.sum())], [int(c) for c in counts]
+
 
 def in_between(v, lb, ub, inclusive: bool = True) -> np.ndarray:
     """Batched ChordKey::InBetween on raw uint256 operands ((q, 4) uint64 each)."""

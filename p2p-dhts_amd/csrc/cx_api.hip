@@ -77,7 +77,9 @@ struct cx_ring {
                                    // 3: 2 + staging, 4: lookahead-tree table (default)
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
-    uint32_t *d_scratch = nullptr; // small device scratch (counts/flags)
+    uint32_t *d_scratch = nullptr; // small device scratch (counts/flags), 1 KiB
+    uint64_t *d_arc_tree = nullptr;   // tree rows of the arc [arc_lo, arc_hi) (arc mode)
+    uint32_t arc_lo = 0, arc_hi = 0;
 
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
     int dir_k = 1;
@@ -169,7 +171,7 @@ int alloc_ring(int device, cx_ring **out) {
         return fail(CX_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
     r->stream = r->own_stream;
-    e = hipMalloc(&r->d_scratch, 64);
+    e = hipMalloc(&r->d_scratch, 1024);
     if (e != hipSuccess) {
         (void)hipStreamDestroy(r->own_stream);
         delete r;
@@ -194,6 +196,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
     (void)hipFree(r->d_scratch);
+    (void)hipFree(r->d_arc_tree);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
     delete r;
 }
@@ -218,6 +221,20 @@ int build_search(cx_ring *r, hipStream_t s) {
     r->d_dir = dir.as<uint4>();
     dir.release();
     return CX_OK;
+}
+
+// Route-table levels [l0, 128): l0 = 128 - R, R = ceil(log2 n) + 8 rounded up
+// to 8 (levels below are almost always "next peer"); ib = index bits of a
+// packed finger.
+void route_geometry(cx_ring *r) {
+    int lg = 0;
+    while (((size_t)1 << lg) < r->n) ++lg;
+    int R = ((lg + 8 + 7) / 8) * 8;
+    if (R < 16) R = 16;
+    if (R > 128) R = 128;
+    r->rt_R = R;
+    r->rt_l0 = 128 - R;
+    r->pk_ib = lg < 1 ? 1 : lg;
 }
 
 // Builds (once per finger build) the table the selected route variant reads.
@@ -399,18 +416,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     }
     CX_HIP(cxk::fingers_build(ring->sv(), ring->d_ring, ring->d_fingers, s));
     ring->fingers_converged = true;
-    // route-table levels [l0, 128): l0 = 128 - R, R = ceil(log2 n) + 8 rounded up
-    // to 8 (levels below are almost always "next peer")
-    {
-        int lg = 0;
-        while (((size_t)1 << lg) < ring->n) ++lg;
-        int R = ((lg + 8 + 7) / 8) * 8;
-        if (R < 16) R = 16;
-        if (R > 128) R = 128;
-        ring->rt_R = R;
-        ring->rt_l0 = 128 - R;
-        ring->pk_ib = lg < 1 ? 1 : lg;
-    }
+    route_geometry(ring);
     ring->rt_valid = ring->pk_valid = ring->tree_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
@@ -780,6 +786,101 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
     CX_HIP(hipSetDevice(device));
     CX_HIP(cxk::fill_splitmix(reinterpret_cast<cell128 *>(out_device), count, seed, offset,
                               static_cast<hipStream_t>(hip_stream)));
+    return CX_OK;
+}
+
+// ---- arc-sharded routing --------------------------------------------------
+int cx_arc_build(cx_ring *ring, uint32_t lo, uint32_t hi) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(lo <= hi && hi <= ring->n, CX_E_INVALID, "arc must satisfy lo <= hi <= n");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    route_geometry(ring);
+    if (!ring->d_ring_ext) {
+        CX_HIP(hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)));
+        CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
+    }
+    (void)hipFree(ring->d_arc_tree);
+    ring->d_arc_tree = nullptr;
+    ring->arc_lo = ring->arc_hi = 0;
+    const size_t rows = (size_t)(hi - lo) * ring->rt_R;
+    if (rows) {
+        if (hipMalloc(&ring->d_arc_tree, rows * 64) != hipSuccess) {
+            ring->d_arc_tree = nullptr;
+            return fail(CX_E_NOMEM, "hipMalloc of the arc tree rows failed");
+        }
+    }
+    SearchView v = ring->sv();
+    v.dir = ring->d_dir;  // the arc build and walk always search the directory
+    CX_HIP(cxk::tree_build_arc(v, ring->d_ring, ring->n, lo, hi, ring->rt_l0, ring->rt_R,
+                               ring->pk_ib, ring->d_arc_tree, s));
+    ring->arc_lo = lo;
+    ring->arc_hi = hi;
+    CX_HIP(hipStreamSynchronize(s));
+    return CX_OK;
+}
+
+int cx_arc_seed(const cx_ring *ring, int rank, const uint32_t *src, const cx_u128 *keys,
+                size_t q, cx_arc_rec *out) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(rank >= 0 && rank < CX_ARC_MAX_RANKS, CX_E_INVALID, "rank out of range");
+    CX_CHECK(q < (1ull << ARC_ORIGIN_SHIFT), CX_E_INVALID, "too many lookups for one rank");
+    CX_CHECK(q == 0 || (src && keys && out), CX_E_INVALID, "null buffer");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    CX_HIP(cxk::arc_seed(src, reinterpret_cast<const cell128 *>(keys), q, rank,
+                         reinterpret_cast<ArcRec *>(out), ring->stream));
+    return CX_OK;
+}
+
+int cx_arc_step(const cx_ring *ring, int rank, const cx_arc_rec *in, size_t q, cx_arc_rec *out,
+                uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ring->d_ring_ext && (ring->d_arc_tree || ring->arc_lo == ring->arc_hi), CX_E_STATE,
+             "arc not built (cx_arc_build)");
+    CX_CHECK(rank >= 0 && rank < CX_ARC_MAX_RANKS, CX_E_INVALID, "rank out of range");
+    CX_CHECK(q == 0 || (in && out && owner && hops), CX_E_INVALID, "null buffer");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    SearchView v = ring->sv();
+    v.dir = ring->d_dir;
+    CX_HIP(cxk::route_arc(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree, ring->rt_l0,
+                          ring->rt_R, ring->pk_ib, v, ring->arc_lo, ring->arc_hi, rank,
+                          reinterpret_cast<const ArcRec *>(in), q,
+                          reinterpret_cast<ArcRec *>(out), owner, hops, status, ring->stream));
+    return CX_OK;
+}
+
+int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t q,
+                  cx_arc_rec *send, uint64_t *counts) {
+    CX_CHECK(ring && counts, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(q == 0 || (recs && send), CX_E_INVALID, "null buffer");
+    CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many records for one step");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    uint32_t *dcnt = ring->d_scratch, *dcur = ring->d_scratch + CX_ARC_MAX_RANKS;
+    CX_HIP(hipMemsetAsync(dcnt, 0, CX_ARC_MAX_RANKS * sizeof(uint32_t), s));
+    CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->n, world, dcnt,
+                           nullptr, nullptr, s, false));
+    uint32_t hc[CX_ARC_MAX_RANKS], hcur[CX_ARC_MAX_RANKS];
+    CX_HIP(hipMemcpyAsync(hc, dcnt, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    uint32_t acc = 0;
+    for (int g = 0; g < world; ++g) {
+        hcur[g] = acc;
+        acc += hc[g];
+        counts[g] = hc[g];
+    }
+    if (acc) {
+        CX_HIP(hipMemcpyAsync(dcur, hcur, world * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->n, world,
+                               nullptr, dcur, reinterpret_cast<ArcRec *>(send), s, true));
+        // hcur is a stack buffer: the copy must complete before we return
+        CX_HIP(hipStreamSynchronize(s));
+    }
     return CX_OK;
 }
 

@@ -1055,7 +1055,20 @@ struct PkCtx {
     int l0, ib, S;
     uint64_t imask;
     u128 W;
+    // arc mode: only rows [lo, hi) are local; F is absent (fingers by search)
+    bool arc;
+    uint32_t lo, hi;
+    SearchView sv;
 };
+
+// finger(p, i) = succ(id_p + 2^i) on the converged ring (k_fingers' rule).
+__device__ __forceinline__ uint32_t finger_of(const SearchView &sv, const cell128 *ring, uint32_t n,
+                                              uint32_t p, int i, u128 idp) {
+    if (n == 1) return 0;
+    const uint32_t nx = (p + 1 == n) ? 0u : p + 1;
+    const u128 step = (u128)1 << i;
+    return (step <= ld128(ring + nx) - idp) ? nx : dir_successor(sv, idp + step);
+}
 
 // Plan the next step from cur (free hops and below-table hops run inline).
 // Returns: 0 = needs a load (mode set), 1 = finished (own/st set).
@@ -1179,10 +1192,12 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_pk3(
             const size_t took = (size_t)__popcll(want);
             head += took < avail ? took : avail;
         }
-        // exit when nothing is in flight and the queue is drained (while work
-        // remains, an all-idle wave always has window room: every result below
-        // head is complete, so the previous flush advanced `flushed`)
-        if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end) break;
+        // exit when nothing is in flight, the queue is drained and every staged
+        // result is written (a flush moves at most two segments per iteration,
+        // so a slow lane can leave several complete segments behind it)
+        if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end &&
+            flushed >= end)  // every staged result written
+            break;
 
         // ---- memory: one round (slot A's load + slot B's pair) ----
         u128 xa = 0, xb = 0;
@@ -1414,14 +1429,16 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
         }
         cs = -1;
         if (i >= c.l0) {
+            if (c.arc && (cur < c.lo || cur >= c.hi)) return 2;  // row lives on another rank
             mode = A_HOP;
             lvl = i;
             return 0;
         }
         // rare: below the table -> exact finger + exact ids
-        const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
-        const u128 idn = ld128(c.ring + nxt);
         const u128 idc = cex ? clo : ld128(c.ring + cur);
+        const uint32_t nxt = c.arc ? finger_of(c.sv, c.ring, c.n, cur, i, idc)
+                                   : c.F[(size_t)cur * CX_FINGERS + i];
+        const u128 idn = ld128(c.ring + nxt);
         ++h;
         if (key - idc <= idn - idc) {
             own = nxt;
@@ -1438,87 +1455,155 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
     }
 }
 
-__global__ __launch_bounds__(RT_BLOCK) void k_route_tree(
-    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const uint4 *tree, int l0, int R,
-    int ib, const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
-    uint32_t *owner, uint8_t *hops, uint8_t *status) {
-    __shared__ uint64_t res_all[RT_BLOCK / 64][RES_WIN];
+// Arguments of the tree walk (replicated ring: lo = 0, hi = n; arc mode: the
+// rank's arc, inputs and outcomes as 32-B ArcRec records).
+struct TreeIO {
+    const cell128 *ring_ext, *ring;
+    uint32_t n;
+    const uint4 *tree;
+    int l0, R, ib;
+    const uint32_t *F;
+    SearchView sv;
+    uint32_t lo, hi;
+    const uint32_t *src;
+    const cell128 *keys;
+    const ArcRec *in;
+    ArcRec *out;
+    int self;
+    size_t q, chunk;
+    uint32_t *owner;
+    uint8_t *hops;
+    uint8_t *status;
+};
+
+template <bool ARC>
+__global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
+    __shared__ uint64_t res_all[ARC ? 1 : RT_BLOCK / 64][ARC ? 1 : RES_WIN];
     __shared__ uint4 ent_all[RT_BLOCK][4];       // each lane's current 64-B entry
     __shared__ uint64_t addr_all[RT_BLOCK];      // entry index + 1 wanted by each lane (0: none)
+    const uint32_t n = io.n;
+    const int l0 = io.l0, R = io.R, ib = io.ib;
     const int lane = threadIdx.x & 63;
     const int quad0 = threadIdx.x & ~3, qs = threadIdx.x & 3;
-    uint64_t *res = res_all[threadIdx.x >> 6];
+    uint64_t *res = res_all[ARC ? 0 : (threadIdx.x >> 6)];
     const uint64_t *ent = reinterpret_cast<const uint64_t *>(ent_all[threadIdx.x]);
-    for (int j = lane; j < RES_WIN; j += 64) res[j] = 0;
+    if (!ARC)
+        for (int j = lane; j < RES_WIN; j += 64) res[j] = 0;
     const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
-    const size_t base = wave * chunk;
-    if (base >= q) return;  // wave-uniform
-    const size_t end = (base + chunk < q) ? base + chunk : q;
+    const size_t base = wave * io.chunk;
+    if (base >= io.q) return;  // wave-uniform
+    const size_t end = (base + io.chunk < io.q) ? base + io.chunk : io.q;
     PkCtx c;
-    c.ring = ring;
-    c.F = F;
+    c.ring = io.ring;
+    c.F = io.F;
     c.n = n;
     c.l0 = l0;
     c.ib = ib;
     c.S = 64 + ib;
     c.imask = (1ull << ib) - 1;
     c.W = ((u128)1 << c.S) - 1;
+    c.arc = ARC;
+    c.lo = io.lo;
+    c.hi = io.hi;
+    c.sv = io.sv;
     size_t head = base, flushed = base;
 
     int mode = A_NONE, lvl = 0, cs = -1, ri = 0;
     size_t qi = 0;
+    uint64_t qid = 0;
     u128 key = 0, clo = 0;
     bool cex = true;
     uint32_t cur = 0, h = 0, pn = 0;
-    int bst = B_EMPTY;
+    int bst = B_EMPTY, pkind = 0;
     size_t pq = 0;
+    uint64_t pqid = 0;
     u128 pkey = 0, pa = 0, pb = 0;
-    uint32_t psrc = 0;
+    uint32_t psrc = 0, ph = 0;
+
+    // outcome of a finished query (ARC: local delivery or a result record)
+    auto deliver = [&](size_t idx, uint64_t id, uint32_t o, uint32_t hh, uint8_t stt) {
+        if (!ARC) {
+            res[idx & (RES_WIN - 1)] = pack_res(o, hh, stt);
+        } else {
+            ArcRec r;
+            if ((int)(id >> ARC_ORIGIN_SHIFT) == io.self) {
+                const size_t li = id & ARC_INDEX_MASK;
+                io.owner[li] = o;
+                io.hops[li] = (uint8_t)hh;
+                if (io.status) io.status[li] = stt;
+                r.w0 = r.w1 = 0;
+                r.qid = id;
+                r.cur = 0;
+                r.hk = ARC_NONE << 8;
+            } else {
+                r.w0 = (uint64_t)o | ((uint64_t)stt << 32);
+                r.w1 = 0;
+                r.qid = id;
+                r.cur = o;
+                r.hk = (hh & 0xFF) | (ARC_RESULT << 8);
+            }
+            io.out[idx] = r;
+        }
+    };
 
     for (;;) {
         // ---- refill slot B ----
         {
-            const size_t lim = (end < flushed + RES_WIN) ? end : flushed + RES_WIN;
+            size_t lim = end;
+            if (!ARC && flushed + RES_WIN < end) lim = flushed + RES_WIN;
             const size_t avail = lim > head ? lim - head : 0;
             const uint64_t want = __ballot(bst == B_EMPTY);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
             if (bst == B_EMPTY && rank < avail) {
                 pq = head + rank;
-                pkey = ld128(keys + pq);
-                psrc = src[pq];
+                if (ARC) {
+                    const ArcRec r = io.in[pq];
+                    pkey = ((u128)r.w1 << 64) | r.w0;
+                    pqid = r.qid;
+                    psrc = r.cur;
+                    ph = r.hk & 0xFF;
+                    pkind = (int)(r.hk >> 8);
+                } else {
+                    pkey = ld128(io.keys + pq);
+                    psrc = io.src[pq];
+                    pqid = pq;
+                    ph = 0;
+                    pkind = ARC_NEW;
+                }
                 bst = B_KS;
             }
             const size_t took = (size_t)__popcll(want);
             head += took < avail ? took : avail;
         }
-        if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end) break;
+        if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end &&
+            (ARC || flushed >= end))  // every staged result written
+            break;
 
         // ---- memory round ----
-        // cooperative 64-B entry loads: the quad loads the entry of each member
         addr_all[threadIdx.x] =
-            mode == A_HOP ? (uint64_t)cur * (unsigned)R + (unsigned)(lvl - l0) + 1 : 0;
+            mode == A_HOP ? (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0) + 1 : 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint64_t a0 = addr_all[quad0], a1 = addr_all[quad0 + 1], a2 = addr_all[quad0 + 2],
                        a3 = addr_all[quad0 + 3];
         uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
-        if (a0) c0 = tree[(a0 - 1) * 4 + qs];
-        if (a1) c1 = tree[(a1 - 1) * 4 + qs];
-        if (a2) c2 = tree[(a2 - 1) * 4 + qs];
-        if (a3) c3 = tree[(a3 - 1) * 4 + qs];
+        if (a0) c0 = io.tree[(a0 - 1) * 4 + qs];
+        if (a1) c1 = io.tree[(a1 - 1) * 4 + qs];
+        if (a2) c2 = io.tree[(a2 - 1) * 4 + qs];
+        if (a3) c3 = io.tree[(a3 - 1) * 4 + qs];
         u128 xa = 0, xb = 0;
         if (mode == A_FIXC) {
-            xa = ld128(ring + cur);
+            xa = ld128(io.ring + cur);
         } else if (mode == A_FIXT) {
-            xa = ld128(ring + cur);
-            xb = ld128(ring + pn);
+            xa = ld128(io.ring + cur);
+            xb = ld128(io.ring + pn);
         }
         if (bst == B_KS) {
-            if (psrc < n) {
-                pa = ld128(ring_ext + psrc);
-                pb = ld128(ring_ext + psrc + 1);
+            if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
+                pa = ld128(io.ring_ext + psrc);
+                pb = ld128(io.ring_ext + psrc + 1);
             }
             bst = B_PAIR;
         }
@@ -1575,54 +1660,100 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(
                 plan = true;
             }
         }
-        if (plan)
-            fin = tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st) == 1;
+        if (plan) {
+            const int r = tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
+            if (r == 1) fin = true;
+            if (ARC && r == 2) {  // continue on the rank that owns cur's row
+                ArcRec o;
+                o.w0 = (uint64_t)key;
+                o.w1 = (uint64_t)(key >> 64);
+                o.qid = qid;
+                o.cur = cur;
+                o.hk = (h & 0xFF) | (ARC_WALK << 8);
+                io.out[qi] = o;
+                mode = A_NONE;
+            }
+        }
         if (fin) {
-            res[qi & (RES_WIN - 1)] = pack_res(own, h, st);
+            deliver(qi, qid, own, h, st);
             mode = A_NONE;
         }
         // ---- promote slot B ----
         if (mode == A_NONE && bst == B_PAIR) {
             bst = B_EMPTY;
             qi = pq;
+            qid = pqid;
             key = pkey;
             cur = psrc;
-            h = 0;
+            h = ph;
             cs = -1;
             own = CX_NONE;
             st = CX_Q_OK;
-            bool done = true;
-            if (cur >= n) {
+            int done = 1;
+            if (ARC && pkind == ARC_RESULT) {
+                // a result coming home: deliver it (w0 = owner | status << 32)
+                deliver(qi, qid, (uint32_t)pkey, h, (uint8_t)((uint64_t)pkey >> 32));
+                done = 0;
+            } else if (ARC && pkind == ARC_NONE) {
+                ArcRec o = {};
+                o.qid = qid;
+                o.hk = ARC_NONE << 8;
+                io.out[qi] = o;
+                done = 0;
+            } else if (cur >= n) {
                 st = CX_Q_BADPEER;
-            } else if (n == 1 || (key - pa - 1) <= (pb - pa - 1)) {
-                own = cur;
+            } else if (pkind == ARC_NEW && (n == 1 || (key - pa - 1) <= (pb - pa - 1))) {
+                own = cur;  // StoredLocally at the source: 0 hops
             } else {
                 clo = pb;
                 cex = true;
-                done = tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st) == 1;
+                done = tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
+                if (ARC && done == 2) {
+                    ArcRec o;
+                    o.w0 = (uint64_t)key;
+                    o.w1 = (uint64_t)(key >> 64);
+                    o.qid = qid;
+                    o.cur = cur;
+                    o.hk = (h & 0xFF) | (ARC_WALK << 8);
+                    io.out[qi] = o;
+                    mode = A_NONE;
+                    done = 0;
+                }
             }
-            if (done) {
-                res[qi & (RES_WIN - 1)] = pack_res(own, h, st);
+            if (done == 1) {
+                deliver(qi, qid, own, h, st);
                 mode = A_NONE;
             }
         }
 
-        // ---- flush complete 64-result segments ----
-        for (int it = 0; it < 2; ++it) {
-            if (flushed >= end) break;
-            const size_t idx = flushed + lane;
-            const bool inr = idx < end;
-            const uint64_t v = inr ? res[idx & (RES_WIN - 1)] : 0ull;
-            if (__ballot(!inr || (v >> 63)) != ~0ull) break;
-            if (inr) {
-                owner[idx] = (uint32_t)v;
-                hops[idx] = (uint8_t)(v >> 32);
-                if (status) status[idx] = (uint8_t)(v >> 40);
-                res[idx & (RES_WIN - 1)] = 0;
+        // ---- flush complete 64-result segments (replicated mode) ----
+        if (!ARC) {
+            for (int it = 0; it < 2; ++it) {
+                if (flushed >= end) break;
+                const size_t idx = flushed + lane;
+                const bool inr = idx < end;
+                const uint64_t v = inr ? res[idx & (RES_WIN - 1)] : 0ull;
+                if (__ballot(!inr || (v >> 63)) != ~0ull) break;
+                if (inr) {
+                    io.owner[idx] = (uint32_t)v;
+                    io.hops[idx] = (uint8_t)(v >> 32);
+                    if (io.status) io.status[idx] = (uint8_t)(v >> 40);
+                    res[idx & (RES_WIN - 1)] = 0;
+                }
+                flushed += 64;
             }
-            flushed += 64;
         }
     }
+}
+
+static void tree_geometry(size_t q, size_t &chunk, unsigned &blocks) {
+    const size_t max_waves = 256 * 32;
+    size_t waves = (q + 1023) / 1024;
+    if (waves > max_waves) waves = max_waves;
+    if (waves == 0) waves = 1;
+    chunk = (q + waves - 1) / waves;
+    waves = (q + chunk - 1) / chunk;
+    blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
 }
 
 hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
@@ -1630,16 +1761,193 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
                       const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
                       uint8_t *hops, uint8_t *status, hipStream_t s) {
     if (q == 0) return hipSuccess;
-    const size_t max_waves = 256 * 32;
-    size_t waves = (q + 1023) / 1024;
-    if (waves > max_waves) waves = max_waves;
-    if (waves == 0) waves = 1;
-    const size_t chunk = (q + waves - 1) / waves;
-    waves = (q + chunk - 1) / chunk;
-    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    k_route_tree<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n,
-                                             reinterpret_cast<const uint4 *>(tree), l0, R, ib, F,
-                                             src, keys, q, chunk, owner, hops, status);
+    TreeIO io = {};
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.tree = reinterpret_cast<const uint4 *>(tree);
+    io.l0 = l0;
+    io.R = R;
+    io.ib = ib;
+    io.F = F;
+    io.lo = 0;
+    io.hi = (uint32_t)n;
+    io.src = src;
+    io.keys = keys;
+    io.q = q;
+    io.owner = owner;
+    io.hops = hops;
+    io.status = status;
+    unsigned blocks;
+    tree_geometry(q, io.chunk, blocks);
+    k_route_tree<false><<<blocks, RT_BLOCK, 0, s>>>(io);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Arc-sharded mode (SURVEY 8e layout 2): rows of the arc [lo, hi) only, built
+// by directory searches on the replicated ring (no full finger table).
+// ---------------------------------------------------------------------------
+__global__ void k_tree_build_arc(SearchView sv, const cell128 *ring, uint32_t n, uint32_t lo,
+                                 uint32_t hi, int l0, int R, int ib, uint64_t *tree) {
+    const size_t total = (size_t)(hi - lo) * R;
+    const int S = 64 + ib;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = t / (unsigned)R;
+        const uint32_t p = lo + (uint32_t)r;
+        const int i = l0 + (int)(t - r * (unsigned)R);
+        const int par[8] = {-1, 0, 0, 1, 0, 1, 2, 3};
+        const int off[8] = {0, 1, 2, 2, 3, 3, 3, 3};
+        uint32_t f[8];
+        u128 id[8];
+        f[0] = finger_of(sv, ring, n, p, i, ld128(ring + p));
+        id[0] = ld128(ring + f[0]);
+#pragma unroll
+        for (int sl = 1; sl < 8; ++sl) {
+            const int lv = i - off[sl];
+            if (lv >= 0 && f[par[sl]] != CX_NONE) {
+                f[sl] = finger_of(sv, ring, n, f[par[sl]], lv, id[par[sl]]);
+                id[sl] = ld128(ring + f[sl]);
+            } else {
+                f[sl] = CX_NONE;
+                id[sl] = 0;
+            }
+        }
+        uint64_t *e = tree + t * 8;
+#pragma unroll
+        for (int sl = 0; sl < 8; ++sl)
+            e[sl] = f[sl] == CX_NONE ? ~0ull : (((uint64_t)(id[sl] >> S) << ib) | f[sl]);
+    }
+}
+
+hipError_t tree_build_arc(const SearchView &sv, const cell128 *ring, size_t n, uint32_t lo,
+                          uint32_t hi, int l0, int R, int ib, uint64_t *tree, hipStream_t s) {
+    if (hi <= lo) return hipSuccess;
+    k_tree_build_arc<<<cx_grid((size_t)(hi - lo) * R, 256), 256, 0, s>>>(sv, ring, (uint32_t)n,
+                                                                         lo, hi, l0, R, ib, tree);
+    return hipGetLastError();
+}
+
+hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *tree,
+                     int l0, int R, int ib, const SearchView &sv, uint32_t lo, uint32_t hi,
+                     int self, const ArcRec *in, size_t q, ArcRec *out, uint32_t *owner,
+                     uint8_t *hops, uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    TreeIO io = {};
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.tree = reinterpret_cast<const uint4 *>(tree);
+    io.l0 = l0;
+    io.R = R;
+    io.ib = ib;
+    io.sv = sv;
+    io.lo = lo;
+    io.hi = hi;
+    io.in = in;
+    io.out = out;
+    io.self = self;
+    io.q = q;
+    io.owner = owner;
+    io.hops = hops;
+    io.status = status;
+    unsigned blocks;
+    tree_geometry(q, io.chunk, blocks);
+    k_route_tree<true><<<blocks, RT_BLOCK, 0, s>>>(io);
+    return hipGetLastError();
+}
+
+// Initial records: query i issued at peer src[i] (kind NEW, qid = self:i).
+__global__ void k_arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self,
+                           ArcRec *out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const u128 k = ld128(keys + i);
+        ArcRec r;
+        r.w0 = (uint64_t)k;
+        r.w1 = (uint64_t)(k >> 64);
+        r.qid = ((uint64_t)self << ARC_ORIGIN_SHIFT) | i;
+        r.cur = src[i];
+        r.hk = ARC_NEW << 8;
+        out[i] = r;
+    }
+}
+
+hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,
+                    hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_arc_seed<<<cx_grid(q, 256), 256, 0, s>>>(src, keys, q, self, out);
+    return hipGetLastError();
+}
+
+// Destination rank of an outcome record: WALK -> owner of cur's row, RESULT
+// -> origin rank, NONE -> -1.  Arc g = [g n / G, (g+1) n / G).
+__device__ __forceinline__ int arc_dest(const ArcRec &r, uint32_t n, int G) {
+    const uint32_t kind = r.hk >> 8;
+    if (kind == ARC_RESULT) {
+        const uint64_t o = r.qid >> ARC_ORIGIN_SHIFT;
+        return o < (uint64_t)G ? (int)o : -1;
+    }
+    if ((kind != ARC_WALK && kind != ARC_NEW) || r.cur >= n) return -1;
+    int g = (int)(((uint64_t)r.cur * (uint64_t)G) / n);
+    if (g >= G) g = G - 1;
+    while (g > 0 && (uint32_t)(((uint64_t)g * n) / G) > r.cur) --g;
+    while (g + 1 < G && (uint32_t)(((uint64_t)(g + 1) * n) / G) <= r.cur) ++g;
+    return g;
+}
+
+// Bucket outcome records by destination: per-block LDS histograms, one global
+// atomic per (block, destination) to reserve ranges, LDS-local offsets.
+constexpr int ARC_MAX_RANKS = 64;
+
+__global__ void k_arc_count(const ArcRec *recs, size_t q, uint32_t n, int G, uint32_t *counts) {
+    __shared__ uint32_t h[ARC_MAX_RANKS];
+    for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+    __syncthreads();
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int d = arc_dest(recs[i], n, G);
+        if (d >= 0) atomicAdd(&h[d], 1u);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < G; j += blockDim.x)
+        if (h[j]) atomicAdd(&counts[j], h[j]);
+}
+
+__global__ void k_arc_scatter(const ArcRec *recs, size_t q, uint32_t n, int G,
+                              uint32_t *cursor, ArcRec *send) {
+    __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
+    for (size_t b0 = (size_t)blockIdx.x * blockDim.x; b0 < q; b0 += (size_t)gridDim.x * blockDim.x) {
+        for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+        __syncthreads();
+        const size_t i = b0 + threadIdx.x;
+        int d = -1;
+        uint32_t slot = 0;
+        ArcRec r;
+        if (i < q) {
+            r = recs[i];
+            d = arc_dest(r, n, G);
+            if (d >= 0) slot = atomicAdd(&h[d], 1u);
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < G; j += blockDim.x)
+            basep[j] = h[j] ? atomicAdd(&cursor[j], h[j]) : 0u;
+        __syncthreads();
+        if (d >= 0) send[basep[d] + slot] = r;
+        __syncthreads();
+    }
+}
+
+hipError_t arc_bucket(const ArcRec *recs, size_t q, size_t n, int G, uint32_t *counts_dev,
+                      uint32_t *cursor_dev, ArcRec *send, hipStream_t s, bool scatter) {
+    if (!scatter) {
+        if (q) k_arc_count<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, (uint32_t)n, G,
+                                                                 counts_dev);
+        return hipGetLastError();
+    }
+    if (q) k_arc_scatter<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, (uint32_t)n, G,
+                                                               cursor_dev, send);
     return hipGetLastError();
 }
 

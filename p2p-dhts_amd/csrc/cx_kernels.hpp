@@ -15,6 +15,19 @@ struct alignas(32) RtEntry {
 };
 static_assert(sizeof(RtEntry) == 32, "RtEntry is 32 B");
 
+// In-flight record of the arc-sharded walk (32 B, the unit exchanged between
+// ranks).  qid = origin rank << ARC_ORIGIN_SHIFT | index at the origin.
+struct alignas(16) ArcRec {
+    uint64_t w0, w1;  // key (queries) / owner | status << 32 (results)
+    uint64_t qid;
+    uint32_t cur;     // peer to continue at (queries) / owner (results)
+    uint32_t hk;      // hops | kind << 8
+};
+static_assert(sizeof(ArcRec) == 32, "ArcRec is 32 B");
+#define ARC_ORIGIN_SHIFT 40
+#define ARC_INDEX_MASK ((1ull << ARC_ORIGIN_SHIFT) - 1)
+enum { ARC_NEW = 0, ARC_RESULT = 1, ARC_WALK = 2, ARC_NONE = 3 };
+
 namespace cxk {
 
 size_t scan_workspace_words(size_t n);
@@ -65,6 +78,16 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
                       const uint64_t *tree, int l0, int R, int ib, const uint32_t *F,
                       const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
                       uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t tree_build_arc(const SearchView &sv, const cell128 *ring, size_t n, uint32_t lo,
+                          uint32_t hi, int l0, int R, int ib, uint64_t *tree, hipStream_t s);
+hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *tree,
+                     int l0, int R, int ib, const SearchView &sv, uint32_t lo, uint32_t hi,
+                     int self, const ArcRec *in, size_t q, ArcRec *out, uint32_t *owner,
+                     uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,
+                    hipStream_t s);
+hipError_t arc_bucket(const ArcRec *recs, size_t q, size_t n, int G, uint32_t *counts_dev,
+                      uint32_t *cursor_dev, ArcRec *send, hipStream_t s, bool scatter);
 hipError_t nsucc(const SearchView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const SearchView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,

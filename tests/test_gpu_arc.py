@@ -1,0 +1,175 @@
+"""Arc-sharded routing (SURVEY 8e layout 2) on one GPU: G engine handles, each
+holding tree rows for its own arc only, exchange records in-process exactly as
+chordx.arc.ArcRouter does over torch.distributed.  Owners, hops and statuses
+must equal the replicated ring's route (variant 4) and the CPU oracle
+bit-for-bit, for every G (including G = 1, where nothing is forwarded)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cx():
+    import chordx
+    if chordx.device_count() == 0:
+        pytest.fail("gpu test without a HIP device")
+    return chordx
+
+
+def simulate(cx, ids_dev, G, srcs, keys, status=True):
+    """Round loop of ArcRouter.route with G in-process 'ranks'."""
+    import torch
+    from chordx.arc import MAX_ROUNDS
+    rings = [cx.Ring(ids_dev) for _ in range(G)]
+    n = rings[0].n
+    for g, r in enumerate(rings):
+        r.arc_build(g * n // G, (g + 1) * n // G)
+    outs = []
+    for g in range(G):
+        q = keys[g].shape[0]
+        outs.append((torch.full((q,), -7, dtype=torch.int32, device="cuda"),
+                     torch.full((q,), 77, dtype=torch.uint8, device="cuda"),
+                     torch.full((q,), 9, dtype=torch.uint8, device="cuda") if status else None))
+    recs = [rings[g].arc_seed(g, srcs[g], keys[g]) for g in range(G)]
+    rounds, sent = 0, 0
+    for rounds in range(1, MAX_ROUNDS + 1):
+        inbox = [[] for _ in range(G)]
+        total = 0
+        for g in range(G):
+            out = rings[g].arc_step(g, recs[g], *outs[g])
+            send, counts = rings[g].arc_bucket(G, out)
+            total += sum(counts)
+            for d, part in enumerate(torch.split(send, counts)):
+                inbox[d].append(part)
+        sent += total
+        if total == 0:
+            break
+        recs = [torch.cat(b) if b else torch.empty((0, 4), dtype=torch.int64, device="cuda")
+                for b in inbox]
+    torch.cuda.synchronize()
+    return outs, rounds, sent
+
+
+def _setup(cx, O, torch, n, q, G, seed):
+    ids = O.splitmix_keys(seed, n)
+    ids_dev = torch.from_numpy(ids.view(np.int64).copy()).cuda()
+    ring = cx.Ring(ids_dev)
+    ring.build_fingers()
+    srcs, keys = [], []
+    for g in range(G):
+        k = O.splitmix_keys(seed + 1, q, offset=g * q)
+        rng = np.random.default_rng(seed + g)
+        s = rng.integers(0, ring.n, q, dtype=np.int64).astype(np.int32)
+        srcs.append(torch.from_numpy(s).cuda())
+        keys.append(torch.from_numpy(k.view(np.int64).copy()).cuda())
+    return ids_dev, ring, srcs, keys
+
+
+@pytest.mark.parametrize("n,G", [(5000, 1), (5000, 2), (5000, 3), (5000, 8), (1 << 16, 8),
+                                 (70001, 5), (2, 2), (1, 1), (3, 4)])
+def test_arc_route_equals_replicated(cx, O, n, G):
+    import torch
+    q = 4096
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C0 + n + G)
+    outs, rounds, sent = simulate(cx, ids_dev, G, srcs, keys)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow), (n, G, g)
+        assert torch.equal(outs[g][1], hp), (n, G, g)
+        assert torch.equal(outs[g][2], st), (n, G, g)
+    if G == 1:
+        assert rounds == 1 and sent == 0
+    assert rounds <= 40
+
+
+def test_arc_route_matches_oracle(cx, O):
+    import torch
+    n, q, G = 3000, 2000, 4
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C1)
+    outs, _, sent = simulate(cx, ids_dev, G, srcs, keys)
+    assert sent > 0
+    R = O.ring_build(ids_dev.cpu().numpy().view(np.uint64))
+    P = O.Peers(R, O.fingers(R))
+    for g in range(G):
+        ow, hp, st = O.route(P, srcs[g].cpu().numpy().astype(np.uint32),
+                             keys[g].cpu().numpy().view(np.uint64).reshape(-1, 2))
+        assert (outs[g][0].cpu().numpy().view(np.uint32) == ow).all()
+        assert (outs[g][1].cpu().numpy() == hp).all()
+        assert (outs[g][2].cpu().numpy() == st).all()
+
+
+def test_arc_bad_source_and_no_status(cx, O):
+    import torch
+    n, q, G = 4000, 1000, 3
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C2)
+    srcs[1][::7] = n + 5          # out-of-range source peers -> CX_Q_BADPEER
+    srcs[2][::11] = -1
+    outs, _, _ = simulate(cx, ids_dev, G, srcs, keys, status=True)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)
+        assert torch.equal(outs[g][2], st)
+    assert int((outs[1][2] == cx.CX_Q_BADPEER).sum()) == len(range(0, q, 7))
+    outs2, _, _ = simulate(cx, ids_dev, G, srcs, keys, status=False)
+    for g in range(G):
+        assert torch.equal(outs2[g][0], outs[g][0]) and torch.equal(outs2[g][1], outs[g][1])
+
+
+def test_arc_clustered_ring(cx, O):
+    """IDs packed in a narrow band: the packed-ID interval checks need their
+    exact-ID fallbacks, which in arc mode run on replicated data."""
+    import torch
+    base = 0x1234_5678_9ABC_DEF0 << 64
+    vals = [base + i * 977 for i in range(3000)] + [(1 << 127) + i for i in range(50)]
+    ids = O.keys_from_ints(vals)
+    ids_dev = torch.from_numpy(ids.view(np.int64).copy()).cuda()
+    ring = cx.Ring(ids_dev)
+    ring.build_fingers()
+    G, q = 3, 3000
+    srcs, keys = [], []
+    for g in range(G):
+        kv = [base + (i * 7919 + g) * 131 for i in range(q // 2)]
+        kv += O.ints_from_keys(O.splitmix_keys(0xC1 + g, q - len(kv)))
+        keys.append(torch.from_numpy(O.keys_from_ints(kv).view(np.int64).copy()).cuda())
+        srcs.append(torch.from_numpy((np.arange(q) * 13 % ring.n).astype(np.int32)).cuda())
+    outs, _, _ = simulate(cx, ids_dev, G, srcs, keys)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)
+        assert torch.equal(outs[g][2], st)
+
+
+def test_arc_bucket_groups_by_destination(cx, O):
+    """Bucket output: every WALK record lands in the block of the rank whose
+    arc holds its peer; RESULT records go to their origin; NONE dropped."""
+    import torch
+    from chordx.arc import arc_of
+    n, G = 1000, 5
+    ring = cx.Ring(torch.from_numpy(O.splitmix_keys(7, n).view(np.int64).copy()).cuda())
+    ring.arc_build(0, n // G)
+    q = 5000
+    rng = np.random.default_rng(3)
+    recs = np.zeros((q, 4), dtype=np.int64)
+    kind = rng.integers(0, 4, q)
+    kind[kind == 0] = 2
+    cur = rng.integers(0, n, q)
+    origin = rng.integers(0, G, q)
+    recs[:, 2] = (origin << 40) | np.arange(q)
+    recs[:, 3] = (cur & 0xFFFFFFFF) | ((5 | (kind << 8)) << 32)
+    send, counts = ring.arc_bucket(G, torch.from_numpy(recs).cuda())
+    want = [0] * G
+    dest = []
+    for i in range(q):
+        d = -1 if kind[i] == 3 else (origin[i] if kind[i] == 1 else arc_of(int(cur[i]), n, G))
+        dest.append(d)
+        if d >= 0:
+            want[d] += 1
+    assert counts == want
+    s = send.cpu().numpy()
+    off = 0
+    for d in range(G):
+        blk = s[off: off + counts[d]]
+        idx = (blk[:, 2] & ((1 << 40) - 1)).tolist()
+        assert sorted(idx) == sorted(i for i in range(q) if dest[i] == d)
+        off += counts[d]

@@ -63,3 +63,134 @@ def test_world2_sharded_route_equals_single_process():
     assert got_owner == owner.tolist() and got_hops == hops.tolist()
     assert out[0][2] == out[1][2] == 2.0           # max over ranks
     assert out[0][3] == 0 and out[0][4] == out[1][4] == int(hops.sum())
+
+
+# ---------------------------------------------------------------------------
+# Arc-sharded exchange protocol (chordx.arc.ArcRouter) over gloo, world 2 and 3.
+# ---------------------------------------------------------------------------
+class OracleArcEngine:
+    """CPU stand-in for the per-rank arc engine (test infrastructure): a NEW
+    lookup is resolved by the oracle, then travels as a WALK record to the
+    rank whose arc holds the owner peer, which finishes it there -- locally or
+    as a RESULT record back to the origin.  Exercises the protocol (buckets,
+    count matrix, all_to_all, homecoming results, termination), not the walk,
+    which tests/test_gpu_arc.py checks on the GPU."""
+
+    def __init__(self, P, n):
+        self.P, self.n = P, n
+
+    def arc_build(self, lo, hi):
+        self.lo, self.hi = lo, hi
+
+    def arc_seed(self, rank, src, keys):
+        import torch
+        q = keys.shape[0]
+        r = torch.zeros((q, 4), dtype=torch.int64)
+        r[:, :2] = keys.view(torch.int64).reshape(q, 2)
+        r[:, 2] = (rank << 40) + torch.arange(q)
+        r[:, 3] = src.to(torch.int64) & 0xFFFFFFFF
+        return r
+
+    def arc_step(self, rank, recs, owner, hops, status):
+        import torch
+        import oracle as O
+        r = recs.numpy().copy()
+        out = np.zeros_like(r)
+        kind = (r[:, 3] >> 40) & 0xFF
+        cur = r[:, 3] & 0xFFFFFFFF
+        h = (r[:, 3] >> 32) & 0xFF
+        new = np.nonzero(kind == 0)[0]
+        res = {}
+        if len(new):
+            ow, hp, st = O.route(self.P, cur[new].astype(np.uint32),
+                                 r[new, :2].view(np.uint64).reshape(-1, 2))
+            for j, i in enumerate(new):
+                o = int(ow[j])
+                if st[j] != 0 or self.lo <= o < self.hi:
+                    res[i] = (o, int(hp[j]), int(st[j]))
+                else:
+                    out[i] = r[i]
+                    out[i, 3] = o | ((int(hp[j]) | (2 << 8)) << 32)
+        for i in np.nonzero(kind == 2)[0]:
+            res[i] = (int(cur[i]), int(h[i]), 0)
+        for i in np.nonzero(kind == 1)[0]:
+            res[i] = (int(r[i, 0]) & 0xFFFFFFFF, int(h[i]), (int(r[i, 0]) >> 32) & 0xFF)
+        for i, (o, hh, st) in res.items():
+            origin, idx = int(r[i, 2]) >> 40, int(r[i, 2]) & ((1 << 40) - 1)
+            out[i, 2] = r[i, 2]
+            if origin == rank:
+                owner[idx] = o if o < (1 << 31) else o - (1 << 32)
+                hops[idx] = hh
+                status[idx] = st
+                out[i, 3] = 3 << 40
+            else:
+                out[i, 0] = o | (st << 32)
+                out[i, 3] = o | ((hh | (1 << 8)) << 32)
+        return torch.from_numpy(out)
+
+    def arc_bucket(self, world, recs):
+        import torch
+        from chordx.arc import arc_of
+        r = recs.numpy()
+        dest = []
+        for row in r:
+            kind = (int(row[3]) >> 40) & 0xFF
+            if kind == 1:
+                dest.append(int(row[2]) >> 40)
+            elif kind == 2:
+                dest.append(arc_of(int(row[3]) & 0xFFFFFFFF, self.n, world))
+            else:
+                dest.append(-1)
+        dest = np.array(dest, dtype=np.int64)
+        order = np.argsort(dest, kind="stable")
+        order = order[dest[order] >= 0]
+        counts = [int((dest == d).sum()) for d in range(world)]
+        return torch.from_numpy(r[order].copy()), counts
+
+
+def _arc_worker(rank, world, port, per_rank, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "p2p-dhts_amd"), os.path.join(root, "oracle"),
+                    os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as tdist
+    import oracle as O
+    from chordx import dist
+    from chordx.arc import ArcRouter
+    from test_multiproc import OracleArcEngine
+    dist.init("gloo")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    P = O.Peers(ring, O.fingers(ring, threads=2))
+    keys = O.splitmix_keys(0x5EED0006, per_rank, offset=rank * per_rank)
+    src = torch.from_numpy(((np.arange(per_rank) * 7 + rank) % len(ring)).astype(np.int32))
+    owner = torch.full((per_rank,), -9, dtype=torch.int32)
+    hops = torch.zeros(per_rank, dtype=torch.uint8)
+    status = torch.full((per_rank,), 7, dtype=torch.uint8)
+    router = ArcRouter(OracleArcEngine(P, len(ring)), len(ring), rank, world)
+    rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status)
+    out[rank] = (owner.numpy().view(np.uint32).tolist(), hops.tolist(), status.tolist(), rounds,
+                 router.records_sent)
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_arc_router_protocol_gloo(world):
+    import oracle as O
+    per_rank = 700
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out), nprocs=world,
+                       join=True, start_method="spawn")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    P = O.Peers(ring, O.fingers(ring))
+    for r in range(world):
+        keys = O.splitmix_keys(0x5EED0006, per_rank, offset=r * per_rank)
+        src = ((np.arange(per_rank) * 7 + r) % len(ring)).astype(np.uint32)
+        ow, hp, st = O.route(P, src, keys)
+        assert out[r][0] == ow.tolist() and out[r][1] == hp.tolist()
+        assert out[r][2] == st.tolist()
+        assert out[r][3] == 3           # walk -> result -> home, then drained
+        assert out[r][4] > 0            # records crossed ranks
