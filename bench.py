@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target wall time of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", choices=("replicated", "arc"), default="replicated",
+                    help="replicated: every rank holds the whole tree table and routes its "
+                         "own keys (default); arc: each rank holds tree rows for its arc only "
+                         "and lookups travel between ranks (chordx.arc)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_route.json"))
     return ap.parse_args()
 
@@ -87,8 +91,90 @@ def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
             "parity_on_sample": ok}
 
 
+def main_arc(args):
+    """Arc-sharded layout (SURVEY 8e layout 2): ring IDs generated in shares
+    and all-gathered (RCCL), tree rows per arc, lookups exchanged as 32-B
+    records by all_to_all every round until none is in flight."""
+    from chordx.arc import ArcRouter
+    world, rank, local = dist.env_rank()
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    dist.init("nccl", dev)
+    N = 1 << args.peers_log2
+    Q = 1 << args.keys_log2
+    lo, hi = rank * N // world, (rank + 1) * N // world
+    t0 = time.perf_counter()
+    share = torch.empty((N // world, 2), dtype=torch.int64, device=dev)
+    assert N % world == 0
+    chordx.fill_splitmix(share, SEED_RING, offset=lo)
+    if world > 1:
+        ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
+        torch.distributed.all_gather_into_tensor(ids, share)
+    else:
+        ids = share
+    ring = chordx.Ring(ids, device=local)
+    del ids, share
+    router = ArcRouter(ring, ring.n, rank, world)
+    torch.cuda.synchronize(dev)
+    t_setup = time.perf_counter() - t0
+    keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
+    q0, q1 = dist.shard(rank, Q)
+    chordx.fill_splitmix(keys, SEED_KEYS, offset=q0)
+    src = (torch.arange(q0, q1, device=dev, dtype=torch.int64) % ring.n).to(torch.int32)
+    owner = torch.empty(Q, dtype=torch.int32, device=dev)
+    hops = torch.empty(Q, dtype=torch.uint8, device=dev)
+    status = torch.empty(Q, dtype=torch.uint8, device=dev)
+    for _ in range(args.warmup):
+        router.route(src, keys, owner, hops, status)
+    torch.cuda.synchronize(dev)
+    router.records_sent = 0
+    dist.barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rounds = router.route(src, keys, owner, hops, status)
+    torch.cuda.synchronize(dev)
+    dist.barrier(world)
+    dt = time.perf_counter() - t0
+    dt_max = dist.max_over_ranks(dt, world, dev)
+    bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
+    sent = dist.sum_over_ranks(router.records_sent, world, dev)
+    sum_hops = dist.sum_over_ranks(int(hops.to(torch.int64).sum().item()), world, dev)
+    if rank == 0:
+        total = world * Q * args.steps
+        line = {
+            "metric": "successor lookups/sec (whole node) + % HBM roofline, 2^24-peer ring, "
+                      "1/2/4/8 GPUs",
+            "value": total / dt_max,
+            "unit": "lookups/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u128",
+            "data": "synthetic",
+            "config": {"workload": "C4 finger-routed lookups with hop counts, arc-sharded: "
+                                   f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step",
+                       "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
+                       "parallelism": f"arc-sharded tree rows x{world}, records by all_to_all"},
+            "rounds_per_step": rounds,
+            "records_exchanged_per_lookup": sent / (world * Q * args.steps),
+            "mean_hops": sum_hops / (world * Q),
+            "bad_status": bad,
+            "setup_s": t_setup,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.mode == "arc":
+        return main_arc(args)
     world, rank, local = dist.env_rank()
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")

@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Arc-sharded routing on ONE GPU with G simulated ranks (SURVEY 8e layout 2).
+
+G engine handles share one MI355X; each holds tree rows for its own arc only,
+and records are exchanged in-process exactly as chordx.arc.ArcRouter does over
+RCCL.  Per round and rank we time the walk step and the bucketing on the GPU
+(HIP events) and count the records that would cross xGMI, so the per-GPU cost
+of an 8-GPU arc-sharded run can be read off one box:
+
+  per-GPU compute  ~ max over ranks of (step + bucket) per round, summed
+  per-GPU exchange ~ records out per rank per round x 32 B over 7 xGMI links
+
+Prints one JSON object (profiles/<round>/arc_sim.json).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
+
+import torch  # noqa: E402
+
+import chordx  # noqa: E402
+from chordx.arc import MAX_ROUNDS, arc_bounds  # noqa: E402
+
+XGMI_LINK = 153e9  # B/s per link per direction (MI355X_MICROARCH.md)
+
+
+def run(G, N, Q, ids, reps):
+    rings = [chordx.Ring(ids) for _ in range(G)]
+    for g, r in enumerate(rings):
+        r.arc_build(*arc_bounds(r.n, G, g))
+    q = Q // G
+    keys, srcs, outs = [], [], []
+    for g in range(G):
+        k = torch.empty((q, 2), dtype=torch.int64, device="cuda")
+        chordx.fill_splitmix(k, 0x5EED0006, offset=g * q)
+        keys.append(k)
+        srcs.append((torch.arange(g * q, (g + 1) * q, device="cuda") % N).to(torch.int32))
+        outs.append((torch.empty(q, dtype=torch.int32, device="cuda"),
+                     torch.empty(q, dtype=torch.uint8, device="cuda"),
+                     torch.empty(q, dtype=torch.uint8, device="cuda")))
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    best = None
+    for _ in range(reps):
+        recs = [rings[g].arc_seed(g, srcs[g], keys[g]) for g in range(G)]
+        per_round = []
+        t0 = time.perf_counter()
+        for rnd in range(MAX_ROUNDS):
+            inbox = [[] for _ in range(G)]
+            total = 0
+            rows = []
+            for g in range(G):
+                a, b, c = ev(), ev(), ev()
+                a.record()
+                out = rings[g].arc_step(g, recs[g], *outs[g])
+                b.record()
+                send, counts = rings[g].arc_bucket(G, out)
+                c.record()
+                torch.cuda.synchronize()
+                rows.append({"in": int(recs[g].shape[0]), "step_ms": a.elapsed_time(b),
+                             "bucket_ms": b.elapsed_time(c),
+                             "out_remote": int(sum(counts) - counts[g])})
+                total += sum(counts)
+                for d, part in enumerate(torch.split(send, counts)):
+                    inbox[d].append(part)
+            per_round.append(rows)
+            if total == 0:
+                break
+            recs = [torch.cat(b) if b else torch.empty((0, 4), dtype=torch.int64,
+                                                       device="cuda") for b in inbox]
+        wall = time.perf_counter() - t0
+        comp = sum(max(r["step_ms"] + r["bucket_ms"] for r in rows) for rows in per_round)
+        xg = sum(max(r["out_remote"] for r in rows) * 32 / (7 * XGMI_LINK) * 1e3
+                 for rows in per_round)
+        res = {"G": G, "keys_total": Q, "keys_per_rank": q, "rounds": len(per_round),
+               "per_gpu_compute_ms": comp, "per_gpu_xgmi_ms_model": xg,
+               "projected_lookups_per_s_per_gpu": q / ((comp + xg) * 1e-3),
+               "sim_wall_s": wall,
+               "records_in_per_round": [sum(r["in"] for r in rows) for rows in per_round],
+               "round_max_ms": [max(r["step_ms"] + r["bucket_ms"] for r in rows)
+                                for rows in per_round]}
+        if best is None or comp < best["per_gpu_compute_ms"]:
+            best = res
+    del rings
+    torch.cuda.empty_cache()
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers-log2", type=int, default=24)
+    ap.add_argument("--keys-log2", type=int, default=25, help="keys in total over the G ranks")
+    ap.add_argument("--groups", default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    N, Q = 1 << a.peers_log2, 1 << a.keys_log2
+    ids = torch.empty((N, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(ids, 0x5EED0005)
+    ref = chordx.Ring(ids)
+    ref.build_fingers()
+    k = torch.empty((Q, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(k, 0x5EED0006)
+    s = (torch.arange(Q, device="cuda") % N).to(torch.int32)
+    o = (torch.empty(Q, dtype=torch.int32, device="cuda"),
+         torch.empty(Q, dtype=torch.uint8, device="cuda"),
+         torch.empty(Q, dtype=torch.uint8, device="cuda"))
+    ref.route(s, k, out=o)
+    a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record()
+    ref.route(s, k, out=o)
+    a1.record()
+    torch.cuda.synchronize()
+    out = {"peers": N, "keys": Q, "replicated_route_ms": a0.elapsed_time(a1), "arc": []}
+    del ref
+    torch.cuda.empty_cache()
+    for G in [int(x) for x in a.groups.split(",")]:
+        out["arc"].append(run(G, N, Q, ids, a.reps))
+        print(json.dumps(out["arc"][-1]), file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

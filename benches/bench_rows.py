@@ -93,17 +93,21 @@ def main():
     joins = keys_dev(N5 // 100, 0x5EED0009)
     pick = keys_dev(N5 // 100, 0x5EED0009, offset=1 << 40)[:, 0].remainder(N5)
     leaves = old.ids_device()[pick].contiguous()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    new, o2n = old.churn(joins, leaves)
-    torch.cuda.synchronize()
-    tc = time.perf_counter() - t0
+    tcv = {}
+    for cv in (0, 1, 1):  # re-sort, merge (twice: the first call warms allocations)
+        old.set_churn_variant(cv)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        new, o2n = old.churn(joins, leaves)
+        torch.cuda.synchronize()
+        tcv[cv] = time.perf_counter() - t0
+    tc = tcv[1]
     tm = ev_time(lambda: old.misplaced(new, o2n, keys, n), reps=2)
     lists, count, mask, target = old.misplaced(new, o2n, keys, n)
     torch.cuda.synchronize()
     out["C5"] = {"ring_old": N5, "ring_new": new.n, "keys": q5, "n": n,
                  "nsucc_s": tl, "nsucc_keys_per_s": q5 / tl,
-                 "churn_s_wall": tc,
+                 "churn_s_wall": tc, "churn_resort_s_wall": tcv[0],
                  "misplaced_s": tm, "misplaced_keys_per_s": q5 / tm,
                  "misplaced_algo_GBps": q5 * 139 / tm / 1e9,
                  "keys_with_misplaced_holder": int((mask != 0).sum()),

@@ -181,6 +181,12 @@ class Ring:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))
 
+    def set_churn_variant(self, v: int):
+        """Internal A/B switch: 0 = full re-sort, 1 = merge of sorted joins (default)."""
+        f = L.lib().cxi_set_churn_variant
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.check(f(self._h, v))
+
     def set_search_variant(self, v: int):
         """Internal A/B switch: 0 = Eytzinger (LDS top levels), 1 = bucket directory."""
         f = L.lib().cxi_set_search_variant

@@ -84,6 +84,7 @@ struct cx_ring {
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
     int dir_k = 1;
     int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory
+    int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
 
     EytView eyt() const {
         EytView v;
@@ -261,6 +262,60 @@ int ensure_route_table(cx_ring *r, hipStream_t s) {
             r->tree_valid = true;
         }
     }
+    return CX_OK;
+}
+
+// Merge-based churn: sorts the joins only; survivors keep their order (see
+// cx_kernels.hip "Merge-based churn").  Fills r->n, r->d_ring and o2n.
+int churn_merge(const cx_ring *old_ring, const cell128 *J0, size_t nj, const cell128 *L,
+                size_t nl, cx_ring *r, DBuf &o2n, hipStream_t s) {
+    const size_t n_old = old_ring->n;
+    SearchView v = old_ring->sv();
+    v.dir = old_ring->d_dir;
+    DBuf G, A, ws, jk0, jk1, jt0, jt1, pos, keep, ringbuf;
+    const size_t sw = cxk::scan_workspace_words(n_old + 2 > nj + 1 ? n_old + 2 : nj + 1);
+    const size_t rw = nj ? cxk::sort_workspace_words(nj) : 0;
+    CX_HIP(ws.alloc((sw > rw ? sw : rw) * sizeof(uint32_t)));
+    CX_HIP(G.alloc((n_old + 1) * sizeof(uint32_t)));
+    CX_HIP(A.alloc((n_old + 2) * sizeof(uint32_t)));
+    CX_HIP(hipMemsetAsync(G.p, 0, (n_old + 1) * sizeof(uint32_t), s));
+    CX_HIP(hipMemsetAsync(A.p, 0, (n_old + 2) * sizeof(uint32_t), s));
+    CX_HIP(cxk::merge_mark(v, old_ring->d_ring, L, nl, G.as<uint32_t>(), s));
+    const cell128 *J = J0;
+    if (nj) {
+        CX_HIP(jk0.alloc(nj * sizeof(cell128)));
+        CX_HIP(jk1.alloc(nj * sizeof(cell128)));
+        CX_HIP(jt0.alloc(nj * sizeof(uint32_t)));
+        CX_HIP(jt1.alloc(nj * sizeof(uint32_t)));
+        CX_HIP(cxk::copy_tagged(J0, nj, 0, jk0.as<cell128>(), jt0.as<uint32_t>(), s));
+        CX_HIP(cxk::radix_sort(jk0.as<cell128>(), jt0.as<uint32_t>(), jk1.as<cell128>(),
+                               jt1.as<uint32_t>(), nj, ws.as<uint32_t>(), s));
+        J = jk0.as<cell128>();
+        CX_HIP(pos.alloc(nj * sizeof(uint32_t)));
+        CX_HIP(keep.alloc((nj + 1) * sizeof(uint32_t)));
+        CX_HIP(hipMemsetAsync(keep.p, 0, (nj + 1) * sizeof(uint32_t), s));
+        CX_HIP(cxk::merge_join_pos(v, old_ring->d_ring, n_old, G.as<uint32_t>(), J, nj,
+                                   pos.as<uint32_t>(), keep.as<uint32_t>(), A.as<uint32_t>(), s));
+        CX_HIP(cxk::exclusive_scan(keep.as<uint32_t>(), nj + 1, ws.as<uint32_t>(), s));
+    }
+    CX_HIP(cxk::exclusive_scan(G.as<uint32_t>(), n_old + 1, ws.as<uint32_t>(), s));
+    CX_HIP(cxk::exclusive_scan(A.as<uint32_t>(), n_old + 2, ws.as<uint32_t>(), s));
+    uint32_t gone = 0, kept = 0;
+    CX_HIP(hipMemcpyAsync(&gone, G.as<uint32_t>() + n_old, sizeof(gone), hipMemcpyDeviceToHost,
+                          s));
+    CX_HIP(hipMemcpyAsync(&kept, A.as<uint32_t>() + n_old + 1, sizeof(kept),
+                          hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    const size_t m = n_old - gone + kept;
+    CX_CHECK(m >= 1, CX_E_INVALID, "churn would leave an empty ring");
+    CX_HIP(ringbuf.alloc(m * sizeof(cell128)));
+    CX_HIP(o2n.alloc(n_old * sizeof(uint32_t)));
+    CX_HIP(cxk::merge_scatter(old_ring->d_ring, n_old, G.as<uint32_t>(), A.as<uint32_t>(), J, nj,
+                              pos.as<uint32_t>(), keep.as<uint32_t>(), ringbuf.as<cell128>(),
+                              o2n.as<uint32_t>(), s));
+    r->n = m;
+    r->d_ring = ringbuf.as<cell128>();
+    ringbuf.release();
     return CX_OK;
 }
 
@@ -600,6 +655,21 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         int e;
         if ((e = stage_in(joins, nj, memkind, tj, &dj, s))) return e;
         if ((e = stage_in(leaves, nl, memkind, tl, &dl, s))) return e;
+        if (old_ring->churn_variant == 1) {
+            e = churn_merge(old_ring, reinterpret_cast<const cell128 *>(dj), nj,
+                            reinterpret_cast<const cell128 *>(dl), nl, r, o2n, s);
+            if (e) return e;
+            r->search_variant = old_ring->search_variant;
+            r->churn_variant = old_ring->churn_variant;
+            if ((e = build_search(r, s))) return e;
+            if (old_to_new) {
+                const hipMemcpyKind kind =
+                    memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+                CX_HIP(hipMemcpyAsync(old_to_new, o2n.p, n_old * sizeof(uint32_t), kind, s));
+            }
+            CX_HIP(hipStreamSynchronize(s));
+            return CX_OK;
+        }
         CX_HIP(gone.alloc(n_old));
         CX_HIP(hipMemsetAsync(gone.p, 0, n_old, s));
         CX_HIP(cxk::mark_leaves(old_ring->sv(), old_ring->d_ring,
@@ -638,6 +708,7 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         r->d_ring = ringbuf.as<cell128>();
         ringbuf.release();
         r->search_variant = old_ring->search_variant;
+        r->churn_variant = old_ring->churn_variant;
         {
             int e2 = build_search(r, s);
             if (e2) return e2;
@@ -892,6 +963,14 @@ int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= 0 && variant <= 4, CX_E_INVALID, "variant must be 0..4");
     ring->route_variant = variant;
+    return CX_OK;
+}
+
+// 0 = full re-sort of survivors + joins, 1 = merge of the sorted joins (default).
+int cxi_set_churn_variant(cx_ring *ring, int variant) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    ring->churn_variant = variant;
     return CX_OK;
 }
 

@@ -1602,7 +1602,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
         }
         if (bst == B_KS) {
             if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
-                pa = ld128(io.ring_ext + psrc);
+                if (pkind == ARC_NEW) pa = ld128(io.ring_ext + psrc);  // pred: local check only
                 pb = ld128(io.ring_ext + psrc + 1);
             }
             bst = B_PAIR;
@@ -2045,6 +2045,99 @@ hipError_t mark_leaves(const SearchView &sv, const cell128 *ring, const cell128 
     else
         k_mark_leaves<false><<<cx_grid(nl, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, ring, leaves,
                                                                                  nl, gone);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Merge-based churn: the surviving old ring is already
+// sorted, so only the joins are sorted; every element's new index follows from
+// two prefix sums over old positions,
+//   G[p] = 1 if old peer p leaves,  A[p] = # kept joins whose lower_bound is p,
+//   new(survivor p) = p - SG[p] + SA[p+1],
+//   new(kept join j) = rank of j among kept joins + pos_j - SG[pos_j],
+// and the new ring is written by one streaming scatter (no full re-sort).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(SUCC_BLOCK) void k_mark_leaves32(SearchView sv, const cell128 *ring,
+                                                              const cell128 *leaves, size_t nl,
+                                                              uint32_t *gone) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nl;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const u128 x = ld128(leaves + i);
+        const uint32_t s0 = dir_successor(sv, x);
+        if (ld128(ring + s0) == x) gone[s0] = 1;
+    }
+}
+
+// pos_j = first old index with id >= x (n if none); keep_j = not a repeat of
+// the previous sorted join and not the ID of a surviving peer (survivors win,
+// remote_peer_list.cpp:56-58).
+__global__ __launch_bounds__(SUCC_BLOCK) void k_join_pos(SearchView sv, const cell128 *ring,
+                                                         uint32_t n, const uint32_t *gone,
+                                                         const cell128 *J, size_t nj,
+                                                         uint32_t *pos, uint32_t *keep,
+                                                         uint32_t *A) {
+    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < nj;
+         j += (size_t)gridDim.x * blockDim.x) {
+        const u128 x = ld128(J + j);
+        uint32_t P = dir_successor(sv, x);
+        const u128 idp = ld128(ring + P);
+        if (P == 0 && idp < x) P = n;  // above the largest ID: appended at the end
+        const bool dup = j > 0 && ld128(J + j - 1) == x;
+        const bool coll = P < n && idp == x && !gone[P];
+        const uint32_t k = (!dup && !coll) ? 1u : 0u;
+        pos[j] = P;
+        keep[j] = k;
+        if (k) atomicAdd(&A[P], 1u);
+    }
+}
+
+__global__ void k_merge_survivors(const cell128 *ring, uint32_t n, const uint32_t *SG,
+                                  const uint32_t *SA, cell128 *out, uint32_t *o2n) {
+    for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < n;
+         p += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t sg = SG[p];
+        if (SG[p + 1] != sg) {
+            o2n[p] = CX_NONE;
+        } else {
+            const uint32_t ni = (uint32_t)p - sg + SA[p + 1];
+            st128(out + ni, ld128(ring + p));
+            o2n[p] = ni;
+        }
+    }
+}
+
+__global__ void k_merge_joins(const cell128 *J, size_t nj, const uint32_t *pos,
+                              const uint32_t *kidx, const uint32_t *SG, cell128 *out) {
+    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < nj;
+         j += (size_t)gridDim.x * blockDim.x) {
+        if (kidx[j + 1] == kidx[j]) continue;
+        const uint32_t P = pos[j];
+        st128(out + (kidx[j] + P - SG[P]), ld128(J + j));
+    }
+}
+
+hipError_t merge_mark(const SearchView &sv, const cell128 *ring, const cell128 *leaves,
+                      size_t nl, uint32_t *gone, hipStream_t s) {
+    if (nl == 0) return hipSuccess;
+    k_mark_leaves32<<<cx_grid(nl, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, ring, leaves, nl,
+                                                                          gone);
+    return hipGetLastError();
+}
+
+hipError_t merge_join_pos(const SearchView &sv, const cell128 *ring, size_t n,
+                          const uint32_t *gone, const cell128 *J, size_t nj, uint32_t *pos,
+                          uint32_t *keep, uint32_t *A, hipStream_t s) {
+    if (nj == 0) return hipSuccess;
+    k_join_pos<<<cx_grid(nj, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, ring, (uint32_t)n, gone,
+                                                                     J, nj, pos, keep, A);
+    return hipGetLastError();
+}
+
+hipError_t merge_scatter(const cell128 *ring, size_t n, const uint32_t *SG, const uint32_t *SA,
+                         const cell128 *J, size_t nj, const uint32_t *pos, const uint32_t *kidx,
+                         cell128 *out, uint32_t *o2n, hipStream_t s) {
+    if (n) k_merge_survivors<<<cx_grid(n, 256), 256, 0, s>>>(ring, (uint32_t)n, SG, SA, out, o2n);
+    if (nj) k_merge_joins<<<cx_grid(nj, 256), 256, 0, s>>>(J, nj, pos, kidx, SG, out);
     return hipGetLastError();
 }
 

@@ -92,6 +92,14 @@ hipError_t nsucc(const SearchView &ev, const cell128 *keys, size_t q, int n, uin
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const SearchView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,
                        uint8_t *gone, hipStream_t s);
+hipError_t merge_mark(const SearchView &sv, const cell128 *ring, const cell128 *leaves,
+                      size_t nl, uint32_t *gone, hipStream_t s);
+hipError_t merge_join_pos(const SearchView &sv, const cell128 *ring, size_t n,
+                          const uint32_t *gone, const cell128 *J, size_t nj, uint32_t *pos,
+                          uint32_t *keep, uint32_t *A, hipStream_t s);
+hipError_t merge_scatter(const cell128 *ring, size_t n, const uint32_t *SG, const uint32_t *SA,
+                         const cell128 *J, size_t nj, const uint32_t *pos, const uint32_t *kidx,
+                         cell128 *out, uint32_t *o2n, hipStream_t s);
 hipError_t misplaced_churn(const SearchView &ev_old, const SearchView &ev_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,

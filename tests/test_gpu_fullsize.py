@@ -65,13 +65,15 @@ def test_c3_routed_lookups(O, c3):
     assert (h1[:sample].cpu().numpy() == wh).all()
 
 
-def test_c5_shaped_churn(O):
+@pytest.mark.parametrize("churn", [0, 1])
+def test_c5_shaped_churn(O, churn):
     """1% joins + 1% leaves on a 2^20 ring; n=14 lists, misplaced mask and
     targets for 2^21 keys: all keys vs oracle."""
     import chordx
     n_old, q = 1 << 20, 1 << 21
     ids = O.splitmix_keys(0x5EED0007, n_old)
     old = chordx.Ring(ids)
+    old.set_churn_variant(churn)
     want_old = O.ring_build(ids)
     rng = np.random.default_rng(0x5EED0009)
     leaves = want_old[rng.choice(n_old, n_old // 100, replace=False)]

@@ -291,12 +291,14 @@ def test_dhash_insufficient(cx, O):
 
 
 # ---------------------------------------------------------------- a12 churn
+@pytest.mark.parametrize("churn", [0, 1])
 @pytest.mark.parametrize("search", [0, 1])
 @pytest.mark.parametrize("n_old,nj,nl", [(1, 1, 0), (5, 0, 2), (60, 3, 4), (20000, 200, 200)])
-def test_churn_and_misplaced(cx, O, n_old, nj, nl, search):
+def test_churn_and_misplaced(cx, O, n_old, nj, nl, search, churn):
     ids = O.splitmix_keys(7000 + n_old, n_old)
     old = cx.Ring(ids)
     old.set_search_variant(search)
+    old.set_churn_variant(churn)
     want_old = O.ring_build(ids)
     rng = np.random.default_rng(n_old)
     joins = O.splitmix_keys(7100 + n_old, nj)
@@ -313,6 +315,35 @@ def test_churn_and_misplaced(cx, O, n_old, nj, nl, search):
         wl, wc, wm, wt = O.misplaced(want_old, want_new, want_o2n, keys, n)
         assert (lists == wl).all() and (count == wc).all()
         assert (mask == wm).all() and (target == wt).all()
+
+
+@pytest.mark.parametrize("churn", [0, 1])
+def test_churn_edge_cases(cx, O, churn):
+    """Joins repeating each other, a join taking a leaving peer's ID, joins
+    below the smallest / above the largest ID, leaves of unknown IDs, and a
+    churn that replaces every peer but one."""
+    base = O.splitmix_keys(4242, 300)
+    want_old = O.ring_build(base)
+    v = O.ints_from_keys(want_old)
+    cases = [
+        (O.keys_from_ints([v[5] + 1, v[5] + 1, v[5] + 1, 0, MAX, v[0] - 1, v[-1] + 1]),
+         O.keys_from_ints([v[7], v[8], 12345])),
+        (O.keys_from_ints([v[7], v[9], (v[9] + v[10]) // 2]),    # join == leaver's ID
+         O.keys_from_ints([v[7], v[9], v[10]])),
+        (O.splitmix_keys(77, 50), want_old[1:]),                   # all but one leave
+        (O.keys_from_ints([]), want_old[:0]),                      # no-op
+        (O.keys_from_ints([v[3], v[4]]), want_old[:0]),            # joins = survivors only
+    ]
+    for joins, leaves in cases:
+        old = cx.Ring(want_old)
+        old.set_churn_variant(churn)
+        new, o2n = old.churn(joins, leaves)
+        want_new, want_o2n = O.churn(want_old, joins, leaves)
+        assert (new.ids() == want_new).all() and (o2n == want_o2n).all()
+    old = cx.Ring(want_old[:2])
+    old.set_churn_variant(churn)
+    with pytest.raises(cx.ChordError):
+        old.churn(O.keys_from_ints([]), want_old[:2])               # empty ring
 
 
 def test_global_maintenance_fixture(cx, O, refvec):
