@@ -184,6 +184,59 @@ int cx_uuid5_dns(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx
 int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t offset,
                      int device, void *hip_stream);
 
+/* ---- hex codec of keys on the wire ----------------------
+ * cx_hex_parse: ChordKey(hex, hashed = true) = uint256("0x" + s) (key.h:73-75)
+ * for each string bytes[offsets[i] .. offsets[i+1]); digits of either case, no
+ * prefix.  out = value mod 2^128 (the engine's ring value), ok[i] = 0 for an
+ * empty string or a non-hex character (where boost's parse throws).
+ * cx_hex_format: std::string(key) = IntToHexStr (key.h:41-47) -- lowercase,
+ * no leading zeros, "0" for zero -- into out[32 i .. 32 i + len[i]), the rest of
+ * each 32-byte slot zero.  Both run on the GPU. */
+int cx_hex_parse(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx_u128 *out,
+                 uint8_t *ok, int memkind, int device);
+int cx_hex_format(const cx_u128 *keys, size_t count, char *out, uint8_t *len, int memkind,
+                  int device);
+
+/* ---- Rabin IDA: DHash payload coding ---------------------
+ * IDA(n, m, p) of src/ida/ida.cpp over a batch of ragged blocks (one datum
+ * each): block b = data[offsets[b] .. offsets[b+1]), S_b = ceil(len_b / m)
+ * segments, seg_offsets[b] = sum of S_c for c < b (cx_ida_segments, host).
+ * cx_ida_encode: IDA::Encode (ida.cpp:59-73): fragment i (index i + 1,
+ *   data_block.cpp:12-13) of block b is frags[n*seg_offsets[b] + i*S_b ..+ S_b).
+ * cx_ida_decode: IDA::Decode (ida.cpp:120-162) from m fragment rows per block
+ *   (frags[m*seg_offsets[b] + k*S_b ..]) with 1-based indices
+ *   indices[b*m + k]: values (< p) at out[m*seg_offsets[b] ..], kept length
+ *   out_len[b] (trailing zeros dropped as the reference does); out_len[b] =
+ *   UINT64_MAX when the indices have no inverse ("N is not invertible",
+ *   matrix_math.cpp:81-82).  The inverse follows matrix_math.cpp:103-168
+ *   including its int arithmetic as compiled (wrap-around).
+ * Limits: 1 <= m < n <= 32, n < p <= 46340.  DHash uses (14, 10, 257). */
+int cx_ida_segments(const uint64_t *offsets, size_t blocks, int m, uint64_t *seg_offsets);
+int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, size_t blocks, int n, int m,
+                  int p, uint16_t *frags, int memkind, int device);
+int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint8_t *indices,
+                  size_t blocks, int m, int p, uint16_t *out, uint64_t *out_len, int memkind,
+                  int device);
+
+/* ---- wire bridge: GET_SUCC over JSON ---------------------
+ * A ring of peers named "ip:port" (IDs = UUIDv5 of the name,
+ * abstract_chord_peer.cpp:21) answering the reference's request objects
+ * (handler map chord_peer.cpp:15-40, server.h:194-210):
+ *   {"COMMAND":"GET_SUCC","KEY":<hex>[,"SRC":"ip:port"]}
+ *     -> {"ID","MIN_KEY","IP_ADDR","PORT","SUCCESS":true}  (remote_peer.cpp:83-91)
+ *   {"COMMAND":"GET_SUCC_BATCH","KEYS":[<hex>...][,"SRC":"ip:port"|"SRCS":[...]]}
+ *     -> {"RESULTS":[{"ID","MIN_KEY","IP_ADDR","PORT","HOPS"}...],"SUCCESS":true}
+ * Failures answer {"SUCCESS":false,"ERRORS":<message>} as server.h:156-165
+ * does.  SRC is the peer the request is issued at (default: ring index 0).
+ * The response is malloc'd; release it with cx_wire_free. */
+typedef struct cx_wire cx_wire;
+int cx_wire_create(const char *const *addrs, size_t n, int device, cx_wire **out);
+int cx_wire_destroy(cx_wire *wire);
+int cx_wire_ring(const cx_wire *wire, const cx_ring **ring);
+int cx_wire_handle(cx_wire *wire, const char *request, size_t len, char **response,
+                   size_t *response_len);
+void cx_wire_free(char *response);
+
 /* ---- arc-sharded routing (multi-GPU layout 2) -------------------
  * Each rank keeps the replicated sorted ring but the lookahead-tree rows of its
  * own arc of peers only, arc g of G = [g n / G, (g+1) n / G).  A lookup walks

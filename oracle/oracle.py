@@ -172,6 +172,12 @@ def lib():
         L.or_misplaced.argtypes = [vp, sz, vp, sz, vp, vp, sz, i, vp, vp, vp, vp, i]
         L.or_misplaced_holders.argtypes = [vp, sz, vp, sz, vp, i, i, vp, vp, vp, vp, i]
         L.or_splitmix_keys.argtypes = [ctypes.c_uint64, sz, sz, vp]
+        L.or_ida_encoding_matrix.argtypes = [i, i, i, vp]
+        L.or_ida_vandermonde_inverse.restype = i
+        L.or_ida_vandermonde_inverse.argtypes = [vp, i, i, vp]
+        L.or_ida_encode_batch.argtypes = [vp, vp, sz, i, i, i, vp]
+        L.or_ida_decode_batch.restype = i
+        L.or_ida_decode_batch.argtypes = [vp, vp, vp, sz, i, i, vp, vp]
         _lib = L
     return _lib
 
@@ -311,4 +317,56 @@ def misplaced_holders(ring, keys, holders, n, threads=None):
 def splitmix_keys(seed: int, count: int, offset: int = 0) -> np.ndarray:
     out = np.empty((count, 2), dtype=np.uint64)
     lib().or_splitmix_keys(seed, offset, count, _p(out))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Rabin IDA (ida_oracle.c): ida.cpp / matrix_math.cpp restated.
+# ---------------------------------------------------------------------------
+def ida_segments(lengths, m):
+    """seg_offsets (blocks + 1,) uint64 of ceil(len / m) segments per block."""
+    S = [(int(n) + m - 1) // m for n in lengths]
+    out = np.zeros(len(S) + 1, dtype=np.uint64)
+    out[1:] = np.cumsum(S, dtype=np.uint64)
+    return out
+
+
+def ida_encode(blocks, n=14, m=10, p=257):
+    """Fragments of each datum: list of (n, S_b) uint16 arrays (IDA::Encode)."""
+    blocks = [bytes(b) for b in blocks]
+    offs = np.zeros(len(blocks) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in blocks], dtype=np.uint64)
+    data = np.frombuffer(b"".join(blocks) + b"\0", dtype=np.uint8)
+    seg = ida_segments([len(b) for b in blocks], m)
+    frags = np.zeros(max(1, int(seg[-1]) * n), dtype=np.uint16)
+    lib().or_ida_encode_batch(_p(data), _p(offs), len(blocks), n, m, p, _p(frags))
+    out = []
+    for b in range(len(blocks)):
+        S = int(seg[b + 1] - seg[b])
+        out.append(frags[n * int(seg[b]): n * int(seg[b]) + n * S].reshape(n, S).copy())
+    return out
+
+
+def ida_decode(frag_rows, indices, m=10, p=257):
+    """IDA::Decode of each block from m fragment rows ((m, S_b) arrays) with
+    1-based indices: list of uint16 value arrays (trailing zeros dropped)."""
+    seg = ida_segments([np.asarray(f).shape[1] * m for f in frag_rows], m)
+    flat = np.concatenate([np.asarray(f, dtype=np.uint16).reshape(-1) for f in frag_rows] +
+                          [np.zeros(1, np.uint16)])
+    idx = np.ascontiguousarray(np.asarray(indices, dtype=np.uint8).reshape(-1, m))
+    out = np.zeros(max(1, int(seg[-1]) * m), dtype=np.uint16)
+    ln = np.zeros(len(frag_rows), dtype=np.uint64)
+    if lib().or_ida_decode_batch(_p(flat), _p(seg), _p(idx), len(frag_rows), m, p, _p(out),
+                                 _p(ln)) != 0:
+        raise RuntimeError("N is not invertible")
+    return [out[m * int(seg[b]): m * int(seg[b]) + int(ln[b])].copy()
+            for b in range(len(frag_rows))]
+
+
+def ida_inverse(basis, p=257):
+    m = len(basis)
+    b = np.asarray(basis, dtype=np.int32)
+    out = np.zeros((m, m), dtype=np.int32)
+    if lib().or_ida_vandermonde_inverse(_p(b), m, p, _p(out)) != 0:
+        raise RuntimeError("N is not invertible")
     return out

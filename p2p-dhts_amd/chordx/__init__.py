@@ -8,9 +8,12 @@ from ._lib import (CX_FINGERS, CX_HOP_CAP, CX_MAX_NSUCC, CX_NONE, CX_Q_BADPEER, 
                    CX_Q_OK, ChordError, device_count, lib)
 from .key import ChordKey
 from .ring import Ring, fill_splitmix, in_between, uuid5_dns
+from .wire import Wire, hex_format, hex_parse
+from . import ida
 
 __all__ = [
     "Ring", "ChordKey", "ChordError", "in_between", "fill_splitmix", "uuid5_dns", "device_count",
+    "Wire", "hex_parse", "hex_format",
     "lib",
     "CX_FINGERS", "CX_NONE", "CX_HOP_CAP", "CX_MAX_NSUCC", "CX_Q_OK", "CX_Q_HOPCAP",
     "CX_Q_BADPEER",

@@ -41,6 +41,9 @@ EXPORTS = (
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
     "cx_uuid5_dns", "cx_fill_splitmix",
     "cx_arc_build", "cx_arc_seed", "cx_arc_step", "cx_arc_bucket",
+    "cx_hex_parse", "cx_hex_format",
+    "cx_ida_segments", "cx_ida_encode", "cx_ida_decode",
+    "cx_wire_create", "cx_wire_destroy", "cx_wire_ring", "cx_wire_handle", "cx_wire_free",
 )
 
 CX_ARC_NEW, CX_ARC_RESULT, CX_ARC_WALK, CX_ARC_NONE = 0, 1, 2, 3
@@ -94,6 +97,17 @@ def lib() -> ctypes.CDLL:
         "cx_in_between": ([vp, vp, vp, sz, i, vp, i], i),
         "cx_uuid5_dns": ([vp, vp, sz, vp, i, i], i),
         "cx_fill_splitmix": ([vp, sz, u64, u64, i, vp], i),
+        "cx_ida_segments": ([vp, sz, i, vp], i),
+        "cx_ida_encode": ([vp, vp, sz, i, i, i, vp, i, i], i),
+        "cx_ida_decode": ([vp, vp, vp, sz, i, i, vp, vp, i, i], i),
+        "cx_hex_parse": ([vp, vp, sz, vp, vp, i, i], i),
+        "cx_hex_format": ([vp, sz, vp, vp, i, i], i),
+        "cx_wire_create": ([ctypes.POINTER(ctypes.c_char_p), sz, i, pp], i),
+        "cx_wire_destroy": ([vp], i),
+        "cx_wire_ring": ([vp, pp], i),
+        "cx_wire_handle": ([vp, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_void_p),
+                            ctypes.POINTER(ctypes.c_size_t)], i),
+        "cx_wire_free": ([vp], None),
         "cx_arc_build": ([vp, ctypes.c_uint32, ctypes.c_uint32], i),
         "cx_arc_seed": ([vp, i, vp, vp, sz, vp], i),
         "cx_arc_step": ([vp, i, vp, sz, vp, vp, vp, vp], i),

@@ -1,0 +1,146 @@
+"""Rabin IDA on the GPU: DHash's payload coding (src/ida/ida.cpp, data_block.cpp).
+
+encode / decode are batched over ragged blocks (cx_ida_encode / cx_ida_decode);
+DataBlock mirrors the reference class of the same name: a value is split into
+n fragments (indices 1..n, data_block.cpp:12-13) of which any m rebuild it
+(DHashPeer::Read decodes from the m lowest indices it collected,
+dhash_peer.cpp:163-197 via std::set ordering).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+try:
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+
+def _is_dev(x) -> bool:
+    return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if _is_dev(a):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def segments(lengths, m: int) -> np.ndarray:
+    """seg_offsets (blocks + 1,) uint64: prefix sums of ceil(len / m)."""
+    offs = np.zeros(len(lengths) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(np.asarray(lengths, dtype=np.uint64))
+    seg = np.zeros_like(offs)
+    L.check(L.lib().cx_ida_segments(_ptr(offs), len(lengths), m, _ptr(seg)))
+    return seg
+
+
+def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0):
+    """Raw batched encode.  data: uint8 bytes, offsets: (blocks + 1,) uint64
+    (numpy, or torch device tensors).  Returns (frags uint16, seg_offsets)."""
+    blocks = offsets.shape[0] - 1
+    off_h = offsets.cpu().numpy() if _is_dev(offsets) else np.asarray(offsets, np.uint64)
+    seg = np.zeros(blocks + 1, dtype=np.uint64)
+    L.check(L.lib().cx_ida_segments(_ptr(np.ascontiguousarray(off_h)), blocks, m, _ptr(seg)))
+    total = int(seg[-1]) * n
+    if _is_dev(data):
+        frags = torch.empty(max(total, 1), dtype=torch.int16, device=data.device)
+        mk = L.CX_MEM_DEVICE
+    else:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        frags = np.zeros(max(total, 1), dtype=np.uint16)
+        mk = L.CX_MEM_HOST
+    L.check(L.lib().cx_ida_encode(_ptr(data), _ptr(offsets if mk == L.CX_MEM_DEVICE else off_h),
+                                  blocks, n, m, p, _ptr(frags), mk, device))
+    return frags, seg
+
+
+def decode_flat(frags, seg_offsets, indices, m=10, p=257, device: int = 0):
+    """Raw batched decode; returns (values uint16, out_len uint64)."""
+    blocks = seg_offsets.shape[0] - 1
+    if _is_dev(frags):
+        total = int(seg_offsets[-1].item()) * m
+        out = torch.empty(max(total, 1), dtype=torch.int16, device=frags.device)
+        ln = torch.empty(max(blocks, 1), dtype=torch.int64, device=frags.device)
+        mk = L.CX_MEM_DEVICE
+    else:
+        frags = np.ascontiguousarray(frags, dtype=np.uint16)
+        seg_offsets = np.ascontiguousarray(seg_offsets, dtype=np.uint64)
+        indices = np.ascontiguousarray(indices, dtype=np.uint8)
+        out = np.zeros(max(int(seg_offsets[-1]) * m, 1), dtype=np.uint16)
+        ln = np.zeros(max(blocks, 1), dtype=np.uint64)
+        mk = L.CX_MEM_HOST
+    L.check(L.lib().cx_ida_decode(_ptr(frags), _ptr(seg_offsets), _ptr(indices), blocks, m, p,
+                                  _ptr(out), _ptr(ln), mk, device))
+    return out, ln
+
+
+def encode(blocks, n=14, m=10, p=257, device: int = 0):
+    """List of (n, S_b) uint16 fragment matrices, one per datum (bytes)."""
+    blocks = [bytes(b) for b in blocks]
+    offs = np.zeros(len(blocks) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in blocks], dtype=np.uint64)
+    data = np.frombuffer(b"".join(blocks) + b"\0", dtype=np.uint8)
+    frags, seg = encode_flat(data, offs, n, m, p, device)
+    return [frags[n * int(seg[b]): n * int(seg[b + 1])].reshape(n, -1).copy()
+            for b in range(len(blocks))]
+
+
+def decode(frag_rows, indices, m=10, p=257, device: int = 0):
+    """Values (uint16 arrays) decoded from m fragment rows per block with their
+    1-based indices; None for a block whose indices have no inverse."""
+    S = [np.asarray(f).shape[1] for f in frag_rows]
+    seg = np.zeros(len(S) + 1, dtype=np.uint64)
+    seg[1:] = np.cumsum(S, dtype=np.uint64)
+    flat = np.concatenate([np.asarray(f, dtype=np.uint16).reshape(-1) for f in frag_rows] +
+                          [np.zeros(1, np.uint16)])
+    idx = np.asarray(indices, dtype=np.uint8).reshape(len(frag_rows), m)
+    out, ln = decode_flat(flat, seg, idx, m, p, device)
+    res = []
+    for b in range(len(frag_rows)):
+        if int(ln[b]) == 0xFFFFFFFFFFFFFFFF:
+            res.append(None)
+        else:
+            res.append(out[m * int(seg[b]): m * int(seg[b]) + int(ln[b])].copy())
+    return res
+
+
+class DataBlock:
+    """DataBlock (data_block.cpp:4-97): a value and its n IDA fragments."""
+
+    def __init__(self, value, n=14, m=10, p=257, device: int = 0):
+        self.n, self.m, self.p, self.device = n, m, p, device
+        raw = value.encode() if isinstance(value, str) else bytes(value)
+        f = encode([raw], n, m, p, device)[0]
+        self.fragments = [(i + 1, f[i]) for i in range(n)]  # (INDEX, FRAGMENT)
+        self.original = np.frombuffer(raw, dtype=np.uint8).astype(np.uint16)
+
+    @classmethod
+    def from_fragments(cls, fragments, n=14, m=10, p=257, device: int = 0):
+        """DataBlock(vector<DataFragment>) (data_block.cpp:30-54): decode from
+        the first m fragments given, then re-encode all n."""
+        if len(fragments) < m:
+            raise L.ChordError(L.CX_E_INSUFFICIENT, f"{m} frags are required to decode.")
+        first = fragments[:m]
+        vals = decode([np.stack([np.asarray(v, np.uint16) for _, v in first])],
+                      [[i for i, _ in first]], m, p, device)[0]
+        if vals is None:
+            raise L.ChordError(L.CX_E_INVALID, "N is not invertible")
+        self = cls.__new__(cls)
+        self.n, self.m, self.p, self.device = n, m, p, device
+        self.original = vals
+        f = encode([bytes((vals & 0xFF).astype(np.uint8))], n, m, p, device)[0] \
+            if vals.max(initial=0) < 256 else None
+        self.fragments = [(i + 1, f[i]) for i in range(n)] if f is not None else []
+        return self
+
+    def decode(self) -> str:
+        """DataBlock::Decode (data_block.cpp:81-97): chars, trailing NULs dropped."""
+        s = "".join(chr(int(c) & 0xFF) for c in self.original)
+        return s.rstrip("\0")

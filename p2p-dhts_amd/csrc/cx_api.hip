@@ -860,6 +860,192 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
     return CX_OK;
 }
 
+int cx_hex_parse(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx_u128 *out,
+                 uint8_t *ok, int memkind, int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    CX_CHECK(device >= 0 && device < ndev, CX_E_INVALID, "bad device ordinal");
+    if (count == 0) return CX_OK;
+    CX_CHECK(offsets && out && ok, CX_E_INVALID, "null argument");
+    CX_HIP(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    DBuf to, tb, tout, tok;
+    const uint64_t *doff;
+    const uint8_t *dbytes;
+    cx_u128 *dout;
+    uint8_t *dok;
+    int rc;
+    if ((rc = stage_in(offsets, count + 1, memkind, to, &doff, s))) return rc;
+    uint64_t nbytes = 0;
+    if (memkind == CX_MEM_HOST) {
+        nbytes = offsets[count];
+        CX_CHECK(offsets[0] == 0, CX_E_INVALID, "offsets[0] must be 0");
+        for (size_t i = 0; i < count; ++i)
+            CX_CHECK(offsets[i] <= offsets[i + 1], CX_E_INVALID, "offsets not ascending");
+    } else {
+        CX_HIP(hipMemcpy(&nbytes, offsets + count, sizeof(nbytes), hipMemcpyDeviceToHost));
+    }
+    if ((rc = stage_in(bytes, (size_t)nbytes, memkind, tb, &dbytes, s))) return rc;
+    if ((rc = stage_out(out, count, memkind, tout, &dout))) return rc;
+    if ((rc = stage_out(ok, count, memkind, tok, &dok))) return rc;
+    CX_HIP(cxk::hex_parse(dbytes, doff, count, reinterpret_cast<cell128 *>(dout), dok, s));
+    if ((rc = finish_out(ok, dok, count, memkind, s))) return rc;
+    return finish_out(out, dout, count, memkind, s);
+}
+
+int cx_hex_format(const cx_u128 *keys, size_t count, char *out, uint8_t *len, int memkind,
+                  int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    CX_CHECK(device >= 0 && device < ndev, CX_E_INVALID, "bad device ordinal");
+    if (count == 0) return CX_OK;
+    CX_CHECK(keys && out && len, CX_E_INVALID, "null argument");
+    CX_HIP(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    DBuf tk, tout, tlen;
+    const cx_u128 *dk;
+    char *dout;
+    uint8_t *dlen;
+    int rc;
+    if ((rc = stage_in(keys, count, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(out, count * 32, memkind, tout, &dout))) return rc;
+    if ((rc = stage_out(len, count, memkind, tlen, &dlen))) return rc;
+    CX_HIP(cxk::hex_format(reinterpret_cast<const cell128 *>(dk), count, dout, dlen, s));
+    if ((rc = finish_out(len, dlen, count, memkind, s))) return rc;
+    return finish_out(out, dout, count * 32, memkind, s);
+}
+
+// ---- Rabin IDA --------------------------------------------------------------
+namespace {
+int ida_check(int n, int m, int p) {
+    CX_CHECK(m >= 1 && n > m && n <= 32, CX_E_INVALID, "IDA needs 1 <= m < n <= 32");
+    CX_CHECK(p > n && p <= 46340, CX_E_INVALID, "IDA needs n < p <= 46340");  // ida.cpp:54-56
+    return CX_OK;
+}
+
+int device_ok(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CX_E_HIP, "no HIP device: chordx has no host compute path");
+    CX_CHECK(device >= 0 && device < ndev, CX_E_INVALID, "bad device ordinal");
+    CX_HIP(hipSetDevice(device));
+    return CX_OK;
+}
+
+// Host copy of a (blocks + 1) offset array given in either memory kind.
+int host_offsets(const uint64_t *offs, size_t blocks, int memkind, std::vector<uint64_t> &h) {
+    h.resize(blocks + 1);
+    if (memkind == CX_MEM_DEVICE)
+        CX_HIP(hipMemcpy(h.data(), offs, (blocks + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    else
+        std::memcpy(h.data(), offs, (blocks + 1) * sizeof(uint64_t));
+    CX_CHECK(h[0] == 0, CX_E_INVALID, "offsets[0] must be 0");
+    for (size_t b = 0; b < blocks; ++b)
+        CX_CHECK(h[b] <= h[b + 1], CX_E_INVALID, "offsets not ascending");
+    return CX_OK;
+}
+}  // namespace
+
+int cx_ida_segments(const uint64_t *offsets, size_t blocks, int m, uint64_t *seg_offsets) {
+    CX_CHECK(offsets && seg_offsets && m >= 1, CX_E_INVALID, "bad argument");
+    seg_offsets[0] = 0;
+    for (size_t b = 0; b < blocks; ++b) {
+        CX_CHECK(offsets[b] <= offsets[b + 1], CX_E_INVALID, "offsets not ascending");
+        seg_offsets[b + 1] = seg_offsets[b] + (offsets[b + 1] - offsets[b] + m - 1) / m;
+    }
+    return CX_OK;
+}
+
+int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, size_t blocks, int n, int m,
+                  int p, uint16_t *frags, int memkind, int device) {
+    int rc;
+    if ((rc = ida_check(n, m, p))) return rc;
+    if ((rc = device_ok(device))) return rc;
+    if (blocks == 0) return CX_OK;
+    CX_CHECK(offsets && frags, CX_E_INVALID, "null argument");
+    std::vector<uint64_t> ho, hs(blocks + 1);
+    if ((rc = host_offsets(offsets, blocks, memkind, ho))) return rc;
+    if ((rc = cx_ida_segments(ho.data(), blocks, m, hs.data()))) return rc;
+    const uint64_t segs = hs[blocks], nbytes = ho[blocks];
+    hipStream_t s = nullptr;
+    DBuf td, to, tseg, tf;
+    const uint8_t *dd;
+    const uint64_t *doff;
+    uint16_t *df;
+    if ((rc = stage_in(data, (size_t)nbytes, memkind, td, &dd, s))) return rc;
+    if ((rc = stage_in(memkind == CX_MEM_DEVICE ? offsets : ho.data(), blocks + 1, memkind, to,
+                       &doff, s)))
+        return rc;
+    CX_HIP(tseg.alloc((blocks + 1) * sizeof(uint64_t)));
+    CX_HIP(hipMemcpyAsync(tseg.p, hs.data(), (blocks + 1) * sizeof(uint64_t),
+                          hipMemcpyHostToDevice, s));
+    if ((rc = stage_out(frags, (size_t)(segs * n), memkind, tf, &df))) return rc;
+    CX_HIP(cxk::ida_encode(dd, doff, tseg.as<uint64_t>(), blocks, segs, n, m, p, df, s));
+    if ((rc = finish_out(frags, df, (size_t)(segs * n), memkind, s))) return rc;
+    CX_HIP(hipStreamSynchronize(s));  // hs is a host stack buffer
+    return CX_OK;
+}
+
+int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint8_t *indices,
+                  size_t blocks, int m, int p, uint16_t *out, uint64_t *out_len, int memkind,
+                  int device) {
+    int rc;
+    CX_CHECK(m >= 1 && m < 32 && p > m + 1 && p <= 46340, CX_E_INVALID,
+             "IDA needs 1 <= m < 32, m + 1 < p <= 46340");
+    if ((rc = device_ok(device))) return rc;
+    if (blocks == 0) return CX_OK;
+    CX_CHECK(seg_offsets && indices && out_len, CX_E_INVALID, "null argument");
+    std::vector<uint64_t> hs;
+    if ((rc = host_offsets(seg_offsets, blocks, memkind, hs))) return rc;
+    const uint64_t segs = hs[blocks];
+    CX_CHECK(segs == 0 || (frags && out), CX_E_INVALID, "null argument");
+    CX_CHECK(blocks < (1ull << 32), CX_E_INVALID, "too many blocks");
+    hipStream_t s = nullptr;
+    DBuf tf, tsg, ti, tout, tlen, flag, flag2, ws, run_of, run_start, inv, okf;
+    const uint16_t *dfr;
+    const uint64_t *dseg;
+    const uint8_t *didx;
+    uint16_t *dout;
+    uint64_t *dlen;
+    if ((rc = stage_in(frags, (size_t)(segs * m), memkind, tf, &dfr, s))) return rc;
+    if ((rc = stage_in(seg_offsets, blocks + 1, memkind, tsg, &dseg, s))) return rc;
+    if ((rc = stage_in(indices, blocks * (size_t)m, memkind, ti, &didx, s))) return rc;
+    if ((rc = stage_out(out, (size_t)(segs * m), memkind, tout, &dout))) return rc;
+    if ((rc = stage_out(out_len, blocks, memkind, tlen, &dlen))) return rc;
+    // runs of equal index lists share one inverse
+    CX_HIP(flag.alloc(blocks * sizeof(uint32_t)));
+    CX_HIP(flag2.alloc(blocks * sizeof(uint32_t)));
+    CX_HIP(ws.alloc(cxk::scan_workspace_words(blocks) * sizeof(uint32_t)));
+    CX_HIP(cxk::ida_runs(didx, blocks, m, flag.as<uint32_t>(), s));
+    CX_HIP(hipMemcpyAsync(flag2.p, flag.p, blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    CX_HIP(cxk::exclusive_scan(flag2.as<uint32_t>(), blocks, ws.as<uint32_t>(), s));
+    uint32_t last_excl = 0, last_raw = 0;
+    CX_HIP(hipMemcpyAsync(&last_excl, flag2.as<uint32_t>() + blocks - 1, 4,
+                          hipMemcpyDeviceToHost, s));
+    CX_HIP(hipMemcpyAsync(&last_raw, flag.as<uint32_t>() + blocks - 1, 4, hipMemcpyDeviceToHost,
+                          s));
+    CX_HIP(hipStreamSynchronize(s));
+    const size_t runs = (size_t)last_excl + last_raw;
+    CX_HIP(run_of.alloc(blocks * sizeof(uint32_t)));
+    CX_HIP(run_start.alloc(runs * sizeof(uint32_t)));
+    CX_HIP(inv.alloc(runs * (size_t)m * m * sizeof(int32_t)));
+    CX_HIP(okf.alloc(runs));
+    CX_HIP(cxk::ida_run_index(flag2.as<uint32_t>(), flag.as<uint32_t>(), blocks,
+                              run_of.as<uint32_t>(), run_start.as<uint32_t>(), s));
+    CX_HIP(cxk::ida_inverse(didx, run_start.as<uint32_t>(), runs, m, p, inv.as<int32_t>(),
+                            okf.as<uint8_t>(), s));
+    CX_HIP(hipMemsetAsync(dlen, 0, blocks * sizeof(uint64_t), s));
+    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, segs, m, p, inv.as<int32_t>(),
+                           run_of.as<uint32_t>(), okf.as<uint8_t>(), dout, dlen, s));
+    CX_HIP(cxk::ida_mark_failed(run_of.as<uint32_t>(), okf.as<uint8_t>(), blocks, dlen, s));
+    if ((rc = finish_out(out_len, dlen, blocks, memkind, s))) return rc;
+    if ((rc = finish_out(out, dout, (size_t)(segs * m), memkind, s))) return rc;
+    CX_HIP(hipStreamSynchronize(s));
+    return CX_OK;
+}
+
 // ---- arc-sharded routing --------------------------------------------------
 int cx_arc_build(cx_ring *ring, uint32_t lo, uint32_t hi) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
@@ -954,6 +1140,9 @@ int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t
     }
     return CX_OK;
 }
+
+// ---- internal (not part of chordx.h): error reporting for cx_wire.cpp
+int cxi_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
 
 // ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
 // and parity tests.  0 = finger + ring gathers per hop, 1 = route table,

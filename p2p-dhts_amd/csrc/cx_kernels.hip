@@ -2433,6 +2433,308 @@ hipError_t uuid5(const uint8_t *bytes, const uint64_t *offs, size_t count, cell1
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Hex codec of keys on the wire.  Parse: ChordKey(hex, hashed = true) =
+// uint256("0x" + s) (key.h:73-75) -- hex digits of either case, no prefix;
+// the engine keeps the value mod 2^128 (what every ring comparison reads,
+// key.h:103-131).  Format: std::string(key) = IntToHexStr (key.h:41-47):
+// lowercase, no leading zeros, "0" for zero; one 32-byte slot per key.
+// ---------------------------------------------------------------------------
+__global__ void k_hex_parse(const uint8_t *bytes, const uint64_t *offs, size_t count,
+                            cell128 *out, uint8_t *ok) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t o = offs[i], e = offs[i + 1];
+        u128 v = 0;
+        bool good = e > o;
+        for (uint64_t k = o; k < e; ++k) {
+            const uint32_t c = bytes[k];
+            uint32_t d;
+            if (c >= '0' && c <= '9') d = c - '0';
+            else if (c >= 'a' && c <= 'f') d = c - 'a' + 10;
+            else if (c >= 'A' && c <= 'F') d = c - 'A' + 10;
+            else { good = false; d = 0; }
+            v = (v << 4) | d;
+        }
+        st128(out + i, good ? v : (u128)0);
+        ok[i] = good ? 1 : 0;
+    }
+}
+
+__global__ void k_hex_format(const cell128 *keys, size_t count, uint4 *out, uint8_t *len) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const u128 v = ld128(keys + i);
+        const int nd = v == 0 ? 1 : msb128(v) / 4 + 1;
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int pos = 4 * j + b;
+                if (pos < nd) {
+                    const uint32_t d = (uint32_t)(v >> (4 * (nd - 1 - pos))) & 15u;
+                    word |= (d < 10 ? '0' + d : 'a' + d - 10) << (8 * b);
+                }
+            }
+            w[j] = word;
+        }
+        out[2 * i] = make_uint4(w[0], w[1], w[2], w[3]);
+        out[2 * i + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+        len[i] = (uint8_t)nd;
+    }
+}
+
+hipError_t hex_parse(const uint8_t *bytes, const uint64_t *offs, size_t count, cell128 *out,
+                     uint8_t *ok, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    k_hex_parse<<<cx_grid(count, 256), 256, 0, s>>>(bytes, offs, count, out, ok);
+    return hipGetLastError();
+}
+
+hipError_t hex_format(const cell128 *keys, size_t count, char *out, uint8_t *len, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    k_hex_format<<<cx_grid(count, 256), 256, 0, s>>>(keys, count, reinterpret_cast<uint4 *>(out),
+                                                     len);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Rabin IDA (DHash payload coding): src/ida/ida.cpp and
+// src/ida/matrix_math.cpp.  Ragged blocks; block b has S_b = ceil(len_b / m)
+// segments of m values and seg[b] = prefix sum of S_b.
+//   encode: fragment i value s = sum_k a^k v_k mod p, a = i + 1
+//           (ConstructEncodingMatrix + InnerProduct, ida.cpp:59-73)
+//   decode: inverse Vandermonde of the fragment indices (VandermondeInverse,
+//           matrix_math.cpp:103-168, int arithmetic wrapping as compiled) times
+//           the fragment rows, read segment-wise, trailing zeros dropped
+//           (ida.cpp:120-162).
+// HBM-bound byte/integer streams: one lane per segment, m-value rows read and
+// written coalesced across the wave; no MFMA (values are mod p, 14 MACs/byte).
+// ---------------------------------------------------------------------------
+constexpr int IDA_MAX_N = 32;
+
+// x mod p for 32-bit x (Lemire: M = floor((2^64 - 1) / p) + 1).
+__device__ __forceinline__ uint32_t fastmod(uint32_t x, uint64_t M, uint32_t p) {
+    return (uint32_t)__umul64hi(M * x, p);
+}
+
+// Block owning global segment g: largest b with seg[b] <= g.
+__device__ __forceinline__ size_t seg_block(const uint64_t *seg, size_t blocks, uint64_t g) {
+    size_t lo = 0, hi = blocks;  // seg[lo] <= g < seg[hi]
+    while (hi - lo > 1) {
+        const size_t mid = (lo + hi) >> 1;
+        if (seg[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const uint64_t *offs,
+                                                    const uint64_t *seg, size_t blocks, int n,
+                                                    int m, uint32_t p, uint64_t M,
+                                                    uint16_t *frags) {
+    __shared__ uint32_t E[IDA_MAX_N * IDA_MAX_N];
+    if ((int)threadIdx.x < n) {  // row a = threadIdx.x + 1: a^0 .. a^(m-1) mod p
+        uint32_t elt = 1;
+        for (int i = 0; i < m; ++i) {
+            E[threadIdx.x * m + i] = elt;
+            elt = (elt * (threadIdx.x + 1)) % p;
+        }
+    }
+    __syncthreads();
+    const uint64_t total = seg[blocks];
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const size_t b = seg_block(seg, blocks, g);
+        const uint64_t s = g - seg[b], S = seg[b + 1] - seg[b];
+        const uint64_t base = offs[b], len = offs[b + 1] - base;
+        uint32_t v[IDA_MAX_N];
+#pragma unroll
+        for (int k = 0; k < IDA_MAX_N; ++k) {
+            if (k < m) {
+                const uint64_t at = s * (uint64_t)m + k;
+                v[k] = at < len ? data[base + at] : 0u;
+            }
+        }
+        uint16_t *out = frags + (uint64_t)n * seg[b] + s;
+        for (int i = 0; i < n; ++i) {
+            uint32_t acc = 0;  // <= m (p-1) 255 < 2^32
+#pragma unroll
+            for (int k = 0; k < IDA_MAX_N; ++k)
+                if (k < m) acc += E[i * m + k] * v[k];
+            out[(uint64_t)i * S] = (uint16_t)fastmod(acc, M, p);
+        }
+    }
+}
+
+// One thread per run of blocks sharing an index list: the run's inverse
+// Vandermonde (m x m, row-major as the reference returns it).  flag = 1 on
+// success, 0 when a denominator has no inverse ("N is not invertible").
+__device__ __forceinline__ int32_t cmod(int32_t x, int32_t p) { return (x % p + p) % p; }
+
+__global__ void k_ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, int m,
+                              int32_t p, int32_t *inv, uint8_t *okf) {
+    for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < runs;
+         r += (size_t)gridDim.x * blockDim.x) {
+        const uint8_t *b = idx + (size_t)run_start[r] * m;
+        // elementary symmetric sums e_0..e_m of the basis, int32 wrap (uint32 ops)
+        uint32_t e[IDA_MAX_N + 1];
+        e[0] = 1;
+        for (int j = 1; j <= m; ++j) e[j] = 0;
+        for (int t = 0; t < m; ++t)
+            for (int j = t + 1; j >= 1; --j) e[j] = e[j] + e[j - 1] * (uint32_t)b[t];
+        int32_t *out = inv + r * (size_t)m * m;
+        bool good = true;
+        for (int i = 0; i < m; ++i) {
+            const int32_t elt = b[i];
+            int32_t prod = 1;
+            for (int j = 0; j < m; ++j)
+                if (j != i) prod = cmod(prod * (elt - (int32_t)b[j]), p);
+            // ModInverse (matrix_math.cpp:66-86)
+            int32_t t = 0, nt = 1, rr = p, nr = prod;
+            while (nr) {
+                const int32_t q = rr / nr;
+                int32_t tmp = t;
+                t = nt;
+                nt = tmp - q * nt;
+                tmp = rr;
+                rr = nr;
+                nr = tmp - q * nr;
+            }
+            if (rr > 1) {
+                good = false;
+                break;
+            }
+            if (t < 0) t += p;
+            // numerators (built from the top), reversed, scaled; stored transposed
+            int32_t row = 1, sign = -1;
+            out[(size_t)(m - 1) * m + i] = cmod(row * t, p);
+            for (int j = 1; j < m; ++j) {
+                const int32_t a = cmod(row * elt, p);
+                row = cmod((int32_t)((uint32_t)a + (uint32_t)sign * e[j]), p);
+                out[(size_t)(m - 1 - j) * m + i] = cmod(row * t, p);
+                sign = -sign;
+            }
+        }
+        okf[r] = good ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const uint64_t *seg,
+                                                    size_t blocks, int m, uint32_t p, uint64_t M,
+                                                    const int32_t *inv, const uint32_t *run_of,
+                                                    const uint8_t *okf, uint16_t *out,
+                                                    unsigned long long *out_len) {
+    const uint64_t total = seg[blocks];
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const size_t b = seg_block(seg, blocks, g);
+        const uint32_t r = run_of[b];
+        if (!okf[r]) continue;
+        const uint64_t s = g - seg[b], S = seg[b + 1] - seg[b];
+        const uint16_t *fr = frags + (uint64_t)m * seg[b] + s;
+        uint32_t f[IDA_MAX_N];
+#pragma unroll
+        for (int k = 0; k < IDA_MAX_N; ++k)
+            if (k < m) f[k] = fr[(uint64_t)k * S];
+        const int32_t *A = inv + (size_t)r * m * m;
+        uint16_t *o = out + (uint64_t)m * seg[b] + s * m;
+        int last = -1;
+        for (int j = 0; j < m; ++j) {
+            uint64_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < IDA_MAX_N; ++k)
+                if (k < m) acc += (uint64_t)(uint32_t)A[j * m + k] * f[k];
+            const uint32_t c = (uint32_t)(acc % p);
+            o[j] = (uint16_t)c;
+            if (c) last = j;
+        }
+        if (last >= 0) atomicMax(out_len + b, (unsigned long long)(s * m + last + 1));
+    }
+}
+
+// Marks the first block of each run of equal index lists.
+__global__ void k_ida_runs(const uint8_t *idx, size_t blocks, int m, uint32_t *flag) {
+    for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < blocks;
+         b += (size_t)gridDim.x * blockDim.x) {
+        uint32_t f = b == 0 ? 1u : 0u;
+        if (b)
+            for (int k = 0; k < m; ++k)
+                if (idx[b * m + k] != idx[(b - 1) * m + k]) f = 1u;
+        flag[b] = f;
+    }
+}
+
+// run_of[b] = run index (inclusive scan - 1), run_start[run] = first block.
+__global__ void k_ida_run_index(const uint32_t *flag_excl, const uint32_t *flag_raw, size_t blocks,
+                                uint32_t *run_of, uint32_t *run_start) {
+    for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < blocks;
+         b += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t r = flag_excl[b] + flag_raw[b] - 1;
+        run_of[b] = r;
+        if (flag_raw[b]) run_start[r] = (uint32_t)b;
+    }
+}
+
+__global__ void k_ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks,
+                                  uint64_t *out_len) {
+    for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < blocks;
+         b += (size_t)gridDim.x * blockDim.x)
+        if (!okf[run_of[b]]) out_len[b] = ~0ull;
+}
+
+hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks,
+                           uint64_t *out_len, hipStream_t s) {
+    if (blocks == 0) return hipSuccess;
+    k_ida_mark_failed<<<cx_grid(blocks, 256), 256, 0, s>>>(run_of, okf, blocks, out_len);
+    return hipGetLastError();
+}
+
+static uint64_t lemire_m(uint32_t p) { return ~0ull / p + 1; }
+
+hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
+                      size_t blocks, uint64_t total_segs, int n, int m, int p, uint16_t *frags,
+                      hipStream_t s) {
+    if (blocks == 0 || total_segs == 0) return hipSuccess;
+    k_ida_encode<<<cx_grid(total_segs, 256, 16384), 256, 0, s>>>(data, offs, seg, blocks, n, m,
+                                                                  (uint32_t)p, lemire_m(p), frags);
+    return hipGetLastError();
+}
+
+hipError_t ida_runs(const uint8_t *idx, size_t blocks, int m, uint32_t *flag, hipStream_t s) {
+    if (blocks == 0) return hipSuccess;
+    k_ida_runs<<<cx_grid(blocks, 256), 256, 0, s>>>(idx, blocks, m, flag);
+    return hipGetLastError();
+}
+
+hipError_t ida_run_index(const uint32_t *flag_excl, const uint32_t *flag_raw, size_t blocks,
+                         uint32_t *run_of, uint32_t *run_start, hipStream_t s) {
+    if (blocks == 0) return hipSuccess;
+    k_ida_run_index<<<cx_grid(blocks, 256), 256, 0, s>>>(flag_excl, flag_raw, blocks, run_of,
+                                                        run_start);
+    return hipGetLastError();
+}
+
+hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, int m, int p,
+                       int32_t *inv, uint8_t *okf, hipStream_t s) {
+    if (runs == 0) return hipSuccess;
+    k_ida_inverse<<<cx_grid(runs, 64), 64, 0, s>>>(idx, run_start, runs, m, p, inv, okf);
+    return hipGetLastError();
+}
+
+hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks,
+                      uint64_t total_segs, int m, int p, const int32_t *inv,
+                      const uint32_t *run_of, const uint8_t *okf, uint16_t *out,
+                      uint64_t *out_len, hipStream_t s) {
+    if (blocks == 0 || total_segs == 0) return hipSuccess;
+    k_ida_decode<<<cx_grid(total_segs, 256, 16384), 256, 0, s>>>(
+        frags, seg, blocks, m, (uint32_t)p, lemire_m(p), inv, run_of, okf, out,
+        reinterpret_cast<unsigned long long *>(out_len));
+    return hipGetLastError();
+}
+
 // Validation of caller-supplied peer indices (finger uploads, preds):
 // *d_bad = 1 if any entry is >= limit (CX_NONE allowed when allow_none).
 __global__ void k_check_indices(const uint32_t *idx, size_t count, uint32_t limit,

@@ -214,6 +214,29 @@ def dhash_create_read():
             "n": d["PEERS"][0]["NUM_SUCCS"], "key": d["KEY"]}
 
 
+def ida_values():
+    """Data the reference's DHash tests store through IDA, with the (n, m, p)
+    each test uses: DataBlock defaults (14, 10, 257) (data_block.h:33-34) in
+    DHashIntegration.CreateAndRead and DHashExchangeNode; SetIdaParams(2, 1,
+    257) in DHashGlobalMaintenance; (3, 2, 257) in DHashSynchronize
+    (dhash_test.cpp:20-150,185-226).  Reading a key back must return it."""
+    out = []
+    d = load("dhash_tests/DHashIntegrationCreateAndReadTest.json")
+    out.append({"source": "dhash_test.cpp:213-226", "nmp": [14, 10, 257], "values": [d["VAL"]]})
+    d = load("dhash_tests/ExchangeNodeTest.json")
+    out.append({"source": "dhash_test.cpp:185-205", "nmp": [14, 10, 257],
+                "values": list(d["NON_EXISTENT_NODE"]["KEYS_TO_INSERT"].values())})
+    d = load("dhash_tests/GlobalMaintenanceTest.json")
+    out.append({"source": "dhash_test.cpp:123-149", "nmp": [2, 1, 257],
+                "values": list(d["MISPLACED_KEYS"]["KEYS_TO_INSERT"].values())})
+    d = load("dhash_tests/LocalMaintenanceTest.json")
+    vals = [d["DEPTH_ONE_SINGLE_KEY"]["VAL_TO_INSERT"],
+            d["SYNCHRONIZE_USES_GIVEN_RANGE"]["VAL_TO_INSERT"]]
+    vals += list(d["HIGH_DEPTH"]["KEYS_TO_INSERT"].values())
+    out.append({"source": "dhash_test.cpp:20-110", "nmp": [3, 2, 257], "values": vals})
+    return out
+
+
 def c1_truth():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -262,6 +285,7 @@ def main():
         "get_succ": get_succ(),
         "global_maintenance": global_maintenance(),
         "dhash_create_read": dhash_create_read(),
+        "ida_values": ida_values(),
     }
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
         json.dump(vec, f, indent=1)

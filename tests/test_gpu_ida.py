@@ -1,0 +1,136 @@
+"""IDA kernels (cx_ida_encode / cx_ida_decode) against the CPU oracle,
+bit-exact, plus the reference's DHash values read back through DataBlock."""
+import itertools
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ida():
+    import chordx
+    if chordx.device_count() == 0:
+        pytest.fail("gpu test without a HIP device")
+    return chordx.ida
+
+
+def ragged(rng, m, count, big=0):
+    lens = [0, 1, m - 1, m, m + 1, 2 * m, 3 * m + 1] + [rng.randrange(0, 200) for _ in range(count)]
+    if big:
+        lens.append(big)
+    return [bytes(rng.getrandbits(8) for _ in range(n)) if n < 5000 else
+            np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+
+
+PARAMS = [(14, 10, 257), (3, 2, 257), (2, 1, 257), (20, 12, 40009), (32, 31, 46337),
+          (9, 4, 263)]
+
+
+@pytest.mark.parametrize("nmp", PARAMS)
+def test_encode_matches_oracle(ida, O, nmp):
+    n, m, p = nmp
+    rng = random.Random(n + m + p)
+    blocks = ragged(rng, m, 60, big=100003)
+    got = ida.encode(blocks, n, m, p)
+    want = O.ida_encode(blocks, n, m, p)
+    for g, w in zip(got, want):
+        assert g.shape == w.shape and (g == w).all()
+
+
+@pytest.mark.parametrize("nmp", PARAMS)
+def test_decode_matches_oracle(ida, O, nmp):
+    n, m, p = nmp
+    rng = random.Random(7 * n + m)
+    blocks = ragged(rng, m, 80, big=50021)
+    frags = O.ida_encode(blocks, n, m, p)
+    rows, idx = [], []
+    for b, f in enumerate(frags):
+        sub = rng.sample(range(n), m)
+        if b % 3 == 0:
+            sub = sorted(sub)
+        if b % 5 == 0 and b:
+            sub = [i - 1 for i in idx[-1]]  # same list as the previous block (shared inverse)
+        rows.append(f[sub])
+        idx.append([s + 1 for s in sub])
+    got = ida.decode(rows, idx, m, p)
+    want = O.ida_decode(rows, idx, m, p)
+    for g, w in zip(got, want):
+        assert g is not None and g.shape == w.shape and (g == w).all()
+
+
+def test_decode_all_subsets_default_params(ida, O):
+    """Every one of the 1001 fragment sets of (14, 10), in shuffled order,
+    including the 7 whose inverse hits the reference's int32 wrap."""
+    rng = random.Random(3)
+    data = bytes(rng.getrandbits(8) for _ in range(997)) + b"\x01"
+    f = O.ida_encode([data])[0]
+    rows, idx = [], []
+    for sub in itertools.combinations(range(14), 10):
+        sub = list(sub)
+        rng.shuffle(sub)
+        rows.append(f[sub])
+        idx.append([s + 1 for s in sub])
+    got = ida.decode(rows, idx)
+    want = O.ida_decode(rows, idx)
+    ok = 0
+    for g, w in zip(got, want):
+        assert (g == w).all() and g.shape == w.shape
+        ok += bytes(g.astype(np.uint8)) == data and g.max() < 256
+    assert ok == 1001 - 7
+
+
+def test_decode_not_invertible_and_ragged_edges(ida, O):
+    f = O.ida_encode([b"abcdefghijklmnop", b"", b"\0\0\0\0"])
+    rows = [f[0][:10], f[0][:10], f[1][:10], f[2][:10]]
+    idx = [[1, 1, 2, 3, 4, 5, 6, 7, 8, 9], list(range(1, 11)), list(range(1, 11)),
+           list(range(1, 11))]
+    got = ida.decode(rows, idx)
+    assert got[0] is None
+    assert bytes(got[1].astype(np.uint8)) == b"abcdefghijklmnop"
+    assert got[2].size == 0 and got[3].size == 0
+
+
+def test_golden_values_through_datablock(ida, refvec):
+    """Create + Read of the reference's DHash test values: the m lowest
+    fragment indices a read collects (std::set order) rebuild the value."""
+    rng = random.Random(11)
+    for case in refvec["ida_values"]:
+        n, m, p = case["nmp"]
+        for v in case["values"]:
+            blk = ida.DataBlock(v, n, m, p)
+            assert blk.decode() == v
+            alive = sorted(rng.sample(blk.fragments, m + rng.randrange(0, n - m + 1)))
+            back = ida.DataBlock.from_fragments(alive, n, m, p)
+            assert back.decode() == v
+            assert all((a[1] == b[1]).all() for a, b in zip(back.fragments, blk.fragments))
+
+
+def test_device_buffers_large(ida, O):
+    """256 MiB in 4 KiB blocks on device memory: encode -> drop 4 fragments per
+    block -> decode reproduces the data (property check at full size) and a
+    sample of blocks equals the oracle."""
+    import torch
+    nb, bl = 1 << 16, 4096
+    g = torch.Generator(device="cuda").manual_seed(5)
+    data = torch.randint(1, 256, (nb * bl,), dtype=torch.uint8, device="cuda", generator=g)
+    offs = torch.arange(0, nb * bl + 1, bl, dtype=torch.int64, device="cuda")
+    frags, seg = ida.encode_flat(data, offs)
+    S = (bl + 9) // 10
+    fr = frags.view(nb, 14, S)
+    keep = torch.tensor([0, 2, 3, 5, 6, 8, 9, 11, 12, 13], device="cuda")
+    rows = fr[:, keep, :].contiguous().view(-1)
+    idx = (keep + 1).to(torch.uint8).repeat(nb).contiguous()
+    segd = torch.from_numpy(seg.astype(np.int64)).cuda()
+    out, ln = ida.decode_flat(rows, segd, idx)
+    torch.cuda.synchronize()
+    vals = out.view(nb, S * 10)[:, :bl]
+    assert bool((ln == bl).all())
+    assert bool((vals.to(torch.int32) == data.view(nb, bl).to(torch.int32)).all())
+    host = data[: 8 * bl].cpu().numpy()
+    want = O.ida_encode([host[i * bl:(i + 1) * bl].tobytes() for i in range(8)])
+    got = fr[:8].cpu().numpy().view(np.uint16)
+    for i in range(8):
+        assert (got[i] == want[i]).all()
