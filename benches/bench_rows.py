@@ -113,6 +113,31 @@ def main():
                  "keys_with_misplaced_holder": int((mask != 0).sum()),
                  "misplaced_pairs": int(sum(int(((mask.to(torch.int32) >> j) & 1).sum())
                                             for j in range(n)))}
+    del old, new, keys, lists, count, mask, target, joins, leaves, pick, o2n
+    torch.cuda.empty_cache()
+
+    # ---------------- IDA (DHash payload coding, 14/10/257) ----------------
+    from chordx import ida
+    res = {}
+    for name, nb, bl in (("4KiB_blocks", 1 << 18, 4096), ("64B_blocks", 1 << 22, 64)):
+        g = torch.Generator(device="cuda").manual_seed(1)
+        data = torch.randint(0, 256, (nb * bl,), dtype=torch.uint8, device="cuda", generator=g)
+        offs = torch.arange(0, nb * bl + 1, bl, dtype=torch.int64, device="cuda")
+        frags, seg = ida.encode_flat(data, offs)
+        te = ev_time(lambda: ida.encode_flat(data, offs, seg_offsets=seg, out=frags))
+        S = (bl + 9) // 10
+        keep = torch.tensor([0, 2, 3, 5, 6, 8, 9, 11, 12, 13], device="cuda")
+        rows = frags.view(nb, 14, S)[:, keep, :].contiguous().view(-1)
+        idx = (keep + 1).to(torch.uint8).repeat(nb).contiguous()
+        dec = ida.decode_flat(rows, seg, idx)
+        td = ev_time(lambda: ida.decode_flat(rows, seg, idx, out=dec))
+        nbytes = nb * bl
+        res[name] = {"bytes": nbytes, "encode_s": te, "encode_GBps_data": nbytes / te / 1e9,
+                     "encode_algo_frac_of_hbm": nbytes * (1 + 2.8) / te / HBM,
+                     "decode_s": td, "decode_GBps_data": nbytes / td / 1e9,
+                     "decode_algo_frac_of_hbm": nbytes * (2 + 2) / td / HBM}
+        del data, offs, frags, rows, idx, seg, dec
+    out["IDA_14_10_257"] = res
     print(json.dumps(out))
 
 

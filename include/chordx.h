@@ -203,17 +203,21 @@ int cx_hex_format(const cx_u128 *keys, size_t count, char *out, uint8_t *len, in
  * segments, seg_offsets[b] = sum of S_c for c < b (cx_ida_segments, host).
  * cx_ida_encode: IDA::Encode (ida.cpp:59-73): fragment i (index i + 1,
  *   data_block.cpp:12-13) of block b is frags[n*seg_offsets[b] + i*S_b ..+ S_b).
+ *   Host buffers are validated (seg_offsets must match offsets); with device
+ *   buffers the call only enqueues kernels on the null stream (no sync).
  * cx_ida_decode: IDA::Decode (ida.cpp:120-162) from m fragment rows per block
  *   (frags[m*seg_offsets[b] + k*S_b ..]) with 1-based indices
  *   indices[b*m + k]: values (< p) at out[m*seg_offsets[b] ..], kept length
  *   out_len[b] (trailing zeros dropped as the reference does); out_len[b] =
  *   UINT64_MAX when the indices have no inverse ("N is not invertible",
- *   matrix_math.cpp:81-82).  The inverse follows matrix_math.cpp:103-168
+ *   matrix_math.cpp:81-82).  Blocks sharing the previous block's index list
+ *   share one inverse (one small device->host read per call to size them).
+ *   The inverse follows matrix_math.cpp:103-168
  *   including its int arithmetic as compiled (wrap-around).
  * Limits: 1 <= m < n <= 32, n < p <= 46340.  DHash uses (14, 10, 257). */
 int cx_ida_segments(const uint64_t *offsets, size_t blocks, int m, uint64_t *seg_offsets);
-int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, size_t blocks, int n, int m,
-                  int p, uint16_t *frags, int memkind, int device);
+int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, const uint64_t *seg_offsets,
+                  size_t blocks, int n, int m, int p, uint16_t *frags, int memkind, int device);
 int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint8_t *indices,
                   size_t blocks, int m, int p, uint16_t *out, uint64_t *out_len, int memkind,
                   int device);

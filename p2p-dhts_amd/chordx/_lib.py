@@ -98,7 +98,7 @@ def lib() -> ctypes.CDLL:
         "cx_uuid5_dns": ([vp, vp, sz, vp, i, i], i),
         "cx_fill_splitmix": ([vp, sz, u64, u64, i, vp], i),
         "cx_ida_segments": ([vp, sz, i, vp], i),
-        "cx_ida_encode": ([vp, vp, sz, i, i, i, vp, i, i], i),
+        "cx_ida_encode": ([vp, vp, vp, sz, i, i, i, vp, i, i], i),
         "cx_ida_decode": ([vp, vp, vp, sz, i, i, vp, vp, i, i], i),
         "cx_hex_parse": ([vp, vp, sz, vp, vp, i, i], i),
         "cx_hex_format": ([vp, sz, vp, vp, i, i], i),

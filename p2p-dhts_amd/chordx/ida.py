@@ -41,33 +41,43 @@ def segments(lengths, m: int) -> np.ndarray:
     return seg
 
 
-def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0):
+def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0, seg_offsets=None, out=None):
     """Raw batched encode.  data: uint8 bytes, offsets: (blocks + 1,) uint64
-    (numpy, or torch device tensors).  Returns (frags uint16, seg_offsets)."""
+    (numpy, or torch device tensors).  Returns (frags uint16, seg_offsets);
+    pass seg_offsets (same memory kind) to skip computing them."""
     blocks = offsets.shape[0] - 1
-    off_h = offsets.cpu().numpy() if _is_dev(offsets) else np.asarray(offsets, np.uint64)
-    seg = np.zeros(blocks + 1, dtype=np.uint64)
-    L.check(L.lib().cx_ida_segments(_ptr(np.ascontiguousarray(off_h)), blocks, m, _ptr(seg)))
-    total = int(seg[-1]) * n
+    if seg_offsets is None:
+        off_h = offsets.cpu().numpy() if _is_dev(offsets) else np.asarray(offsets, np.uint64)
+        seg = np.zeros(blocks + 1, dtype=np.uint64)
+        L.check(L.lib().cx_ida_segments(_ptr(np.ascontiguousarray(off_h)), blocks, m,
+                                        _ptr(seg)))
+        seg_offsets = torch.from_numpy(seg.astype(np.int64)).to(offsets.device) \
+            if _is_dev(offsets) else seg
     if _is_dev(data):
-        frags = torch.empty(max(total, 1), dtype=torch.int16, device=data.device)
+        frags = out if out is not None else torch.empty(
+            max(int(seg_offsets[-1]) * n, 1), dtype=torch.int16, device=data.device)
         mk = L.CX_MEM_DEVICE
     else:
         data = np.ascontiguousarray(data, dtype=np.uint8)
-        frags = np.zeros(max(total, 1), dtype=np.uint16)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        frags = np.zeros(max(int(seg_offsets[-1]) * n, 1), dtype=np.uint16)
         mk = L.CX_MEM_HOST
-    L.check(L.lib().cx_ida_encode(_ptr(data), _ptr(offsets if mk == L.CX_MEM_DEVICE else off_h),
-                                  blocks, n, m, p, _ptr(frags), mk, device))
-    return frags, seg
+    L.check(L.lib().cx_ida_encode(_ptr(data), _ptr(offsets), _ptr(seg_offsets), blocks, n, m,
+                                  p, _ptr(frags), mk, device))
+    return frags, seg_offsets
 
 
-def decode_flat(frags, seg_offsets, indices, m=10, p=257, device: int = 0):
-    """Raw batched decode; returns (values uint16, out_len uint64)."""
+def decode_flat(frags, seg_offsets, indices, m=10, p=257, device: int = 0, total=None,
+                out=None):
+    """Raw batched decode; returns (values uint16, out_len uint64).  With
+    device tensors, pass total (= seg_offsets[-1]) to avoid reading it back."""
     blocks = seg_offsets.shape[0] - 1
     if _is_dev(frags):
-        total = int(seg_offsets[-1].item()) * m
-        out = torch.empty(max(total, 1), dtype=torch.int16, device=frags.device)
-        ln = torch.empty(max(blocks, 1), dtype=torch.int64, device=frags.device)
+        if out is None:
+            total = (int(seg_offsets[-1].item()) if total is None else int(total)) * m
+            out = (torch.empty(max(total, 1), dtype=torch.int16, device=frags.device),
+                   torch.empty(max(blocks, 1), dtype=torch.int64, device=frags.device))
+        out, ln = out
         mk = L.CX_MEM_DEVICE
     else:
         frags = np.ascontiguousarray(frags, dtype=np.uint16)

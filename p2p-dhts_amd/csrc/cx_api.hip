@@ -53,6 +53,24 @@ struct DBuf {
     }
 };
 
+// Stream-ordered temporary (hipMallocAsync / hipFreeAsync): no device-wide
+// synchronisation on free, unlike hipFree.
+struct ABuf {
+    void *p = nullptr;
+    hipStream_t s = nullptr;
+    ~ABuf() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+    hipError_t alloc(size_t bytes, hipStream_t st) {
+        s = st;
+        return hipMallocAsync(&p, bytes ? bytes : 16, st);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
 }  // namespace
 
 struct cx_ring {
@@ -958,34 +976,38 @@ int cx_ida_segments(const uint64_t *offsets, size_t blocks, int m, uint64_t *seg
     return CX_OK;
 }
 
-int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, size_t blocks, int n, int m,
-                  int p, uint16_t *frags, int memkind, int device) {
+int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, const uint64_t *seg_offsets,
+                  size_t blocks, int n, int m, int p, uint16_t *frags, int memkind,
+                  int device) {
     int rc;
     if ((rc = ida_check(n, m, p))) return rc;
     if ((rc = device_ok(device))) return rc;
     if (blocks == 0) return CX_OK;
-    CX_CHECK(offsets && frags, CX_E_INVALID, "null argument");
-    std::vector<uint64_t> ho, hs(blocks + 1);
-    if ((rc = host_offsets(offsets, blocks, memkind, ho))) return rc;
-    if ((rc = cx_ida_segments(ho.data(), blocks, m, hs.data()))) return rc;
-    const uint64_t segs = hs[blocks], nbytes = ho[blocks];
+    CX_CHECK(offsets && seg_offsets, CX_E_INVALID, "null argument");
     hipStream_t s = nullptr;
+    if (memkind == CX_MEM_DEVICE) {  // device-resident: no host round trip
+        CX_CHECK(frags != nullptr, CX_E_INVALID, "null argument");
+        CX_HIP(cxk::ida_encode(data, offsets, seg_offsets, blocks, n, m, p, frags, s));
+        return CX_OK;
+    }
+    CX_CHECK(memkind == CX_MEM_HOST, CX_E_INVALID, "bad memkind");
+    std::vector<uint64_t> ho, hs;
+    if ((rc = host_offsets(offsets, blocks, memkind, ho))) return rc;
+    if ((rc = host_offsets(seg_offsets, blocks, memkind, hs))) return rc;
+    for (size_t b = 0; b < blocks; ++b)
+        CX_CHECK(hs[b + 1] - hs[b] == (ho[b + 1] - ho[b] + m - 1) / m, CX_E_INVALID,
+                 "seg_offsets do not match offsets (cx_ida_segments)");
+    const uint64_t segs = hs[blocks], nbytes = ho[blocks];
     DBuf td, to, tseg, tf;
     const uint8_t *dd;
-    const uint64_t *doff;
+    const uint64_t *doff, *dseg;
     uint16_t *df;
     if ((rc = stage_in(data, (size_t)nbytes, memkind, td, &dd, s))) return rc;
-    if ((rc = stage_in(memkind == CX_MEM_DEVICE ? offsets : ho.data(), blocks + 1, memkind, to,
-                       &doff, s)))
-        return rc;
-    CX_HIP(tseg.alloc((blocks + 1) * sizeof(uint64_t)));
-    CX_HIP(hipMemcpyAsync(tseg.p, hs.data(), (blocks + 1) * sizeof(uint64_t),
-                          hipMemcpyHostToDevice, s));
+    if ((rc = stage_in(offsets, blocks + 1, memkind, to, &doff, s))) return rc;
+    if ((rc = stage_in(seg_offsets, blocks + 1, memkind, tseg, &dseg, s))) return rc;
     if ((rc = stage_out(frags, (size_t)(segs * n), memkind, tf, &df))) return rc;
-    CX_HIP(cxk::ida_encode(dd, doff, tseg.as<uint64_t>(), blocks, segs, n, m, p, df, s));
-    if ((rc = finish_out(frags, df, (size_t)(segs * n), memkind, s))) return rc;
-    CX_HIP(hipStreamSynchronize(s));  // hs is a host stack buffer
-    return CX_OK;
+    CX_HIP(cxk::ida_encode(dd, doff, dseg, blocks, n, m, p, df, s));
+    return finish_out(frags, df, (size_t)(segs * n), memkind, s);
 }
 
 int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint8_t *indices,
@@ -997,52 +1019,60 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
     if ((rc = device_ok(device))) return rc;
     if (blocks == 0) return CX_OK;
     CX_CHECK(seg_offsets && indices && out_len, CX_E_INVALID, "null argument");
-    std::vector<uint64_t> hs;
-    if ((rc = host_offsets(seg_offsets, blocks, memkind, hs))) return rc;
-    const uint64_t segs = hs[blocks];
-    CX_CHECK(segs == 0 || (frags && out), CX_E_INVALID, "null argument");
     CX_CHECK(blocks < (1ull << 32), CX_E_INVALID, "too many blocks");
+    CX_CHECK(memkind == CX_MEM_HOST || memkind == CX_MEM_DEVICE, CX_E_INVALID, "bad memkind");
     hipStream_t s = nullptr;
-    DBuf tf, tsg, ti, tout, tlen, flag, flag2, ws, run_of, run_start, inv, okf;
-    const uint16_t *dfr;
-    const uint64_t *dseg;
-    const uint8_t *didx;
-    uint16_t *dout;
-    uint64_t *dlen;
-    if ((rc = stage_in(frags, (size_t)(segs * m), memkind, tf, &dfr, s))) return rc;
-    if ((rc = stage_in(seg_offsets, blocks + 1, memkind, tsg, &dseg, s))) return rc;
-    if ((rc = stage_in(indices, blocks * (size_t)m, memkind, ti, &didx, s))) return rc;
-    if ((rc = stage_out(out, (size_t)(segs * m), memkind, tout, &dout))) return rc;
-    if ((rc = stage_out(out_len, blocks, memkind, tlen, &dlen))) return rc;
+    uint64_t segs = 0;
+    if (memkind == CX_MEM_HOST) {
+        std::vector<uint64_t> hs;
+        if ((rc = host_offsets(seg_offsets, blocks, memkind, hs))) return rc;
+        segs = hs[blocks];
+        CX_CHECK(segs == 0 || (frags && out), CX_E_INVALID, "null argument");
+    }
+    DBuf tf, tsg, ti, tout, tlen;
+    const uint16_t *dfr = frags;
+    const uint64_t *dseg = seg_offsets;
+    const uint8_t *didx = indices;
+    uint16_t *dout = out;
+    uint64_t *dlen = out_len;
+    if (memkind == CX_MEM_HOST) {
+        if ((rc = stage_in(frags, (size_t)(segs * m), memkind, tf, &dfr, s))) return rc;
+        if ((rc = stage_in(seg_offsets, blocks + 1, memkind, tsg, &dseg, s))) return rc;
+        if ((rc = stage_in(indices, blocks * (size_t)m, memkind, ti, &didx, s))) return rc;
+        if ((rc = stage_out(out, (size_t)(segs * m), memkind, tout, &dout))) return rc;
+        if ((rc = stage_out(out_len, blocks, memkind, tlen, &dlen))) return rc;
+    }
     // runs of equal index lists share one inverse
-    CX_HIP(flag.alloc(blocks * sizeof(uint32_t)));
-    CX_HIP(flag2.alloc(blocks * sizeof(uint32_t)));
-    CX_HIP(ws.alloc(cxk::scan_workspace_words(blocks) * sizeof(uint32_t)));
+    ABuf flag, flag2, ws, run_of, run_start, inv, okf, cnt;
+    CX_HIP(flag.alloc(blocks * sizeof(uint32_t), s));
+    CX_HIP(flag2.alloc(blocks * sizeof(uint32_t), s));
+    CX_HIP(ws.alloc(cxk::scan_workspace_words(blocks) * sizeof(uint32_t), s));
+    CX_HIP(cnt.alloc(2 * sizeof(uint32_t), s));
     CX_HIP(cxk::ida_runs(didx, blocks, m, flag.as<uint32_t>(), s));
     CX_HIP(hipMemcpyAsync(flag2.p, flag.p, blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     CX_HIP(cxk::exclusive_scan(flag2.as<uint32_t>(), blocks, ws.as<uint32_t>(), s));
-    uint32_t last_excl = 0, last_raw = 0;
-    CX_HIP(hipMemcpyAsync(&last_excl, flag2.as<uint32_t>() + blocks - 1, 4,
-                          hipMemcpyDeviceToHost, s));
-    CX_HIP(hipMemcpyAsync(&last_raw, flag.as<uint32_t>() + blocks - 1, 4, hipMemcpyDeviceToHost,
+    uint32_t last[2] = {0, 0};
+    CX_HIP(hipMemcpyAsync(&last[0], flag2.as<uint32_t>() + blocks - 1, 4, hipMemcpyDeviceToHost,
                           s));
+    CX_HIP(hipMemcpyAsync(&last[1], flag.as<uint32_t>() + blocks - 1, 4, hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
-    const size_t runs = (size_t)last_excl + last_raw;
-    CX_HIP(run_of.alloc(blocks * sizeof(uint32_t)));
-    CX_HIP(run_start.alloc(runs * sizeof(uint32_t)));
-    CX_HIP(inv.alloc(runs * (size_t)m * m * sizeof(int32_t)));
-    CX_HIP(okf.alloc(runs));
+    const size_t runs = (size_t)last[0] + last[1];
+    CX_HIP(run_of.alloc(blocks * sizeof(uint32_t), s));
+    CX_HIP(run_start.alloc(runs * sizeof(uint32_t), s));
+    CX_HIP(inv.alloc(runs * (size_t)m * m * sizeof(int32_t), s));
+    CX_HIP(okf.alloc(runs, s));
     CX_HIP(cxk::ida_run_index(flag2.as<uint32_t>(), flag.as<uint32_t>(), blocks,
                               run_of.as<uint32_t>(), run_start.as<uint32_t>(), s));
     CX_HIP(cxk::ida_inverse(didx, run_start.as<uint32_t>(), runs, m, p, inv.as<int32_t>(),
                             okf.as<uint8_t>(), s));
     CX_HIP(hipMemsetAsync(dlen, 0, blocks * sizeof(uint64_t), s));
-    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, segs, m, p, inv.as<int32_t>(),
-                           run_of.as<uint32_t>(), okf.as<uint8_t>(), dout, dlen, s));
+    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, m, p, inv.as<int32_t>(), run_of.as<uint32_t>(),
+                           okf.as<uint8_t>(), dout, dlen, s));
     CX_HIP(cxk::ida_mark_failed(run_of.as<uint32_t>(), okf.as<uint8_t>(), blocks, dlen, s));
-    if ((rc = finish_out(out_len, dlen, blocks, memkind, s))) return rc;
-    if ((rc = finish_out(out, dout, (size_t)(segs * m), memkind, s))) return rc;
-    CX_HIP(hipStreamSynchronize(s));
+    if (memkind == CX_MEM_HOST) {
+        if ((rc = finish_out(out_len, dlen, blocks, memkind, s))) return rc;
+        if ((rc = finish_out(out, dout, (size_t)(segs * m), memkind, s))) return rc;
+    }
     return CX_OK;
 }
 

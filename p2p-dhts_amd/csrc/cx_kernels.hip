@@ -2515,11 +2515,6 @@ hipError_t hex_format(const cell128 *keys, size_t count, char *out, uint8_t *len
 // ---------------------------------------------------------------------------
 constexpr int IDA_MAX_N = 32;
 
-// x mod p for 32-bit x (Lemire: M = floor((2^64 - 1) / p) + 1).
-__device__ __forceinline__ uint32_t fastmod(uint32_t x, uint64_t M, uint32_t p) {
-    return (uint32_t)__umul64hi(M * x, p);
-}
-
 // Block owning global segment g: largest b with seg[b] <= g.
 __device__ __forceinline__ size_t seg_block(const uint64_t *seg, size_t blocks, uint64_t g) {
     size_t lo = 0, hi = blocks;  // seg[lo] <= g < seg[hi]
@@ -2531,41 +2526,155 @@ __device__ __forceinline__ size_t seg_block(const uint64_t *seg, size_t blocks, 
     return lo;
 }
 
+// x mod p via a float reciprocal when the quotient is < 2^21 (every use
+// below: encode sums < m (p-1) 255, decode sums < m (p-1) 65535 with
+// quotient < m 65535): the estimate is off by at most one, fixed up with
+// two selects; 24-bit multiply, all full-rate VALU.
+__device__ __forceinline__ uint32_t modp_f(uint32_t x, uint32_t p, float inv_p) {
+    const uint32_t q = (uint32_t)((float)x * inv_p);
+    int32_t r = (int32_t)(x - __umul24(q, p));
+    r += r < 0 ? (int32_t)p : 0;
+    r -= r >= (int32_t)p ? (int32_t)p : 0;
+    return (uint32_t)r;
+}
+
+// Segment g's block, for the 64 consecutive segments of one wave chunk: one
+// binary search for the chunk's first segment (uniform), then a short forward
+// scan per lane (blocks of a chunk are consecutive in seg order).
+__device__ __forceinline__ size_t chunk_block(const uint64_t *seg, size_t blocks, uint64_t g0,
+                                              uint64_t g) {
+    size_t b = seg_block(seg, blocks, g0);
+    while (seg[b + 1] <= g) ++b;
+    return b;
+}
+
+typedef unsigned short cx_us2 __attribute__((ext_vector_type(2)));
+
+// Encoding rows in LDS, bytes packed for v_dot4_u32_u8: row i = 8 words of
+// low bytes of E[i][0..31] then 8 words of high bytes (E < 46340 < 2^16).
+constexpr int IDA_EROW = 16;
+
+// Each wave takes a contiguous range of 64-segment chunks: one binary search
+// for its first chunk, then the chunk's first block only moves forward.  The
+// chunk's bytes (one contiguous span) are staged in LDS; each lane forms its
+// segment as packed words and takes 4 byte-products per v_dot4_u32_u8.
 __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const uint64_t *offs,
                                                     const uint64_t *seg, size_t blocks, int n,
-                                                    int m, uint32_t p, uint64_t M,
+                                                    int m, uint32_t p, float inv_p,
                                                     uint16_t *frags) {
-    __shared__ uint32_t E[IDA_MAX_N * IDA_MAX_N];
-    if ((int)threadIdx.x < n) {  // row a = threadIdx.x + 1: a^0 .. a^(m-1) mod p
-        uint32_t elt = 1;
-        for (int i = 0; i < m; ++i) {
-            E[threadIdx.x * m + i] = elt;
-            elt = (elt * (threadIdx.x + 1)) % p;
+    __shared__ __attribute__((aligned(16))) uint32_t Epk[IDA_MAX_N * IDA_EROW];
+    __shared__ uint32_t stage[256 / 64][IDA_MAX_N * 16 + 12];  // a wave's bytes (<= 64 m)
+    for (int t = threadIdx.x; t < n * 8; t += blockDim.x) {
+        const int i = t >> 3, w = t & 7;
+        uint32_t lo = 0, hi = 0, e = 1;
+        for (int k = 0; k < 4 * w + 4; ++k) {  // e = (i+1)^k mod p
+            if (k >= 4 * w && k < m) {
+                lo |= (e & 0xFFu) << (8 * (k - 4 * w));
+                hi |= (e >> 8) << (8 * (k - 4 * w));
+            }
+            e = (e * (uint32_t)(i + 1)) % p;
         }
+        Epk[i * IDA_EROW + w] = lo;
+        Epk[i * IDA_EROW + 8 + w] = hi;
     }
     __syncthreads();
+    const bool hi_any = p > 256;
+    const int nw = (m + 3) >> 2;
+    const int lane = threadIdx.x & 63;
+    uint32_t *st = stage[threadIdx.x >> 6];
     const uint64_t total = seg[blocks];
-    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total;
-         g += (uint64_t)gridDim.x * blockDim.x) {
-        const size_t b = seg_block(seg, blocks, g);
-        const uint64_t s = g - seg[b], S = seg[b + 1] - seg[b];
+    const uint64_t nbytes = offs[blocks];
+    const uint64_t chunks = (total + 63) / 64;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t cpw = (chunks + waves - 1) / waves;
+    const uint64_t c0 = wave * cpw, c1 = c0 + cpw < chunks ? c0 + cpw : chunks;
+    if (c0 >= c1) return;  // wave-uniform, after the only block barrier
+    size_t bb = seg_block(seg, blocks, c0 * 64);
+    for (uint64_t c = c0; c < c1; ++c) {
+        const uint64_t g0 = c * 64, g = g0 + lane;
+        while (seg[bb + 1] <= g0) ++bb;
+        const bool live = g < total;
+        const uint64_t gl = live ? g : total - 1;
+        size_t b = bb;
+        while (seg[b + 1] <= gl) ++b;
+        const uint64_t s = gl - seg[b];
         const uint64_t base = offs[b], len = offs[b + 1] - base;
-        uint32_t v[IDA_MAX_N];
+        const uint64_t my_lo = base + s * m;
+        uint64_t my_hi = my_lo + m;
+        if (my_hi > base + len) my_hi = base + len;
+        const uint64_t span_lo = __shfl(my_lo, 0) & ~3ull;
+        const uint64_t span_hi = __shfl(my_hi, 63);
+        const uint32_t words = (uint32_t)((span_hi - span_lo + 3) >> 2);
+        for (uint32_t w = lane; w < words; w += 64) {
+            const uint64_t at = span_lo + 4ull * w;
+            uint32_t v;
+            if (at + 4 <= nbytes) {
+                v = *reinterpret_cast<const uint32_t *>(data + at);
+            } else {
+                v = 0;
+                for (int k = 0; k < 4; ++k)
+                    if (at + k < nbytes) v |= (uint32_t)data[at + k] << (8 * k);
+            }
+            st[w] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // this lane's segment as packed words W[0..nw), bytes past `have` zero
+        const uint32_t off = (uint32_t)(my_lo - span_lo);
+        const int have = (int)(my_hi - my_lo);
+        const uint32_t bw = off >> 2, sh = off & 3;
+        uint32_t W[8];
+        uint32_t prev = st[bw];
 #pragma unroll
-        for (int k = 0; k < IDA_MAX_N; ++k) {
-            if (k < m) {
-                const uint64_t at = s * (uint64_t)m + k;
-                v[k] = at < len ? data[base + at] : 0u;
+        for (int j = 0; j < 8; ++j) {
+            if (j < nw) {
+                const uint32_t nxt = st[bw + j + 1];
+                uint32_t x = __builtin_amdgcn_alignbyte(nxt, prev, sh);
+                const int valid = have - 4 * j;
+                x &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
+                W[j] = x;
+                prev = nxt;
+            } else {
+                W[j] = 0;
             }
         }
-        uint16_t *out = frags + (uint64_t)n * seg[b] + s;
-        for (int i = 0; i < n; ++i) {
-            uint32_t acc = 0;  // <= m (p-1) 255 < 2^32
-#pragma unroll
-            for (int k = 0; k < IDA_MAX_N; ++k)
-                if (k < m) acc += E[i * m + k] * v[k];
-            out[(uint64_t)i * S] = (uint16_t)fastmod(acc, M, p);
+        if (live) {
+            const uint64_t S = seg[b + 1] - seg[b];
+            uint16_t *out = frags + (uint64_t)n * seg[b] + s;
+            for (int i = 0; i < n; ++i) {
+                const uint4 *er = reinterpret_cast<const uint4 *>(Epk + i * IDA_EROW);
+                const uint4 l0 = er[0];
+                uint32_t acc = __builtin_amdgcn_udot4(l0.x, W[0], 0u, false);
+                if (nw > 1) acc = __builtin_amdgcn_udot4(l0.y, W[1], acc, false);
+                if (nw > 2) acc = __builtin_amdgcn_udot4(l0.z, W[2], acc, false);
+                if (nw > 3) acc = __builtin_amdgcn_udot4(l0.w, W[3], acc, false);
+                if (nw > 4) {
+                    const uint4 l1 = er[1];
+                    acc = __builtin_amdgcn_udot4(l1.x, W[4], acc, false);
+                    if (nw > 5) acc = __builtin_amdgcn_udot4(l1.y, W[5], acc, false);
+                    if (nw > 6) acc = __builtin_amdgcn_udot4(l1.z, W[6], acc, false);
+                    if (nw > 7) acc = __builtin_amdgcn_udot4(l1.w, W[7], acc, false);
+                }
+                if (hi_any) {  // E >= 256: high bytes times 256
+                    const uint4 h0 = er[2], h1 = er[3];
+                    uint32_t ah = __builtin_amdgcn_udot4(h0.x, W[0], 0u, false);
+                    ah = __builtin_amdgcn_udot4(h0.y, W[1], ah, false);
+                    ah = __builtin_amdgcn_udot4(h0.z, W[2], ah, false);
+                    ah = __builtin_amdgcn_udot4(h0.w, W[3], ah, false);
+                    if (nw > 4) {
+                        ah = __builtin_amdgcn_udot4(h1.x, W[4], ah, false);
+                        ah = __builtin_amdgcn_udot4(h1.y, W[5], ah, false);
+                        ah = __builtin_amdgcn_udot4(h1.z, W[6], ah, false);
+                        ah = __builtin_amdgcn_udot4(h1.w, W[7], ah, false);
+                    }
+                    acc += ah << 8;  // total <= m (p-1) 255 < 2^29
+                }
+                out[(uint64_t)i * S] = (uint16_t)modp_f(acc, p, inv_p);
+            }
         }
+        __builtin_amdgcn_wave_barrier();  // stage reused by the next chunk
     }
 }
 
@@ -2622,36 +2731,133 @@ __global__ void k_ida_inverse(const uint8_t *idx, const uint32_t *run_start, siz
     }
 }
 
+// Decode: each lane rebuilds one segment (m values) from its m fragment
+// values.  When the wave's blocks share one inverse it is staged in LDS as
+// u16 pairs and each output takes ceil(m/2) v_dot2_u32_u16 (sums fit 32 bits
+// unless WIDE: m (p-1) 65535 >= 2^32, which takes a 64-bit path).
+constexpr int IDA_AROW = 16;  // u16-pair words per staged inverse row
+
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const uint64_t *seg,
-                                                    size_t blocks, int m, uint32_t p, uint64_t M,
-                                                    const int32_t *inv, const uint32_t *run_of,
-                                                    const uint8_t *okf, uint16_t *out,
-                                                    unsigned long long *out_len) {
+                                                    size_t blocks, int m, uint32_t p,
+                                                    float inv_p, const int32_t *inv,
+                                                    const uint32_t *run_of, const uint8_t *okf,
+                                                    uint16_t *out, unsigned long long *out_len) {
+    __shared__ __attribute__((aligned(16))) uint32_t Ainv[256 / 64][IDA_MAX_N * IDA_AROW];
+    const int lane = threadIdx.x & 63;
+    uint32_t *As = Ainv[threadIdx.x >> 6];
+    const int nw = (m + 1) >> 1;
     const uint64_t total = seg[blocks];
-    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < total;
-         g += (uint64_t)gridDim.x * blockDim.x) {
-        const size_t b = seg_block(seg, blocks, g);
+    const uint64_t chunks = (total + 63) / 64;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t cpw = (chunks + waves - 1) / waves;
+    const uint64_t c0 = wave * cpw, c1 = c0 + cpw < chunks ? c0 + cpw : chunks;
+    if (c0 >= c1) return;
+    size_t bb = seg_block(seg, blocks, c0 * 64);
+    uint32_t staged = 0xFFFFFFFFu;  // run whose inverse is in As
+    for (uint64_t c = c0; c < c1; ++c) {
+        const uint64_t g0 = c * 64, g = g0 + lane;
+        while (seg[bb + 1] <= g0) ++bb;
+        const bool live = g < total;
+        const uint64_t gl = live ? g : total - 1;
+        size_t b = bb;
+        while (seg[b + 1] <= gl) ++b;
         const uint32_t r = run_of[b];
-        if (!okf[r]) continue;
-        const uint64_t s = g - seg[b], S = seg[b + 1] - seg[b];
-        const uint16_t *fr = frags + (uint64_t)m * seg[b] + s;
-        uint32_t f[IDA_MAX_N];
-#pragma unroll
-        for (int k = 0; k < IDA_MAX_N; ++k)
-            if (k < m) f[k] = fr[(uint64_t)k * S];
-        const int32_t *A = inv + (size_t)r * m * m;
-        uint16_t *o = out + (uint64_t)m * seg[b] + s * m;
-        int last = -1;
-        for (int j = 0; j < m; ++j) {
-            uint64_t acc = 0;
-#pragma unroll
-            for (int k = 0; k < IDA_MAX_N; ++k)
-                if (k < m) acc += (uint64_t)(uint32_t)A[j * m + k] * f[k];
-            const uint32_t c = (uint32_t)(acc % p);
-            o[j] = (uint16_t)c;
-            if (c) last = j;
+        const uint32_t r0 = __shfl(r, 0);
+        const bool uniform = __ballot(r != r0) == 0;
+        if (uniform && r0 != staged) {  // stage the shared inverse (wave-uniform branch)
+            const int32_t *A = inv + (size_t)r0 * m * m;
+            for (int t = lane; t < m * IDA_AROW; t += 64) {
+                const int j = t / IDA_AROW, w = t - j * IDA_AROW;
+                const uint32_t a0 = 2 * w < m ? (uint32_t)A[j * m + 2 * w] : 0u;
+                const uint32_t a1 = 2 * w + 1 < m ? (uint32_t)A[j * m + 2 * w + 1] : 0u;
+                As[t] = a0 | (a1 << 16);
+            }
+            staged = r0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (last >= 0) atomicMax(out_len + b, (unsigned long long)(s * m + last + 1));
+        int last = -1;
+        uint64_t s = 0;
+        if (live && okf[r]) {
+            s = g - seg[b];
+            const uint64_t S = seg[b + 1] - seg[b];
+            const uint16_t *fr = frags + (uint64_t)m * seg[b] + s;
+            uint32_t f[IDA_MAX_N];
+#pragma unroll
+            for (int k = 0; k < IDA_MAX_N; ++k) f[k] = k < m ? fr[(uint64_t)k * S] : 0u;
+            uint16_t *o = out + (uint64_t)m * g;  // = m seg[b] + s m
+            if (!WIDE && uniform) {
+                uint32_t F[16];
+#pragma unroll
+                for (int w = 0; w < 16; ++w) F[w] = f[2 * w] | (f[2 * w + 1] << 16);
+                uint32_t cprev = 0;
+                for (int j = 0; j < m; ++j) {
+                    const uint4 *ar = reinterpret_cast<const uint4 *>(As + j * IDA_AROW);
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (4 * q < nw) {
+                            const uint4 a4 = ar[q];
+                            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(cx_us2, a4.x),
+                                                         __builtin_bit_cast(cx_us2, F[4 * q]),
+                                                         acc, false);
+                            if (4 * q + 1 < nw)
+                                acc = __builtin_amdgcn_udot2(
+                                    __builtin_bit_cast(cx_us2, a4.y),
+                                    __builtin_bit_cast(cx_us2, F[4 * q + 1]), acc, false);
+                            if (4 * q + 2 < nw)
+                                acc = __builtin_amdgcn_udot2(
+                                    __builtin_bit_cast(cx_us2, a4.z),
+                                    __builtin_bit_cast(cx_us2, F[4 * q + 2]), acc, false);
+                            if (4 * q + 3 < nw)
+                                acc = __builtin_amdgcn_udot2(
+                                    __builtin_bit_cast(cx_us2, a4.w),
+                                    __builtin_bit_cast(cx_us2, F[4 * q + 3]), acc, false);
+                        }
+                    }
+                    const uint32_t cv = modp_f(acc, p, inv_p);
+                    if (cv) last = j;
+                    if ((m & 1) == 0) {  // m even: 4-byte aligned pairs
+                        if (j & 1)
+                            reinterpret_cast<uint32_t *>(o)[j >> 1] = cprev | (cv << 16);
+                        else
+                            cprev = cv;
+                    } else {
+                        o[j] = (uint16_t)cv;
+                    }
+                }
+            } else {
+                const int32_t *A = inv + (size_t)r * m * m;
+                for (int j = 0; j < m; ++j) {
+                    uint32_t cv;
+                    if (WIDE) {
+                        uint64_t acc = 0;
+#pragma unroll
+                        for (int k = 0; k < IDA_MAX_N; ++k)
+                            if (k < m) acc += (uint64_t)(uint32_t)A[j * m + k] * f[k];
+                        cv = (uint32_t)(acc % p);
+                    } else {
+                        uint32_t acc = 0;
+#pragma unroll
+                        for (int k = 0; k < IDA_MAX_N; ++k)
+                            if (k < m) acc += (uint32_t)A[j * m + k] * f[k];
+                        cv = modp_f(acc, p, inv_p);
+                    }
+                    o[j] = (uint16_t)cv;
+                    if (cv) last = j;
+                }
+            }
+        }
+        // kept length: per block, the highest lane holding a nonzero value
+        const uint64_t nz = __ballot(last >= 0);
+        const uint64_t above = lane == 63 ? 0ull : nz >> (lane + 1);
+        const int nxt = above ? lane + 1 + __builtin_ctzll(above) : 64;
+        const size_t bn = __shfl((unsigned long long)b, nxt & 63);
+        if (last >= 0 && (nxt == 64 || bn != b))
+            atomicMax(out_len + b, (unsigned long long)(s * m + last + 1));
     }
 }
 
@@ -2692,14 +2898,12 @@ hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t bl
     return hipGetLastError();
 }
 
-static uint64_t lemire_m(uint32_t p) { return ~0ull / p + 1; }
-
+// Persistent grid (the segment count lives on the device): 2048 x 4 waves.
 hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
-                      size_t blocks, uint64_t total_segs, int n, int m, int p, uint16_t *frags,
-                      hipStream_t s) {
-    if (blocks == 0 || total_segs == 0) return hipSuccess;
-    k_ida_encode<<<cx_grid(total_segs, 256, 16384), 256, 0, s>>>(data, offs, seg, blocks, n, m,
-                                                                  (uint32_t)p, lemire_m(p), frags);
+                      size_t blocks, int n, int m, int p, uint16_t *frags, hipStream_t s) {
+    if (blocks == 0) return hipSuccess;
+    k_ida_encode<<<2048, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p, 1.0f / p,
+                                      frags);
     return hipGetLastError();
 }
 
@@ -2724,14 +2928,20 @@ hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t run
     return hipGetLastError();
 }
 
-hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks,
-                      uint64_t total_segs, int m, int p, const int32_t *inv,
-                      const uint32_t *run_of, const uint8_t *okf, uint16_t *out,
-                      uint64_t *out_len, hipStream_t s) {
-    if (blocks == 0 || total_segs == 0) return hipSuccess;
-    k_ida_decode<<<cx_grid(total_segs, 256, 16384), 256, 0, s>>>(
-        frags, seg, blocks, m, (uint32_t)p, lemire_m(p), inv, run_of, okf, out,
-        reinterpret_cast<unsigned long long *>(out_len));
+hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m, int p,
+                      const int32_t *inv, const uint32_t *run_of, const uint8_t *okf,
+                      uint16_t *out, uint64_t *out_len, hipStream_t s) {
+    if (blocks == 0) return hipSuccess;
+    const bool wide = (uint64_t)m * (p - 1) * 65535ull >= (1ull << 32);
+    const unsigned grid = 2048;
+    if (wide)
+        k_ida_decode<true><<<grid, 256, 0, s>>>(frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv,
+                                                run_of, okf, out,
+                                                reinterpret_cast<unsigned long long *>(out_len));
+    else
+        k_ida_decode<false><<<grid, 256, 0, s>>>(frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv,
+                                                 run_of, okf, out,
+                                                 reinterpret_cast<unsigned long long *>(out_len));
     return hipGetLastError();
 }
 

@@ -117,17 +117,15 @@ hipError_t hex_parse(const uint8_t *bytes, const uint64_t *offs, size_t count, c
                      uint8_t *ok, hipStream_t s);
 hipError_t hex_format(const cell128 *keys, size_t count, char *out, uint8_t *len, hipStream_t s);
 hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
-                      size_t blocks, uint64_t total_segs, int n, int m, int p, uint16_t *frags,
-                      hipStream_t s);
+                      size_t blocks, int n, int m, int p, uint16_t *frags, hipStream_t s);
 hipError_t ida_runs(const uint8_t *idx, size_t blocks, int m, uint32_t *flag, hipStream_t s);
 hipError_t ida_run_index(const uint32_t *flag_excl, const uint32_t *flag_raw, size_t blocks,
                          uint32_t *run_of, uint32_t *run_start, hipStream_t s);
 hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, int m, int p,
                        int32_t *inv, uint8_t *okf, hipStream_t s);
-hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks,
-                      uint64_t total_segs, int m, int p, const int32_t *inv,
-                      const uint32_t *run_of, const uint8_t *okf, uint16_t *out,
-                      uint64_t *out_len, hipStream_t s);
+hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m, int p,
+                      const int32_t *inv, const uint32_t *run_of, const uint8_t *okf,
+                      uint16_t *out, uint64_t *out_len, hipStream_t s);
 hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks,
                            uint64_t *out_len, hipStream_t s);
 hipError_t check_indices(const uint32_t *idx, size_t count, uint32_t limit, bool allow_none,

@@ -123,8 +123,7 @@ def test_device_buffers_large(ida, O):
     keep = torch.tensor([0, 2, 3, 5, 6, 8, 9, 11, 12, 13], device="cuda")
     rows = fr[:, keep, :].contiguous().view(-1)
     idx = (keep + 1).to(torch.uint8).repeat(nb).contiguous()
-    segd = torch.from_numpy(seg.astype(np.int64)).cuda()
-    out, ln = ida.decode_flat(rows, segd, idx)
+    out, ln = ida.decode_flat(rows, seg, idx)
     torch.cuda.synchronize()
     vals = out.view(nb, S * 10)[:, :bl]
     assert bool((ln == bl).all())
