@@ -2554,10 +2554,47 @@ typedef unsigned short cx_us2 __attribute__((ext_vector_type(2)));
 // low bytes of E[i][0..31] then 8 words of high bytes (E < 46340 < 2^16).
 constexpr int IDA_EROW = 16;
 
-// Each wave takes a contiguous range of 64-segment chunks: one binary search
-// for its first chunk, then the chunk's first block only moves forward.  The
-// chunk's bytes (one contiguous span) are staged in LDS; each lane forms its
-// segment as packed words and takes 4 byte-products per v_dot4_u32_u8.
+// Per-lane cursor over blocks: the block holding segment g and its bounds,
+// reloaded only when g passes the block's end (segments only move forward).
+struct BlockCursor {
+    size_t b;
+    uint64_t sb, sb1;  // seg[b], seg[b+1]
+    uint64_t ob, ob1;  // offs[b], offs[b+1] (encode only)
+};
+
+template <bool OFFS>
+__device__ __forceinline__ void cursor_init(BlockCursor &k, const uint64_t *seg,
+                                            const uint64_t *offs, size_t b) {
+    k.b = b;
+    k.sb = seg[b];
+    k.sb1 = seg[b + 1];
+    if (OFFS) {
+        k.ob = offs[b];
+        k.ob1 = offs[b + 1];
+    }
+}
+
+template <bool OFFS>
+__device__ __forceinline__ void cursor_advance(BlockCursor &k, const uint64_t *seg,
+                                               const uint64_t *offs, uint64_t g) {
+    while (g >= k.sb1) {
+        ++k.b;
+        k.sb = k.sb1;
+        k.sb1 = seg[k.b + 1];
+        if (OFFS) {
+            k.ob = k.ob1;
+            k.ob1 = offs[k.b + 1];
+        }
+    }
+}
+
+// Each wave takes a contiguous range of 64-segment chunks.  Chunk c+1's bytes
+// (one contiguous span of data) are loaded into registers while chunk c is
+// computed; they pass through LDS so each lane can take its own m bytes as
+// packed words for v_dot4_u32_u8 (4 byte-products per instruction).
+// PRE = dwords per lane in flight: a chunk spans <= 64 m bytes + alignment,
+// i.e. <= 16 m + 1 words: PRE 3 covers m <= 11 (DHash's 10), PRE 8 any m.
+template <int PRE>
 __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const uint64_t *offs,
                                                     const uint64_t *seg, size_t blocks, int n,
                                                     int m, uint32_t p, float inv_p,
@@ -2590,40 +2627,61 @@ __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const u
     const uint64_t cpw = (chunks + waves - 1) / waves;
     const uint64_t c0 = wave * cpw, c1 = c0 + cpw < chunks ? c0 + cpw : chunks;
     if (c0 >= c1) return;  // wave-uniform, after the only block barrier
-    size_t bb = seg_block(seg, blocks, c0 * 64);
-    for (uint64_t c = c0; c < c1; ++c) {
-        const uint64_t g0 = c * 64, g = g0 + lane;
-        while (seg[bb + 1] <= g0) ++bb;
-        const bool live = g < total;
-        const uint64_t gl = live ? g : total - 1;
-        size_t b = bb;
-        while (seg[b + 1] <= gl) ++b;
-        const uint64_t s = gl - seg[b];
-        const uint64_t base = offs[b], len = offs[b + 1] - base;
-        const uint64_t my_lo = base + s * m;
+    BlockCursor cur;
+    cursor_init<true>(cur, seg, offs, seg_block(seg, blocks, c0 * 64));
+
+    // chunk descriptor of the chunk in flight
+    uint64_t n_segb = 0, n_S = 0, n_s = 0, n_span = 0;
+    uint32_t n_off = 0, n_words = 0;
+    int n_have = 0;
+    bool n_live = false;
+    uint32_t pre[PRE];
+    auto issue = [&](uint64_t c) {
+        const uint64_t g = c * 64 + lane;
+        n_live = g < total;
+        cursor_advance<true>(cur, seg, offs, n_live ? g : total - 1);
+        n_s = (n_live ? g : total - 1) - cur.sb;
+        n_segb = cur.sb;
+        n_S = cur.sb1 - cur.sb;
+        const uint64_t my_lo = cur.ob + n_s * m;
         uint64_t my_hi = my_lo + m;
-        if (my_hi > base + len) my_hi = base + len;
-        const uint64_t span_lo = __shfl(my_lo, 0) & ~3ull;
+        if (my_hi > cur.ob1) my_hi = cur.ob1;
+        n_span = __shfl(my_lo, 0) & ~3ull;
         const uint64_t span_hi = __shfl(my_hi, 63);
-        const uint32_t words = (uint32_t)((span_hi - span_lo + 3) >> 2);
-        for (uint32_t w = lane; w < words; w += 64) {
-            const uint64_t at = span_lo + 4ull * w;
-            uint32_t v;
-            if (at + 4 <= nbytes) {
-                v = *reinterpret_cast<const uint32_t *>(data + at);
-            } else {
-                v = 0;
-                for (int k = 0; k < 4; ++k)
-                    if (at + k < nbytes) v |= (uint32_t)data[at + k] << (8 * k);
+        n_words = (uint32_t)((span_hi - n_span + 3) >> 2);
+        n_off = (uint32_t)(my_lo - n_span);
+        n_have = (int)(my_hi - my_lo);
+#pragma unroll
+        for (int t = 0; t < PRE; ++t) {
+            const uint32_t w = lane + 64 * t;
+            const uint64_t at = n_span + 4ull * w;
+            uint32_t v = 0;
+            if (w < n_words) {
+                if (at + 4 <= nbytes) {
+                    v = *reinterpret_cast<const uint32_t *>(data + at);
+                } else {
+                    for (int k = 0; k < 4; ++k)
+                        if (at + k < nbytes) v |= (uint32_t)data[at + k] << (8 * k);
+                }
             }
-            st[w] = v;
+            pre[t] = v;
         }
+    };
+    issue(c0);
+    for (uint64_t c = c0; c < c1; ++c) {
+        // take over the chunk in flight
+        const uint64_t segb = n_segb, S = n_S, sg = n_s;
+        const uint32_t off = n_off, words = n_words;
+        const int have = n_have;
+        const bool live = n_live;
+#pragma unroll
+        for (int t = 0; t < PRE; ++t)
+            if (lane + 64 * t < (int)words) st[lane + 64 * t] = pre[t];
+        if (c + 1 < c1) issue(c + 1);  // next chunk's loads overlap this chunk's math
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // this lane's segment as packed words W[0..nw), bytes past `have` zero
-        const uint32_t off = (uint32_t)(my_lo - span_lo);
-        const int have = (int)(my_hi - my_lo);
         const uint32_t bw = off >> 2, sh = off & 3;
         uint32_t W[8];
         uint32_t prev = st[bw];
@@ -2641,8 +2699,7 @@ __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const u
             }
         }
         if (live) {
-            const uint64_t S = seg[b + 1] - seg[b];
-            uint16_t *out = frags + (uint64_t)n * seg[b] + s;
+            uint16_t *out = frags + (uint64_t)n * segb + sg;
             for (int i = 0; i < n; ++i) {
                 const uint4 *er = reinterpret_cast<const uint4 *>(Epk + i * IDA_EROW);
                 const uint4 l0 = er[0];
@@ -2898,12 +2955,29 @@ hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t bl
     return hipGetLastError();
 }
 
-// Persistent grid (the segment count lives on the device): 2048 x 4 waves.
+// Persistent grid (the segment count lives on the device): as many blocks as
+// fit on the chip at once, from the occupancy API.
+template <class K>
+static unsigned resident_grid(K kernel, int block) {
+    int dev = 0, cus = 256, per = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess ||
+        per < 1)
+        per = 1;
+    return (unsigned)(per * cus);
+}
 hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
                       size_t blocks, int n, int m, int p, uint16_t *frags, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
-    k_ida_encode<<<2048, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p, 1.0f / p,
-                                      frags);
+    static const unsigned g3 = resident_grid(k_ida_encode<3>, 256);
+    static const unsigned g8 = resident_grid(k_ida_encode<8>, 256);
+    if (16 * m + 1 <= 64 * 3)
+        k_ida_encode<3><<<g3, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p, 1.0f / p,
+                                           frags);
+    else
+        k_ida_encode<8><<<g8, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p, 1.0f / p,
+                                           frags);
     return hipGetLastError();
 }
 
@@ -2933,7 +3007,9 @@ hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks,
                       uint16_t *out, uint64_t *out_len, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
     const bool wide = (uint64_t)m * (p - 1) * 65535ull >= (1ull << 32);
-    const unsigned grid = 2048;
+    static const unsigned gw = resident_grid(k_ida_decode<true>, 256);
+    static const unsigned gn = resident_grid(k_ida_decode<false>, 256);
+    const unsigned grid = wide ? gw : gn;
     if (wide)
         k_ida_decode<true><<<grid, 256, 0, s>>>(frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv,
                                                 run_of, okf, out,
