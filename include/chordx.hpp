@@ -230,4 +230,73 @@ private:
     cx_ring *h_ = nullptr;
 };
 
+// Wire bridge (cx_wire_*): answers GET_SUCC request objects for a ring of
+// peers named "ip:port" (chord_peer.cpp:15-40, server.h:194-210).
+class Wire {
+public:
+    Wire(const std::vector<std::string> &addrs, int device = 0) {
+        std::vector<const char *> p;
+        for (const auto &a : addrs) p.push_back(a.c_str());
+        check(cx_wire_create(p.data(), p.size(), device, &h_));
+    }
+    ~Wire() { cx_wire_destroy(h_); }
+    Wire(const Wire &) = delete;
+    Wire &operator=(const Wire &) = delete;
+
+    // JSON request text -> JSON response text.
+    std::string Handle(const std::string &request) {
+        char *out = nullptr;
+        size_t len = 0;
+        check(cx_wire_handle(h_, request.data(), request.size(), &out, &len));
+        std::string r(out, len);
+        cx_wire_free(out);
+        return r;
+    }
+
+private:
+    cx_wire *h_ = nullptr;
+};
+
+// Rabin IDA (cx_ida_*): DataBlock's encode/decode (ida.cpp:59-162).
+namespace ida {
+// Fragments of one value: n rows of ceil(len / m) values (fragment i has index i + 1).
+inline std::vector<std::vector<uint16_t>> Encode(const std::string &value, int n = 14, int m = 10,
+                                                 int p = 257, int device = 0) {
+    const uint64_t offs[2] = {0, value.size()};
+    uint64_t seg[2];
+    check(cx_ida_segments(offs, 1, m, seg));
+    const size_t S = seg[1];
+    std::vector<uint16_t> flat(n * S + 1);
+    check(cx_ida_encode(reinterpret_cast<const uint8_t *>(value.data()), offs, seg, 1, n, m, p,
+                        flat.data(), CX_MEM_HOST, device));
+    std::vector<std::vector<uint16_t>> rows(n);
+    for (int i = 0; i < n; ++i) rows[i].assign(flat.begin() + i * S, flat.begin() + (i + 1) * S);
+    return rows;
+}
+
+// IDA::Decode from m fragments (index, values), trailing zeros dropped;
+// throws "N is not invertible" like matrix_math.cpp:81-82.
+inline std::vector<uint16_t> Decode(const std::vector<std::pair<int, std::vector<uint16_t>>> &frags,
+                                    int m = 10, int p = 257, int device = 0) {
+    if ((int)frags.size() < m)
+        throw Error(CX_E_INSUFFICIENT, std::to_string(m) + " frags are required to decode.");
+    const size_t S = frags[0].second.size();
+    std::vector<uint16_t> flat;
+    std::vector<uint8_t> idx;
+    for (int k = 0; k < m; ++k) {
+        flat.insert(flat.end(), frags[k].second.begin(), frags[k].second.end());
+        idx.push_back((uint8_t)frags[k].first);
+    }
+    flat.push_back(0);
+    const uint64_t seg[2] = {0, S};
+    std::vector<uint16_t> out(m * S + 1);
+    uint64_t len = 0;
+    check(cx_ida_decode(flat.data(), seg, idx.data(), 1, m, p, out.data(), &len, CX_MEM_HOST,
+                        device));
+    if (len == UINT64_MAX) throw Error(CX_E_INVALID, "N is not invertible");
+    out.resize(len);
+    return out;
+}
+}  // namespace ida
+
 }  // namespace chordx

@@ -126,6 +126,37 @@ TEST(DHashPeer, InsufficientSuccs) {
     EXPECT_EQ(ring.GetNSuccessors(Key(0, 5), 14).size(), 9u);
 }
 
+TEST(Wire, GetSuccJoinFixture) {
+    // ChordIntegration.Join peers by name; key1 belongs to 94227b6d... (port 5003)
+    chordx::Wire w({"127.0.0.1:5000", "127.0.0.1:5001", "127.0.0.1:5002", "127.0.0.1:5003",
+                    "127.0.0.1:5004", "127.0.0.1:5005"});
+    const std::string r = w.Handle("{\"COMMAND\":\"GET_SUCC\",\"KEY\":\"8f218246f4e35dc7b60419ff9fcbce73\"}");
+    EXPECT_TRUE(r.find("\"ID\":\"94227b6ddb5a5ee68a4b8c7627640f5d\"") != std::string::npos);
+    EXPECT_TRUE(r.find("\"PORT\":5003") != std::string::npos);
+    EXPECT_TRUE(r.find("\"SUCCESS\":true") != std::string::npos);
+    const std::string bad = w.Handle("{\"COMMAND\":\"NOPE\"}");
+    EXPECT_TRUE(bad.find("Invalid command.") != std::string::npos);
+}
+
+TEST(DataBlock, EncodeDecodeVal1) {
+    // DHashIntegration.CreateAndRead stores "val1" (dhash_test.cpp:213-226)
+    const std::string v = "val1";
+    auto rows = chordx::ida::Encode(v);
+    EXPECT_EQ(rows.size(), 14u);
+    std::vector<std::pair<int, std::vector<uint16_t>>> alive;
+    for (int i : {1, 2, 4, 5, 6, 8, 9, 10, 12, 13}) alive.push_back({i + 1, rows[i]});
+    std::vector<uint16_t> back = chordx::ida::Decode(alive);
+    EXPECT_EQ(std::string(back.begin(), back.end()), v);
+    bool threw = false;
+    alive[1].first = alive[0].first;  // repeated index
+    try {
+        chordx::ida::Decode(alive);
+    } catch (const chordx::Error &e) {
+        threw = std::string(e.what()) == "N is not invertible";
+    }
+    EXPECT_TRUE(threw);
+}
+
 int main() {
     RUN(KeyInBetweenTest, ExclusiveNoModulo);
     RUN(KeyInBetweenTest, ExclusiveWithModulo);
@@ -137,6 +168,8 @@ int main() {
     RUN(ChordGetSucc, FromPredecessor);
     RUN(ChordGetSucc, Failing);
     RUN(DHashPeer, InsufficientSuccs);
+    RUN(Wire, GetSuccJoinFixture);
+    RUN(DataBlock, EncodeDecodeVal1);
     std::printf(failures ? "FAILED (%d)\n" : "PASSED\n", failures);
     return failures ? 1 : 0;
 }
