@@ -205,6 +205,10 @@ def main():
     status = torch.empty(Q, dtype=torch.uint8, device=dev)
     out = (owner, hops, status)
 
+    route_variant, cz_escapes, table_bytes = ring.route_info()
+    kernel_name = {5: "k_route_tree<false, true>", 4: "k_route_tree<false, false>"}.get(
+        route_variant, f"route variant {route_variant}")
+
     # ---- warmup ----
     for _ in range(args.warmup):
         ring.route(src, keys, out=out)
@@ -255,7 +259,7 @@ def main():
     ring.set_search_variant(1)
     # A/B: the other route kernels on the same batch (bit-identical results)
     variant_ms = {}
-    for v in (0, 1, 2, 3, 4):
+    for v in (0, 1, 2, 3, 4, 5):
         ring.set_route_variant(v)
         ring.route(src, keys, out=out)
         e0.record(stream)
@@ -264,7 +268,7 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize(dev)
         variant_ms[v] = e0.elapsed_time(e1) / 3
-    ring.set_route_variant(4)
+    ring.set_route_variant(-1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -281,7 +285,7 @@ def main():
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == "k_route_tree":
+        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == kernel_name:
             traffic = tj.get("hbm_bytes_per_launch")
             req = tj["fetch_bytes"] / 64 / (kern_ms * 1e-3)
             gather = {"requests_per_s": req, "ceiling": GATHER_CEILING,
@@ -314,10 +318,13 @@ def main():
                        "parallelism": f"replicated ring, keys sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "kernel": "k_route_tree", "kernel_ms": kern_ms,
+                         "kernel": kernel_name, "kernel_ms": kern_ms,
                          "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             "gather_roofline": gather,
+            "route_variant": route_variant,
+            "route_table_bytes": table_bytes,
+            "route_cz_escapes": cz_escapes,
             "mean_hops": sum_hops / Q,
             "bad_status": bad,
             "route_owner_equals_successor": owner_eq,

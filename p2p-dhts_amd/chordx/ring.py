@@ -176,10 +176,21 @@ class Ring:
         return _wrap_device(p.value, (self.n, L.CX_FINGERS), torch.int32, self.device, self)
 
     def set_route_variant(self, v: int):
-        """Internal A/B switch: 0 = finger + ring gather per hop, 1 = route table."""
+        """Internal A/B switch: 0 = finger + ring gather per hop, 1 = route table,
+        2/3 = packed table, 4 = lookahead tree, 5 = pattern-keyed window table,
+        -1 = automatic (5 up to 2^24 peers, else 4)."""
         f = L.lib().cxi_set_route_variant
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))
+
+    def route_info(self):
+        """(variant in effect, variant-5 nodes not representable, route-table bytes)."""
+        f = L.lib().cxi_route_info
+        f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        v, e, b = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        L.check(f(self._h, ctypes.byref(v), ctypes.byref(e), ctypes.byref(b)))
+        return v.value, e.value, b.value
 
     def set_churn_variant(self, v: int):
         """Internal A/B switch: 0 = full re-sort, 1 = merge of sorted joins (default)."""

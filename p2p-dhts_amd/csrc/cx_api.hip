@@ -91,8 +91,12 @@ struct cx_ring {
     uint64_t *d_tree = nullptr;    // lookahead-tree table [n][rt_R][8] (variant 4)
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
-    int route_variant = 4;         // 0: finger+ring gathers, 1: route table, 2: packed table,
-                                   // 3: 2 + staging, 4: lookahead-tree table (default)
+    uint64_t *d_cz = nullptr;      // pattern-keyed window table [n][rt_R][2][8 x u64] (variant 5)
+    bool cz_valid = false;
+    uint64_t cz_escapes = 0;       // nodes the compressed format could not represent
+    int route_variant = -1;        // 0: finger+ring gathers, 1: route table, 2: packed table,
+                                   // 3: 2 + staging, 4: lookahead-tree table, 5: pattern-keyed
+                                   // window table; -1: automatic (5 up to 2^24 peers, else 4)
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags), 1 KiB
@@ -120,6 +124,11 @@ struct cx_ring {
         return v;
     }
     bool literal() const { return !fingers_converged || d_min_keys || d_preds; }
+    int variant() const {
+        if (route_variant >= 0) return route_variant;
+        return (pk_ib <= 24 && !cz_failed) ? 5 : 4;
+    }
+    bool cz_failed = false;        // automatic mode: no HBM for the variant-5 table
 };
 
 namespace {
@@ -211,6 +220,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_rt);
     (void)hipFree(r->d_pk);
     (void)hipFree(r->d_tree);
+    (void)hipFree(r->d_cz);
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
@@ -261,19 +271,35 @@ void route_geometry(cx_ring *r) {
 int ensure_route_table(cx_ring *r, hipStream_t s) {
     if (!r->fingers_converged || !r->d_ring_ext) return CX_OK;
     const size_t ent = r->n * (size_t)r->rt_R;
-    if (r->route_variant == 1 && !r->rt_valid) {
+    if (r->variant() == 5 && !r->cz_valid) {
+        if (!r->d_cz && hipMalloc(&r->d_cz, ent * 128) != hipSuccess) {
+            r->d_cz = nullptr;
+            if (r->route_variant < 0) r->cz_failed = true;  // automatic: use variant 4
+        }
+        if (r->d_cz) {
+            CX_HIP(hipMemsetAsync(r->d_scratch, 0, sizeof(uint32_t), s));
+            CX_HIP(cxk::cz_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib,
+                                 r->d_cz, r->d_scratch, s));
+            uint32_t esc = 0;
+            CX_HIP(hipMemcpyAsync(&esc, r->d_scratch, sizeof(esc), hipMemcpyDeviceToHost, s));
+            CX_HIP(hipStreamSynchronize(s));
+            r->cz_escapes = esc;
+            r->cz_valid = true;
+        }
+    }
+    if (r->variant() == 1 && !r->rt_valid) {
         if (!r->d_rt && hipMalloc(&r->d_rt, ent * sizeof(RtEntry)) != hipSuccess) r->d_rt = nullptr;
         if (r->d_rt) {
             CX_HIP(cxk::rt_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->d_rt, r->d_ring_ext, s));
             r->rt_valid = true;
         }
-    } else if ((r->route_variant == 2 || r->route_variant == 3) && !r->pk_valid) {
+    } else if ((r->variant() == 2 || r->variant() == 3) && !r->pk_valid) {
         if (!r->d_pk && hipMalloc(&r->d_pk, ent * 16) != hipSuccess) r->d_pk = nullptr;
         if (r->d_pk) {
             CX_HIP(cxk::pk_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_pk, s));
             r->pk_valid = true;
         }
-    } else if (r->route_variant == 4 && !r->tree_valid) {
+    } else if (r->variant() == 4 && !r->tree_valid) {
         if (!r->d_tree && hipMalloc(&r->d_tree, ent * 64) != hipSuccess) r->d_tree = nullptr;
         if (r->d_tree) {
             CX_HIP(cxk::tree_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_tree, s));
@@ -490,7 +516,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     CX_HIP(cxk::fingers_build(ring->sv(), ring->d_ring, ring->d_fingers, s));
     ring->fingers_converged = true;
     route_geometry(ring);
-    ring->rt_valid = ring->pk_valid = ring->tree_valid = false;  // tables follow the fingers
+    ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
@@ -528,7 +554,7 @@ int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
     CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
     ring->fingers_converged = false;
-    ring->rt_valid = ring->pk_valid = ring->tree_valid = false;
+    ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
     CX_CHECK(!bad, CX_E_INVALID, "finger entry is not a ring index");
     return CX_OK;
 }
@@ -591,8 +617,12 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
         int e2 = ensure_route_table(const_cast<cx_ring *>(ring), s);
         if (e2) return e2;
     }
-    const int v = ring->literal() ? -1 : ring->route_variant;
-    if (v == 4 && ring->tree_valid)
+    const int v = ring->literal() ? -1 : ring->variant();
+    if (v == 5 && ring->cz_valid)
+        CX_HIP(cxk::route_cz(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
+                             ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
+                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
+    else if (v == 4 && ring->tree_valid)
         CX_HIP(cxk::route_tree(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_tree, ring->rt_l0,
                                ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
                                reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
@@ -1177,11 +1207,29 @@ int cxi_set_error(int code, const char *msg) { return fail(code, msg ? msg : "")
 // ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
 // and parity tests.  0 = finger + ring gathers per hop, 1 = route table,
 // 2 = packed route table with one-level lookahead, 3 = 2 + staged results and
-// prefetched source pairs, 4 = lookahead-tree table (default).
+// prefetched source pairs, 4 = lookahead-tree table, 5 = pattern-keyed window
+// table, -1 = automatic (default: 5 up to 2^24 peers, else 4).
 int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 4, CX_E_INVALID, "variant must be 0..4");
+    CX_CHECK(variant >= -1 && variant <= 5, CX_E_INVALID, "variant must be -1 (auto) or 0..5");
     ring->route_variant = variant;
+    return CX_OK;
+}
+
+// Route variant in effect, variant-5 nodes its format could not represent, and
+// the bytes of the route table the variant reads (0 if not built).
+int cxi_route_info(const cx_ring *ring, int *variant, uint64_t *cz_escapes,
+                   uint64_t *table_bytes) {
+    CX_CHECK(ring && variant && cz_escapes && table_bytes, CX_E_INVALID, "null argument");
+    const int v = ring->literal() ? -1 : ring->variant();
+    const size_t ent = ring->n * (size_t)ring->rt_R;
+    *variant = v;
+    *cz_escapes = ring->cz_escapes;
+    *table_bytes = v == 5 && ring->cz_valid     ? ent * 128
+                   : v == 4 && ring->tree_valid ? ent * 64
+                   : (v == 2 || v == 3) && ring->pk_valid ? ent * 16
+                   : v == 1 && ring->rt_valid ? ent * sizeof(RtEntry)
+                                              : 0;
     return CX_OK;
 }
 

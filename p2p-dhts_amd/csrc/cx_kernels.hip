@@ -1055,6 +1055,8 @@ struct PkCtx {
     int l0, ib, S;
     uint64_t imask;
     u128 W;
+    // variant 5 (cz): gap-code shift of a compressed node
+    int gs;
     // arc mode: only rows [lo, hi) are local; F is absent (fingers by search)
     bool arc;
     uint32_t lo, hi;
@@ -1455,6 +1457,238 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
     }
 }
 
+// ---------------------------------------------------------------------------
+// Variant 5 ("cz"): pattern-keyed window entries of sixteen 4-B nodes.
+//
+// The walk consumes the bits of d = key - id_cur from the top: a hop at level
+// i = msb(d) clears bit i (plus the successor gap, ~2^104 at 2^24 peers), so
+// the levels a walk visits after A = finger(p, i) follow the set bits of d
+// below i.  Entry (p, i, b) is keyed by b = bit i-1 of d - 2^i, read by the
+// gathering lane, and holds the peers of the window of four levels after the
+// forced part of the path:
+//   b = 0: slot v (v = a 4-bit subset of the levels i-2..i-5, bit w <-> level
+//          i-2-w) = the peer reached from A by hops at v's levels (in
+//          descending order); slot 0 = A itself;
+//   b = 1: slot 15 = A; slot v = the peer reached from A' = finger(A, i-1) by
+//          hops at v's levels (v = 15 is not stored).
+// Simulated on a 2^24 ring: 0.34 gathers per hop, vs 0.44 for the 8-finger
+// tree of variant 4 (0.39 for a 1-bit pattern with 8 fingers, 0.38 for a
+// 16-finger tree), at twice variant 4's table size (one 64-B entry per bit b).
+//
+// A node is stored relative to its parent (the peer the hop leaves, at level
+// l): bits 0..15 = idx - idx_par - E(l) + 2^15 (mod n, signed), with
+// E(l) = round(n * 2^(l-128)) the expected index advance; bits 16..31 =
+// (id - id_par - 2^l) >> gs, the successor gap in units of 2^gs (gs = 116 - ib:
+// 16x the mean gap fits).  CZ_NONE = not representable (the walk then
+// gathers or takes the exact finger).  Decoded IDs are intervals whose width
+// grows by 2^gs - 1 per relative hop; every decision is taken on the
+// interval, and an undecided one fetches the exact IDs (A_FIXC / A_FIXT).
+// ---------------------------------------------------------------------------
+constexpr uint32_t CZ_NONE = 0xFFFFFFFFu;
+
+__host__ __device__ __forceinline__ int cz_shift(int ib) { return 116 - ib; }
+
+__device__ __forceinline__ uint32_t cz_expect(uint32_t n, int l) {
+    const int sh = 128 - l;
+    return sh > 40 ? 0u : (uint32_t)(((uint64_t)n + (1ull << (sh - 1))) >> sh);
+}
+
+__device__ __forceinline__ uint32_t cz_encode(uint32_t n, int gs, uint32_t par, u128 pid, int l,
+                                              uint32_t x, u128 xid) {
+    int64_t d = ((int64_t)x - (int64_t)par - (int64_t)cz_expect(n, l)) % (int64_t)n;
+    if (d < 0) d += n;
+    if (d > (int64_t)(n / 2)) d -= n;  // (-n/2, n/2]
+    const u128 code = (xid - pid - ((u128)1 << l)) >> gs;
+    if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
+    return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
+}
+
+__device__ __forceinline__ uint32_t cz_next(uint32_t n, uint32_t cur, int l, uint32_t wd) {
+    int t = (int)cur + (int)cz_expect(n, l) + (int)(wd & 0xFFFF) - 32768;  // n < 2^30
+    if (t < 0)
+        t += (int)n;
+    else if (t >= (int)n)
+        t -= (int)n;
+    return (uint32_t)t;
+}
+
+__global__ void k_cz_build(const uint32_t *F, const cell128 *ring, uint32_t n, int l0, int R,
+                           int gs, uint4 *cz, uint32_t *esc) {
+    const size_t total = (size_t)n * R * 2;
+    uint32_t bad = 0;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        const int b = (int)(t & 1);
+        const size_t r = t >> 1;
+        const size_t p = r / (unsigned)R;
+        const int i = l0 + (int)(r - p * (unsigned)R);
+        uint32_t node[16], out[16];
+        u128 nid[16];
+        const u128 idp = ld128(ring + p);
+        uint32_t a = (uint32_t)p;
+        u128 aid = idp;
+        int al = i;
+        if (b) {
+            node[15] = F[p * CX_FINGERS + i];
+            nid[15] = ld128(ring + node[15]);
+            out[15] = cz_encode(n, gs, (uint32_t)p, idp, i, node[15], nid[15]);
+            a = node[15];
+            aid = nid[15];
+            al = i - 1;
+        }
+        node[0] = F[(size_t)a * CX_FINGERS + al];
+        nid[0] = ld128(ring + node[0]);
+        out[0] = cz_encode(n, gs, a, aid, al, node[0], nid[0]);
+#pragma unroll
+        for (int v = 1; v < 15; ++v) {
+            const int hb = 31 - __builtin_clz((unsigned)v);
+            const int pv = v & ~(1 << hb);
+            const int lv = i - 2 - hb;
+            node[v] = F[(size_t)node[pv] * CX_FINGERS + lv];
+            nid[v] = ld128(ring + node[v]);
+            out[v] = cz_encode(n, gs, node[pv], nid[pv], lv, node[v], nid[v]);
+        }
+        if (!b) {  // v = 15: parent 7, level i - 5
+            node[15] = F[(size_t)node[7] * CX_FINGERS + i - 5];
+            nid[15] = ld128(ring + node[15]);
+            out[15] = cz_encode(n, gs, node[7], nid[7], i - 5, node[15], nid[15]);
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) bad += out[v] == CZ_NONE;
+        uint4 *e = cz + t * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            e[k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
+    }
+    if (bad) atomicAdd(esc, bad);
+}
+
+hipError_t cz_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
+                    uint64_t *cz, uint32_t *esc, hipStream_t s) {
+    k_cz_build<<<cx_grid(n * (size_t)R * 2, 256), 256, 0, s>>>(
+        F, ring, (uint32_t)n, l0, R, cz_shift(ib), reinterpret_cast<uint4 *>(cz), esc);
+    return hipGetLastError();
+}
+
+// The cz walk runs in units of u = 2^gs: d = key - id_cur lies in
+// [dmin * u, dmax * u + u - 1] (two u64).  Every threshold it is compared with
+// (2^l, 2^l + gap) is a multiple of u up to the gap's sub-unit part, so a hop
+// is exact integer arithmetic on (dmin, dmax): with e = 2^(l-gs) + code,
+//   StoredLocally(nxt) holds     if dmax <  e,
+//   fails (d' = d - 2^l - gap)   if dmin >  e  ->  [dmin - e - 1, dmax - e],
+//   is undecided otherwise (A_FIXT: exact IDs of cur and nxt).
+// The level is gs + msb(dmin) when msb(dmin) == msb(dmax); otherwise, or
+// when d < u, the walk needs cur's exact ID (cex: clo = id_cur).
+__device__ __forceinline__ void cz_exact_d(const PkCtx &c, u128 key, u128 idc, uint64_t &dmin,
+                                           uint64_t &dmax) {
+    dmin = dmax = (uint64_t)((key - idc) >> c.gs);
+}
+
+// Exact hop from cur at level i through the finger table (below the table,
+// or a root the entry cannot represent); needs clo = id_cur (cex).
+// 1 = finished (own/st set), 0 = moved (cur, clo exact, dmin/dmax).
+__device__ __forceinline__ int cz_exact(const PkCtx &c, u128 key, u128 &clo, uint64_t &dmin,
+                                        uint64_t &dmax, uint32_t &cur, uint32_t &h, int i,
+                                        uint32_t &own, uint8_t &st) {
+    const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
+    const u128 idn = ld128(c.ring + nxt);
+    ++h;
+    if (key - clo <= idn - clo) {
+        own = nxt;
+        return 1;
+    }
+    if (h == CX_HOP_CAP) {
+        own = CX_NONE;
+        st = CX_Q_HOPCAP;
+        return 1;
+    }
+    cur = nxt;
+    clo = idn;
+    cz_exact_d(c, key, idn, dmin, dmax);
+    return 0;
+}
+
+// One relative hop through node word wd at level i.  1 = finished, -1 =
+// undecided (A_FIXT), 0 = moved.
+__device__ __forceinline__ int cz_hop(const PkCtx &c, uint32_t wd, int i, uint64_t &dmin,
+                                      uint64_t &dmax, uint32_t &cur, uint32_t &h, uint32_t &pn,
+                                      uint32_t &own, uint8_t &st) {
+    const uint64_t e = (1ull << (i - c.gs)) + (wd >> 16);
+    const uint32_t nxt = cz_next(c.n, cur, i, wd);
+    ++h;
+    if (dmax < e) {
+        own = nxt;
+        return 1;
+    }
+    if (dmin <= e) {
+        pn = nxt;
+        return -1;
+    }
+    if (h == CX_HOP_CAP) {
+        own = CX_NONE;
+        st = CX_Q_HOPCAP;
+        return 1;
+    }
+    cur = nxt;
+    dmin -= e + 1;
+    dmax -= e;
+    return 0;
+}
+
+// Plan from cur using the lane's LDS entry (16 nodes) for free hops.  cs = the
+// window subset we stand on (-1: none, 16: the root A of a b = 1 entry), ri =
+// the entry's level.  Returns 0 = needs a load (mode set), 1 = finished.
+__device__ __forceinline__ int cz_plan(const PkCtx &c, u128 key, u128 &clo, bool &cex,
+                                       uint64_t &dmin, uint64_t &dmax, uint32_t &cur,
+                                       uint32_t &h, uint32_t &pn, int &mode, int &lvl, int &rb,
+                                       int &cs, int ri, const uint32_t *ent, uint32_t &own,
+                                       uint8_t &st) {
+    for (;;) {
+        int i;
+        const int ma = 63 - __builtin_clzll(dmin | 1), mb = 63 - __builtin_clzll(dmax | 1);
+        if (dmin != 0 && ma == mb) {
+            i = ma + c.gs;
+        } else if (!cex) {
+            mode = A_FIXC;
+            return 0;
+        } else {
+            i = msb128(key - clo);  // d < 2^gs, exact
+        }
+        const int o = ri - i;
+        int v = -1;
+        if (cs == 16) {
+            if (o == 1) v = 0;
+        } else if (cs >= 0 && o >= 2 && o <= 5) {
+            v = cs | (1 << (o - 2));
+            if (rb && v == 15) v = -1;
+        }
+        const uint32_t wd = v >= 0 ? ent[v] : CZ_NONE;
+        if (wd != CZ_NONE) {
+            const int t = cz_hop(c, wd, i, dmin, dmax, cur, h, pn, own, st);
+            if (t > 0) return 1;
+            if (t < 0) {
+                mode = A_FIXT;
+                return 0;
+            }
+            cs = v;
+            cex = false;
+            continue;
+        }
+        cs = -1;
+        if (i >= c.l0) {
+            mode = A_HOP;
+            lvl = i;
+            rb = (int)((dmax >> (i - 1 - c.gs)) & 1);  // bit i-1 of d - 2^i
+            return 0;
+        }
+        if (!cex) {
+            mode = A_FIXC;
+            return 0;
+        }
+        if (cz_exact(c, key, clo, dmin, dmax, cur, h, i, own, st)) return 1;
+    }
+}
+
 // Arguments of the tree walk (replicated ring: lo = 0, hi = n; arc mode: the
 // rank's arc, inputs and outcomes as 32-B ArcRec records).
 struct TreeIO {
@@ -1476,8 +1710,9 @@ struct TreeIO {
     uint8_t *status;
 };
 
-template <bool ARC>
+template <bool ARC, bool CZ>
 __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
+    static_assert(!(ARC && CZ), "arc mode walks variant-4 rows");
     __shared__ uint64_t res_all[ARC ? 1 : RT_BLOCK / 64][ARC ? 1 : RES_WIN];
     __shared__ uint4 ent_all[RT_BLOCK][4];       // each lane's current 64-B entry
     __shared__ uint64_t addr_all[RT_BLOCK];      // entry index + 1 wanted by each lane (0: none)
@@ -1487,6 +1722,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
     const int quad0 = threadIdx.x & ~3, qs = threadIdx.x & 3;
     uint64_t *res = res_all[ARC ? 0 : (threadIdx.x >> 6)];
     const uint64_t *ent = reinterpret_cast<const uint64_t *>(ent_all[threadIdx.x]);
+    const uint32_t *ent32 = reinterpret_cast<const uint32_t *>(ent_all[threadIdx.x]);
     if (!ARC)
         for (int j = lane; j < RES_WIN; j += 64) res[j] = 0;
     const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
@@ -1502,6 +1738,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
     c.S = 64 + ib;
     c.imask = (1ull << ib) - 1;
     c.W = ((u128)1 << c.S) - 1;
+    c.gs = cz_shift(ib);
     c.arc = ARC;
     c.lo = io.lo;
     c.hi = io.hi;
@@ -1512,7 +1749,9 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
     size_t qi = 0;
     uint64_t qid = 0;
     u128 key = 0, clo = 0;
-    bool cex = true;
+    bool cex = true;          // id(cur) = clo exactly (tree: else in [clo, clo + W])
+    uint64_t dmin = 0, dmax = 0;  // cz: d = key - id(cur) in units of 2^gs
+    int rb = 0;               // cz: pattern bit of the wanted entry
     uint32_t cur = 0, h = 0, pn = 0;
     int bst = B_EMPTY, pkind = 0;
     size_t pq = 0;
@@ -1581,8 +1820,11 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
             break;
 
         // ---- memory round ----
-        addr_all[threadIdx.x] =
-            mode == A_HOP ? (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0) + 1 : 0;
+        {
+            uint64_t e = (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0);
+            if (CZ) e = e * 2 + rb;
+            addr_all[threadIdx.x] = mode == A_HOP ? e + 1 : 0;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1619,7 +1861,33 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
         bool fin = false, plan = false;
         uint32_t own = CX_NONE;
         uint8_t st = CX_Q_OK;
-        if (mode == A_HOP) {
+        if (mode == A_HOP && CZ) {
+            // root of entry (cur, lvl, rb): A = finger(cur, lvl)
+            const uint32_t wd = ent32[rb ? 15 : 0];
+            ri = lvl;
+            if (wd != CZ_NONE) {
+                const int t = cz_hop(c, wd, lvl, dmin, dmax, cur, h, pn, own, st);
+                if (t > 0) {
+                    fin = true;
+                } else if (t < 0) {
+                    mode = A_FIXT;
+                } else {
+                    cex = false;
+                    cs = rb ? 16 : 0;
+                    plan = true;
+                }
+            } else {
+                cs = -1;
+                if (!cex) {  // rare: exact id of cur for the exact hop
+                    clo = ld128(io.ring + cur);
+                    cex = true;
+                }
+                if (cz_exact(c, key, clo, dmin, dmax, cur, h, lvl, own, st))
+                    fin = true;
+                else
+                    plan = true;
+            }
+        } else if (mode == A_HOP) {
             const uint64_t m0 = ent[0];
             ri = lvl;
             cs = 0;
@@ -1645,6 +1913,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
         } else if (mode == A_FIXC) {
             clo = xa;
             cex = true;
+            if (CZ) cz_exact_d(c, key, xa, dmin, dmax);
             plan = true;
         } else if (mode == A_FIXT) {
             if (key - xa <= xb - xa) {
@@ -1657,11 +1926,15 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
                 cur = pn;
                 clo = xb;
                 cex = true;
+                if (CZ) cz_exact_d(c, key, xb, dmin, dmax);
                 plan = true;
             }
         }
         if (plan) {
-            const int r = tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
+            const int r =
+                CZ ? cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs, ri, ent32,
+                             own, st)
+                   : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
             if (r == 1) fin = true;
             if (ARC && r == 2) {  // continue on the rank that owns cur's row
                 ArcRec o;
@@ -1707,7 +1980,11 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
             } else {
                 clo = pb;
                 cex = true;
-                done = tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
+                if (CZ) cz_exact_d(c, key, pb, dmin, dmax);
+                done = CZ ? cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs,
+                                    ri, ent32, own, st)
+                          : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own,
+                                      st);
                 if (ARC && done == 2) {
                     ArcRec o;
                     o.w0 = (uint64_t)key;
@@ -1780,7 +2057,35 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
     io.status = status;
     unsigned blocks;
     tree_geometry(q, io.chunk, blocks);
-    k_route_tree<false><<<blocks, RT_BLOCK, 0, s>>>(io);
+    k_route_tree<false, false><<<blocks, RT_BLOCK, 0, s>>>(io);
+    return hipGetLastError();
+}
+
+hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
+                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                    uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    TreeIO io = {};
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.tree = reinterpret_cast<const uint4 *>(cz);
+    io.l0 = l0;
+    io.R = R;
+    io.ib = ib;
+    io.F = F;
+    io.lo = 0;
+    io.hi = (uint32_t)n;
+    io.src = src;
+    io.keys = keys;
+    io.q = q;
+    io.owner = owner;
+    io.hops = hops;
+    io.status = status;
+    unsigned blocks;
+    tree_geometry(q, io.chunk, blocks);
+    k_route_tree<false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 
@@ -1854,7 +2159,7 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
     io.status = status;
     unsigned blocks;
     tree_geometry(q, io.chunk, blocks);
-    k_route_tree<true><<<blocks, RT_BLOCK, 0, s>>>(io);
+    k_route_tree<true, false><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 

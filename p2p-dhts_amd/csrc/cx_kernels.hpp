@@ -78,6 +78,12 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
                       const uint64_t *tree, int l0, int R, int ib, const uint32_t *F,
                       const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
                       uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t cz_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
+                    uint64_t *cz, uint32_t *esc, hipStream_t s);
+hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
+                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                    uint8_t *status, hipStream_t s);
 hipError_t tree_build_arc(const SearchView &sv, const cell128 *ring, size_t n, uint32_t lo,
                           uint32_t hi, int l0, int R, int ib, uint64_t *tree, hipStream_t s);
 hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *tree,

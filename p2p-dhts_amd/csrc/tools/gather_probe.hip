@@ -148,6 +148,17 @@ int main(int argc, char **argv) {
         fflush(stdout);
     };
     const int full = 256 * 2048;  // 32 waves/CU x 256 CUs
+    if (argc > 2 && !strcmp(argv[2], "coop_sweep")) {
+        // cooperative 64-B / 128-B entries against table size (TLB reach)
+        for (size_t gb : {8ull, 16ull, 32ull, 64ull, 128ull, 192ull}) {
+            const size_t bytes = gb << 30;
+            if (bytes > max_bytes) continue;
+            row("64B/4lanes", 1, bytes, full, run_coop<4>(t, bytes, full, 64, sink));
+            row("128B/8lanes", 1, bytes, full, run_coop<8>(t, bytes, full, 64, sink));
+        }
+        printf("\n]}\n");
+        return 0;
+    }
     // table size sweep at full occupancy, 16-B loads
     for (size_t mb : {64ull, 256ull, 1024ull, 4096ull, 16384ull}) {
         size_t bytes = mb << 20;

@@ -47,6 +47,9 @@ def test_c3_routed_lookups(O, c3):
     o3, h3, s3 = ring.route(src, keys)
     ring.set_route_variant(2)
     o2, h2, s2 = ring.route(src, keys)
+    ring.set_route_variant(5)
+    o5, h5, s5 = ring.route(src, keys)
+    assert ring.route_info()[0] == 5
     succ = ring.successor(keys)
     torch.cuda.synchronize()
     assert int((s1 != 0).sum()) == 0 and int((s0 != 0).sum()) == 0 and int((s2 != 0).sum()) == 0
@@ -54,6 +57,7 @@ def test_c3_routed_lookups(O, c3):
     assert bool((o2 == o1).all()) and bool((h2 == h1).all())
     assert bool((o3 == o1).all()) and bool((h3 == h1).all()) and int((s3 != 0).sum()) == 0
     assert bool((o4 == o1).all()) and bool((h4 == h1).all()) and int((s4 != 0).sum()) == 0
+    assert bool((o5 == o1).all()) and bool((h5 == h1).all()) and int((s5 != 0).sum()) == 0
     mean = float(h1.double().mean())
     assert 9.0 < mean < 11.0  # ~log2(N)/2 for uniform rings
     # oracle literal walk on a sample, with the oracle's own finger table

@@ -101,7 +101,7 @@ def test_fingers_c2_ring(cx, O):
 
 
 # ---------------------------------------------------------------- a7-a9 route
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_route_c1_golden(cx, O, c1truth, variant):
     """Config C1 ground truth (8 peers, key0..key999 from every peer)."""
     ids = O.keys_from_ints([O.uuid5_key(p) for p in c1truth["peers"]])
@@ -117,7 +117,7 @@ def test_route_c1_golden(cx, O, c1truth, variant):
     assert (status == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("n", [1, 2, 3, 9, 1000, 20000])
 def test_route_converged(cx, O, n, variant):
     ids = edge_ring(O, n, 900 + n)
@@ -201,7 +201,7 @@ def test_successor_clustered_rings(cx, O, search, spread):
     assert (lists == wl).all() and (count == wc).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("spread", [8, 40, 90, 100])
 def test_route_clustered_rings(cx, O, variant, spread):
     ids = clustered_ring(O, 3000, spread, spread)
@@ -218,6 +218,27 @@ def test_route_clustered_rings(cx, O, variant, spread):
            for j in rng.integers(0, len(ints), 6000)]
     keys = O.keys_from_ints(kv)
     src = rng.integers(0, len(ints), len(keys)).astype(np.uint32)
+    owner, hops, status = ring.route(src, keys)
+    wo, wh, ws = O.route(O.Peers(want_ring, F), src, keys)
+    assert (owner == wo).all() and (hops == wh).all() and (status == ws).all()
+
+
+def test_route_default_variant_and_escapes(cx, O):
+    """Automatic variant: the pattern-keyed window table (5) up to 2^24 peers.
+    A uniform ring encodes every node; a clustered one cannot (large index
+    jumps, huge gaps) and still routes exactly through the fallbacks."""
+    ring = cx.Ring(O.splitmix_keys(77, 20000))
+    ring.build_fingers()
+    v, esc, nbytes = ring.route_info()
+    assert v == 5 and esc == 0 and nbytes == 20000 * 24 * 128
+    ids = clustered_ring(O, 3000, 5, 8)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    v, esc, _ = ring.route_info()
+    assert v == 5 and esc > 0
+    want_ring = O.ring_build(ids)
+    keys = O.splitmix_keys(78, 5000)
+    src = np.random.default_rng(5).integers(0, len(want_ring), len(keys)).astype(np.uint32)
     owner, hops, status = ring.route(src, keys)
     wo, wh, ws = O.route(O.Peers(want_ring, F), src, keys)
     assert (owner == wo).all() and (hops == wh).all() and (status == ws).all()
@@ -249,7 +270,7 @@ def test_route_literal_random_edits(cx, O):
     assert (status == 1).any()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_route_bad_src_is_flagged(cx, O, variant):
     ring = cx.Ring(O.splitmix_keys(3, 50))
     ring.build_fingers()
