@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libchordx.so")
+# CHORDX_LIB: an alternative build of the same library (A/B kernel experiments).
+LIB_PATH = os.environ.get("CHORDX_LIB") or os.path.join(HERE, "libchordx.so")
 
 CX_OK = 0
 CX_E_INVALID = 1

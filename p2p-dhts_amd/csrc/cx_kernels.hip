@@ -1485,6 +1485,8 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
 // interval, and an undecided one fetches the exact IDs (A_FIXC / A_FIXT).
 // ---------------------------------------------------------------------------
 constexpr uint32_t CZ_NONE = 0xFFFFFFFFu;
+constexpr int CZ_RES_WIN = 256;  // 26 KB of LDS per 256-lane block: 6 blocks per CU
+constexpr int CZ_WAVES = 6;      // waves per SIMD the VGPR budget must allow (80 VGPRs)
 
 __host__ __device__ __forceinline__ int cz_shift(int ib) { return 116 - ib; }
 
@@ -1711,9 +1713,11 @@ struct TreeIO {
 };
 
 template <bool ARC, bool CZ>
-__global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
+__global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(CZ ? CZ_WAVES : 1)))
+void k_route_tree(TreeIO io) {
+    constexpr int RW = CZ ? CZ_RES_WIN : RES_WIN;  // cz: smaller window, more waves per CU
     static_assert(!(ARC && CZ), "arc mode walks variant-4 rows");
-    __shared__ uint64_t res_all[ARC ? 1 : RT_BLOCK / 64][ARC ? 1 : RES_WIN];
+    __shared__ uint64_t res_all[ARC ? 1 : RT_BLOCK / 64][ARC ? 1 : RW];
     __shared__ uint4 ent_all[RT_BLOCK][4];       // each lane's current 64-B entry
     __shared__ uint64_t addr_all[RT_BLOCK];      // entry index + 1 wanted by each lane (0: none)
     const uint32_t n = io.n;
@@ -1724,7 +1728,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
     const uint64_t *ent = reinterpret_cast<const uint64_t *>(ent_all[threadIdx.x]);
     const uint32_t *ent32 = reinterpret_cast<const uint32_t *>(ent_all[threadIdx.x]);
     if (!ARC)
-        for (int j = lane; j < RES_WIN; j += 64) res[j] = 0;
+        for (int j = lane; j < RW; j += 64) res[j] = 0;
     const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
     const size_t base = wave * io.chunk;
     if (base >= io.q) return;  // wave-uniform
@@ -1762,7 +1766,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
     // outcome of a finished query (ARC: local delivery or a result record)
     auto deliver = [&](size_t idx, uint64_t id, uint32_t o, uint32_t hh, uint8_t stt) {
         if (!ARC) {
-            res[idx & (RES_WIN - 1)] = pack_res(o, hh, stt);
+            res[idx & (RW - 1)] = pack_res(o, hh, stt);
         } else {
             ArcRec r;
             if ((int)(id >> ARC_ORIGIN_SHIFT) == io.self) {
@@ -1789,7 +1793,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
         // ---- refill slot B ----
         {
             size_t lim = end;
-            if (!ARC && flushed + RES_WIN < end) lim = flushed + RES_WIN;
+            if (!ARC && flushed + RW < end) lim = flushed + RW;
             const size_t avail = lim > head ? lim - head : 0;
             const uint64_t want = __ballot(bst == B_EMPTY);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
@@ -2009,13 +2013,13 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_tree(TreeIO io) {
                 if (flushed >= end) break;
                 const size_t idx = flushed + lane;
                 const bool inr = idx < end;
-                const uint64_t v = inr ? res[idx & (RES_WIN - 1)] : 0ull;
+                const uint64_t v = inr ? res[idx & (RW - 1)] : 0ull;
                 if (__ballot(!inr || (v >> 63)) != ~0ull) break;
                 if (inr) {
                     io.owner[idx] = (uint32_t)v;
                     io.hops[idx] = (uint8_t)(v >> 32);
                     if (io.status) io.status[idx] = (uint8_t)(v >> 40);
-                    res[idx & (RES_WIN - 1)] = 0;
+                    res[idx & (RW - 1)] = 0;
                 }
                 flushed += 64;
             }
@@ -2061,6 +2065,9 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
     return hipGetLastError();
 }
 
+template <class K>
+static unsigned resident_grid(K kernel, int block);
+
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
@@ -2083,8 +2090,14 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
     io.owner = owner;
     io.hops = hops;
     io.status = status;
-    unsigned blocks;
-    tree_geometry(q, io.chunk, blocks);
+    // one resident round of waves (no second, partial round of blocks)
+    static const unsigned resident = resident_grid(k_route_tree<false, true>, RT_BLOCK);
+    size_t waves = (size_t)resident * (RT_BLOCK / 64);
+    const size_t small = (q + 1023) / 1024;
+    if (small < waves) waves = small ? small : 1;
+    io.chunk = (q + waves - 1) / waves;
+    waves = (q + io.chunk - 1) / io.chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
     k_route_tree<false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
