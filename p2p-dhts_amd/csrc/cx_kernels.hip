@@ -1486,7 +1486,7 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
 // ---------------------------------------------------------------------------
 constexpr uint32_t CZ_NONE = 0xFFFFFFFFu;
 constexpr int CZ_RES_WIN = 256;  // 26 KB of LDS per 256-lane block: 6 blocks per CU
-constexpr int CZ_WAVES = 6;      // waves per SIMD the VGPR budget must allow (80 VGPRs)
+constexpr int CZ_WAVES = 5;      // waves per SIMD the VGPR budget allows (88 VGPRs; 6 spills)
 
 __host__ __device__ __forceinline__ int cz_shift(int ib) { return 116 - ib; }
 
