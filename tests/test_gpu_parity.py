@@ -338,6 +338,35 @@ def test_churn_and_misplaced(cx, O, n_old, nj, nl, search, churn):
         assert (mask == wm).all() and (target == wt).all()
 
 
+def test_misplaced_caller_mapping(cx, O):
+    """old_to_new is caller data: shifted, swapped, out-of-range or all-NONE
+    mappings give exactly the oracle's answer.  A value other than CX_NONE that
+    is not a new-ring index is a holder outside every list (oracle misplaced_one)."""
+    ids = O.splitmix_keys(8080, 3000)
+    old = cx.Ring(ids)
+    want_old = O.ring_build(ids)
+    joins = O.splitmix_keys(8081, 40)
+    leaves = want_old[np.random.default_rng(3).choice(3000, 40, replace=False)]
+    new, o2n = old.churn(joins, leaves)
+    want_new, _ = O.churn(want_old, joins, leaves)
+    keys = edge_keys(O, want_new, 78, 20000)
+    rng = np.random.default_rng(4)
+    shifted = np.where(o2n != 0xFFFFFFFF, (o2n + 1) % len(want_new), o2n).astype(np.uint32)
+    swapped = o2n.copy()
+    k = rng.choice(3000, 300, replace=False)
+    swapped[k] = swapped[np.roll(k, 1)]
+    wild = o2n.copy()
+    sel = rng.random(3000) < 0.1
+    wild[sel] = rng.integers(0, 2**32, sel.sum(), dtype=np.uint64).astype(np.uint32)
+    wild[rng.random(3000) < 0.1] = 0x80000005  # out of range
+    for m in (o2n, shifted, swapped, wild, np.full(3000, 0xFFFFFFFF, np.uint32)):
+        m = np.ascontiguousarray(m, dtype=np.uint32)
+        got = old.misplaced(new, m, keys, 14)
+        exp = O.misplaced(want_old, want_new, m, keys, 14)
+        for a, b in zip(got, exp):
+            assert (a == b).all()
+
+
 @pytest.mark.parametrize("churn", [0, 1])
 def test_churn_edge_cases(cx, O, churn):
     """Joins repeating each other, a join taking a leaving peer's ID, joins
@@ -386,6 +415,7 @@ def test_misplaced_holders_random(cx, O):
     keys = O.splitmix_keys(31338, 5000)
     holders = rng.integers(0, 500, (5000, 6)).astype(np.uint32)
     holders[rng.random((5000, 6)) < 0.2] = 0xFFFFFFFF
+    holders[rng.random((5000, 6)) < 0.05] = 500 + 7  # not a ring index: never in a list
     s = O.successor(want, keys)
     holders[:, 0] = s  # make some holders correct
     got = ring.misplaced_holders(keys, holders, 4)
