@@ -91,7 +91,7 @@ struct cx_ring {
     uint64_t *d_tree = nullptr;    // lookahead-tree table [n][rt_R][8] (variant 4)
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
-    uint64_t *d_cz = nullptr;      // pattern-keyed window table [n][rt_R][2][8 x u64] (variant 5)
+    uint64_t *d_cz = nullptr;      // pattern-keyed window table [rt_R][2][n][8 x u64] (variant 5)
     bool cz_valid = false;
     uint64_t cz_escapes = 0;       // nodes the compressed format could not represent
     int route_variant = -1;        // 0: finger+ring gathers, 1: route table, 2: packed table,

@@ -1520,10 +1520,11 @@ __global__ void k_cz_build(const uint32_t *F, const cell128 *ring, uint32_t n, i
     uint32_t bad = 0;
     for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
          t += (size_t)gridDim.x * blockDim.x) {
-        const int b = (int)(t & 1);
-        const size_t r = t >> 1;
-        const size_t p = r / (unsigned)R;
-        const int i = l0 + (int)(r - p * (unsigned)R);
+        // level-major: t = ((i - l0) * 2 + b) * n + p (see the walk's entry index)
+        const size_t plane = t / n;
+        const size_t p = t - plane * n;
+        const int b = (int)(plane & 1);
+        const int i = l0 + (int)(plane >> 1);
         uint32_t node[16], out[16];
         u128 nid[16];
         const u128 idp = ld128(ring + p);
@@ -1825,8 +1826,13 @@ void k_route_tree(TreeIO io) {
 
         // ---- memory round ----
         {
-            uint64_t e = (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0);
-            if (CZ) e = e * 2 + rb;
+            // v4 rows are peer-major ([peer][level]); the cz table is level-major
+            // ([level][b][peer]): a wave's first hops leave ~64 consecutive
+            // source peers, mostly at the top level or two, so their entries
+            // share DRAM pages and 128-B lines instead of lying 4 KiB apart.
+            const uint64_t e =
+                CZ ? (uint64_t)((lvl - l0) * 2 + rb) * n + cur
+                   : (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0);
             addr_all[threadIdx.x] = mode == A_HOP ? e + 1 : 0;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
