@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-end validation on the GPU box (repo root): GPU tests, smoke, default bench,
+# rocprofv3 kernel stats of the bench. Each GPU step has its own limit; chained by &&.
+set -eo pipefail
+TAG=${1:-final}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > "$OUT/pytest_gpu.log" 2>&1
+tail -3 "$OUT/pytest_gpu.log"
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+tail -1 "$OUT/smoke.log"
+timeout -k 10 400 python -u bench.py > "$OUT/bench_default.log" 2>&1
+tail -1 "$OUT/bench_default.log" | cut -c1-300
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+  -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu > "$OUT/bench_trace.log" 2>&1
+echo done
