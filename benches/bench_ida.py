@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""IDA (14, 10, 257) encode/decode throughput on one MI355X: 1 GiB in 4 KiB
+blocks and 256 MiB in 64-B blocks, HIP-event timed on the launch stream, with a
+decode(encode(x)) == x round-trip check on every block.  Pipeline depths come
+from CX_IDA_ENC_D / CX_IDA_DEC_D (A/B knob, read once per process)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
+import torch  # noqa: E402
+
+from chordx import ida  # noqa: E402
+
+HBM = 8.0e12
+
+
+def ev_time(fn, reps=5):
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e-3
+
+
+out = {"enc_depth": os.environ.get("CX_IDA_ENC_D", "default"),
+       "dec_depth": os.environ.get("CX_IDA_DEC_D", "default")}
+for name, nb, bl in (("4KiB_blocks", 1 << 18, 4096), ("64B_blocks", 1 << 22, 64)):
+    g = torch.Generator(device="cuda").manual_seed(1)
+    data = torch.randint(0, 256, (nb * bl,), dtype=torch.uint8, device="cuda", generator=g)
+    offs = torch.arange(0, nb * bl + 1, bl, dtype=torch.int64, device="cuda")
+    frags, seg = ida.encode_flat(data, offs)
+    te = ev_time(lambda: ida.encode_flat(data, offs, seg_offsets=seg, out=frags))
+    S = (bl + 9) // 10
+    keep = torch.tensor([0, 2, 3, 5, 6, 8, 9, 11, 12, 13], device="cuda")
+    rows = frags.view(nb, 14, S)[:, keep, :].contiguous().view(-1)
+    idx = (keep + 1).to(torch.uint8).repeat(nb).contiguous()
+    dec = ida.decode_flat(rows, seg, idx)
+    td = ev_time(lambda: ida.decode_flat(rows, seg, idx, out=dec))
+    vals = dec[0] if isinstance(dec, tuple) else dec
+    v = vals.view(nb, -1)[:, :bl].to(torch.int32)
+    ok = bool((v == data.view(nb, bl).to(torch.int32)).all())
+    nbytes = nb * bl
+    out[name] = {"encode_ms": te * 1e3, "encode_GBps_data": nbytes / te / 1e9,
+                 "encode_algo_frac_of_hbm": nbytes * (1 + 2.8) / te / HBM,
+                 "decode_ms": td * 1e3, "decode_GBps_data": nbytes / td / 1e9,
+                 "decode_algo_frac_of_hbm": nbytes * (2 + 2) / td / HBM,
+                 "round_trip_ok": ok}
+    del data, offs, frags, rows, idx, seg, dec
+    torch.cuda.empty_cache()
+print(json.dumps(out))

@@ -2869,6 +2869,16 @@ __device__ __forceinline__ uint32_t modp_f(uint32_t x, uint32_t p, float inv_p) 
     return (uint32_t)r;
 }
 
+// x mod p with one fix-up: the biased estimate q = floor(x/p - 1/2 +- err) is
+// floor(x/p) or one less while |err| < 1/2, i.e. x/p < 2^20 (encode: x/p <
+// m 255; decode with m <= 12: x/p < m 65535); r in [0, 2p) then needs one
+// unsigned min.  cvt, fma, cvt, mul24, sub, sub, min: 7 full-rate VALU.
+__device__ __forceinline__ uint32_t modp_fast(uint32_t x, uint32_t p, float inv_p) {
+    const uint32_t q = (uint32_t)__builtin_fmaf((float)x, inv_p, -0.5f);  // < 0 -> 0
+    const uint32_t r = x - __umul24(q, p);
+    return r < r - p ? r : r - p;
+}
+
 // Segment g's block, for the 64 consecutive segments of one wave chunk: one
 // binary search for the chunk's first segment (uniform), then a short forward
 // scan per lane (blocks of a chunk are consecutive in seg order).
@@ -2919,13 +2929,23 @@ __device__ __forceinline__ void cursor_advance(BlockCursor &k, const uint64_t *s
     }
 }
 
-// Each wave takes a contiguous range of 64-segment chunks.  Chunk c+1's bytes
-// (one contiguous span of data) are loaded into registers while chunk c is
-// computed; they pass through LDS so each lane can take its own m bytes as
+// Each wave takes a contiguous range of 64-segment chunks.  The bytes of the
+// next D chunks (each one contiguous span of data) are in flight in registers
+// while chunk c is computed (D-slot ring, fully unrolled so every slot lives in
+// registers); they pass through LDS so each lane can take its own m bytes as
 // packed words for v_dot4_u32_u8 (4 byte-products per instruction).
-// PRE = dwords per lane in flight: a chunk spans <= 64 m bytes + alignment,
+// PRE = dwords per lane per chunk: a chunk spans <= 64 m bytes + alignment,
 // i.e. <= 16 m + 1 words: PRE 3 covers m <= 11 (DHash's 10), PRE 8 any m.
 template <int PRE>
+struct EncSlot {
+    uint64_t segb, S, s, span;
+    uint32_t off, words;
+    int have;
+    bool live;
+    uint32_t pre[PRE];
+};
+
+template <int PRE, int D>
 __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const uint64_t *offs,
                                                     const uint64_t *seg, size_t blocks, int n,
                                                     int m, uint32_t p, float inv_p,
@@ -2961,33 +2981,30 @@ __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const u
     BlockCursor cur;
     cursor_init<true>(cur, seg, offs, seg_block(seg, blocks, c0 * 64));
 
-    // chunk descriptor of the chunk in flight
-    uint64_t n_segb = 0, n_S = 0, n_s = 0, n_span = 0;
-    uint32_t n_off = 0, n_words = 0;
-    int n_have = 0;
-    bool n_live = false;
-    uint32_t pre[PRE];
-    auto issue = [&](uint64_t c) {
+    EncSlot<PRE> sl[D];
+    // descriptor + loads of chunk c into slot x (chunks are issued in order,
+    // so the per-lane block cursor only moves forward)
+    auto issue = [&](EncSlot<PRE> &x, uint64_t c) {
         const uint64_t g = c * 64 + lane;
-        n_live = g < total;
-        cursor_advance<true>(cur, seg, offs, n_live ? g : total - 1);
-        n_s = (n_live ? g : total - 1) - cur.sb;
-        n_segb = cur.sb;
-        n_S = cur.sb1 - cur.sb;
-        const uint64_t my_lo = cur.ob + n_s * m;
+        x.live = g < total;
+        cursor_advance<true>(cur, seg, offs, x.live ? g : total - 1);
+        x.s = (x.live ? g : total - 1) - cur.sb;
+        x.segb = cur.sb;
+        x.S = cur.sb1 - cur.sb;
+        const uint64_t my_lo = cur.ob + x.s * m;
         uint64_t my_hi = my_lo + m;
         if (my_hi > cur.ob1) my_hi = cur.ob1;
-        n_span = __shfl(my_lo, 0) & ~3ull;
+        x.span = __shfl(my_lo, 0) & ~3ull;
         const uint64_t span_hi = __shfl(my_hi, 63);
-        n_words = (uint32_t)((span_hi - n_span + 3) >> 2);
-        n_off = (uint32_t)(my_lo - n_span);
-        n_have = (int)(my_hi - my_lo);
+        x.words = (uint32_t)((span_hi - x.span + 3) >> 2);
+        x.off = (uint32_t)(my_lo - x.span);
+        x.have = (int)(my_hi - my_lo);
 #pragma unroll
         for (int t = 0; t < PRE; ++t) {
             const uint32_t w = lane + 64 * t;
-            const uint64_t at = n_span + 4ull * w;
+            const uint64_t at = x.span + 4ull * w;
             uint32_t v = 0;
-            if (w < n_words) {
+            if (w < x.words) {
                 if (at + 4 <= nbytes) {
                     v = *reinterpret_cast<const uint32_t *>(data + at);
                 } else {
@@ -2995,74 +3012,82 @@ __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const u
                         if (at + k < nbytes) v |= (uint32_t)data[at + k] << (8 * k);
                 }
             }
-            pre[t] = v;
+            x.pre[t] = v;
         }
     };
-    issue(c0);
-    for (uint64_t c = c0; c < c1; ++c) {
-        // take over the chunk in flight
-        const uint64_t segb = n_segb, S = n_S, sg = n_s;
-        const uint32_t off = n_off, words = n_words;
-        const int have = n_have;
-        const bool live = n_live;
 #pragma unroll
-        for (int t = 0; t < PRE; ++t)
-            if (lane + 64 * t < (int)words) st[lane + 64 * t] = pre[t];
-        if (c + 1 < c1) issue(c + 1);  // next chunk's loads overlap this chunk's math
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // this lane's segment as packed words W[0..nw), bytes past `have` zero
-        const uint32_t bw = off >> 2, sh = off & 3;
-        uint32_t W[8];
-        uint32_t prev = st[bw];
+    for (int k = 0; k < D; ++k)
+        if (c0 + k < c1) issue(sl[k], c0 + k);
+    for (uint64_t cb = c0; cb < c1; cb += D) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (j < nw) {
-                const uint32_t nxt = st[bw + j + 1];
-                uint32_t x = __builtin_amdgcn_alignbyte(nxt, prev, sh);
-                const int valid = have - 4 * j;
-                x &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
-                W[j] = x;
-                prev = nxt;
-            } else {
-                W[j] = 0;
-            }
-        }
-        if (live) {
-            uint16_t *out = frags + (uint64_t)n * segb + sg;
-            for (int i = 0; i < n; ++i) {
-                const uint4 *er = reinterpret_cast<const uint4 *>(Epk + i * IDA_EROW);
-                const uint4 l0 = er[0];
-                uint32_t acc = __builtin_amdgcn_udot4(l0.x, W[0], 0u, false);
-                if (nw > 1) acc = __builtin_amdgcn_udot4(l0.y, W[1], acc, false);
-                if (nw > 2) acc = __builtin_amdgcn_udot4(l0.z, W[2], acc, false);
-                if (nw > 3) acc = __builtin_amdgcn_udot4(l0.w, W[3], acc, false);
-                if (nw > 4) {
-                    const uint4 l1 = er[1];
-                    acc = __builtin_amdgcn_udot4(l1.x, W[4], acc, false);
-                    if (nw > 5) acc = __builtin_amdgcn_udot4(l1.y, W[5], acc, false);
-                    if (nw > 6) acc = __builtin_amdgcn_udot4(l1.z, W[6], acc, false);
-                    if (nw > 7) acc = __builtin_amdgcn_udot4(l1.w, W[7], acc, false);
+        for (int k = 0; k < D; ++k) {
+            const uint64_t c = cb + k;
+            if (c >= c1) break;  // wave-uniform
+            // take over slot k, then refill it with chunk c + D
+            const uint64_t segb = sl[k].segb, S = sl[k].S, sg = sl[k].s;
+            const uint32_t off = sl[k].off, words = sl[k].words;
+            const int have = sl[k].have;
+            const bool live = sl[k].live;
+#pragma unroll
+            for (int t = 0; t < PRE; ++t)
+                if (lane + 64 * t < (int)words) st[lane + 64 * t] = sl[k].pre[t];
+            if (c + D < c1) issue(sl[k], c + D);  // loads overlap this chunk's math
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // this lane's segment as packed words W[0..nw), bytes past `have` zero
+            const uint32_t bw = off >> 2, sh = off & 3;
+            uint32_t W[8];
+            uint32_t prev = st[bw];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j < nw) {
+                    const uint32_t nxt = st[bw + j + 1];
+                    uint32_t x = __builtin_amdgcn_alignbyte(nxt, prev, sh);
+                    const int valid = have - 4 * j;
+                    x &= valid >= 4 ? 0xFFFFFFFFu
+                                    : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
+                    W[j] = x;
+                    prev = nxt;
+                } else {
+                    W[j] = 0;
                 }
-                if (hi_any) {  // E >= 256: high bytes times 256
-                    const uint4 h0 = er[2], h1 = er[3];
-                    uint32_t ah = __builtin_amdgcn_udot4(h0.x, W[0], 0u, false);
-                    ah = __builtin_amdgcn_udot4(h0.y, W[1], ah, false);
-                    ah = __builtin_amdgcn_udot4(h0.z, W[2], ah, false);
-                    ah = __builtin_amdgcn_udot4(h0.w, W[3], ah, false);
+            }
+            if (live) {
+                uint16_t *out = frags + (uint64_t)n * segb + sg;
+                for (int i = 0; i < n; ++i) {
+                    const uint4 *er = reinterpret_cast<const uint4 *>(Epk + i * IDA_EROW);
+                    const uint4 l0 = er[0];
+                    uint32_t acc = __builtin_amdgcn_udot4(l0.x, W[0], 0u, false);
+                    if (nw > 1) acc = __builtin_amdgcn_udot4(l0.y, W[1], acc, false);
+                    if (nw > 2) acc = __builtin_amdgcn_udot4(l0.z, W[2], acc, false);
+                    if (nw > 3) acc = __builtin_amdgcn_udot4(l0.w, W[3], acc, false);
                     if (nw > 4) {
-                        ah = __builtin_amdgcn_udot4(h1.x, W[4], ah, false);
-                        ah = __builtin_amdgcn_udot4(h1.y, W[5], ah, false);
-                        ah = __builtin_amdgcn_udot4(h1.z, W[6], ah, false);
-                        ah = __builtin_amdgcn_udot4(h1.w, W[7], ah, false);
+                        const uint4 l1 = er[1];
+                        acc = __builtin_amdgcn_udot4(l1.x, W[4], acc, false);
+                        if (nw > 5) acc = __builtin_amdgcn_udot4(l1.y, W[5], acc, false);
+                        if (nw > 6) acc = __builtin_amdgcn_udot4(l1.z, W[6], acc, false);
+                        if (nw > 7) acc = __builtin_amdgcn_udot4(l1.w, W[7], acc, false);
                     }
-                    acc += ah << 8;  // total <= m (p-1) 255 < 2^29
+                    if (hi_any) {  // E >= 256: high bytes times 256
+                        const uint4 h0 = er[2], h1 = er[3];
+                        uint32_t ah = __builtin_amdgcn_udot4(h0.x, W[0], 0u, false);
+                        ah = __builtin_amdgcn_udot4(h0.y, W[1], ah, false);
+                        ah = __builtin_amdgcn_udot4(h0.z, W[2], ah, false);
+                        ah = __builtin_amdgcn_udot4(h0.w, W[3], ah, false);
+                        if (nw > 4) {
+                            ah = __builtin_amdgcn_udot4(h1.x, W[4], ah, false);
+                            ah = __builtin_amdgcn_udot4(h1.y, W[5], ah, false);
+                            ah = __builtin_amdgcn_udot4(h1.z, W[6], ah, false);
+                            ah = __builtin_amdgcn_udot4(h1.w, W[7], ah, false);
+                        }
+                        acc += ah << 8;  // total <= m (p-1) 255 < 2^29
+                    }
+                    out[(uint64_t)i * S] = (uint16_t)modp_f(acc, p, inv_p);
                 }
-                out[(uint64_t)i * S] = (uint16_t)modp_f(acc, p, inv_p);
             }
+            __builtin_amdgcn_wave_barrier();  // stage reused by the next chunk
         }
-        __builtin_amdgcn_wave_barrier();  // stage reused by the next chunk
     }
 }
 
@@ -3125,7 +3150,19 @@ __global__ void k_ida_inverse(const uint8_t *idx, const uint32_t *run_start, siz
 // unless WIDE: m (p-1) 65535 >= 2^32, which takes a 64-bit path).
 constexpr int IDA_AROW = 16;  // u16-pair words per staged inverse row
 
-template <bool WIDE>
+// Each wave takes a contiguous range of 64-segment chunks; the fragment values
+// of the next D chunks are in flight in registers (D-slot ring, unrolled)
+// while chunk c is computed.  FM >= m bounds the per-lane fragment registers.
+template <int FM>
+struct DecSlot {
+    uint64_t s;
+    size_t b;
+    uint32_t r;
+    bool live, ok;
+    uint32_t f[FM];
+};
+
+template <bool WIDE, int FM, int D>
 __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const uint64_t *seg,
                                                     size_t blocks, int m, uint32_t p,
                                                     float inv_p, const int32_t *inv,
@@ -3142,110 +3179,117 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
     const uint64_t cpw = (chunks + waves - 1) / waves;
     const uint64_t c0 = wave * cpw, c1 = c0 + cpw < chunks ? c0 + cpw : chunks;
     if (c0 >= c1) return;
-    size_t bb = seg_block(seg, blocks, c0 * 64);
+    size_t bl = seg_block(seg, blocks, c0 * 64);  // per-lane block cursor (moves forward)
+    uint64_t bl1 = seg[bl + 1];
     uint32_t staged = 0xFFFFFFFFu;  // run whose inverse is in As
-    for (uint64_t c = c0; c < c1; ++c) {
-        const uint64_t g0 = c * 64, g = g0 + lane;
-        while (seg[bb + 1] <= g0) ++bb;
-        const bool live = g < total;
-        const uint64_t gl = live ? g : total - 1;
-        size_t b = bb;
-        while (seg[b + 1] <= gl) ++b;
-        const uint32_t r = run_of[b];
-        const uint32_t r0 = __shfl(r, 0);
-        const bool uniform = __ballot(r != r0) == 0;
-        if (uniform && r0 != staged) {  // stage the shared inverse (wave-uniform branch)
-            const int32_t *A = inv + (size_t)r0 * m * m;
-            for (int t = lane; t < m * IDA_AROW; t += 64) {
-                const int j = t / IDA_AROW, w = t - j * IDA_AROW;
-                const uint32_t a0 = 2 * w < m ? (uint32_t)A[j * m + 2 * w] : 0u;
-                const uint32_t a1 = 2 * w + 1 < m ? (uint32_t)A[j * m + 2 * w + 1] : 0u;
-                As[t] = a0 | (a1 << 16);
-            }
-            staged = r0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        int last = -1;
-        uint64_t s = 0;
-        if (live && okf[r]) {
-            s = g - seg[b];
-            const uint64_t S = seg[b + 1] - seg[b];
-            const uint16_t *fr = frags + (uint64_t)m * seg[b] + s;
-            uint32_t f[IDA_MAX_N];
+    DecSlot<FM> sl[D];
+    auto issue = [&](DecSlot<FM> &x, uint64_t c) {
+        const uint64_t g = c * 64 + lane;
+        x.live = g < total;
+        const uint64_t gl = x.live ? g : total - 1;
+        while (bl1 <= gl) bl1 = seg[++bl + 1];
+        x.b = bl;
+        x.r = run_of[bl];
+        x.ok = x.live && okf[x.r];
+        const uint64_t sb = seg[bl];
+        x.s = gl - sb;
+        const uint64_t S = bl1 - sb;
+        const uint16_t *fr = frags + (uint64_t)m * sb + x.s;
 #pragma unroll
-            for (int k = 0; k < IDA_MAX_N; ++k) f[k] = k < m ? fr[(uint64_t)k * S] : 0u;
-            uint16_t *o = out + (uint64_t)m * g;  // = m seg[b] + s m
-            if (!WIDE && uniform) {
-                uint32_t F[16];
+        for (int k = 0; k < FM; ++k) x.f[k] = (x.ok && k < m) ? fr[(uint64_t)k * S] : 0u;
+    };
 #pragma unroll
-                for (int w = 0; w < 16; ++w) F[w] = f[2 * w] | (f[2 * w + 1] << 16);
-                uint32_t cprev = 0;
-                for (int j = 0; j < m; ++j) {
-                    const uint4 *ar = reinterpret_cast<const uint4 *>(As + j * IDA_AROW);
-                    uint32_t acc = 0;
+    for (int k = 0; k < D; ++k)
+        if (c0 + k < c1) issue(sl[k], c0 + k);
+    for (uint64_t cb = c0; cb < c1; cb += D) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (4 * q < nw) {
-                            const uint4 a4 = ar[q];
-                            acc = __builtin_amdgcn_udot2(__builtin_bit_cast(cx_us2, a4.x),
-                                                         __builtin_bit_cast(cx_us2, F[4 * q]),
-                                                         acc, false);
-                            if (4 * q + 1 < nw)
-                                acc = __builtin_amdgcn_udot2(
-                                    __builtin_bit_cast(cx_us2, a4.y),
-                                    __builtin_bit_cast(cx_us2, F[4 * q + 1]), acc, false);
-                            if (4 * q + 2 < nw)
-                                acc = __builtin_amdgcn_udot2(
-                                    __builtin_bit_cast(cx_us2, a4.z),
-                                    __builtin_bit_cast(cx_us2, F[4 * q + 2]), acc, false);
-                            if (4 * q + 3 < nw)
-                                acc = __builtin_amdgcn_udot2(
-                                    __builtin_bit_cast(cx_us2, a4.w),
-                                    __builtin_bit_cast(cx_us2, F[4 * q + 3]), acc, false);
-                        }
-                    }
-                    const uint32_t cv = modp_f(acc, p, inv_p);
-                    if (cv) last = j;
-                    if ((m & 1) == 0) {  // m even: 4-byte aligned pairs
-                        if (j & 1)
-                            reinterpret_cast<uint32_t *>(o)[j >> 1] = cprev | (cv << 16);
-                        else
-                            cprev = cv;
-                    } else {
-                        o[j] = (uint16_t)cv;
-                    }
+        for (int k = 0; k < D; ++k) {
+            const uint64_t c = cb + k;
+            if (c >= c1) break;  // wave-uniform
+            const uint64_t g = c * 64 + lane;
+            const size_t b = sl[k].b;
+            const uint32_t r = sl[k].r;
+            const bool ok = sl[k].ok;
+            const uint64_t s = sl[k].s;
+            uint32_t f[FM];
+#pragma unroll
+            for (int q = 0; q < FM; ++q) f[q] = sl[k].f[q];
+            if (c + D < c1) issue(sl[k], c + D);  // loads overlap this chunk's math
+            const uint32_t r0 = __shfl(r, 0);
+            const bool uniform = __ballot(r != r0) == 0;
+            if (uniform && r0 != staged) {  // stage the shared inverse (wave-uniform branch)
+                __builtin_amdgcn_wave_barrier();  // previous readers of As are done
+                const int32_t *A = inv + (size_t)r0 * m * m;
+                for (int t = lane; t < m * IDA_AROW; t += 64) {
+                    const int j = t / IDA_AROW, w = t - j * IDA_AROW;
+                    const uint32_t a0 = 2 * w < m ? (uint32_t)A[j * m + 2 * w] : 0u;
+                    const uint32_t a1 = 2 * w + 1 < m ? (uint32_t)A[j * m + 2 * w + 1] : 0u;
+                    As[t] = a0 | (a1 << 16);
                 }
-            } else {
-                const int32_t *A = inv + (size_t)r * m * m;
-                for (int j = 0; j < m; ++j) {
-                    uint32_t cv;
-                    if (WIDE) {
-                        uint64_t acc = 0;
+                staged = r0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            int last = -1;
+            if (ok) {
+                uint16_t *o = out + (uint64_t)m * g;  // = m seg[b] + s m
+                if (!WIDE && uniform) {
+                    uint32_t F[(FM + 1) / 2];
 #pragma unroll
-                        for (int k = 0; k < IDA_MAX_N; ++k)
-                            if (k < m) acc += (uint64_t)(uint32_t)A[j * m + k] * f[k];
-                        cv = (uint32_t)(acc % p);
-                    } else {
+                    for (int w = 0; w < (FM + 1) / 2; ++w)
+                        F[w] = f[2 * w] | (2 * w + 1 < FM ? f[2 * w + 1] << 16 : 0u);
+                    uint32_t cprev = 0;
+                    for (int j = 0; j < m; ++j) {
+                        const uint32_t *ar = As + j * IDA_AROW;
                         uint32_t acc = 0;
 #pragma unroll
-                        for (int k = 0; k < IDA_MAX_N; ++k)
-                            if (k < m) acc += (uint32_t)A[j * m + k] * f[k];
-                        cv = modp_f(acc, p, inv_p);
+                        for (int w = 0; w < (FM + 1) / 2; ++w)
+                            if (w < nw)
+                                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(cx_us2, ar[w]),
+                                                             __builtin_bit_cast(cx_us2, F[w]),
+                                                             acc, false);
+                        const uint32_t cv = modp_f(acc, p, inv_p);
+                        if (cv) last = j;
+                        if ((m & 1) == 0) {  // m even: 4-byte aligned pairs
+                            if (j & 1)
+                                reinterpret_cast<uint32_t *>(o)[j >> 1] = cprev | (cv << 16);
+                            else
+                                cprev = cv;
+                        } else {
+                            o[j] = (uint16_t)cv;
+                        }
                     }
-                    o[j] = (uint16_t)cv;
-                    if (cv) last = j;
+                } else {
+                    const int32_t *A = inv + (size_t)r * m * m;
+                    for (int j = 0; j < m; ++j) {
+                        uint32_t cv;
+                        if (WIDE) {
+                            uint64_t acc = 0;
+#pragma unroll
+                            for (int q = 0; q < FM; ++q)
+                                if (q < m) acc += (uint64_t)(uint32_t)A[j * m + q] * f[q];
+                            cv = (uint32_t)(acc % p);
+                        } else {
+                            uint32_t acc = 0;
+#pragma unroll
+                            for (int q = 0; q < FM; ++q)
+                                if (q < m) acc += (uint32_t)A[j * m + q] * f[q];
+                            cv = modp_f(acc, p, inv_p);
+                        }
+                        o[j] = (uint16_t)cv;
+                        if (cv) last = j;
+                    }
                 }
             }
+            // kept length: per block, the highest lane holding a nonzero value
+            const uint64_t nz = __ballot(last >= 0);
+            const uint64_t above = lane == 63 ? 0ull : nz >> (lane + 1);
+            const int nxt = above ? lane + 1 + __builtin_ctzll(above) : 64;
+            const size_t bn = __shfl((unsigned long long)b, nxt & 63);
+            if (last >= 0 && (nxt == 64 || bn != b))
+                atomicMax(out_len + b, (unsigned long long)(s * m + last + 1));
         }
-        // kept length: per block, the highest lane holding a nonzero value
-        const uint64_t nz = __ballot(last >= 0);
-        const uint64_t above = lane == 63 ? 0ull : nz >> (lane + 1);
-        const int nxt = above ? lane + 1 + __builtin_ctzll(above) : 64;
-        const size_t bn = __shfl((unsigned long long)b, nxt & 63);
-        if (last >= 0 && (nxt == 64 || bn != b))
-            atomicMax(out_len + b, (unsigned long long)(s * m + last + 1));
     }
 }
 
@@ -3298,17 +3342,196 @@ static unsigned resident_grid(K kernel, int block) {
         per = 1;
     return (unsigned)(per * cus);
 }
+// Encoding rows for the fixed-shape kernel, passed by value as kernel
+// arguments so the rows sit in SGPRs (v_dot4 takes them as scalar operands):
+// lo[i][w] = low bytes of E[i][4w..4w+3], hi[i][w] the high bytes, and
+// himask bit i = row i has an E >= 256 (for p = 257 only rows a = 2, 4, 8,
+// where a^k = -1 for some k < 10).
+struct IdaEncTab {
+    uint32_t lo[IDA_MAX_N][4];
+    uint32_t hi[IDA_MAX_N][4];
+    uint32_t himask;
+};
+
+// Fixed-shape encode (N fragments, NW = ceil(m / 4) words per segment, DHash's
+// (14, 10): N = 14, NW = 3): the same wave/chunk/LDS-staging scheme as
+// k_ida_encode, with every row unrolled, E in SGPRs instead of LDS (no LDS
+// round trip per row) and a one-fix-up reduction.  The generic kernel spent
+// ~500 VALU + 5 serialised LDS reads per row-chunk; this one ~12 VALU per row.
+template <int N, int NW, int D, bool P257>
+__global__ __launch_bounds__(256) void k_ida_encode_fixed(const uint8_t *data,
+                                                          const uint64_t *offs,
+                                                          const uint64_t *seg, size_t blocks,
+                                                          int m, uint32_t p, float inv_p,
+                                                          uint16_t *frags, IdaEncTab tab) {
+    constexpr int PRE = NW + 1 <= 3 ? 3 : NW + 1;  // chunk span <= 16 NW + 1 words
+    __shared__ uint32_t stage[256 / 64][64 * PRE + 4];
+    __shared__ uint32_t hi_s[N][NW];  // high-byte rows (rare: himask) stay in LDS
+    for (int t = threadIdx.x; t < N * NW; t += blockDim.x) hi_s[t / NW][t % NW] = tab.hi[t / NW][t % NW];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    uint32_t *st = stage[threadIdx.x >> 6];
+    const uint64_t total = seg[blocks];
+    const uint64_t nbytes = offs[blocks];
+    const uint64_t chunks = (total + 63) / 64;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t cpw = (chunks + waves - 1) / waves;
+    const uint64_t c0 = wave * cpw, c1 = c0 + cpw < chunks ? c0 + cpw : chunks;
+    if (c0 >= c1) return;  // wave-uniform, after the only block barrier
+    BlockCursor cur;
+    cursor_init<true>(cur, seg, offs, seg_block(seg, blocks, c0 * 64));
+    EncSlot<PRE> sl[D];
+    auto issue = [&](EncSlot<PRE> &x, uint64_t c) {
+        const uint64_t g = c * 64 + lane;
+        x.live = g < total;
+        cursor_advance<true>(cur, seg, offs, x.live ? g : total - 1);
+        x.s = (x.live ? g : total - 1) - cur.sb;
+        x.segb = cur.sb;
+        x.S = cur.sb1 - cur.sb;
+        const uint64_t my_lo = cur.ob + x.s * m;
+        uint64_t my_hi = my_lo + m;
+        if (my_hi > cur.ob1) my_hi = cur.ob1;
+        x.span = __shfl(my_lo, 0) & ~3ull;
+        const uint64_t span_hi = __shfl(my_hi, 63);
+        x.words = (uint32_t)((span_hi - x.span + 3) >> 2);
+        x.off = (uint32_t)(my_lo - x.span);
+        x.have = (int)(my_hi - my_lo);
+#pragma unroll
+        for (int t = 0; t < PRE; ++t) {
+            const uint32_t w = lane + 64 * t;
+            const uint64_t at = x.span + 4ull * w;
+            uint32_t v = 0;
+            if (w < x.words) {
+                if (at + 4 <= nbytes) {
+                    v = *reinterpret_cast<const uint32_t *>(data + at);
+                } else {
+                    for (int k = 0; k < 4; ++k)
+                        if (at + k < nbytes) v |= (uint32_t)data[at + k] << (8 * k);
+                }
+            }
+            x.pre[t] = v;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+        if (c0 + k < c1) issue(sl[k], c0 + k);
+    for (uint64_t cb = c0; cb < c1; cb += D) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            const uint64_t c = cb + k;
+            if (c >= c1) break;  // wave-uniform
+            const uint64_t segb = sl[k].segb, S = sl[k].S, sg = sl[k].s;
+            const uint32_t off = sl[k].off, words = sl[k].words;
+            const int have = sl[k].have;
+            const bool live = sl[k].live;
+#pragma unroll
+            for (int t = 0; t < PRE; ++t)
+                if (lane + 64 * t < (int)words) st[lane + 64 * t] = sl[k].pre[t];
+            if (c + D < c1) issue(sl[k], c + D);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t bw = off >> 2, sh = off & 3;
+            uint32_t W[NW];
+            uint32_t prev = st[bw];
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const uint32_t nxt = st[bw + j + 1];
+                uint32_t x = __builtin_amdgcn_alignbyte(nxt, prev, sh);
+                const int valid = have - 4 * j;
+                x &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
+                W[j] = x;
+                prev = nxt;
+            }
+            __builtin_amdgcn_wave_barrier();  // stage reused by the next chunk
+            if (live) {
+                uint16_t *o = frags + (uint64_t)N * segb + sg;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int j = 0; j < NW; ++j)
+                        acc = __builtin_amdgcn_udot4(tab.lo[i][j], W[j], acc, false);
+                    if (P257) {
+                        // p = 257, 9 <= m <= 12: E >= 256 only where a^k = -1, i.e.
+                        // E = 256 at (a, k) = (2, 8), (4, 4), (8, 8) (a = i + 1;
+                        // 2 has order 16 mod 257): add 256 v_k directly
+                        if (i == 1 || i == 7) acc += (W[2] & 0xFFu) << 8;
+                        if (i == 3) acc += (W[1] & 0xFFu) << 8;
+                    } else if ((tab.himask >> i) & 1) {  // scalar branch
+                        uint32_t ah = 0;
+#pragma unroll
+                        for (int j = 0; j < NW; ++j)
+                            ah = __builtin_amdgcn_udot4(hi_s[i][j], W[j], ah, false);
+                        acc += ah << 8;  // <= m (p-1) 255 < 2^29
+                    }
+                    *o = (uint16_t)modp_fast(acc, p, inv_p);
+                    o += S;
+                }
+            }
+        }
+    }
+}
+
+template <int PRE, int D>
+static void ida_encode_launch(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
+                              size_t blocks, int n, int m, int p, uint16_t *frags,
+                              hipStream_t s) {
+    static const unsigned grid = resident_grid(k_ida_encode<PRE, D>, 256);
+    k_ida_encode<PRE, D><<<grid, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p,
+                                              1.0f / p, frags);
+}
+
+static int ida_depth(const char *var, int dflt);
+
 hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
                       size_t blocks, int n, int m, int p, uint16_t *frags, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
-    static const unsigned g3 = resident_grid(k_ida_encode<3>, 256);
-    static const unsigned g8 = resident_grid(k_ida_encode<8>, 256);
-    if (16 * m + 1 <= 64 * 3)
-        k_ida_encode<3><<<g3, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p, 1.0f / p,
-                                           frags);
+    static const int D = ida_depth("CX_IDA_ENC_D", 3);
+    static const int FD = ida_depth("CX_IDA_ENCF_D", 1);
+    static const bool fixed_on = !getenv("CX_IDA_GENERIC");
+    if (fixed_on && n == 14 && m > 8 && m <= 12) {  // DHash (14, 10) and neighbours
+        IdaEncTab tab = {};
+        for (int i = 0; i < n; ++i) {
+            uint32_t e = 1;
+            for (int k = 0; k < m; ++k) {  // e = (i+1)^k mod p (ida.cpp:59-73)
+                tab.lo[i][k >> 2] |= (e & 0xFFu) << (8 * (k & 3));
+                tab.hi[i][k >> 2] |= (e >> 8) << (8 * (k & 3));
+                if (e >> 8) tab.himask |= 1u << i;
+                e = (uint32_t)(((uint64_t)e * (uint32_t)(i + 1)) % (uint32_t)p);
+            }
+        }
+        // rows 1, 3, 7 hold the only E = 256 entries when p = 257 (see the kernel)
+        const bool p257 = p == 257 && tab.himask == ((1u << 1) | (1u << 3) | (1u << 7));
+        if (p257) {
+            for (int i = 0; i < n; ++i)
+                for (int w = 0; w < 4; ++w) tab.hi[i][w] = 0;
+        }
+#define CX_ENC_FIXED(DD, PP)                                                                 \
+    do {                                                                                     \
+        static const unsigned g = resident_grid(k_ida_encode_fixed<14, 3, DD, PP>, 256);     \
+        k_ida_encode_fixed<14, 3, DD, PP><<<g, 256, 0, s>>>(data, offs, seg, blocks, m,      \
+                                                            (uint32_t)p, 1.0f / p, frags,    \
+                                                            tab);                            \
+    } while (0)
+        if (p257 && FD == 1) CX_ENC_FIXED(1, true);
+        else if (p257) CX_ENC_FIXED(2, true);
+        else if (FD == 1) CX_ENC_FIXED(1, false);
+        else CX_ENC_FIXED(2, false);
+#undef CX_ENC_FIXED
+        return hipGetLastError();
+    }
+    if (16 * m + 1 > 64 * 3)
+        ida_encode_launch<8, 2>(data, offs, seg, blocks, n, m, p, frags, s);
+    else if (D == 1)
+        ida_encode_launch<3, 1>(data, offs, seg, blocks, n, m, p, frags, s);
+    else if (D == 2)
+        ida_encode_launch<3, 2>(data, offs, seg, blocks, n, m, p, frags, s);
+    else if (D == 3)
+        ida_encode_launch<3, 3>(data, offs, seg, blocks, n, m, p, frags, s);
     else
-        k_ida_encode<8><<<g8, 256, 0, s>>>(data, offs, seg, blocks, n, m, (uint32_t)p, 1.0f / p,
-                                           frags);
+        ida_encode_launch<3, 4>(data, offs, seg, blocks, n, m, p, frags, s);
     return hipGetLastError();
 }
 
@@ -3333,22 +3556,45 @@ hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t run
     return hipGetLastError();
 }
 
+template <bool WIDE, int FM, int D>
+static void ida_decode_launch(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m,
+                              int p, const int32_t *inv, const uint32_t *run_of,
+                              const uint8_t *okf, uint16_t *out, uint64_t *out_len,
+                              hipStream_t s) {
+    static const unsigned grid = resident_grid(k_ida_decode<WIDE, FM, D>, 256);
+    k_ida_decode<WIDE, FM, D><<<grid, 256, 0, s>>>(
+        frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv, run_of, okf, out,
+        reinterpret_cast<unsigned long long *>(out_len));
+}
+
+// A/B knob for the pipeline depths (chunks in flight per wave): CX_IDA_ENC_D,
+// CX_IDA_DEC_D in {1, 2, 3, 4}; defaults are the measured best.
+static int ida_depth(const char *var, int dflt) {
+    const char *e = getenv(var);
+    const int d = e ? atoi(e) : dflt;
+    return d >= 1 && d <= 4 ? d : dflt;
+}
+
 hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m, int p,
                       const int32_t *inv, const uint32_t *run_of, const uint8_t *okf,
                       uint16_t *out, uint64_t *out_len, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
     const bool wide = (uint64_t)m * (p - 1) * 65535ull >= (1ull << 32);
-    static const unsigned gw = resident_grid(k_ida_decode<true>, 256);
-    static const unsigned gn = resident_grid(k_ida_decode<false>, 256);
-    const unsigned grid = wide ? gw : gn;
+    static const int D = ida_depth("CX_IDA_DEC_D", 2);
     if (wide)
-        k_ida_decode<true><<<grid, 256, 0, s>>>(frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv,
-                                                run_of, okf, out,
-                                                reinterpret_cast<unsigned long long *>(out_len));
+        ida_decode_launch<true, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out,
+                                              out_len, s);
+    else if (m > 12)
+        ida_decode_launch<false, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out,
+                                               out_len, s);
+    else if (D == 1)
+        ida_decode_launch<false, 12, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
+    else if (D == 2)
+        ida_decode_launch<false, 12, 2>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
+    else if (D == 3)
+        ida_decode_launch<false, 12, 3>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
     else
-        k_ida_decode<false><<<grid, 256, 0, s>>>(frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv,
-                                                 run_of, okf, out,
-                                                 reinterpret_cast<unsigned long long *>(out_len));
+        ida_decode_launch<false, 12, 4>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
     return hipGetLastError();
 }
 
