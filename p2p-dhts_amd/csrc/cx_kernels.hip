@@ -3162,7 +3162,7 @@ struct DecSlot {
     uint32_t f[FM];
 };
 
-template <bool WIDE, int FM, int D>
+template <bool WIDE, int FM, int D, int MF>
 __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const uint64_t *seg,
                                                     size_t blocks, int m, uint32_t p,
                                                     float inv_p, const int32_t *inv,
@@ -3171,6 +3171,7 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
     __shared__ __attribute__((aligned(16))) uint32_t Ainv[256 / 64][IDA_MAX_N * IDA_AROW];
     const int lane = threadIdx.x & 63;
     uint32_t *As = Ainv[threadIdx.x >> 6];
+    if (MF) m = MF;  // fixed shape (DHash m = 10): rows unrolled, one-fix-up reduction
     const int nw = (m + 1) >> 1;
     const uint64_t total = seg[blocks];
     const uint64_t chunks = (total + 63) / 64;
@@ -3240,7 +3241,9 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
                     for (int w = 0; w < (FM + 1) / 2; ++w)
                         F[w] = f[2 * w] | (2 * w + 1 < FM ? f[2 * w + 1] << 16 : 0u);
                     uint32_t cprev = 0;
-                    for (int j = 0; j < m; ++j) {
+#pragma unroll
+                    for (int j = 0; j < (MF ? MF : FM); ++j) {
+                        if (j >= m) break;
                         const uint32_t *ar = As + j * IDA_AROW;
                         uint32_t acc = 0;
 #pragma unroll
@@ -3249,7 +3252,9 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
                                 acc = __builtin_amdgcn_udot2(__builtin_bit_cast(cx_us2, ar[w]),
                                                              __builtin_bit_cast(cx_us2, F[w]),
                                                              acc, false);
-                        const uint32_t cv = modp_f(acc, p, inv_p);
+                        // acc / p < m 65535 < 2^20 for m <= 12 (FM = 12)
+                        const uint32_t cv = FM <= 12 ? modp_fast(acc, p, inv_p)
+                                                     : modp_f(acc, p, inv_p);
                         if (cv) last = j;
                         if ((m & 1) == 0) {  // m even: 4-byte aligned pairs
                             if (j & 1)
@@ -3556,13 +3561,13 @@ hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t run
     return hipGetLastError();
 }
 
-template <bool WIDE, int FM, int D>
+template <bool WIDE, int FM, int D, int MF = 0>
 static void ida_decode_launch(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m,
                               int p, const int32_t *inv, const uint32_t *run_of,
                               const uint8_t *okf, uint16_t *out, uint64_t *out_len,
                               hipStream_t s) {
-    static const unsigned grid = resident_grid(k_ida_decode<WIDE, FM, D>, 256);
-    k_ida_decode<WIDE, FM, D><<<grid, 256, 0, s>>>(
+    static const unsigned grid = resident_grid(k_ida_decode<WIDE, FM, D, MF>, 256);
+    k_ida_decode<WIDE, FM, D, MF><<<grid, 256, 0, s>>>(
         frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv, run_of, okf, out,
         reinterpret_cast<unsigned long long *>(out_len));
 }
@@ -3584,6 +3589,12 @@ hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks,
     if (wide)
         ida_decode_launch<true, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out,
                                               out_len, s);
+    else if (m == 10 && !getenv("CX_IDA_GENERIC") && D == 1)  // DHash (14, 10)
+        ida_decode_launch<false, 12, 1, 10>(frags, seg, blocks, m, p, inv, run_of, okf, out,
+                                            out_len, s);
+    else if (m == 10 && !getenv("CX_IDA_GENERIC"))
+        ida_decode_launch<false, 12, 2, 10>(frags, seg, blocks, m, p, inv, run_of, okf, out,
+                                            out_len, s);
     else if (m > 12)
         ida_decode_launch<false, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out,
                                                out_len, s);

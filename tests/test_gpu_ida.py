@@ -25,8 +25,11 @@ def ragged(rng, m, count, big=0):
             np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
 
 
+# (14, 9..12, p) run the fixed-shape encode (p = 257: folded high bytes; else the
+# high-byte mask); m = 10 the fixed decode, up to its largest non-wide p (6553)
 PARAMS = [(14, 10, 257), (3, 2, 257), (2, 1, 257), (20, 12, 40009), (32, 31, 46337),
-          (9, 4, 263)]
+          (9, 4, 263), (14, 9, 257), (14, 12, 257), (14, 10, 263), (14, 11, 6551),
+          (14, 10, 6553)]
 
 
 @pytest.mark.parametrize("nmp", PARAMS)

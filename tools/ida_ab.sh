@@ -6,5 +6,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_ida.py -m gpu -x -q --timeo
 tail -2 gpurun_out/ida_ab/pytest.log
 run() { timeout -k 10 120 env "$@" python -u benches/bench_ida.py > gpurun_out/ida_ab/$1.json 2>gpurun_out/ida_ab/$1.err; echo "$1 $(cat gpurun_out/ida_ab/$1.json)"; }
 run CX_IDA_GENERIC=1
-run CX_IDA_ENCF_D=1
-run CX_IDA_ENCF_D=2
+run CX_IDA_DEC_D=1
+run CX_IDA_DEC_D=2
