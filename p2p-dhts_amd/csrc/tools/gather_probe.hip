@@ -148,6 +148,17 @@ int main(int argc, char **argv) {
         fflush(stdout);
     };
     const int full = 256 * 2048;  // 32 waves/CU x 256 CUs
+    if (argc > 2 && !strcmp(argv[2], "calib")) {
+        // one known workload for calibrating PMC FETCH_SIZE on this access
+        // pattern (MI355X_MICROARCH.md: other widths than wide streams are
+        // uncalibrated): a warm-up dispatch of 4 hops, then one of 64 hops, each
+        // lane quad gathering one random 64-B entry per hop from the table
+        const double rate = run_coop<4>(t, max_bytes, full, 64, sink);
+        printf("{\"width\":\"64B/4lanes\",\"table_MiB\":%zu,\"entries_warmup\":%d,"
+               "\"entries_timed\":%d,\"Gloads_per_s\":%.2f}]}\n",
+               max_bytes >> 20, full / 4 * 4, full / 4 * 64, rate / 1e9);
+        return 0;
+    }
     if (argc > 2 && !strcmp(argv[2], "coop_sweep")) {
         // cooperative 64-B / 128-B entries against table size (TLB reach)
         for (size_t gb : {8ull, 16ull, 32ull, 64ull, 128ull, 192ull}) {
