@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -230,6 +231,10 @@ void free_ring(cx_ring *r) {
     delete r;
 }
 
+#ifndef CX_DIR_EXTRA_DEFAULT
+#define CX_DIR_EXTRA_DEFAULT 1
+#endif
+
 // Eytzinger copy + bucket directory of r->d_ring (r->n set).
 int build_search(cx_ring *r, hipStream_t s) {
     const size_t m = r->n;
@@ -238,9 +243,19 @@ int build_search(cx_ring *r, hipStream_t s) {
     CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
     r->d_eyt = E.as<cell128>();
     E.release();
+    // 2^k buckets, k = ceil(log2 n) + extra: a query's bucket entry resolves it
+    // unless the bucket holds >= 2 peers and the key lies past the first; each
+    // extra bit halves the load factor (fewer second gathers, 2x the bytes).
+    // CX_DIR_EXTRA (0..3) is the A/B knob; the default is the measured best.
+    static const int extra = [] {
+        const char *e = getenv("CX_DIR_EXTRA");
+        const int v = e ? atoi(e) : CX_DIR_EXTRA_DEFAULT;
+        return v < 0 ? 0 : (v > 3 ? 3 : v);
+    }();
     int k = 1;
     while (((size_t)1 << k) < m) ++k;
-    if (k > 28) k = 28;
+    k += extra;
+    if (k > 29) k = 29;
     r->dir_k = k;
     DBuf lo, dir;
     CX_HIP(lo.alloc((((size_t)1 << k) + 1) * sizeof(uint32_t)));
