@@ -176,9 +176,12 @@ def main():
     if args.mode == "arc":
         return main_arc(args)
     world, rank, local = dist.env_rank()
+    # one rank per GPU; CX_DIST_BACKEND=gloo with more ranks than GPUs is the
+    # rehearsal of the N > 1 flow on a one-GPU box (ranks share devices)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
-    dist.init("nccl", dev)
+    dist.init(os.environ.get("CX_DIST_BACKEND", "nccl"), dev)
     N = 1 << args.peers_log2
     Q = 1 << args.keys_log2
 
