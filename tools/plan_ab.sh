@@ -1,3 +1,4 @@
+# (Experiment record: the CX_CZ_PLAN knob was measured slower and removed; see DESIGN.md.)
 # cz walk plan-budget A/B: route parity tests at budget 2, then the bench per budget.
 set -eo pipefail
 cd $GRAFT_REPO_ROOT
