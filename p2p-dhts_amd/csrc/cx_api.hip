@@ -54,18 +54,18 @@ struct DBuf {
     }
 };
 
-// Stream-ordered temporary (hipMallocAsync / hipFreeAsync): no device-wide
-// synchronisation on free, unlike hipFree.
+// Per-call temporary.  This was a stream-ordered pool allocation
+// (hipMallocAsync / hipFreeAsync on the null stream); a kernel reading such a
+// buffer (the IDA decode's inverse table, reused from the previous call's
+// freed blocks) intermittently hit "illegal memory access" (about 1 in 15
+// runs of tests/cpp's DataBlock case; none in 60 runs with plain hipMalloc),
+// so temporaries use hipMalloc / hipFree like DBuf.
 struct ABuf {
     void *p = nullptr;
-    hipStream_t s = nullptr;
     ~ABuf() {
-        if (p) (void)hipFreeAsync(p, s);
+        if (p) (void)hipFree(p);
     }
-    hipError_t alloc(size_t bytes, hipStream_t st) {
-        s = st;
-        return hipMallocAsync(&p, bytes ? bytes : 16, st);
-    }
+    hipError_t alloc(size_t bytes, hipStream_t) { return hipMalloc(&p, bytes ? bytes : 16); }
     template <class T>
     T *as() const {
         return static_cast<T *>(p);

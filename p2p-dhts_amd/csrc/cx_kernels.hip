@@ -2504,6 +2504,8 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
     const int no = CHURN ? ((uint32_t)nlist < n_old ? nlist : (int)n_old) : nh;
     const int nslots = CHURN ? nlist : nh;
     const uint32_t full = (nn >= 32) ? 0xFFFFFFFFu : ((1u << nn) - 1u);
+    const bool o2n_al = CHURN && ((uintptr_t)old_to_new & 15) == 0;
+    static_assert(CX_MAX_NSUCC <= 17, "five 16-B o2n loads cover 17 entries");
     for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q;
          base += (size_t)gridDim.x * ROW_BLOCK) {
         const size_t i = base + threadIdx.x;
@@ -2526,8 +2528,32 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
             count[i] = (uint8_t)nn;
             // holders: old n-window mapped to the new ring, or the caller's list
             uint32_t hv[CX_MAX_NSUCC];
+            // the old window's o2n entries are contiguous: five aligned 16-B loads
+            // cover [so, so + no) for no <= 17 (one request each instead of one
+            // dword request per entry); the window may not wrap or pass the end
+            const uint32_t ob = so & ~3u;
+            const bool wide = CHURN && o2n_al && (size_t)ob + 20 <= n_old;
+            if (wide) {
+                const uint4 *w4 = reinterpret_cast<const uint4 *>(old_to_new + ob);
+                uint32_t w[20];
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                    const uint4 x = w4[t];
+                    w[4 * t] = x.x;
+                    w[4 * t + 1] = x.y;
+                    w[4 * t + 2] = x.z;
+                    w[4 * t + 3] = x.w;
+                }
+                const uint32_t sh = so & 3u;
+#pragma unroll
+                for (int j = 0; j < CX_MAX_NSUCC; ++j)
+                    hv[j] = j >= no ? CX_NONE
+                                    : (sh == 0 ? w[j] : sh == 1 ? w[j + 1] : sh == 2 ? w[j + 2]
+                                                                           : w[j + 3]);
+            }
 #pragma unroll
             for (int j = 0; j < CX_MAX_NSUCC; ++j) {
+                if (wide) break;
                 uint32_t hj = CX_NONE;
                 if (j < no) {
                     if (CHURN) {

@@ -150,9 +150,11 @@ TEST(DataBlock, EncodeDecodeVal1) {
     bool threw = false;
     alive[1].first = alive[0].first;  // repeated index
     try {
-        chordx::ida::Decode(alive);
+        const std::vector<uint16_t> got = chordx::ida::Decode(alive);
+        std::printf("no error: decoded %zu values\n", got.size());
     } catch (const chordx::Error &e) {
         threw = std::string(e.what()) == "N is not invertible";
+        if (!threw) std::printf("unexpected error: %s\n", e.what());
     }
     EXPECT_TRUE(threw);
 }
