@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -54,23 +56,44 @@ struct DBuf {
     }
 };
 
-// Per-call temporary.  This was a stream-ordered pool allocation
-// (hipMallocAsync / hipFreeAsync on the null stream); a kernel reading such a
-// buffer (the IDA decode's inverse table, reused from the previous call's
-// freed blocks) intermittently hit "illegal memory access" (about 1 in 15
-// runs of tests/cpp's DataBlock case; none in 60 runs with plain hipMalloc),
-// so temporaries use hipMalloc / hipFree like DBuf.
-struct ABuf {
-    void *p = nullptr;
-    ~ABuf() {
-        if (p) (void)hipFree(p);
-    }
-    hipError_t alloc(size_t bytes, hipStream_t) { return hipMalloc(&p, bytes ? bytes : 16); }
-    template <class T>
-    T *as() const {
-        return static_cast<T *>(p);
-    }
+// IDA decode temporaries: a grow-only device arena per device and phase,
+// reused across calls (calls on a device serialise on its mutex; growth
+// hipFree-s the old block, which waits for the work still using it).  These
+// were stream-ordered pool allocations (hipMallocAsync / hipFreeAsync on the
+// null stream) and the decode kernel reading a reused pool block
+// intermittently hit "illegal memory access" (about 1 in 15 runs of
+// tests/cpp's DataBlock case, 0 in 90 with plain hipMalloc); per-call hipMalloc
+// / hipFree cost 0.5 ms per call on 2^22 tiny blocks, hence the arena.
+struct IdaArena {
+    std::mutex mu;
+    void *p[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
 };
+IdaArena &ida_arena(int device) {
+    static IdaArena arenas[64];
+    return arenas[device & 63];
+}
+// Carves 256-B aligned pieces of `sizes` bytes out of arena slot `slot`.
+hipError_t arena_carve(IdaArena &a, int slot, std::initializer_list<size_t> sizes,
+                       std::initializer_list<void **> outs) {
+    size_t total = 0;
+    for (size_t b : sizes) total += (b + 255) & ~(size_t)255;
+    if (total > a.cap[slot]) {
+        if (a.p[slot]) (void)hipFree(a.p[slot]);
+        a.p[slot] = nullptr;
+        a.cap[slot] = 0;
+        hipError_t e = hipMalloc(&a.p[slot], total ? total : 256);
+        if (e != hipSuccess) return e;
+        a.cap[slot] = total ? total : 256;
+    }
+    char *c = static_cast<char *>(a.p[slot]);
+    auto o = outs.begin();
+    for (size_t b : sizes) {
+        **o++ = c;
+        c += (b + 255) & ~(size_t)255;
+    }
+    return hipSuccess;
+}
 
 }  // namespace
 
@@ -1088,32 +1111,32 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
         if ((rc = stage_out(out_len, blocks, memkind, tlen, &dlen))) return rc;
     }
     // runs of equal index lists share one inverse
-    ABuf flag, flag2, ws, run_of, run_start, inv, okf, cnt;
-    CX_HIP(flag.alloc(blocks * sizeof(uint32_t), s));
-    CX_HIP(flag2.alloc(blocks * sizeof(uint32_t), s));
-    CX_HIP(ws.alloc(cxk::scan_workspace_words(blocks) * sizeof(uint32_t), s));
-    CX_HIP(cnt.alloc(2 * sizeof(uint32_t), s));
-    CX_HIP(cxk::ida_runs(didx, blocks, m, flag.as<uint32_t>(), s));
-    CX_HIP(hipMemcpyAsync(flag2.p, flag.p, blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    CX_HIP(cxk::exclusive_scan(flag2.as<uint32_t>(), blocks, ws.as<uint32_t>(), s));
+    IdaArena &arena = ida_arena(device);
+    std::lock_guard<std::mutex> lock(arena.mu);
+    uint32_t *flag, *flag2, *ws, *run_of, *run_start;
+    int32_t *inv;
+    uint8_t *okf;
+    CX_HIP(arena_carve(arena, 0,
+                       {blocks * sizeof(uint32_t), blocks * sizeof(uint32_t),
+                        cxk::scan_workspace_words(blocks) * sizeof(uint32_t)},
+                       {(void **)&flag, (void **)&flag2, (void **)&ws}));
+    CX_HIP(cxk::ida_runs(didx, blocks, m, flag, s));
+    CX_HIP(hipMemcpyAsync(flag2, flag, blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    CX_HIP(cxk::exclusive_scan(flag2, blocks, ws, s));
     uint32_t last[2] = {0, 0};
-    CX_HIP(hipMemcpyAsync(&last[0], flag2.as<uint32_t>() + blocks - 1, 4, hipMemcpyDeviceToHost,
-                          s));
-    CX_HIP(hipMemcpyAsync(&last[1], flag.as<uint32_t>() + blocks - 1, 4, hipMemcpyDeviceToHost, s));
+    CX_HIP(hipMemcpyAsync(&last[0], flag2 + blocks - 1, 4, hipMemcpyDeviceToHost, s));
+    CX_HIP(hipMemcpyAsync(&last[1], flag + blocks - 1, 4, hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
     const size_t runs = (size_t)last[0] + last[1];
-    CX_HIP(run_of.alloc(blocks * sizeof(uint32_t), s));
-    CX_HIP(run_start.alloc(runs * sizeof(uint32_t), s));
-    CX_HIP(inv.alloc(runs * (size_t)m * m * sizeof(int32_t), s));
-    CX_HIP(okf.alloc(runs, s));
-    CX_HIP(cxk::ida_run_index(flag2.as<uint32_t>(), flag.as<uint32_t>(), blocks,
-                              run_of.as<uint32_t>(), run_start.as<uint32_t>(), s));
-    CX_HIP(cxk::ida_inverse(didx, run_start.as<uint32_t>(), runs, m, p, inv.as<int32_t>(),
-                            okf.as<uint8_t>(), s));
+    CX_HIP(arena_carve(arena, 1,
+                       {blocks * sizeof(uint32_t), runs * sizeof(uint32_t),
+                        runs * (size_t)m * m * sizeof(int32_t), runs},
+                       {(void **)&run_of, (void **)&run_start, (void **)&inv, (void **)&okf}));
+    CX_HIP(cxk::ida_run_index(flag2, flag, blocks, run_of, run_start, s));
+    CX_HIP(cxk::ida_inverse(didx, run_start, runs, m, p, inv, okf, s));
     CX_HIP(hipMemsetAsync(dlen, 0, blocks * sizeof(uint64_t), s));
-    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, m, p, inv.as<int32_t>(), run_of.as<uint32_t>(),
-                           okf.as<uint8_t>(), dout, dlen, s));
-    CX_HIP(cxk::ida_mark_failed(run_of.as<uint32_t>(), okf.as<uint8_t>(), blocks, dlen, s));
+    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, m, p, inv, run_of, okf, dout, dlen, s));
+    CX_HIP(cxk::ida_mark_failed(run_of, okf, blocks, dlen, s));
     if (memkind == CX_MEM_HOST) {
         if ((rc = finish_out(out_len, dlen, blocks, memkind, s))) return rc;
         if ((rc = finish_out(out, dout, (size_t)(segs * m), memkind, s))) return rc;

@@ -3269,7 +3269,7 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
                     uint32_t cprev = 0;
 #pragma unroll
                     for (int j = 0; j < (MF ? MF : FM); ++j) {
-                        if (j >= m) break;
+                        if (!MF && j >= m) continue;  // uniform; MF: m == MF
                         const uint32_t *ar = As + j * IDA_AROW;
                         uint32_t acc = 0;
 #pragma unroll
