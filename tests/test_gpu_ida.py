@@ -96,6 +96,20 @@ def test_decode_not_invertible_and_ragged_edges(ida, O):
     assert got[2].size == 0 and got[3].size == 0
 
 
+def test_decode_repeated_calls_reuse_temporaries(ida, O):
+    """Valid and non-invertible decodes alternating in one process: the decode
+    temporaries are reused across calls (an earlier stream-ordered pool version
+    faulted intermittently on exactly this sequence, DESIGN.md IDA notes)."""
+    f = O.ida_encode([b"val1"])
+    good = [list(range(1, 11))]
+    bad = [[2, 2, 5, 6, 7, 9, 10, 11, 13, 14]]
+    rows = [f[0][:10]]
+    for _ in range(50):
+        got = ida.decode(rows, good)
+        assert bytes(got[0].astype(np.uint8)) == b"val1"
+        assert ida.decode(rows, bad)[0] is None
+
+
 def test_golden_values_through_datablock(ida, refvec):
     """Create + Read of the reference's DHash test values: the m lowest
     fragment indices a read collects (std::set order) rebuild the value."""

@@ -16,4 +16,6 @@ tail -1 "$OUT/bench_default.log" | cut -c1-300
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu > "$OUT/bench_trace.log" 2>&1
+
+DIAG_RUNS=30 bash $GRAFT_REPO_ROOT/tools/cpp_fault_diag.sh
 echo done
