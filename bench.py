@@ -12,13 +12,27 @@ timing are the only cross-rank traffic.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Rank 0 prints ONE JSON line.
+With --gpus N > 1 and no torch.distributed environment, bench.py starts
+`torch.distributed.run --nproc-per-node N` itself as a child process (before
+anything touches the GPU) and exits with its status; rank 0 of the child job
+prints the line.  Rank 0 prints ONE JSON line.
+
+Roofline (per launch of the timed route kernel): `achieved` counts the bytes
+the walk must move -- its streams (key, source, (pred, self) pair, owner, hops,
+status) plus one 64-B granule per random gather it actually issues (window-table
+entries, exact ring IDs, finger entries), counted by the counting build of the
+same kernel on the same batch -- over the kernel time from HIP events on the
+launch stream.  SURVEY 8(d)'s reference-work model (128 B per hop) is reported
+separately as `reference_work_model`: it prices hops the window table resolves
+without a gather and is not a byte count of this kernel.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,16 +50,13 @@ from chordx import dist  # noqa: E402
 SEED_RING = 0x5EED0005
 SEED_KEYS = 0x5EED0006
 HBM_PEAK = 8.0e12  # B/s per MI355X (MI355X_MICROARCH.md, HBM3E spec)
-# Measured random-gather ceiling for 64-B entries loaded by 4 cooperating lanes
-# on an 8-16 GiB table (p2p-dhts_amd/csrc/tools/gather_probe.hip,
-# profiles/r01/gather_probe.json): the bound the walk actually runs against.
-GATHER_CEILING = 46.0e9  # dependent random 64-B requests / s
-# Algorithmic bytes of one routed lookup: 25 B streamed
-# (16 key + 4 src + 4 owner + 1 hops) + 64 B source-peer record (first
-# StoredLocally) + 128 B per hop (finger granule + ring granule).
-BYTES_STREAM = 25
-BYTES_SRC = 64
-BYTES_HOP = 128
+# Bytes the walk must move per lookup in streams: key 16 + source 4 +
+# (pred, self) ID pair 32 + owner 4 + hops 1 + status 1.
+BYTES_STREAM = 58
+GRANULE = 64  # one dependent random gather
+# SURVEY 8(d) reference-work model: 25 B streamed + 64 B source-peer record +
+# 128 B per hop (finger granule + ring granule).
+REF_STREAM, REF_SRC, REF_HOP = 25, 64, 128
 
 
 def parse():
@@ -66,29 +77,101 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    """One process per GPU.  Without a torch.distributed environment and with
+    --gpus N > 1, run this script under torch.distributed.run as a CHILD
+    process (nothing here has touched the GPU yet) and return its exit
+    status; None = run the benchmark in this process."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus <= 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.run(cmd).returncode
+    if int(ws) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    return None
+
+
+def host_threads() -> int:
+    """Host cores this process may use: its CPU affinity, capped by the
+    job's thread budget (OMP_NUM_THREADS; 16 on a one-GPU box, whose nproc
+    shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
     """Literal restatement (oracle/chord_oracle.c or_route: linear 128-entry
     InBetween scan per hop, StoredLocally, ForwardRequest substitution) timed on
-    this host's cores over a bounded sample of the same key stream; also checks
-    the GPU's owner/hops on that sample."""
+    this host's cores over a bounded sample of the same key stream (about
+    2/3 of budget_s on all usable cores, 1/3 on one core); also checks the
+    GPU's owner/hops on the sample."""
     import oracle as O
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = host_threads()
     ring_np = ring.ids()
     P = O.Peers(ring_np, F_host)
-    cal = 2048
-    t0 = time.perf_counter()
-    O.route(P, src_np[:cal], keys_np[:cal], threads=threads)
-    per = (time.perf_counter() - t0) / cal
-    q = int(min(len(keys_np), max(cal, budget_s / max(per, 1e-9))))
-    t0 = time.perf_counter()
-    wo, wh, ws = O.route(P, src_np[:q], keys_np[:q], threads=threads)
-    dt = time.perf_counter() - t0
-    ok = bool((wo == gpu_owner[:q]).all() and (wh == gpu_hops[:q]).all() and (ws == 0).all())
-    return {"value": q / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
-            "sample": f"first {q} keys of the rank-0 stream (of {len(keys_np)}), "
-                      f"{dt:.1f} s wall, oracle/chord_oracle.c or_route",
+
+    def timed(q, th):
+        t0 = time.perf_counter()
+        r = O.route(P, src_np[:q], keys_np[:q], threads=th)
+        return r, time.perf_counter() - t0
+
+    _, t_cal = timed(4096, 1)
+    per1 = t_cal / 4096
+    q1 = int(min(len(keys_np), max(4096, budget_s / 3 / max(per1, 1e-9))))
+    _, dt1 = timed(q1, 1)
+    qa = int(min(len(keys_np), max(q1, budget_s * 2 / 3 * threads / max(per1, 1e-9))))
+    (wo, wh, ws), dta = timed(qa, threads)
+    ok = bool((wo == gpu_owner[:qa]).all() and (wh == gpu_hops[:qa]).all() and (ws == 0).all())
+    return {"value": qa / dta, "unit": "lookups/s", "cores": threads, "kind": "port",
+            "value_1core": q1 / dt1,
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "sample": f"first {qa} keys of the rank-0 stream (of {len(keys_np)}) on {threads} "
+                      f"threads ({dta:.1f} s), first {q1} on 1 thread ({dt1:.1f} s); "
+                      "oracle/chord_oracle.c or_route, -O3 -march=native",
             "parity_on_sample": ok}
+
+
+def dry_run(args):
+    """CX_BENCH_DRYRUN=1: the launch / rendezvous / timing / reporting flow
+    without a GPU (CPU tests of the N > 1 path over gloo)."""
+    world, rank, _ = dist.env_rank()
+    dist.init("gloo")
+    dist.barrier(world)
+    t0 = time.perf_counter()
+    dist.barrier(world)
+    dt_max = dist.max_over_ranks(time.perf_counter() - t0, world)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run", "value": 0.0, "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": dt_max * 1e3 / max(1, args.steps)}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def main_arc(args):
@@ -173,6 +256,11 @@ def main_arc(args):
 
 def main():
     args = parse()
+    rc = launch(args)
+    if rc is not None:
+        sys.exit(rc)
+    if os.environ.get("CX_BENCH_DRYRUN") == "1":
+        return dry_run(args)
     if args.mode == "arc":
         return main_arc(args)
     world, rank, local = dist.env_rank()
@@ -236,8 +324,16 @@ def main():
     # ---- results ----
     bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
     sum_hops = int(hops.to(torch.int64).sum().item())
-    algo_bytes = Q * (BYTES_STREAM + BYTES_SRC) + BYTES_HOP * sum_hops
+    # gathers the walk issues on this batch: the counting build of the same
+    # kernel, run once after the timed region (same inputs, same outputs)
+    ring.route_counters(True)
+    ring.route(src, keys, out=out)
+    g64, r16, xc, nq = ring.route_counters(False)
+    gathers = g64 + r16 + 2 * xc
+    algo_bytes = Q * BYTES_STREAM + GRANULE * gathers
     achieved = algo_bytes / (kern_ms * 1e-3)
+    ref_bytes = Q * (REF_STREAM + REF_SRC) + REF_HOP * sum_hops
+    probe = ring.gather_probe()  # request-rate ceiling on this table, this box, this run
     # exact-successor rate on the same keys (row a5, C2 kernel at C4 size)
     succ_out = torch.empty(Q, dtype=torch.int32, device=dev)
     ring.successor(keys, out=succ_out)
@@ -284,19 +380,19 @@ def main():
                            hops[:cs].cpu().numpy(), args.cpu_seconds)
         del F_host
 
-    traffic = gather = None
+    traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == kernel_name:
             traffic = tj.get("hbm_bytes_per_launch")
-            req = tj["fetch_bytes"] / 64 / (kern_ms * 1e-3)
-            gather = {"requests_per_s": req, "ceiling": GATHER_CEILING,
-                      "frac": req / GATHER_CEILING,
-                      "traffic_frac_of_hbm": traffic / (kern_ms * 1e-3) / HBM_PEAK,
-                      "note": "PMC FETCH_SIZE / 64 B per launch (profiles/traffic_route.json) "
-                              "over this run's kernel time, vs the measured dependent "
-                              "random-gather ceiling"}
+    req = gathers / (kern_ms * 1e-3)
+    gather = {"requests_per_s": req, "ceiling": probe, "frac": req / probe,
+              "gathers_per_lookup": gathers / Q, "table_gathers": g64, "exact_id_gathers": r16,
+              "exact_hops": xc,
+              "note": "random 64-B requests the walk issued (counting build, same batch) per "
+                      "second of kernel time, vs dependent quad-cooperative 64-B gathers/s "
+                      "measured on the same route table in this run"}
 
     if rank == 0:
         total = world * Q * args.steps
@@ -322,7 +418,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "kernel": kernel_name, "kernel_ms": kern_ms,
-                         "algo_bytes_per_launch": algo_bytes},
+                         "algo_bytes_per_launch": algo_bytes,
+                         "algo_model": f"{BYTES_STREAM} B streams per lookup + {GRANULE} B per "
+                                       "random gather issued (counted)"},
+            "reference_work_model": {"bytes_per_launch": ref_bytes,
+                                     "GBps": ref_bytes / (kern_ms * 1e-3) / 1e9,
+                                     "note": "SURVEY 8(d): 128 B per hop; hops the window "
+                                             "table resolves without a gather are priced too, "
+                                             "so this is not a byte count of the kernel"},
             "cpu_baseline": cpu,
             "gather_roofline": gather,
             "route_variant": route_variant,

@@ -61,8 +61,22 @@ enum cx_err {
 
 enum cx_memkind { CX_MEM_HOST = 0, CX_MEM_DEVICE = 1 };
 
-/* Per-query status of cx_route. */
-enum cx_qstatus { CX_Q_OK = 0, CX_Q_HOPCAP = 1, CX_Q_BADPEER = 2 /* src or finger entry >= ring size */ };
+/* Per-query status of cx_route (the reference throws; a batch reports them
+ * per lookup and does not fail as a whole). */
+enum cx_qstatus {
+    CX_Q_OK = 0,
+    CX_Q_HOPCAP = 1,    /* more than CX_HOP_CAP forwards (the reference livelocks) */
+    CX_Q_BADPEER = 2,   /* src >= ring size */
+    CX_Q_FAILED = 3,    /* "Lookup failed" (chord_peer.cpp:206, dhash_peer.cpp:524) */
+    CX_Q_NOT_FOUND = 4  /* "ChordKey not found": no finger for the key's range
+                           (finger_table.h:129, table not populated) */
+};
+
+/* Which ForwardRequest's dead-finger fallback the literal walk applies. */
+enum cx_fwd_rule {
+    CX_FWD_CHORD = 0, /* ChordPeer::ForwardRequest, chord_peer.cpp:185-211 */
+    CX_FWD_DHASH = 1  /* DHashPeer::ForwardRequest, dhash_peer.cpp:500-529 */
+};
 
 /* ---- library --------------------------------------------------------- */
 int cx_version(void);
@@ -91,8 +105,9 @@ int cx_ring_sync(const cx_ring *ring);
 /* ---- a5/a7: exact successor --------------------------------------------
  * owner[i] = index of the peer whose StoredLocally(keys[i]) holds in the
  * converged ring (abstract_chord_peer.cpp:720-725, min_key = pred+1,
- * chord_peer.cpp:275): the first ID >= key, wrapping to 0.  Eytzinger search
- * with the top levels staged in LDS. */
+ * chord_peer.cpp:275): the first ID >= key, wrapping to 0.  Default search: a
+ * bucket directory over the top ID bits (one gather answers most keys); A/B
+ * alternatives: Eytzinger with LDS-staged top levels. */
 int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *owner,
                  int memkind);
 
@@ -103,26 +118,40 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
  * fingers_out (n x 128 uint32, may be NULL) receives a copy. */
 int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind);
 /* Hand-edited / churned finger table (EditNthFinger, AdjustFingers,
- * ReplaceDeadPeer: finger_table.h:137-168), n x 128 peer indices.  Switches
- * cx_route to the literal ForwardRequest walk. */
+ * ReplaceDeadPeer: finger_table.h:137-168), n x 128 peer indices; CX_NONE =
+ * no finger added for that range (a table PopulateFingerTable never filled:
+ * lookups through it report CX_Q_NOT_FOUND).  Validated before it replaces
+ * the current table (a rejected upload changes nothing).  Switches cx_route
+ * to the literal ForwardRequest walk. */
 int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind);
 /* Device pointer to the n x 128 finger table (NULL until built/uploaded). */
 int cx_fingers_device(const cx_ring *ring, const uint32_t **fingers);
-/* Per-peer min_key_ and predecessor_ (CX_NONE = predecessor not alive),
- * as white-box tests set them (chord_test.cpp:18-90).  Either may be NULL
- * (= converged value: pred+1 / ring[p-1]).  Switches cx_route to the literal
- * walk. */
+/* Per-peer min_key_ and predecessor_ (CX_NONE = predecessor not set, never
+ * alive), as white-box tests set them (chord_test.cpp:18-123).  Either may be
+ * NULL (= converged value: pred+1 / ring[p-1]).  Validated before it replaces
+ * the current state.  Switches cx_route to the literal walk. */
 int cx_peer_state_upload(cx_ring *ring, const cx_u128 *min_keys, const uint32_t *preds,
                          int memkind);
+/* Peer liveness and successor lists for ForwardRequest's dead-finger branch
+ * (chord_peer.cpp:193-208, dhash_peer.cpp:505-526).  alive: n bytes, 0 = the
+ * peer's server does not answer (RemotePeer::IsAlive, remote_peer.cpp:43-46;
+ * a Fail()ed peer, chord_peer.cpp:293-300), NULL = all alive.  succ_lists:
+ * n x ns peer indices in list order, CX_NONE-padded (successors_, a
+ * RemotePeerList whose starting key is the peer's id, abstract_chord_peer.cpp:
+ * 25), NULL = the converged lists (next min(ns, n-1) peers clockwise).
+ * forward_rule: cx_fwd_rule.  0 <= ns <= 64.  Validated before it replaces the
+ * current state; switches cx_route to the literal walk. */
+int cx_liveness_upload(cx_ring *ring, const uint8_t *alive, const uint32_t *succ_lists, int ns,
+                       int forward_rule, int memkind);
 
 /* ---- a7-a9: finger-routed lookup with hop counts -------------------------
  * GetSuccessor(key) issued at peer src[i] (abstract_chord_peer.cpp:318-330),
  * forwarded hop by hop through ChordPeer::ForwardRequest (chord_peer.cpp:
  * 185-211): FingerTable::Lookup's first matching finger (finger_table.h:
- * 115-130), self -> live predecessor substitution.  hops[i] = GET_SUCC
- * requests sent (0 if src stores the key).  status[i] = CX_Q_HOPCAP (owner =
- * CX_NONE) if the walk exceeds CX_HOP_CAP forwards.  status may be NULL.
- * Needs fingers (cx_fingers_build or cx_fingers_upload). */
+ * 115-130), self -> live predecessor substitution, dead finger -> successor
+ * list (cx_liveness_upload).  hops[i] = GET_SUCC requests sent (0 if src
+ * stores the key).  status[i] = cx_qstatus; owner = CX_NONE unless CX_Q_OK.
+ * status may be NULL.  Needs fingers (cx_fingers_build or cx_fingers_upload). */
 int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
              uint32_t *owner, uint8_t *hops, uint8_t *status, int memkind);
 
@@ -246,7 +275,7 @@ void cx_wire_free(char *response);
  * own arc of peers only, arc g of G = [g n / G, (g+1) n / G).  A lookup walks
  * on the rank that owns the row it needs next, as the reference's
  * GET_SUCC request travels to the peer it is forwarded to
- * (ChordPeer::ForwardRequest, chord_peer.cpp:293-325): one bulk-synchronous
+ * (ChordPeer::ForwardRequest, chord_peer.cpp:185-211): one bulk-synchronous
  * step per exchange, in-flight lookups travel between ranks as 32-B records.
  * Owners, hops and statuses equal cx_route's on the replicated ring.
  * All arc buffers are device memory (CX_MEM_DEVICE). */

@@ -100,7 +100,7 @@ struct Key {
 struct Lookup {
     uint32_t owner;  // ring index of the peer whose StoredLocally(key) holds
     uint8_t hops;    // GET_SUCC requests sent (0 if the source stores the key)
-    uint8_t status;  // CX_Q_OK / CX_Q_HOPCAP / CX_Q_BADPEER
+    uint8_t status;  // cx_qstatus: CX_Q_OK, _HOPCAP, _BADPEER, _FAILED, _NOT_FOUND
 };
 
 // A converged ring of peers on one GPU.
@@ -169,7 +169,18 @@ public:
         check(cx_fingers_upload(h_, F.data(), CX_MEM_HOST));
     }
 
-    // min_key_ / predecessor_ per peer (CX_NONE = predecessor not alive).
+    // Liveness and successors_ lists (n x ns, CX_NONE-padded; nullptr = the
+    // converged lists) for ForwardRequest's dead-finger branch; rule =
+    // CX_FWD_CHORD (chord_peer.cpp:201-208) or CX_FWD_DHASH (dhash_peer.cpp:516-526).
+    void SetLiveness(const std::vector<uint8_t> *alive, const std::vector<uint32_t> *succs, int ns,
+                     int rule = CX_FWD_CHORD) {
+        if (alive && alive->size() != Size()) throw Error(CX_E_INVALID, "alive size");
+        if (succs && succs->size() != Size() * (size_t)ns) throw Error(CX_E_INVALID, "succs size");
+        check(cx_liveness_upload(h_, alive ? alive->data() : nullptr,
+                                 succs ? succs->data() : nullptr, ns, rule, CX_MEM_HOST));
+    }
+
+    // min_key_ / predecessor_ per peer (CX_NONE = predecessor not set).
     void SetPeerState(const std::vector<Key> *min_keys, const std::vector<uint32_t> *preds) {
         std::vector<cx_u128> mk;
         if (min_keys) mk = pack(*min_keys);
@@ -190,10 +201,14 @@ public:
         return r;
     }
 
-    // GetSuccessor(key) at peer src; throws "Lookup failed" if the walk livelocks.
+    // GetSuccessor(key) at peer src, throwing the reference's messages:
+    // "Lookup failed" (chord_peer.cpp:206, dhash_peer.cpp:524; also the walk
+    // livelocking past the hop cap), "ChordKey not found" (finger_table.h:129).
     Lookup GetSuccessor(uint32_t src, const Key &key) const {
         Lookup l = Route({src}, {key})[0];
-        if (l.status == CX_Q_HOPCAP) throw Error(CX_E_LOOKUP_FAILED, "Lookup failed");
+        if (l.status == CX_Q_HOPCAP || l.status == CX_Q_FAILED)
+            throw Error(CX_E_LOOKUP_FAILED, "Lookup failed");
+        if (l.status == CX_Q_NOT_FOUND) throw Error(CX_E_NOT_FOUND, "ChordKey not found");
         if (l.status == CX_Q_BADPEER) throw Error(CX_E_INVALID, "Peer is down.");
         return l;
     }

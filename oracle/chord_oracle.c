@@ -294,6 +294,56 @@ static uint32_t peer_pred(const or_peers *P, uint32_t p) {
     if (P->n == 1) return OR_NONE;
     return p == 0 ? (uint32_t)(P->n - 1) : p - 1;
 }
+/* RemotePeer::IsAlive (remote_peer.cpp:43-46): a TCP connect to the peer's
+ * server; an unset peer (OR_NONE, port 0) never answers. */
+static int peer_alive(const or_peers *P, uint32_t p) {
+    if (p == OR_NONE || p >= P->n) return 0;
+    return P->alive ? P->alive[p] != 0 : 1;
+}
+/* Entry j of peer p's successors_ list, OR_NONE past its end. */
+static uint32_t succ_entry(const or_peers *P, uint32_t p, int j) {
+    if (j >= P->ns) return OR_NONE;
+    if (P->succs) return P->succs[(size_t)p * P->ns + j];
+    if ((size_t)j >= P->n - 1) return OR_NONE; /* converged: n-1 other peers */
+    return (uint32_t)((p + 1 + (uint32_t)j) % P->n);
+}
+static int succ_list_size(const or_peers *P, uint32_t p) {
+    int k = 0;
+    while (k < P->ns && succ_entry(P, p, k) != OR_NONE) ++k;
+    return k;
+}
+/* RemotePeerList::Lookup(key, succ = true), remote_peer_list.cpp:86-110:
+ * first entry i with key in [previous, id_i] (InBetween inclusive, previous
+ * starting at the list's starting key = the owner's id), else none. */
+static uint32_t succ_list_lookup(const or_peers *P, uint32_t p, or_key key) {
+    or_u256 prev = u256_from128(k2u(P->ring[p]));
+    or_u256 v = u256_from128(k2u(key));
+    const int sz = succ_list_size(P, p);
+    for (int i = 0; i < sz; ++i) {
+        uint32_t e = succ_entry(P, p, i);
+        or_u256 id = u256_from128(k2u(P->ring[e]));
+        if (or_in_between(v, prev, id, 1)) return e;
+        prev = id;
+    }
+    return OR_NONE;
+}
+/* RemotePeerList::LookupLiving, remote_peer_list.cpp:112-132, as written: the
+ * found entry if alive; the scan for a later living entry runs
+ * `for (i = succ_ind; i % size < succ_ind; ++i)`, whose condition is false on
+ * entry (succ_ind < size), so it never executes. */
+static uint32_t succ_list_lookup_living(const or_peers *P, uint32_t p, or_key key) {
+    uint32_t s = succ_list_lookup(P, p, key);
+    if (s == OR_NONE) return OR_NONE;
+    if (peer_alive(P, s)) return s;
+    const int sz = succ_list_size(P, p);
+    int succ_ind = 0;
+    while (succ_ind < sz && succ_entry(P, p, succ_ind) != s) ++succ_ind; /* GetIndex */
+    for (int i = succ_ind; (size_t)i % (size_t)sz < (size_t)succ_ind; ++i) {
+        uint32_t e = succ_entry(P, p, i % sz);
+        if (peer_alive(P, e)) return e;
+    }
+    return OR_NONE;
+}
 /* StoredLocally, abstract_chord_peer.cpp:720-725. */
 static int stored_locally(const or_peers *P, uint32_t p, or_key key) {
     return or_in_between(u256_from128(k2u(key)), peer_min_key(P, p),
@@ -318,9 +368,38 @@ int or_route(const or_peers *P, uint32_t src, or_key key, uint32_t *owner, uint8
             return OR_Q_HOPCAP;
         }
         uint32_t nxt = P->F[(size_t)cur * OR_FINGERS + fi];
+        if (nxt == OR_NONE) { /* the matching finger was never added: Lookup
+                               * scans table_ and throws (finger_table.h:119-129) */
+            *owner = OR_NONE;
+            *hops = (uint8_t)h;
+            return OR_Q_NOT_FOUND;
+        }
         uint32_t pr = peer_pred(P, cur);
-        /* chord_peer.cpp:195-197: finger points at self and predecessor alive */
-        if (nxt == cur && pr != OR_NONE) nxt = pr;
+        /* chord_peer.cpp:195-197 / dhash_peer.cpp:508-510: finger points at
+         * self and the predecessor is alive */
+        if (nxt == cur && peer_alive(P, pr)) {
+            nxt = pr;
+        } else if (!peer_alive(P, nxt)) {
+            if (P->rule == OR_FWD_DHASH) {
+                /* dhash_peer.cpp:516-526: LookupLiving, else successors_[0]
+                 * if alive, else throw.  (An empty list makes the reference's
+                 * GetNthEntry(0) dereference end(); treated as the throw.) */
+                uint32_t s = succ_list_lookup_living(P, cur, key);
+                uint32_t s0 = succ_entry(P, cur, 0);
+                if (s != OR_NONE) nxt = s;
+                else if (peer_alive(P, s0)) nxt = s0;
+                else nxt = OR_NONE;
+            } else {
+                /* chord_peer.cpp:201-208: successors_.Lookup, used if alive */
+                uint32_t s = succ_list_lookup(P, cur, key);
+                nxt = (s != OR_NONE && peer_alive(P, s)) ? s : OR_NONE;
+            }
+            if (nxt == OR_NONE) { /* throw std::runtime_error("Lookup failed") */
+                *owner = OR_NONE;
+                *hops = (uint8_t)h;
+                return OR_Q_FAILED;
+            }
+        }
         /* chord_peer.cpp:210 SendRequest = one hop; the receiver's
          * GetSuccHandler (abstract_chord_peer.cpp:332-337) recurses. */
         if (h == OR_HOP_CAP) {

@@ -38,6 +38,11 @@ typedef struct { uint64_t lo, hi; } or_key;
 /* Per-query route status (mirrors cx_status in include/chordx.h). */
 #define OR_Q_OK 0
 #define OR_Q_HOPCAP 1
+#define OR_Q_NOT_FOUND 4 /* "ChordKey not found" (finger_table.h:129): no finger
+                          for the key's range (OR_NONE entry = never added) */
+#define OR_Q_FAILED 3 /* "Lookup failed" (chord_peer.cpp:206, dhash_peer.cpp:524) */
+#define OR_FWD_CHORD 0 /* ChordPeer::ForwardRequest, chord_peer.cpp:185-211 */
+#define OR_FWD_DHASH 1 /* DHashPeer::ForwardRequest, dhash_peer.cpp:500-529 */
 #define OR_HOP_CAP 255
 
 /* ---- a1: identifiers ------------------------------------------------- */
@@ -86,13 +91,25 @@ int or_finger_index(or_key id, or_key key);
 /* Per-peer state a ChordPeer carries into GetSuccessor/ForwardRequest.
  * min_keys == NULL -> converged min_key = ring[p-1]+1 (ring[p]+1 when n==1,
  *                     StartChord abstract_chord_peer.cpp:69)
- * preds    == NULL -> converged predecessor ring[p-1] (OR_NONE when n==1). */
+ * preds    == NULL -> converged predecessor ring[p-1] (OR_NONE when n==1).
+ * alive    == NULL -> every peer's server answers (RemotePeer::IsAlive,
+ *                     remote_peer.cpp:43-46); else alive[p] = 0/1.
+ * succs    == NULL -> converged successors_ list: the next min(ns, n-1) peers
+ *                     clockwise; else n*ns peer indices per list, OR_NONE-padded
+ *                     (RemotePeerList, starting key = the peer's id, ctor
+ *                     abstract_chord_peer.cpp:25).
+ * rule: OR_FWD_CHORD / OR_FWD_DHASH -- which ForwardRequest's dead-finger
+ *       branch applies. */
 typedef struct {
     const or_key *ring;
     size_t n;
     const uint32_t *F;        /* n*128 finger successors (peer indices) */
     const or_key *min_keys;   /* optional */
-    const uint32_t *preds;    /* optional; OR_NONE = no live predecessor */
+    const uint32_t *preds;    /* optional; OR_NONE = no predecessor set */
+    const uint8_t *alive;     /* optional */
+    const uint32_t *succs;    /* optional */
+    int ns;                   /* successor-list length (num_succs_) */
+    int rule;
 } or_peers;
 
 /* GetSuccessor (abstract_chord_peer.cpp:318-330) recursing through

@@ -140,7 +140,15 @@ class _Peers(ctypes.Structure):
         ("F", ctypes.c_void_p),
         ("min_keys", ctypes.c_void_p),
         ("preds", ctypes.c_void_p),
+        ("alive", ctypes.c_void_p),
+        ("succs", ctypes.c_void_p),
+        ("ns", ctypes.c_int),
+        ("rule", ctypes.c_int),
     ]
+
+
+Q_OK, Q_HOPCAP, Q_BADPEER, Q_FAILED, Q_NOT_FOUND = 0, 1, 2, 3, 4
+FWD_CHORD, FWD_DHASH = 0, 1
 
 
 _lib = None
@@ -243,16 +251,26 @@ def fingers(ring, threads=None, rows=None) -> np.ndarray:
 
 
 class Peers:
-    """Keeps the arrays alive for an or_peers struct."""
+    """Keeps the arrays alive for an or_peers struct.
 
-    def __init__(self, ring, F, min_keys=None, preds=None):
+    alive: per-peer 0/1 (None = every server answers); succs: (n, ns) successor
+    lists (None = the converged next-ns window); rule: FWD_CHORD / FWD_DHASH."""
+
+    def __init__(self, ring, F, min_keys=None, preds=None, alive=None, succs=None, ns=0,
+                 rule=FWD_CHORD):
         self.ring = _keys(ring)
         self.F = np.ascontiguousarray(F, dtype=np.uint32)
         self.min_keys = None if min_keys is None else _keys(min_keys)
         self.preds = None if preds is None else np.ascontiguousarray(preds, dtype=np.uint32)
+        self.alive = None if alive is None else np.ascontiguousarray(alive, dtype=np.uint8)
+        self.succs = None
+        if succs is not None:
+            self.succs = np.ascontiguousarray(succs, dtype=np.uint32).reshape(len(self.ring), -1)
+            ns = self.succs.shape[1]
+        ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
         self.s = _Peers(self.ring.ctypes.data, len(self.ring), self.F.ctypes.data,
-                        None if self.min_keys is None else self.min_keys.ctypes.data,
-                        None if self.preds is None else self.preds.ctypes.data)
+                        ptr(self.min_keys), ptr(self.preds), ptr(self.alive), ptr(self.succs),
+                        int(ns), int(rule))
 
 
 def route(peers: Peers, src, keys, threads=None):

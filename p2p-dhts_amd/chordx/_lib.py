@@ -30,7 +30,8 @@ CX_FINGERS = 128
 CX_NONE = 0xFFFFFFFF
 CX_HOP_CAP = 255
 CX_MAX_NSUCC = 16
-CX_Q_OK, CX_Q_HOPCAP, CX_Q_BADPEER = 0, 1, 2
+CX_Q_OK, CX_Q_HOPCAP, CX_Q_BADPEER, CX_Q_FAILED, CX_Q_NOT_FOUND = 0, 1, 2, 3, 4
+CX_FWD_CHORD, CX_FWD_DHASH = 0, 1
 
 # Every symbol include/chordx.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -38,7 +39,7 @@ EXPORTS = (
     "cx_ring_create", "cx_ring_destroy", "cx_ring_size", "cx_ring_ids",
     "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_use_own_stream", "cx_ring_sync",
     "cx_successor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
-    "cx_peer_state_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
+    "cx_peer_state_upload", "cx_liveness_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
     "cx_uuid5_dns", "cx_fill_splitmix",
     "cx_arc_build", "cx_arc_seed", "cx_arc_step", "cx_arc_bucket",
@@ -89,6 +90,7 @@ def lib() -> ctypes.CDLL:
         "cx_fingers_upload": ([vp, vp, i], i),
         "cx_fingers_device": ([vp, pp], i),
         "cx_peer_state_upload": ([vp, vp, vp, i], i),
+        "cx_liveness_upload": ([vp, vp, vp, i, i, i], i),
         "cx_route": ([vp, vp, vp, sz, vp, vp, vp, i], i),
         "cx_nsucc": ([vp, vp, sz, i, vp, vp, i], i),
         "cx_dhash_check": ([vp, i, i], i),

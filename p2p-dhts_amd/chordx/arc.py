@@ -5,7 +5,7 @@ When a ring's lookahead-tree table (n x R x 64 B: 32 GiB at 2^24 peers,
 (16 B per peer) but tree rows only for its own arc of peers,
 arc g of G = [g n / G, (g+1) n / G).  A lookup walks on the rank that owns the
 row it needs next -- the GET_SUCC request travelling to the peer it was
-forwarded to (ChordPeer::ForwardRequest, chord_peer.cpp:293-325) -- and comes
+forwarded to (ChordPeer::ForwardRequest, chord_peer.cpp:185-211) -- and comes
 home as a RESULT record when it ends.  Owners, hops and statuses equal the
 replicated-ring route's (tests/test_gpu_arc.py).
 

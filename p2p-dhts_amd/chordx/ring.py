@@ -44,6 +44,23 @@ def _keys_np(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1, 2))
 
 
+def _check_dev(t, esize: int, name: str, device=None, count=None):
+    """A device tensor handed to the library as a raw pointer must have the
+    element width the C ABI reads/writes, be contiguous, live on the ring's
+    GPU and hold `count` elements (first dimension); anything else would be an
+    out-of-bounds or misread GPU access, so it is rejected here."""
+    if not _is_dev(t):
+        return
+    if t.element_size() != esize or t.is_floating_point() or t.is_complex():
+        raise TypeError(f"{name}: expected a {8 * esize}-bit integer tensor, got {t.dtype}")
+    if not t.is_contiguous():
+        raise TypeError(f"{name}: tensor must be contiguous")
+    if device is not None and (t.device.index or 0) != device:
+        raise TypeError(f"{name}: tensor on cuda:{t.device.index}, ring on cuda:{device}")
+    if count is not None and (t.dim() == 0 or t.shape[0] != count):
+        raise TypeError(f"{name}: expected first dimension {count}, got {tuple(t.shape)}")
+
+
 def _ptr(a):
     if a is None:
         return None
@@ -111,17 +128,37 @@ class Ring:
             return torch.empty(shape, dtype=th_dtype, device=like.device)
         return np.empty(shape, dtype=np_dtype)
 
-    @staticmethod
-    def _prep_keys(keys):
+    def _prep_keys(self, keys, name="keys"):
         if _is_dev(keys):
-            return keys.contiguous().view(-1, 2)
+            if keys.element_size() != 8 or keys.is_floating_point() or keys.numel() % 2:
+                raise TypeError(f"{name}: 128-bit values are (q, 2) int64 device tensors, "
+                                f"got {keys.dtype} {tuple(keys.shape)}")
+            keys = keys.contiguous().view(-1, 2)
+            _check_dev(keys, 8, name, self.device)
+            return keys
         return _keys_np(keys)
 
-    @staticmethod
-    def _prep_u32(a):
+    def _prep_u32(self, a, name="indices", count=None):
         if _is_dev(a):
-            return a.contiguous()
-        return np.ascontiguousarray(a, dtype=np.uint32)
+            a = a.contiguous()
+            _check_dev(a, 4, name, self.device, count)
+            return a
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        if count is not None and a.shape[0] != count:
+            raise TypeError(f"{name}: expected first dimension {count}, got {a.shape}")
+        return a
+
+    def _check_out(self, arrays, q):
+        """Caller-supplied outputs: (array, element bytes, name) triples."""
+        for a, esize, name in arrays:
+            if a is None:
+                continue
+            if _is_dev(a):
+                _check_dev(a, esize, name, self.device, q)
+            elif (not isinstance(a, np.ndarray) or a.dtype.itemsize != esize
+                  or not a.flags.c_contiguous or a.shape[0] != q):
+                raise TypeError(f"{name}: expected a contiguous ({q}, ...) array of "
+                                f"{esize}-byte integers")
 
     def ids(self) -> np.ndarray:
         out = np.empty((self.n, 2), dtype=np.uint64)
@@ -142,6 +179,7 @@ class Ring:
         keys = self._prep_keys(keys)
         q = keys.shape[0]
         owner = out if out is not None else self._empty(keys, (q,), np.uint32, torch and torch.int32)
+        self._check_out([(owner, 4, "owner")], q)
         mk = self._mem(keys, owner)
         L.check(L.lib().cx_successor(self._h, _ptr(keys), q, _ptr(owner), mk))
         return owner
@@ -157,16 +195,38 @@ class Ring:
         return None
 
     def upload_fingers(self, F):
-        F = self._prep_u32(F)
+        F = self._prep_u32(F, "fingers", self.n)
         assert tuple(F.shape) == (self.n, L.CX_FINGERS)
         mk = self._mem(F)
         L.check(L.lib().cx_fingers_upload(self._h, _ptr(F), mk))
 
     def upload_peer_state(self, min_keys=None, preds=None):
-        mk_arr = None if min_keys is None else self._prep_keys(min_keys)
-        pr = None if preds is None else self._prep_u32(preds)
+        mk_arr = None if min_keys is None else self._prep_keys(min_keys, "min_keys")
+        pr = None if preds is None else self._prep_u32(preds, "preds", self.n)
+        if mk_arr is not None and mk_arr.shape[0] != self.n:
+            raise TypeError(f"min_keys: expected {self.n} values, got {mk_arr.shape[0]}")
         mk = self._mem(*(a for a in (mk_arr, pr) if a is not None)) if (mk_arr is not None or pr is not None) else L.CX_MEM_HOST
         L.check(L.lib().cx_peer_state_upload(self._h, _ptr(mk_arr), _ptr(pr), mk))
+
+    def upload_liveness(self, alive=None, succs=None, ns: int = 0, rule: int = 0):
+        """Peer liveness (n bytes, None = all alive) and successors_ lists
+        ((n, ns) indices in list order, CX_NONE-padded; None = the converged
+        next-ns window) for ForwardRequest's dead-finger branch; rule =
+        CX_FWD_CHORD (chord_peer.cpp:201-208) or CX_FWD_DHASH
+        (dhash_peer.cpp:516-526).  Switches route() to the literal walk."""
+        al = None
+        if alive is not None:
+            al = alive.contiguous() if _is_dev(alive) else np.ascontiguousarray(alive, np.uint8)
+            _check_dev(al, 1, "alive", self.device, self.n)
+            if al.shape[0] != self.n:
+                raise TypeError(f"alive: expected {self.n} entries")
+        sl = None
+        if succs is not None:
+            sl = self._prep_u32(succs, "succs", self.n)
+            ns = 1 if sl.ndim == 1 else int(sl.shape[1])
+        arrs = [a for a in (al, sl) if a is not None]
+        mk = self._mem(*arrs) if arrs else L.CX_MEM_HOST
+        L.check(L.lib().cx_liveness_upload(self._h, _ptr(al), _ptr(sl), int(ns), int(rule), mk))
 
     def fingers_device(self):
         p = ctypes.c_void_p()
@@ -192,6 +252,27 @@ class Ring:
         L.check(f(self._h, ctypes.byref(v), ctypes.byref(e), ctypes.byref(b)))
         return v.value, e.value, b.value
 
+    def route_counters(self, enable: bool):
+        """Internal: gather counters of the default route kernel.  enable=True
+        zeroes them and makes later route() calls run the counting build of
+        the walk; enable=False switches back and returns
+        (64-B table gathers, exact 16-B ring gathers, exact hops, lookups)."""
+        f = L.lib().cxi_route_counters
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        out = np.zeros(4, dtype=np.uint64)
+        L.check(f(self._h, int(bool(enable)), _ptr(out)))
+        return None if enable else tuple(int(x) for x in out)
+
+    def gather_probe(self, lanes: int = 1 << 19, hops: int = 64) -> float:
+        """Internal: dependent random 64-B gathers/s on this ring's own route
+        table (the walk's access pattern without the walk)."""
+        f = L.lib().cxi_gather_probe
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                      ctypes.POINTER(ctypes.c_double)]
+        r = ctypes.c_double()
+        L.check(f(self._h, lanes, hops, ctypes.byref(r)))
+        return r.value
+
     def set_churn_variant(self, v: int):
         """Internal A/B switch: 0 = full re-sort, 1 = merge of sorted joins (default)."""
         f = L.lib().cxi_set_churn_variant
@@ -208,14 +289,15 @@ class Ring:
     def route(self, src, keys, out=None):
         """GetSuccessor(key) issued at peer src: (owner, hops, status)."""
         keys = self._prep_keys(keys)
-        src = self._prep_u32(src)
         q = keys.shape[0]
+        src = self._prep_u32(src, "src", q)
         if out is None:
             owner = self._empty(keys, (q,), np.uint32, torch and torch.int32)
             hops = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
             status = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
         else:
             owner, hops, status = out
+        self._check_out([(owner, 4, "owner"), (hops, 1, "hops"), (status, 1, "status")], q)
         mk = self._mem(keys, src, owner, hops)
         L.check(L.lib().cx_route(self._h, _ptr(src), _ptr(keys), q, _ptr(owner), _ptr(hops),
                                  _ptr(status), mk))
@@ -246,7 +328,7 @@ class Ring:
 
     def misplaced(self, new_ring: "Ring", old_to_new, keys, n: int):
         keys = self._prep_keys(keys)
-        o2n = self._prep_u32(old_to_new)
+        o2n = self._prep_u32(old_to_new, "old_to_new", self.n)
         q = keys.shape[0]
         lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
         count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
@@ -259,7 +341,9 @@ class Ring:
 
     def misplaced_holders(self, keys, holders, n: int):
         keys = self._prep_keys(keys)
-        holders = self._prep_u32(holders)
+        holders = self._prep_u32(holders, "holders", keys.shape[0])
+        if holders.ndim != 2:
+            raise TypeError("holders: expected a (q, nh) array")
         q, nh = holders.shape
         lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
         count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
@@ -283,7 +367,7 @@ class Ring:
     def arc_seed(self, rank: int, src, keys):
         """(q, 4) int64 device tensor of NEW records (32 B each)."""
         keys = self._prep_keys(keys)
-        src = self._prep_u32(src)
+        src = self._prep_u32(src, "src", keys.shape[0])
         if not (_is_dev(keys) and _is_dev(src)):
             raise TypeError("arc routing takes device tensors")
         q = keys.shape[0]

@@ -58,12 +58,13 @@ struct DBuf {
 
 // IDA decode temporaries: a grow-only device arena per device and phase,
 // reused across calls (calls on a device serialise on its mutex; growth
-// hipFree-s the old block, which waits for the work still using it).  These
-// were stream-ordered pool allocations (hipMallocAsync / hipFreeAsync on the
-// null stream) and the decode kernel reading a reused pool block
-// intermittently hit "illegal memory access" (about 1 in 15 runs of
-// tests/cpp's DataBlock case, 0 in 90 with plain hipMalloc); per-call hipMalloc
-// / hipFree cost 0.5 ms per call on 2^22 tiny blocks, hence the arena.
+// hipFree-s the old block, which waits for the work still using it).  The
+// arena is a performance measure only (per-call hipMalloc / hipFree cost
+// 0.5 ms per call on 2^22 tiny blocks).  Pieces are packed tightly (8-B
+// alignment, no padding), so an out-of-bounds index lands in a neighbouring
+// piece instead of unmapped memory; the kernels bounds-check every index they
+// derive (run_of, run_start, the block cursor) and a guard region after the
+// inverse table is verified after each checked call ("IDA").
 struct IdaArena {
     std::mutex mu;
     void *p[2] = {nullptr, nullptr};
@@ -73,11 +74,12 @@ IdaArena &ida_arena(int device) {
     static IdaArena arenas[64];
     return arenas[device & 63];
 }
-// Carves 256-B aligned pieces of `sizes` bytes out of arena slot `slot`.
+// Carves tightly packed (8-B aligned) pieces of `sizes` bytes out of arena
+// slot `slot`.
 hipError_t arena_carve(IdaArena &a, int slot, std::initializer_list<size_t> sizes,
                        std::initializer_list<void **> outs) {
     size_t total = 0;
-    for (size_t b : sizes) total += (b + 255) & ~(size_t)255;
+    for (size_t b : sizes) total += (b + 7) & ~(size_t)7;
     if (total > a.cap[slot]) {
         if (a.p[slot]) (void)hipFree(a.p[slot]);
         a.p[slot] = nullptr;
@@ -90,7 +92,7 @@ hipError_t arena_carve(IdaArena &a, int slot, std::initializer_list<size_t> size
     auto o = outs.begin();
     for (size_t b : sizes) {
         **o++ = c;
-        c += (b + 255) & ~(size_t)255;
+        c += (b + 7) & ~(size_t)7;
     }
     return hipSuccess;
 }
@@ -123,7 +125,14 @@ struct cx_ring {
                                    // window table; -1: automatic (5 up to 2^24 peers, else 4)
     cell128 *d_min_keys = nullptr; // optional per-peer min_key_
     uint32_t *d_preds = nullptr;   // optional per-peer predecessor_
+    uint8_t *d_alive = nullptr;    // optional per-peer liveness (cx_liveness_upload)
+    uint32_t *d_succs = nullptr;   // optional successors_ lists [n][succ_ns]
+    int succ_ns = 0;
+    int fwd_rule = CX_FWD_CHORD;
+    bool liveness = false;         // cx_liveness_upload called: literal walk
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags), 1 KiB
+    unsigned long long *d_stats = nullptr;  // route gather counters (cxi_route_counters)
+    bool counting = false;
     uint64_t *d_arc_tree = nullptr;   // tree rows of the arc [arc_lo, arc_hi) (arc mode)
     uint32_t arc_lo = 0, arc_hi = 0;
 
@@ -147,7 +156,15 @@ struct cx_ring {
         v.ring = d_ring;
         return v;
     }
-    bool literal() const { return !fingers_converged || d_min_keys || d_preds; }
+    bool literal() const { return !fingers_converged || d_min_keys || d_preds || liveness; }
+    LitState lit() const {
+        LitState l;
+        l.alive = d_alive;
+        l.succs = d_succs;
+        l.ns = succ_ns;
+        l.rule = fwd_rule;
+        return l;
+    }
     int variant() const {
         if (route_variant >= 0) return route_variant;
         return (pk_ib <= 24 && !cz_failed) ? 5 : 4;
@@ -248,8 +265,11 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
+    (void)hipFree(r->d_alive);
+    (void)hipFree(r->d_succs);
     (void)hipFree(r->d_scratch);
     (void)hipFree(r->d_arc_tree);
+    (void)hipFree(r->d_stats);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
     delete r;
 }
@@ -573,27 +593,29 @@ int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
     CX_CHECK(ring && fingers, CX_E_INVALID, "null argument");
     int rc = use_device(ring);
     if (rc) return rc;
+    CX_CHECK(memkind == CX_MEM_HOST || memkind == CX_MEM_DEVICE, CX_E_INVALID, "bad memkind");
     hipStream_t s = ring->stream;
     const size_t cnt = ring->n * CX_FINGERS;
-    if (!ring->d_fingers) {
-        hipError_t e = hipMalloc(&ring->d_fingers, cnt * sizeof(uint32_t));
-        if (e != hipSuccess) {
-            ring->d_fingers = nullptr;
-            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
-        }
-    }
+    // validated in a staging buffer first: a rejected upload leaves the
+    // ring's current table (and route state) untouched
+    DBuf staged;
+    if (staged.alloc(cnt * sizeof(uint32_t)) != hipSuccess)
+        return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
     const hipMemcpyKind kind =
         memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    CX_HIP(hipMemcpyAsync(ring->d_fingers, fingers, cnt * sizeof(uint32_t), kind, s));
+    CX_HIP(hipMemcpyAsync(staged.p, fingers, cnt * sizeof(uint32_t), kind, s));
     CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
-    CX_HIP(cxk::check_indices(ring->d_fingers, cnt, (uint32_t)ring->n, false, ring->d_scratch,
-                              s));
+    CX_HIP(cxk::check_indices(staged.as<uint32_t>(), cnt, (uint32_t)ring->n, true,
+                              ring->d_scratch, s));
     uint32_t bad = 0;
     CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
+    CX_CHECK(!bad, CX_E_INVALID, "finger entry is neither a ring index nor CX_NONE");
+    (void)hipFree(ring->d_fingers);
+    ring->d_fingers = staged.as<uint32_t>();
+    staged.release();
     ring->fingers_converged = false;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
-    CX_CHECK(!bad, CX_E_INVALID, "finger entry is not a ring index");
     return CX_OK;
 }
 
@@ -608,29 +630,77 @@ int cx_peer_state_upload(cx_ring *ring, const cx_u128 *min_keys, const uint32_t 
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     int rc = use_device(ring);
     if (rc) return rc;
+    CX_CHECK(memkind == CX_MEM_HOST || memkind == CX_MEM_DEVICE, CX_E_INVALID, "bad memkind");
     hipStream_t s = ring->stream;
     const hipMemcpyKind kind =
         memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    (void)hipFree(ring->d_min_keys);
-    (void)hipFree(ring->d_preds);
-    ring->d_min_keys = nullptr;
-    ring->d_preds = nullptr;
+    // staged and validated first: a rejected upload leaves the current state
+    DBuf mk, pr;
     if (min_keys) {
-        CX_HIP(hipMalloc(&ring->d_min_keys, ring->n * sizeof(cell128)));
-        CX_HIP(hipMemcpyAsync(ring->d_min_keys, min_keys, ring->n * sizeof(cell128), kind, s));
+        CX_HIP(mk.alloc(ring->n * sizeof(cell128)));
+        CX_HIP(hipMemcpyAsync(mk.p, min_keys, ring->n * sizeof(cell128), kind, s));
     }
     if (preds) {
-        CX_HIP(hipMalloc(&ring->d_preds, ring->n * sizeof(uint32_t)));
-        CX_HIP(hipMemcpyAsync(ring->d_preds, preds, ring->n * sizeof(uint32_t), kind, s));
+        CX_HIP(pr.alloc(ring->n * sizeof(uint32_t)));
+        CX_HIP(hipMemcpyAsync(pr.p, preds, ring->n * sizeof(uint32_t), kind, s));
         CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
-        CX_HIP(cxk::check_indices(ring->d_preds, ring->n, (uint32_t)ring->n, true,
+        CX_HIP(cxk::check_indices(pr.as<uint32_t>(), ring->n, (uint32_t)ring->n, true,
                                   ring->d_scratch, s));
         uint32_t bad = 0;
         CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
         CX_HIP(hipStreamSynchronize(s));
         CX_CHECK(!bad, CX_E_INVALID, "predecessor is neither a ring index nor CX_NONE");
     }
-    return sync_if_host(memkind, s);
+    CX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(ring->d_min_keys);
+    (void)hipFree(ring->d_preds);
+    ring->d_min_keys = mk.as<cell128>();
+    ring->d_preds = pr.as<uint32_t>();
+    mk.release();
+    pr.release();
+    return CX_OK;
+}
+
+int cx_liveness_upload(cx_ring *ring, const uint8_t *alive, const uint32_t *succ_lists, int ns,
+                       int forward_rule, int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ns >= 0 && ns <= 64, CX_E_INVALID, "ns must be in [0, 64]");
+    CX_CHECK(forward_rule == CX_FWD_CHORD || forward_rule == CX_FWD_DHASH, CX_E_INVALID,
+             "forward_rule must be CX_FWD_CHORD or CX_FWD_DHASH");
+    CX_CHECK(memkind == CX_MEM_HOST || memkind == CX_MEM_DEVICE, CX_E_INVALID, "bad memkind");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    const hipMemcpyKind kind =
+        memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    DBuf al, sl;
+    if (alive) {
+        CX_HIP(al.alloc(ring->n));
+        CX_HIP(hipMemcpyAsync(al.p, alive, ring->n, kind, s));
+    }
+    if (succ_lists && ns > 0) {
+        const size_t cnt = ring->n * (size_t)ns;
+        CX_HIP(sl.alloc(cnt * sizeof(uint32_t)));
+        CX_HIP(hipMemcpyAsync(sl.p, succ_lists, cnt * sizeof(uint32_t), kind, s));
+        CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
+        CX_HIP(cxk::check_indices(sl.as<uint32_t>(), cnt, (uint32_t)ring->n, true,
+                                  ring->d_scratch, s));
+        uint32_t bad = 0;
+        CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        CX_CHECK(!bad, CX_E_INVALID, "successor entry is neither a ring index nor CX_NONE");
+    }
+    CX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(ring->d_alive);
+    (void)hipFree(ring->d_succs);
+    ring->d_alive = al.as<uint8_t>();
+    ring->d_succs = sl.as<uint32_t>();
+    al.release();
+    sl.release();
+    ring->succ_ns = ns;
+    ring->fwd_rule = forward_rule;
+    ring->liveness = true;
+    return CX_OK;
 }
 
 int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
@@ -659,7 +729,8 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     if (v == 5 && ring->cz_valid)
         CX_HIP(cxk::route_cz(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
                              ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
-                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
+                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst,
+                             ring->counting ? ring->d_stats : nullptr, s));
     else if (v == 4 && ring->tree_valid)
         CX_HIP(cxk::route_tree(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_tree, ring->rt_l0,
                                ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
@@ -678,7 +749,7 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
     else
         CX_HIP(cxk::route(ring->d_ring, ring->n, ring->d_fingers, ring->d_min_keys,
-                          ring->d_preds, ring->literal(), dsrc,
+                          ring->d_preds, ring->lit(), ring->literal(), dsrc,
                           reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(owner, dow, q * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -1113,13 +1184,14 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
     // runs of equal index lists share one inverse
     IdaArena &arena = ida_arena(device);
     std::lock_guard<std::mutex> lock(arena.mu);
-    uint32_t *flag, *flag2, *ws, *run_of, *run_start;
+    uint32_t *flag, *flag2, *ws, *run_of, *run_start, *guard, *err;
     int32_t *inv;
     uint8_t *okf;
     CX_HIP(arena_carve(arena, 0,
-                       {blocks * sizeof(uint32_t), blocks * sizeof(uint32_t),
+                       {sizeof(uint32_t), blocks * sizeof(uint32_t), blocks * sizeof(uint32_t),
                         cxk::scan_workspace_words(blocks) * sizeof(uint32_t)},
-                       {(void **)&flag, (void **)&flag2, (void **)&ws}));
+                       {(void **)&err, (void **)&flag, (void **)&flag2, (void **)&ws}));
+    CX_HIP(hipMemsetAsync(err, 0, sizeof(uint32_t), s));
     CX_HIP(cxk::ida_runs(didx, blocks, m, flag, s));
     CX_HIP(hipMemcpyAsync(flag2, flag, blocks * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     CX_HIP(cxk::exclusive_scan(flag2, blocks, ws, s));
@@ -1128,18 +1200,28 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
     CX_HIP(hipMemcpyAsync(&last[1], flag + blocks - 1, 4, hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
     const size_t runs = (size_t)last[0] + last[1];
+    CX_CHECK(runs >= 1 && runs <= blocks, CX_E_HIP, "IDA decode: invalid run count");
     CX_HIP(arena_carve(arena, 1,
                        {blocks * sizeof(uint32_t), runs * sizeof(uint32_t),
-                        runs * (size_t)m * m * sizeof(int32_t), runs},
-                       {(void **)&run_of, (void **)&run_start, (void **)&inv, (void **)&okf}));
-    CX_HIP(cxk::ida_run_index(flag2, flag, blocks, run_of, run_start, s));
-    CX_HIP(cxk::ida_inverse(didx, run_start, runs, m, p, inv, okf, s));
+                        runs * (size_t)m * m * sizeof(int32_t),
+                        IDA_GUARD_WORDS * sizeof(uint32_t), runs},
+                       {(void **)&run_of, (void **)&run_start, (void **)&inv, (void **)&guard,
+                        (void **)&okf}));
+    CX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(guard), IDA_GUARD_WORD,
+                             IDA_GUARD_WORDS, s));
+    CX_HIP(cxk::ida_run_index(flag2, flag, blocks, runs, run_of, run_start, err, s));
+    CX_HIP(cxk::ida_inverse(didx, run_start, runs, blocks, m, p, inv, okf, err, s));
     CX_HIP(hipMemsetAsync(dlen, 0, blocks * sizeof(uint64_t), s));
-    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, m, p, inv, run_of, okf, dout, dlen, s));
-    CX_HIP(cxk::ida_mark_failed(run_of, okf, blocks, dlen, s));
+    CX_HIP(cxk::ida_decode(dfr, dseg, blocks, m, p, inv, run_of, runs, okf, dout, dlen, err, s));
+    CX_HIP(cxk::ida_mark_failed(run_of, okf, blocks, runs, dlen, err, s));
+    CX_HIP(cxk::ida_check_guard(guard, IDA_GUARD_WORDS, err, s));
     if (memkind == CX_MEM_HOST) {
         if ((rc = finish_out(out_len, dlen, blocks, memkind, s))) return rc;
         if ((rc = finish_out(out, dout, (size_t)(segs * m), memkind, s))) return rc;
+        uint32_t e = 0;
+        CX_HIP(hipMemcpy(&e, err, sizeof(e), hipMemcpyDeviceToHost));
+        CX_CHECK(e == 0, CX_E_HIP,
+                 "IDA decode: index bounds check failed (flags " + std::to_string(e) + ")");
     }
     return CX_OK;
 }
@@ -1268,6 +1350,52 @@ int cxi_route_info(const cx_ring *ring, int *variant, uint64_t *cz_escapes,
                    : (v == 2 || v == 3) && ring->pk_valid ? ent * 16
                    : v == 1 && ring->rt_valid ? ent * sizeof(RtEntry)
                                               : 0;
+    return CX_OK;
+}
+
+// Gather counters of the default route kernel (bench.py's byte model):
+// enable = 1 zeroes them and makes later cx_route calls run the counting
+// instantiation of the walk; enable = 0 switches back and copies the totals to
+// out[4] = {64-B table gathers, exact 16-B ring gathers, exact hops (F + ring
+// gather each), lookups}.
+int cxi_route_counters(cx_ring *ring, int enable, uint64_t *out) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    if (!ring->d_stats) CX_HIP(hipMalloc(&ring->d_stats, 4 * sizeof(unsigned long long)));
+    if (enable) {
+        CX_HIP(hipMemsetAsync(ring->d_stats, 0, 4 * sizeof(unsigned long long), s));
+        ring->counting = true;
+        return CX_OK;
+    }
+    ring->counting = false;
+    CX_CHECK(out != nullptr, CX_E_INVALID, "null out");
+    unsigned long long h[4];
+    CX_HIP(hipMemcpyAsync(h, ring->d_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < 4; ++k) out[k] = h[k];
+    return CX_OK;
+}
+
+// Request-rate ceiling measured on this ring's own route table (the
+// pattern-keyed window table, else the finger table): dependent random 64-B
+// gathers by quads of lanes, entries/s.  Read only.
+int cxi_gather_probe(const cx_ring *ring, int lanes, int hops, double *rate) {
+    CX_CHECK(ring && rate, CX_E_INVALID, "null argument");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    const void *t = nullptr;
+    size_t bytes = 0;
+    if (ring->cz_valid) {
+        t = ring->d_cz;
+        bytes = ring->n * (size_t)ring->rt_R * 128;
+    } else if (ring->d_fingers) {
+        t = ring->d_fingers;
+        bytes = ring->n * (size_t)CX_FINGERS * sizeof(uint32_t);
+    }
+    CX_CHECK(t != nullptr, CX_E_STATE, "no route table built");
+    CX_HIP(cxk::gather_probe(t, bytes, lanes, hops, rate, ring->stream));
     return CX_OK;
 }
 

@@ -497,19 +497,60 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route_conv(const cell128 *ring,
     }
 }
 
-// Literal walk for hand-edited tables / peer state: StoredLocally with the
-// peer's own min_key_ (InBetween(min_key, id, true), key.h:103-131 on
-// canonical operands), first-match finger, self -> predecessor substitution.
+// ChordKey::InBetween(lb, ub, true) (key.h:103-131) on canonical operands.
 __device__ __forceinline__ bool in_between128(u128 v, u128 lb, u128 ub) {
     if (lb == ub) return v == ub;
     if (lb < ub) return lb <= v && v <= ub;
     return !(ub < v && v < lb);
 }
 
+// Liveness and successors_ lists of the peers (LitState): the dead-finger
+// branch of ForwardRequest.  alive == nullptr: every server answers; succs ==
+// nullptr: converged lists (the next min(ns, n-1) peers clockwise).
+__device__ __forceinline__ bool lit_alive(const LitState &ls, uint32_t n, uint32_t p) {
+    if (p >= n) return false;  // also CX_NONE: an unset RemotePeer never answers
+    return ls.alive ? ls.alive[p] != 0 : true;
+}
+__device__ __forceinline__ uint32_t lit_succ(const LitState &ls, uint32_t n, uint32_t p, int j) {
+    if (j >= ls.ns) return CX_NONE;
+    if (ls.succs) return ls.succs[(size_t)p * ls.ns + j];
+    if ((uint32_t)j >= n - 1) return CX_NONE;
+    uint32_t e = p + 1 + (uint32_t)j;
+    return e >= n ? e - n : e;
+}
+// RemotePeerList::Lookup(key, succ = true) (remote_peer_list.cpp:86-110): the
+// first entry whose (previous, id] -- InBetween inclusive, previous starting at
+// the list owner's id -- holds the key.  Also returns the list index.
+__device__ __forceinline__ uint32_t lit_list_lookup(const LitState &ls, const cell128 *ring,
+                                                    uint32_t n, uint32_t p, u128 key, int &at) {
+    u128 prev = ld128(ring + p);
+    for (int j = 0; j < ls.ns; ++j) {
+        const uint32_t e = lit_succ(ls, n, p, j);
+        if (e == CX_NONE) break;
+        const u128 id = ld128(ring + e);
+        if (in_between128(key, prev, id)) {
+            at = j;
+            return e;
+        }
+        prev = id;
+    }
+    at = -1;
+    return CX_NONE;
+}
+
+// Literal walk for hand-edited tables / peer state: StoredLocally with the
+// peer's own min_key_ (InBetween(min_key, id, true), key.h:103-131 on
+// canonical operands), first-match finger (CX_NONE = no finger added for that
+// range: "ChordKey not found", finger_table.h:129), self -> live predecessor
+// substitution, and the dead-finger fallback of ChordPeer::ForwardRequest
+// (chord_peer.cpp:201-208: successors_.Lookup if alive, else "Lookup failed")
+// or DHashPeer::ForwardRequest (dhash_peer.cpp:516-526: LookupLiving -- whose
+// scan for a later living entry never runs, remote_peer_list.cpp:123 -- else
+// successors_[0] if alive, else "Lookup failed").
 __global__ __launch_bounds__(ROUTE_BLOCK) void k_route_literal(
     const cell128 *ring, uint32_t n, const uint32_t *F, const cell128 *min_keys,
-    const uint32_t *preds, const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
-    uint8_t *hops, uint8_t *status) {
+    const uint32_t *preds, LitState ls, const uint32_t *src, const cell128 *keys, size_t q,
+    uint32_t *owner, uint8_t *hops, uint8_t *status) {
     for (size_t qi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; qi < q;
          qi += (size_t)gridDim.x * blockDim.x) {
         const u128 key = ld128(keys + qi);
@@ -531,8 +572,29 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route_literal(
             }
             const int i = msb128(key - id);  // key != id here (id is always local)
             uint32_t nxt = F[(size_t)cur * CX_FINGERS + i];
+            if (nxt == CX_NONE) {  // the range's finger was never added
+                st = CX_Q_NOT_FOUND;
+                own = CX_NONE;
+                break;
+            }
             const uint32_t pr = preds ? preds[cur] : pdef;
-            if (nxt == cur && pr != CX_NONE) nxt = pr;
+            if (nxt == cur && lit_alive(ls, n, pr)) {
+                nxt = pr;
+            } else if (!lit_alive(ls, n, nxt)) {
+                int at;
+                const uint32_t sl = lit_list_lookup(ls, ring, n, cur, key, at);
+                if (ls.rule == CX_FWD_DHASH) {
+                    const uint32_t s0 = lit_succ(ls, n, cur, 0);
+                    nxt = lit_alive(ls, n, sl) ? sl : (lit_alive(ls, n, s0) ? s0 : CX_NONE);
+                } else {
+                    nxt = lit_alive(ls, n, sl) ? sl : CX_NONE;
+                }
+                if (nxt == CX_NONE) {
+                    st = CX_Q_FAILED;
+                    own = CX_NONE;
+                    break;
+                }
+            }
             if (h == CX_HOP_CAP) {
                 st = CX_Q_HOPCAP;
                 own = CX_NONE;
@@ -1592,7 +1654,8 @@ __device__ __forceinline__ void cz_exact_d(const PkCtx &c, u128 key, u128 idc, u
 // 1 = finished (own/st set), 0 = moved (cur, clo exact, dmin/dmax).
 __device__ __forceinline__ int cz_exact(const PkCtx &c, u128 key, u128 &clo, uint64_t &dmin,
                                         uint64_t &dmax, uint32_t &cur, uint32_t &h, int i,
-                                        uint32_t &own, uint8_t &st) {
+                                        uint32_t &own, uint8_t &st, uint32_t *xc = nullptr) {
+    if (xc) ++*xc;  // counter build only: one F gather + one ring gather
     const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
     const u128 idn = ld128(c.ring + nxt);
     ++h;
@@ -1645,7 +1708,7 @@ __device__ __forceinline__ int cz_plan(const PkCtx &c, u128 key, u128 &clo, bool
                                        uint64_t &dmin, uint64_t &dmax, uint32_t &cur,
                                        uint32_t &h, uint32_t &pn, int &mode, int &lvl, int &rb,
                                        int &cs, int ri, const uint32_t *ent, uint32_t &own,
-                                       uint8_t &st) {
+                                       uint8_t &st, uint32_t *xc = nullptr) {
     for (;;) {
         int i;
         const int ma = 63 - __builtin_clzll(dmin | 1), mb = 63 - __builtin_clzll(dmax | 1);
@@ -1688,7 +1751,7 @@ __device__ __forceinline__ int cz_plan(const PkCtx &c, u128 key, u128 &clo, bool
             mode = A_FIXC;
             return 0;
         }
-        if (cz_exact(c, key, clo, dmin, dmax, cur, h, i, own, st)) return 1;
+        if (cz_exact(c, key, clo, dmin, dmax, cur, h, i, own, st, xc)) return 1;
     }
 }
 
@@ -1711,9 +1774,15 @@ struct TreeIO {
     uint32_t *owner;
     uint8_t *hops;
     uint8_t *status;
+    // STATS build only: [0] 64-B table gathers, [1] exact 16-B ring gathers,
+    // [2] exact hops (one F + one ring gather each), [3] lookups started
+    unsigned long long *stats;
 };
 
-template <bool ARC, bool CZ>
+// STATS: the same walk, additionally counting the random gathers it issues
+// (bench.py's algorithmic-bytes model and request-rate roofline); the timed
+// kernel is the STATS = false instantiation.
+template <bool ARC, bool CZ, bool STATS = false>
 __global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(CZ ? CZ_WAVES : 1)))
 void k_route_tree(TreeIO io) {
     constexpr int RW = CZ ? CZ_RES_WIN : RES_WIN;  // cz: smaller window, more waves per CU
@@ -1763,6 +1832,8 @@ void k_route_tree(TreeIO io) {
     uint64_t pqid = 0;
     u128 pkey = 0, pa = 0, pb = 0;
     uint32_t psrc = 0, ph = 0;
+    uint32_t n_g64 = 0, n_r16 = 0, n_xc = 0, n_q = 0;  // STATS counters
+    uint32_t *xcp = STATS ? &n_xc : nullptr;
 
     // outcome of a finished query (ARC: local delivery or a result record)
     auto deliver = [&](size_t idx, uint64_t id, uint32_t o, uint32_t hh, uint8_t stt) {
@@ -1834,6 +1905,10 @@ void k_route_tree(TreeIO io) {
                 CZ ? (uint64_t)((lvl - l0) * 2 + rb) * n + cur
                    : (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0);
             addr_all[threadIdx.x] = mode == A_HOP ? e + 1 : 0;
+            if (STATS) {
+                n_g64 += mode == A_HOP;
+                n_r16 += mode == A_FIXC ? 1u : (mode == A_FIXT ? 2u : 0u);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1891,8 +1966,9 @@ void k_route_tree(TreeIO io) {
                 if (!cex) {  // rare: exact id of cur for the exact hop
                     clo = ld128(io.ring + cur);
                     cex = true;
+                    if (STATS) ++n_r16;
                 }
-                if (cz_exact(c, key, clo, dmin, dmax, cur, h, lvl, own, st))
+                if (cz_exact(c, key, clo, dmin, dmax, cur, h, lvl, own, st, xcp))
                     fin = true;
                 else
                     plan = true;
@@ -1943,7 +2019,7 @@ void k_route_tree(TreeIO io) {
         if (plan) {
             const int r =
                 CZ ? cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs, ri, ent32,
-                             own, st)
+                             own, st, xcp)
                    : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
             if (r == 1) fin = true;
             if (ARC && r == 2) {  // continue on the rank that owns cur's row
@@ -1972,6 +2048,7 @@ void k_route_tree(TreeIO io) {
             cs = -1;
             own = CX_NONE;
             st = CX_Q_OK;
+            if (STATS) ++n_q;
             int done = 1;
             if (ARC && pkind == ARC_RESULT) {
                 // a result coming home: deliver it (w0 = owner | status << 32)
@@ -1992,7 +2069,7 @@ void k_route_tree(TreeIO io) {
                 cex = true;
                 if (CZ) cz_exact_d(c, key, pb, dmin, dmax);
                 done = CZ ? cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs,
-                                    ri, ent32, own, st)
+                                    ri, ent32, own, st, xcp)
                           : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own,
                                       st);
                 if (ARC && done == 2) {
@@ -2030,6 +2107,17 @@ void k_route_tree(TreeIO io) {
                 flushed += 64;
             }
         }
+    }
+    if (STATS) {
+        uint64_t v[4] = {n_g64, n_r16, n_xc, n_q};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) atomicAdd(io.stats + k, (unsigned long long)v[k]);
     }
 }
 
@@ -2077,12 +2165,13 @@ static unsigned resident_grid(K kernel, int block);
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                    uint8_t *status, hipStream_t s) {
+                    uint8_t *status, unsigned long long *stats, hipStream_t s) {
     if (q == 0) return hipSuccess;
     TreeIO io = {};
     io.ring_ext = ring_ext;
     io.ring = ring;
     io.n = (uint32_t)n;
+    io.stats = stats;
     io.tree = reinterpret_cast<const uint4 *>(cz);
     io.l0 = l0;
     io.R = R;
@@ -2104,7 +2193,10 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
     io.chunk = (q + waves - 1) / waves;
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    k_route_tree<false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
+    if (stats)
+        k_route_tree<false, true, true><<<blocks, RT_BLOCK, 0, s>>>(io);
+    else
+        k_route_tree<false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 
@@ -2276,12 +2368,13 @@ hipError_t arc_bucket(const ArcRec *recs, size_t q, size_t n, int G, uint32_t *c
 }
 
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
-                 const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
-                 size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
+                 const uint32_t *preds, const LitState &ls, bool literal, const uint32_t *src,
+                 const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status,
+                 hipStream_t s) {
     if (q == 0) return hipSuccess;
     const unsigned g = cx_grid(q, ROUTE_BLOCK, 1u << 20);
     if (literal)
-        k_route_literal<<<g, ROUTE_BLOCK, 0, s>>>(ring, (uint32_t)n, F, min_keys, preds, src,
+        k_route_literal<<<g, ROUTE_BLOCK, 0, s>>>(ring, (uint32_t)n, F, min_keys, preds, ls, src,
                                                   keys, q, owner, hops, status);
     else
         k_route_conv<<<g, ROUTE_BLOCK, 0, s>>>(ring, (uint32_t)n, F, src, keys, q, owner, hops,
@@ -2872,6 +2965,17 @@ hipError_t hex_format(const cell128 *keys, size_t count, char *out, uint8_t *len
 // ---------------------------------------------------------------------------
 constexpr int IDA_MAX_N = 32;
 
+// Bounds checks of the decode path's index arithmetic (run_of, run_start,
+// the block cursor, fragment offsets): a violation skips the access and sets
+// a bit in the call's error word, which cx_ida_decode reports.
+enum : uint32_t {
+    IDA_ERR_RUN_OF = 1u,      // run_of[b] >= runs
+    IDA_ERR_RUN_START = 2u,   // run_start[r] >= blocks
+    IDA_ERR_CURSOR = 4u,      // block cursor past the last block / segment outside it
+    IDA_ERR_RUN_INDEX = 8u,   // k_ida_run_index produced r >= runs
+    IDA_ERR_GUARD = 16u       // the guard words after the inverses were overwritten
+};
+
 // Block owning global segment g: largest b with seg[b] <= g.
 __device__ __forceinline__ size_t seg_block(const uint64_t *seg, size_t blocks, uint64_t g) {
     size_t lo = 0, hi = blocks;  // seg[lo] <= g < seg[hi]
@@ -3122,10 +3226,16 @@ __global__ __launch_bounds__(256) void k_ida_encode(const uint8_t *data, const u
 // success, 0 when a denominator has no inverse ("N is not invertible").
 __device__ __forceinline__ int32_t cmod(int32_t x, int32_t p) { return (x % p + p) % p; }
 
-__global__ void k_ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, int m,
-                              int32_t p, int32_t *inv, uint8_t *okf) {
+__global__ void k_ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs,
+                              size_t blocks, int m, int32_t p, int32_t *inv, uint8_t *okf,
+                              uint32_t *err) {
     for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < runs;
          r += (size_t)gridDim.x * blockDim.x) {
+        if (run_start[r] >= blocks) {  // bounds check (never taken on valid runs)
+            atomicOr(err, IDA_ERR_RUN_START);
+            okf[r] = 0;
+            continue;
+        }
         const uint8_t *b = idx + (size_t)run_start[r] * m;
         // elementary symmetric sums e_0..e_m of the basis, int32 wrap (uint32 ops)
         uint32_t e[IDA_MAX_N + 1];
@@ -3192,8 +3302,9 @@ template <bool WIDE, int FM, int D, int MF>
 __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const uint64_t *seg,
                                                     size_t blocks, int m, uint32_t p,
                                                     float inv_p, const int32_t *inv,
-                                                    const uint32_t *run_of, const uint8_t *okf,
-                                                    uint16_t *out, unsigned long long *out_len) {
+                                                    const uint32_t *run_of, size_t runs,
+                                                    const uint8_t *okf, uint16_t *out,
+                                                    unsigned long long *out_len, uint32_t *err) {
     __shared__ __attribute__((aligned(16))) uint32_t Ainv[256 / 64][IDA_MAX_N * IDA_AROW];
     const int lane = threadIdx.x & 63;
     uint32_t *As = Ainv[threadIdx.x >> 6];
@@ -3214,11 +3325,19 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
         const uint64_t g = c * 64 + lane;
         x.live = g < total;
         const uint64_t gl = x.live ? g : total - 1;
-        while (bl1 <= gl) bl1 = seg[++bl + 1];
+        while (bl1 <= gl && bl + 1 < blocks) bl1 = seg[++bl + 1];
         x.b = bl;
-        x.r = run_of[bl];
-        x.ok = x.live && okf[x.r];
         const uint64_t sb = seg[bl];
+        bool inb = sb <= gl && gl < bl1;  // the segment lies in the cursor's block
+        x.r = run_of[bl];
+        if (x.r >= runs) {
+            inb = false;
+            x.r = 0;
+            atomicOr(err, IDA_ERR_RUN_OF);
+        } else if (!inb) {
+            atomicOr(err, IDA_ERR_CURSOR);
+        }
+        x.ok = x.live && inb && okf[x.r];
         x.s = gl - sb;
         const uint64_t S = bl1 - sb;
         const uint16_t *fr = frags + (uint64_t)m * sb + x.s;
@@ -3242,7 +3361,7 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
 #pragma unroll
             for (int q = 0; q < FM; ++q) f[q] = sl[k].f[q];
             if (c + D < c1) issue(sl[k], c + D);  // loads overlap this chunk's math
-            const uint32_t r0 = __shfl(r, 0);
+            const uint32_t r0 = __shfl(r, 0);  // r < runs (checked at issue)
             const bool uniform = __ballot(r != r0) == 0;
             if (uniform && r0 != staged) {  // stage the shared inverse (wave-uniform branch)
                 __builtin_amdgcn_wave_barrier();  // previous readers of As are done
@@ -3338,26 +3457,50 @@ __global__ void k_ida_runs(const uint8_t *idx, size_t blocks, int m, uint32_t *f
 
 // run_of[b] = run index (inclusive scan - 1), run_start[run] = first block.
 __global__ void k_ida_run_index(const uint32_t *flag_excl, const uint32_t *flag_raw, size_t blocks,
-                                uint32_t *run_of, uint32_t *run_start) {
+                                size_t runs, uint32_t *run_of, uint32_t *run_start,
+                                uint32_t *err) {
     for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < blocks;
          b += (size_t)gridDim.x * blockDim.x) {
         const uint32_t r = flag_excl[b] + flag_raw[b] - 1;
+        if (r >= runs) {
+            atomicOr(err, IDA_ERR_RUN_INDEX);
+            run_of[b] = 0;
+            continue;
+        }
         run_of[b] = r;
         if (flag_raw[b]) run_start[r] = (uint32_t)b;
     }
 }
 
+// Guard words after the inverse table: any overwrite is reported.
+__global__ void k_ida_check_guard(const uint32_t *guard, int words, uint32_t *err) {
+    for (int i = threadIdx.x; i < words; i += blockDim.x)
+        if (guard[i] != IDA_GUARD_WORD) atomicOr(err, IDA_ERR_GUARD);
+}
+
 __global__ void k_ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks,
-                                  uint64_t *out_len) {
+                                  size_t runs, uint64_t *out_len, uint32_t *err) {
     for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < blocks;
-         b += (size_t)gridDim.x * blockDim.x)
-        if (!okf[run_of[b]]) out_len[b] = ~0ull;
+         b += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t r = run_of[b];
+        if (r >= runs) {
+            atomicOr(err, IDA_ERR_RUN_OF);
+            continue;
+        }
+        if (!okf[r]) out_len[b] = ~0ull;
+    }
 }
 
 hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks,
-                           uint64_t *out_len, hipStream_t s) {
+                           size_t runs, uint64_t *out_len, uint32_t *err, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
-    k_ida_mark_failed<<<cx_grid(blocks, 256), 256, 0, s>>>(run_of, okf, blocks, out_len);
+    k_ida_mark_failed<<<cx_grid(blocks, 256), 256, 0, s>>>(run_of, okf, blocks, runs, out_len,
+                                                          err);
+    return hipGetLastError();
+}
+
+hipError_t ida_check_guard(const uint32_t *guard, int words, uint32_t *err, hipStream_t s) {
+    k_ida_check_guard<<<1, 256, 0, s>>>(guard, words, err);
     return hipGetLastError();
 }
 
@@ -3573,29 +3716,31 @@ hipError_t ida_runs(const uint8_t *idx, size_t blocks, int m, uint32_t *flag, hi
 }
 
 hipError_t ida_run_index(const uint32_t *flag_excl, const uint32_t *flag_raw, size_t blocks,
-                         uint32_t *run_of, uint32_t *run_start, hipStream_t s) {
+                         size_t runs, uint32_t *run_of, uint32_t *run_start, uint32_t *err,
+                         hipStream_t s) {
     if (blocks == 0) return hipSuccess;
-    k_ida_run_index<<<cx_grid(blocks, 256), 256, 0, s>>>(flag_excl, flag_raw, blocks, run_of,
-                                                        run_start);
+    k_ida_run_index<<<cx_grid(blocks, 256), 256, 0, s>>>(flag_excl, flag_raw, blocks, runs, run_of,
+                                                        run_start, err);
     return hipGetLastError();
 }
 
-hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, int m, int p,
-                       int32_t *inv, uint8_t *okf, hipStream_t s) {
+hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, size_t blocks,
+                       int m, int p, int32_t *inv, uint8_t *okf, uint32_t *err, hipStream_t s) {
     if (runs == 0) return hipSuccess;
-    k_ida_inverse<<<cx_grid(runs, 64), 64, 0, s>>>(idx, run_start, runs, m, p, inv, okf);
+    k_ida_inverse<<<cx_grid(runs, 64), 64, 0, s>>>(idx, run_start, runs, blocks, m, p, inv, okf,
+                                                   err);
     return hipGetLastError();
 }
 
 template <bool WIDE, int FM, int D, int MF = 0>
 static void ida_decode_launch(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m,
-                              int p, const int32_t *inv, const uint32_t *run_of,
+                              int p, const int32_t *inv, const uint32_t *run_of, size_t runs,
                               const uint8_t *okf, uint16_t *out, uint64_t *out_len,
-                              hipStream_t s) {
+                              uint32_t *err, hipStream_t s) {
     static const unsigned grid = resident_grid(k_ida_decode<WIDE, FM, D, MF>, 256);
     k_ida_decode<WIDE, FM, D, MF><<<grid, 256, 0, s>>>(
-        frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv, run_of, okf, out,
-        reinterpret_cast<unsigned long long *>(out_len));
+        frags, seg, blocks, m, (uint32_t)p, 1.0f / p, inv, run_of, runs, okf, out,
+        reinterpret_cast<unsigned long long *>(out_len), err);
 }
 
 // A/B knob for the pipeline depths (chunks in flight per wave): CX_IDA_ENC_D,
@@ -3607,31 +3752,31 @@ static int ida_depth(const char *var, int dflt) {
 }
 
 hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m, int p,
-                      const int32_t *inv, const uint32_t *run_of, const uint8_t *okf,
-                      uint16_t *out, uint64_t *out_len, hipStream_t s) {
+                      const int32_t *inv, const uint32_t *run_of, size_t runs, const uint8_t *okf,
+                      uint16_t *out, uint64_t *out_len, uint32_t *err, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
     const bool wide = (uint64_t)m * (p - 1) * 65535ull >= (1ull << 32);
     static const int D = ida_depth("CX_IDA_DEC_D", 2);
     if (wide)
-        ida_decode_launch<true, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out,
-                                              out_len, s);
+        ida_decode_launch<true, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
+                                              out_len, err, s);
     else if (m == 10 && !getenv("CX_IDA_GENERIC") && D == 1)  // DHash (14, 10)
-        ida_decode_launch<false, 12, 1, 10>(frags, seg, blocks, m, p, inv, run_of, okf, out,
-                                            out_len, s);
+        ida_decode_launch<false, 12, 1, 10>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
+                                            out_len, err, s);
     else if (m == 10 && !getenv("CX_IDA_GENERIC"))
-        ida_decode_launch<false, 12, 2, 10>(frags, seg, blocks, m, p, inv, run_of, okf, out,
-                                            out_len, s);
+        ida_decode_launch<false, 12, 2, 10>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
+                                            out_len, err, s);
     else if (m > 12)
-        ida_decode_launch<false, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out,
-                                               out_len, s);
+        ida_decode_launch<false, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
+                                               out_len, err, s);
     else if (D == 1)
-        ida_decode_launch<false, 12, 1>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
+        ida_decode_launch<false, 12, 1>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
     else if (D == 2)
-        ida_decode_launch<false, 12, 2>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
+        ida_decode_launch<false, 12, 2>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
     else if (D == 3)
-        ida_decode_launch<false, 12, 3>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
+        ida_decode_launch<false, 12, 3>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
     else
-        ida_decode_launch<false, 12, 4>(frags, seg, blocks, m, p, inv, run_of, okf, out, out_len, s);
+        ida_decode_launch<false, 12, 4>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
     return hipGetLastError();
 }
 
@@ -3652,6 +3797,63 @@ hipError_t check_indices(const uint32_t *idx, size_t count, uint32_t limit, bool
     k_check_indices<<<cx_grid(count, 256), 256, 0, s>>>(idx, count, limit, allow_none ? 1 : 0,
                                                         d_bad);
     return hipGetLastError();
+}
+
+// ===========================================================================
+// Request-rate probe: the walk's memory access pattern without the walk.
+// Four lanes cooperate on one chain: each loads 16 B of a 64-B entry (one
+// wave instruction, adjacent addresses), lane 0's data picks the next entry,
+// so every step is one dependent random 64-B request.  Read only.
+// ===========================================================================
+__device__ __forceinline__ uint64_t probe_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_gather_probe(const uint4 *t, uint64_t slots, int hops,
+                                                      unsigned long long *sink) {
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const int sub = threadIdx.x & 3;
+    uint64_t x = probe_mix(tid / 4 + 777);
+    for (int h = 0; h < hops; ++h) {
+        const uint64_t slot = x % slots;
+        const uint4 a = t[slot * 4 + sub];
+        uint64_t v = ((uint64_t)a.y << 32 | a.x) ^ a.z;
+        v = __shfl(v, (threadIdx.x & 63) & ~3, 64);
+        x = probe_mix(v + x);
+    }
+    if (x == 0x1234567ull) atomicAdd(sink, 1ull);  // keeps the chain live
+}
+
+hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, double *rate,
+                        hipStream_t s) {
+    const uint64_t slots = bytes / 64;
+    if (slots == 0 || lanes < 256 || hops < 1) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)(lanes / 256);
+    const uint4 *t = static_cast<const uint4 *>(table);
+    unsigned long long *sink = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
+    hipError_t e = hipMalloc(&sink, sizeof(*sink));
+    if (e == hipSuccess) e = hipEventCreate(&a);
+    if (e == hipSuccess) e = hipEventCreate(&b);
+    if (e == hipSuccess) {
+        k_gather_probe<<<blocks, 256, 0, s>>>(t, slots, 4, sink);  // warm-up
+        e = hipEventRecord(a, s);
+    }
+    if (e == hipSuccess) {
+        k_gather_probe<<<blocks, 256, 0, s>>>(t, slots, hops, sink);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipEventRecord(b, s);
+    if (e == hipSuccess) e = hipEventSynchronize(b);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+    if (e == hipSuccess) *rate = (double)(lanes / 4) * hops / (ms * 1e-3);
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    if (sink) (void)hipFree(sink);
+    return e;
 }
 
 }  // namespace cxk

@@ -28,6 +28,19 @@ static_assert(sizeof(ArcRec) == 32, "ArcRec is 32 B");
 #define ARC_INDEX_MASK ((1ull << ARC_ORIGIN_SHIFT) - 1)
 enum { ARC_NEW = 0, ARC_RESULT = 1, ARC_WALK = 2, ARC_NONE = 3 };
 
+// Peer liveness and successors_ lists for the literal walk's dead-finger
+// branch (cx_liveness_upload).
+// Guard words written right after the decode's inverse table (cx_api.hip).
+#define IDA_GUARD_WORD 0xA5C3A5C3u
+#define IDA_GUARD_WORDS 64
+
+struct LitState {
+    const uint8_t *alive;   // n bytes, nullptr = all alive
+    const uint32_t *succs;  // n x ns, CX_NONE-padded, nullptr = converged window
+    int ns;                 // successor-list length
+    int rule;               // CX_FWD_CHORD / CX_FWD_DHASH
+};
+
 namespace cxk {
 
 size_t scan_workspace_words(size_t n);
@@ -54,8 +67,9 @@ hipError_t successor(const SearchView &ev, const cell128 *keys, size_t q, uint32
                      hipStream_t s);
 hipError_t fingers_build(const SearchView &ev, const cell128 *ring, uint32_t *F, hipStream_t s);
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
-                 const uint32_t *preds, bool literal, const uint32_t *src, const cell128 *keys,
-                 size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
+                 const uint32_t *preds, const LitState &ls, bool literal, const uint32_t *src,
+                 const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status,
+                 hipStream_t s);
 hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
                     cell128 *ring_ext, hipStream_t s);
 hipError_t ring_ext_build(const cell128 *ring, size_t n, cell128 *ring_ext, hipStream_t s);
@@ -83,7 +97,11 @@ hipError_t cz_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, in
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                    uint8_t *status, hipStream_t s);
+                    uint8_t *status, unsigned long long *stats, hipStream_t s);
+// Dependent random gathers of 64-B entries (four lanes, one 16-B load each),
+// the walk's access pattern, over `bytes` of `table` (read only): entries/s.
+hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, double *rate,
+                        hipStream_t s);
 hipError_t tree_build_arc(const SearchView &sv, const cell128 *ring, size_t n, uint32_t lo,
                           uint32_t hi, int l0, int R, int ib, uint64_t *tree, hipStream_t s);
 hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *tree,
@@ -126,14 +144,16 @@ hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t 
                       size_t blocks, int n, int m, int p, uint16_t *frags, hipStream_t s);
 hipError_t ida_runs(const uint8_t *idx, size_t blocks, int m, uint32_t *flag, hipStream_t s);
 hipError_t ida_run_index(const uint32_t *flag_excl, const uint32_t *flag_raw, size_t blocks,
-                         uint32_t *run_of, uint32_t *run_start, hipStream_t s);
-hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, int m, int p,
-                       int32_t *inv, uint8_t *okf, hipStream_t s);
+                         size_t runs, uint32_t *run_of, uint32_t *run_start, uint32_t *err,
+                         hipStream_t s);
+hipError_t ida_inverse(const uint8_t *idx, const uint32_t *run_start, size_t runs, size_t blocks,
+                       int m, int p, int32_t *inv, uint8_t *okf, uint32_t *err, hipStream_t s);
 hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m, int p,
-                      const int32_t *inv, const uint32_t *run_of, const uint8_t *okf,
-                      uint16_t *out, uint64_t *out_len, hipStream_t s);
-hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks,
-                           uint64_t *out_len, hipStream_t s);
+                      const int32_t *inv, const uint32_t *run_of, size_t runs, const uint8_t *okf,
+                      uint16_t *out, uint64_t *out_len, uint32_t *err, hipStream_t s);
+hipError_t ida_mark_failed(const uint32_t *run_of, const uint8_t *okf, size_t blocks, size_t runs,
+                           uint64_t *out_len, uint32_t *err, hipStream_t s);
+hipError_t ida_check_guard(const uint32_t *guard, int words, uint32_t *err, hipStream_t s);
 hipError_t check_indices(const uint32_t *idx, size_t count, uint32_t limit, bool allow_none,
                          uint32_t *d_bad, hipStream_t s);
 

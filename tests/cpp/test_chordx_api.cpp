@@ -94,22 +94,59 @@ TEST(ChordGetSucc, FromPredecessor) {
     EXPECT_EQ(l.hops, 1);
 }
 
+// GET_SUCC_FAILING (GetSuccTest.json): peer 127.0.0.1:7003 (constructed, its
+// server answers, min_key_ = id_, StartChord never called -> empty finger
+// table); its predecessor_ and only successor are a peer with ID
+// fff...f (31 f) on port 1 that never answers.  EXPECT_ANY_THROW.
+static std::string failing_throw(bool fill_fingers, int rule) {
+    const Key p = Key::FromHex("61b23792c54457c5ac5b7a95b35722db");  // UUIDv5("127.0.0.1:7003")
+    const Key dead = Key::FromHex("fffffffffffffffffffffffffffffff");
+    Ring ring({p, dead});
+    const uint32_t ip = ring.IndexOf(p), id = ring.IndexOf(dead);
+    std::vector<uint32_t> F(2 * CX_FINGERS, CX_NONE);  // empty table: no finger added
+    if (fill_fingers)  // what the test's comment intends AdjustFingers(succ) to do
+        for (unsigned i = 0; i < CX_FINGERS; ++i) F[ip * CX_FINGERS + i] = id;
+    ring.EditFingers(F);
+    std::vector<Key> mk(2);
+    mk[ip] = p;                       // min_key_(id_), abstract_chord_peer.cpp:22
+    mk[id] = Key::FromHex("0");       // the fixture's MIN_KEY
+    std::vector<uint32_t> preds(2, CX_NONE);
+    preds[ip] = id;                   // predecessor_.Set(succ)
+    ring.SetPeerState(&mk, &preds);
+    std::vector<uint8_t> alive(2, 0);
+    alive[ip] = 1;                    // port 1 never answers
+    std::vector<uint32_t> succs(2 * 3, CX_NONE);
+    succs[ip * 3] = id;               // successors_.Insert(succ)
+    ring.SetLiveness(&alive, &succs, 3, rule);
+    try {
+        ring.GetSuccessor(ip, Key::FromHex("0000000000000000000000000000000"));
+    } catch (const chordx::Error &e) {
+        return e.what();
+    }
+    return "";
+}
+
 TEST(ChordGetSucc, Failing) {
-    // every finger points at the peer itself and it has no live predecessor:
-    // the reference livelocks / throws; chordx reports "Lookup failed"
+    // literal: FingerTable::Lookup over the empty table throws (finger_table.h:129)
+    EXPECT_EQ(failing_throw(false, CX_FWD_CHORD), std::string("ChordKey not found"));
+    // every finger = the dead succ: successors_.Lookup -> dead -> chord_peer.cpp:206
+    EXPECT_EQ(failing_throw(true, CX_FWD_CHORD), std::string("Lookup failed"));
+    // DHash rule: LookupLiving none, successors_[0] dead -> dhash_peer.cpp:524
+    EXPECT_EQ(failing_throw(true, CX_FWD_DHASH), std::string("Lookup failed"));
+}
+
+TEST(ChordGetSucc, LivelockHitsHopCap) {
+    // every finger points at the peer itself and its predecessor is unset: the
+    // reference forwards to itself forever; chordx stops at the hop cap
     Ring ring({Key::FromHex("62a0959bff135ad296fbdc29252d927a"), Key::FromHex("5c22f4050c375657b05b35732eef0130")});
     std::vector<uint32_t> F = ring.FingerTable();
     for (unsigned i = 0; i < CX_FINGERS; ++i) F[i] = 0;
     ring.EditFingers(F);
     std::vector<uint32_t> preds = {CX_NONE, 0};
     ring.SetPeerState(nullptr, &preds);
-    bool threw = false;
-    try {
-        ring.GetSuccessor(0, Key(ring.Ids()[1].value()));
-    } catch (const chordx::Error &e) {
-        threw = std::string(e.what()) == "Lookup failed";
-    }
-    EXPECT_TRUE(threw);
+    chordx::Lookup l = ring.Route({0}, {Key(ring.Ids()[1].value())})[0];
+    EXPECT_EQ(l.status, CX_Q_HOPCAP);
+    EXPECT_EQ(l.hops, CX_HOP_CAP);
 }
 
 TEST(DHashPeer, InsufficientSuccs) {
@@ -169,6 +206,7 @@ int main() {
     RUN(ChordGetSucc, FromFingerTable);
     RUN(ChordGetSucc, FromPredecessor);
     RUN(ChordGetSucc, Failing);
+    RUN(ChordGetSucc, LivelockHitsHopCap);
     RUN(DHashPeer, InsufficientSuccs);
     RUN(Wire, GetSuccJoinFixture);
     RUN(DataBlock, EncodeDecodeVal1);

@@ -169,6 +169,7 @@ def get_succ():
     loc = d["GET_SUCC_OF_LOCAL_KEY"]
     ft = d["GET_SUCC_FROM_FINGER_TABLE"]
     pr = d["GET_SUCC_FROM_PREDECESSOR"]
+    fa = d["GET_SUCC_FAILING"]
     return {
         "source": "chord_test.cpp:18-123 + GetSuccTest.json",
         # LocalKey: a lone peer with min_key set to 0 owns [0, id]; the key is local.
@@ -186,6 +187,16 @@ def get_succ():
         "from_predecessor": {"peers": [uuid5_hex(peer_name(p)) for p in pr["PEERS"]],
                              "src": uuid5_hex(peer_name(pr["PEERS"][0])),
                              "key": pr["KEY_TO_LOOKUP"]},
+        # Failing (chord_test.cpp:101-123): a constructed (server running,
+        # StartChord never called) peer whose predecessor_ and only successor
+        # are a peer that does not answer (port 1); AdjustFingers(succ) runs on
+        # an empty finger table.  EXPECT_ANY_THROW(GetSuccessor(key)).
+        "failing": {"peer": uuid5_hex(peer_name(fa["PEER"])),
+                    "num_succs": fa["PEER"]["NUM_SUCCS"],
+                    "dead_succ": fa["PEER"]["SUCCESSOR"]["ID"],
+                    "dead_succ_min_key": fa["PEER"]["SUCCESSOR"]["MIN_KEY"],
+                    "dead_succ_port": fa["PEER"]["SUCCESSOR"]["PORT"],
+                    "key": fa["KEY_TO_LOOKUP"]},
     }
 
 

@@ -1,0 +1,110 @@
+"""BASELINE configs C4 (per GPU) and C5 at their full sizes on the GPU.
+
+C4 per GPU: the headline workload -- 2^24-peer ring (seed 0x5EED0005), 2^25
+keys (seed 0x5EED0006), src = q mod N, the default route kernel.
+  * every lookup: status OK and owner == exact successor (lower_bound with
+    wrap, StoredLocally's converged answer, abstract_chord_peer.cpp:720-725);
+  * owner and hops == the oracle's literal ForwardRequest walk
+    (oracle/chord_oracle.c or_route, chord_peer.cpp:185-211) on a 2^20-key
+    sample, over the engine's finger table;
+  * that finger table == the oracle's PopulateFingerTable restatement
+    (or_fingers_rows, abstract_chord_peer.cpp:564-613) on three 4096-row
+    blocks (start, middle, end of the ring).
+C5: 2^24-peer ring (seed 0x5EED0007), 2^26 keys (seed 0x5EED0008), n = 14,
+1 % joins + 1 % leaves (seed 0x5EED0009, leaves chosen by index):
+  * churned ring and old->new map == the oracle's;
+  * new lists, counts, misplaced masks and transfer targets == the oracle's
+    RunGlobalMaintenance restatement (dhash_peer.cpp:298-348) on ALL keys;
+  * n-successor lists on the old ring == the successor window on all keys.
+"""
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+N4, Q4 = 1 << 24, 1 << 25
+
+
+@pytest.fixture(scope="module")
+def c4(O):
+    import torch
+
+    import chordx
+    ids = torch.empty((N4, 2), dtype=torch.int64, device="cuda:0")
+    chordx.fill_splitmix(ids, 0x5EED0005)
+    ring = chordx.Ring(ids)
+    del ids
+    ring.build_fingers()
+    ring.sync()
+    keys = torch.empty((Q4, 2), dtype=torch.int64, device="cuda:0")
+    chordx.fill_splitmix(keys, 0x5EED0006)
+    src = (torch.arange(Q4, device="cuda:0", dtype=torch.int64) % ring.n).to(torch.int32)
+    owner, hops, status = ring.route(src, keys)
+    torch.cuda.synchronize()
+    yield ring, keys, src, owner, hops, status
+    del ring
+    torch.cuda.empty_cache()
+
+
+def test_c4_every_lookup_reaches_the_successor(c4):
+    import torch
+    ring, keys, src, owner, hops, status = c4
+    assert ring.n == N4  # no duplicate IDs among 2^24 splitmix values
+    assert ring.route_info()[0] == 5  # the default (benchmarked) kernel
+    assert int((status != 0).sum()) == 0
+    succ = ring.successor(keys)
+    torch.cuda.synchronize()
+    assert bool((owner == succ).all())
+    mean = float(hops.double().mean())
+    assert 11.5 < mean < 12.3  # ~ log2(N)/2 on a uniform ring
+
+
+def test_c4_oracle_walk_and_fingers_on_samples(O, c4):
+    ring, keys, src, owner, hops, status = c4
+    want_ring = O.ring_build(O.splitmix_keys(0x5EED0005, N4))
+    ids = ring.ids()
+    assert (ids == want_ring).all()
+    F = ring.fingers_device().cpu().numpy().view(np.uint32)
+    for p0 in (0, N4 // 2 - 2048, N4 - 4096):
+        assert (F[p0:p0 + 4096] == O.fingers(want_ring, rows=(p0, p0 + 4096))).all(), p0
+    sample = 1 << 20
+    kh = keys[:sample].cpu().numpy().view(np.uint64)
+    sh = src[:sample].cpu().numpy().view(np.uint32)
+    wo, wh, ws = O.route(O.Peers(want_ring, F), sh, kh)
+    assert (ws == 0).all()
+    assert (owner[:sample].cpu().numpy().view(np.uint32) == wo).all()
+    assert (hops[:sample].cpu().numpy() == wh).all()
+
+
+def test_c5_full_size_churn_and_misplaced_scan(O):
+    import torch
+
+    import chordx
+    N5, q, n = 1 << 24, 1 << 26, 14
+    ids = O.splitmix_keys(0x5EED0007, N5)
+    want_old = O.ring_build(ids)
+    old = chordx.Ring(ids)
+    assert old.n == len(want_old)
+    rng = np.random.default_rng(0x5EED0009)
+    leaves = want_old[rng.choice(len(want_old), N5 // 100, replace=False)]
+    joins = O.splitmix_keys(0x5EED0009, N5 // 100)
+    new, o2n = old.churn(joins, leaves)
+    want_new, want_o2n = O.churn(want_old, joins, leaves)
+    assert (new.ids() == want_new).all() and (o2n == want_o2n).all()
+
+    # n-successor windows on the old ring, every key (device-side property)
+    keys_d = torch.empty((q, 2), dtype=torch.int64, device="cuda:0")
+    chordx.fill_splitmix(keys_d, 0x5EED0008)
+    lists_d, count_d = old.nsucc(keys_d, n)
+    succ = old.successor(keys_d).to(torch.int64)
+    want = (succ[:, None] + torch.arange(n, device="cuda:0")) % old.n
+    torch.cuda.synchronize()
+    assert bool((lists_d.to(torch.int64) == want).all()) and bool((count_d == n).all())
+    del keys_d, lists_d, count_d, succ, want
+
+    keys = O.splitmix_keys(0x5EED0008, q)
+    lists, count, mask, target = old.misplaced(new, o2n, keys, n)
+    wl, wc, wm, wt = O.misplaced(want_old, want_new, want_o2n, keys, n)
+    assert (count == wc).all() and (mask == wm).all()
+    assert (lists == wl).all() and (target == wt).all()
+    assert 0 < int((mask != 0).sum()) < q

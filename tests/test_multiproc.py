@@ -194,3 +194,34 @@ def test_arc_router_protocol_gloo(world):
         assert out[r][2] == st.tolist()
         assert out[r][3] == 3           # walk -> result -> home, then drained
         assert out[r][4] > 0            # records crossed ranks
+
+
+def test_bench_launches_n_ranks_itself():
+    """`bench.py --gpus 2` without torchrun starts torch.distributed.run as a
+    child and rank 0 of that job reports n_gpus = 2 (CX_BENCH_DRYRUN: the
+    launch / rendezvous / barrier / max-over-ranks flow without a GPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(CX_BENCH_DRYRUN="1", CX_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0", CX_BENCH_DRYRUN="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr

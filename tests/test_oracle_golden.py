@@ -316,3 +316,96 @@ def test_churn_rejects_duplicate_join(O):
     new_ids, old_ids = O.ints_from_keys(new), O.ints_from_keys(old)
     assert len(set(new_ids)) == 12 and new_ids == sorted(new_ids)
     assert all(new_ids[o2n[p]] == old_ids[p] for p in range(10))
+
+
+# ---- a9: ForwardRequest's dead-finger branch (chord_peer.cpp:193-208,
+# dhash_peer.cpp:505-526) --------------------------------------------------
+def failing_state(O, g, fill_fingers, rule):
+    """ChordGetSucc.Failing (chord_test.cpp:101-123) as peer state: peer P
+    (127.0.0.1:7003) was constructed -- its server answers, min_key_ = id_
+    (abstract_chord_peer.cpp:21-22) -- but never started a chord, so its finger
+    table is empty; its predecessor_ and only successor are `succ` (port 1,
+    never answers).  AdjustFingers(succ) walks the empty table and changes
+    nothing.  fill_fingers=True is the state the test's comment intends (every
+    finger = succ)."""
+    p_id, s_id = H(g["peer"]), H(g["dead_succ"])
+    ring = _ring(O, [p_id, s_id])
+    ids = O.ints_from_keys(ring)
+    p, sd = ids.index(p_id), ids.index(s_id)
+    F = np.full((2, 128), O.NONE, np.uint32)
+    if fill_fingers:
+        F[p, :] = sd
+    min_keys = [0, 0]
+    min_keys[p], min_keys[sd] = p_id, H(g["dead_succ_min_key"])
+    preds = np.full(2, O.NONE, np.uint32)
+    preds[p] = sd
+    alive = np.zeros(2, np.uint8)
+    alive[p] = 1
+    succs = np.full((2, g["num_succs"]), O.NONE, np.uint32)
+    succs[p, 0] = sd
+    return ring, p, dict(F=F, min_keys=O.keys_from_ints(min_keys), preds=preds, alive=alive,
+                         succs=succs, rule=rule)
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_get_succ_failing_literal(O, refvec, rule):
+    """The literal test state: GetSuccessor throws -- from FingerTable::Lookup
+    over the empty table ("ChordKey not found", finger_table.h:129)."""
+    g = refvec["get_succ"]["failing"]
+    ring, p, st = failing_state(O, g, False, rule)
+    P = O.Peers(ring, **st)
+    owner, hops, status = O.route(P, [p], O.keys_from_ints([H(g["key"])]))
+    assert status[0] == O.Q_NOT_FOUND and owner[0] == O.NONE and hops[0] == 0
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_get_succ_failing_dead_finger(O, refvec, rule):
+    """Every finger = the dead succ: not self -> IsAlive fails -> Chord:
+    successors_.Lookup(0) finds succ (the wrapped range (id_P, succ]) dead;
+    DHash: LookupLiving gives none, successors_[0] is dead -> "Lookup failed"."""
+    g = refvec["get_succ"]["failing"]
+    ring, p, st = failing_state(O, g, True, rule)
+    P = O.Peers(ring, **st)
+    owner, hops, status = O.route(P, [p], O.keys_from_ints([H(g["key"])]))
+    assert status[0] == O.Q_FAILED and owner[0] == O.NONE and hops[0] == 0
+
+
+def _five_peer(O, dead, rule):
+    ring = O.keys_from_ints([k << 124 for k in range(1, 6)])
+    alive = np.ones(5, np.uint8)
+    alive[list(dead)] = 0
+    return O.Peers(ring, O.fingers(ring), alive=alive, ns=3, rule=rule)
+
+
+@pytest.mark.parametrize("dead,rule,want", [
+    # key in (id2, id3]; from peer 0 the walk is 0 -> 2 -> 3 when all answer
+    ((), 0, (3, 1 + 1, 0)),
+    ((2,), 0, (3, 1, 0)),        # finger 2 dead: successors_.Lookup -> 3 (alive)
+    ((2,), 1, (3, 1, 0)),        # LookupLiving -> 3
+    ((3,), 0, (None, 1, 3)),     # at 2: finger 3 dead, list lookup 3 dead -> failed
+    ((3,), 1, (None, 1, 3)),     # LookupLiving none, successors_[0] = 3 dead
+    ((2, 3), 0, (None, 0, 3)),   # Chord: list lookup gives dead 3 at the source
+    ((2, 3), 1, (None, 1, 3)),   # DHash: successors_[0] = 1 alive -> at 1 both dead
+])
+def test_dead_finger_fallback_hand_derived(O, dead, rule, want):
+    P = _five_peer(O, dead, rule)
+    owner, hops, status = O.route(P, [0], O.keys_from_ints([0x38 << 120]))
+    w_owner, w_hops, w_st = want
+    assert status[0] == w_st and hops[0] == w_hops
+    assert owner[0] == (O.NONE if w_owner is None else w_owner)
+
+
+def test_lookup_living_scan_never_runs(O):
+    """RemotePeerList::LookupLiving's scan for a later living entry has a
+    condition that is false on entry (remote_peer_list.cpp:123): with the found
+    entry dead and a live one after it, DHash still falls back to
+    successors_[0] rather than the later living entry."""
+    ring = O.keys_from_ints([k << 124 for k in range(1, 6)])
+    F = O.fingers(ring)
+    alive = np.array([1, 1, 0, 0, 1], np.uint8)
+    succs = np.array([[2, 3, 4], [2, 3, 4], [3, 4, 0], [4, 0, 1], [0, 1, 2]], np.uint32)
+    # peer 0's list starts at a dead peer: successors_[0] dead too -> failed,
+    # although entry 4 (alive) follows the dead 3 in the list
+    P = O.Peers(ring, F, alive=alive, succs=succs, rule=1)
+    owner, hops, status = O.route(P, [0], O.keys_from_ints([0x38 << 120]))
+    assert status[0] == O.Q_FAILED and hops[0] == 0
