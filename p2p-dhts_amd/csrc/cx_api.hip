@@ -137,6 +137,7 @@ struct cx_ring {
     uint32_t arc_lo = 0, arc_hi = 0;
 
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
+    uint32_t *d_ring_key = nullptr; // ID slices [n] of the streaming finger build
     int dir_k = 1;
     int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory
     int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
@@ -257,6 +258,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_ring);
     (void)hipFree(r->d_eyt);
     (void)hipFree(r->d_dir);
+    (void)hipFree(r->d_ring_key);
     (void)hipFree(r->d_fingers);
     (void)hipFree(r->d_rt);
     (void)hipFree(r->d_pk);
@@ -571,7 +573,23 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
             return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
         }
     }
-    CX_HIP(cxk::fingers_build(ring->sv(), ring->d_ring, ring->d_fingers, s));
+    // streaming per-block window build (needs the directory and the top
+    // halves); CX_FINGERS_SEARCH=1 keeps the one-search-per-entry kernel (A/B)
+    static const bool search_only = getenv("CX_FINGERS_SEARCH") != nullptr;
+    SearchView fv = ring->sv();
+    fv.dir = ring->d_dir;
+    if (!search_only && !ring->d_ring_key) {
+        if (hipMalloc(&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
+            CX_HIP(cxk::ring_slice_build(ring->d_ring, ring->n, cxk::finger_key_shift(ring->n),
+                                         ring->d_ring_key, s));
+        else
+            ring->d_ring_key = nullptr;  // no HBM for it: one search per entry
+    }
+    DBuf fws;
+    const bool streaming = !search_only && ring->d_ring_key &&
+                           fws.alloc(cxk::fingers_workspace_bytes(ring->n)) == hipSuccess;
+    CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
+                              streaming ? fws.p : nullptr, ring->d_fingers, s));
     ring->fingers_converged = true;
     route_geometry(ring);
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers

@@ -425,8 +425,262 @@ __global__ __launch_bounds__(SUCC_BLOCK) void k_fingers(SearchView sv, const cel
     }
 }
 
-hipError_t fingers_build(const SearchView &sv, const cell128 *ring, uint32_t *F, hipStream_t s) {
-    const size_t total = (size_t)sv.ev.n * CX_FINGERS;
+// ---------------------------------------------------------------------------
+// Streaming finger build.  For a fixed level i the starts
+// id_p + 2^i are increasing in p (clockwise from the first start of a block
+// of consecutive peers), so their successors are too.  Two kernels:
+//  * plan (one wave per block of FT_P peers): gap exponents glog_p (finger i
+//    is the next peer iff i <= glog_p), the block's first level that needs a
+//    search anywhere, and s0(i) = succ(id_a + 2^i) for the block's first peer
+//    a and every search level i >= FT_L0 -- one directory search each, all in
+//    parallel across the grid;
+//  * tile (256 threads per block): each wave loads the ring windows
+//    s0(i) .. s0(i) + FT_W - 1 of its levels of a chunk at once as 32-bit
+//    ID slices (bits [kb, kb + 32) of each ID, kb = 108 - log2 n: coalesced
+//    4-B reads of a per-ring slice array), keys them relative to the level's
+//    first start, and every peer's successor is a branch-free binary search
+//    in its level's window in LDS; the block's FT_P rows leave as full-line
+//    16-B stores (next-peer entries filled at write-back).
+// Decisions on the keys are exact unless a window key equals the start's or
+// the start lies past the window: those entries take the exact directory
+// search, as do search levels below FT_L0 = 80 (gaps under 2^80: clustered
+// rings only).
+// ---------------------------------------------------------------------------
+constexpr int FT_P = 128;   // peers per block (rows of the LDS tile)
+constexpr int FT_W = 192;   // window elements per level (block span + ~4 sigma)
+constexpr int FT_CH = 8;    // levels whose windows are in LDS at once
+constexpr int FT_COLS = 40; // tile columns: levels FT_L0..127
+constexpr int FT_L0 = CX_FINGERS - FT_COLS;
+static_assert(FT_L0 >= 64, "tile levels need 2^i >= 2^64 (window keys from the top halves)");
+constexpr int FT_ROW = FT_COLS + 1;  // padded row: conflict-free column writes
+
+__global__ void k_ring_slice(const cell128 *ring, size_t n, int kb, uint32_t *key) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        key[i] = (uint32_t)(ld128(ring + i) >> kb);
+}
+
+__global__ __launch_bounds__(256) void k_fingers_plan(SearchView sv, const cell128 *ring,
+                                                      uint8_t *glog, uint8_t *lvl0,
+                                                      uint32_t *S0, uint32_t nblk) {
+    const uint32_t n = sv.ev.n;
+    const int lane = threadIdx.x & 63;
+    const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (b >= nblk) return;  // wave-uniform
+    const uint32_t a = b * FT_P;
+    int g = 127;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t p = a + lane + 64 * k;
+        if (p < n) {
+            const uint32_t nx = p + 1 == n ? 0u : p + 1;
+            const int gp = msb128(ld128(ring + nx) - ld128(ring + p));
+            glog[p] = (uint8_t)gp;
+            g = gp < g ? gp : g;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int o = __shfl_xor(g, off, 64);
+        g = o < g ? o : g;
+    }
+    const int l0 = g + 1;
+    if (lane == 0) lvl0[b] = (uint8_t)(l0 > 128 ? 128 : l0);
+    const int i = FT_L0 + lane;
+    if (lane < FT_COLS && i >= l0)
+        S0[(size_t)b * FT_COLS + lane] = dir_successor(sv, ld128(ring + a) + ((u128)1 << i));
+}
+
+__global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell128 *ring,
+                                                      const uint32_t *ring_key, int kb,
+                                                      const uint8_t *glog_g, const uint8_t *lvl0_g,
+                                                      const uint32_t *S0, uint32_t *F) {
+    constexpr int LPW = FT_CH / 4;    // levels per wave per chunk
+    constexpr int EPL = FT_W / 64;    // window elements per lane per level
+    static_assert(EPL * 64 == FT_W && LPW * 4 == FT_CH, "window geometry");
+    __shared__ uint32_t tile[FT_P * FT_ROW];
+    __shared__ uint32_t win[4][LPW][256];  // per wave: 32-bit window keys, padded with ~0
+    __shared__ uint32_t s0[FT_COLS];
+    __shared__ uint8_t glog[FT_P];
+    const uint32_t n = sv.ev.n;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t b = blockIdx.x, a = b * FT_P;
+    const uint32_t rows = n - a < (uint32_t)FT_P ? n - a : (uint32_t)FT_P;
+    const int l0 = lvl0_g[b];
+    const int lt = l0 > FT_L0 ? l0 : FT_L0;  // first tile level
+    if (threadIdx.x < FT_COLS)
+        s0[threadIdx.x] = threadIdx.x + FT_L0 >= (unsigned)l0 ? S0[(size_t)b * FT_COLS + threadIdx.x]
+                                                             : 0u;
+    if (threadIdx.x < rows) glog[threadIdx.x] = glog_g[a + threadIdx.x];
+    const u128 ida = ld128(ring + a);
+    const uint32_t ka = (uint32_t)(ida >> kb);
+    // Window keys: for a level i >= kb the start t_p = id_p + 2^i carries
+    // nothing into bits [kb, kb + 32) from below, so its slice is
+    // slice(id_p) + 2^(i - kb) (mod 2^32) and the key of t_p relative to the
+    // level's first start t_a, e_p = slice(t_p) - slice(t_a) = slice(id_p) -
+    // slice(id_a) (mod 2^32), is the same at every tile level.  Relative keys
+    // order correctly while offsets from t_a stay below 2^(kb + 32) (checked
+    // on each window's exact last element and on each peer's offset); equal
+    // keys are ties (exact search).
+    const u128 lim = (u128)1 << (kb + 32);
+    u128 idp[2];
+    uint32_t cp[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t r = lane + 64 * k;
+        idp[k] = r < rows ? ld128(ring + a + r) : ida;
+        cp[k] = (uint32_t)(idp[k] >> kb) - ka;
+        if (idp[k] - ida >= lim) cp[k] = 0xFFFFFFFFu;  // off the key range: exact search
+    }
+    __syncthreads();
+    // Each wave owns levels c0 + wave + 4q of every chunk: it loads their
+    // windows (all EPL x LPW loads in flight at once), converts them to keys
+    // in its own LDS rows and searches them; no block barrier until the tile
+    // is complete.
+    for (int c0 = lt; c0 < CX_FINGERS; c0 += FT_CH) {
+        const int nl = CX_FINGERS - c0 < FT_CH ? CX_FINGERS - c0 : FT_CH;
+        uint32_t v[LPW][EPL];
+#pragma unroll
+        for (int q = 0; q < LPW; ++q) {
+            const int lv = wave + 4 * q;
+            if (lv >= nl) break;  // wave-uniform
+            const uint32_t base = s0[c0 + lv - FT_L0];
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) {
+                uint32_t e = base + (uint32_t)(lane + 64 * m);
+                e = e >= n ? e - n : e;  // n > FT_W (launcher)
+                v[q][m] = ring_key[e];
+            }
+        }
+        // lane q: the arc of level q's window, from its exact last element
+        bool arc = false;
+        if (lane < LPW && wave + 4 * lane < nl) {
+            const int lv = wave + 4 * lane;
+            uint32_t e = s0[c0 + lv - FT_L0] + FT_W - 1;
+            e = e >= n ? e - n : e;
+            arc = (ld128(ring + e) - (ida + ((u128)1 << (c0 + lv)))) < lim;
+        }
+        const uint32_t arcbits = (uint32_t)__ballot(arc);
+#pragma unroll
+        for (int q = 0; q < LPW; ++q) {
+            const int lv = wave + 4 * q;
+            if (lv >= nl) break;
+            const int lvl = c0 + lv;
+            const uint32_t kta = ka + (lvl - kb < 32 ? 1u << (lvl - kb) : 0u);  // slice(t_a)
+#pragma unroll
+            for (int m = 0; m < EPL; ++m) win[wave][q][lane + 64 * m] = v[q][m] - kta;
+            if (lane < 256 - FT_W) win[wave][q][FT_W + lane] = 0xFFFFFFFFu;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // both peers x LPW levels: independent branch-free searches, their LDS
+        // reads issued together step by step
+        uint32_t j[LPW][2];
+#pragma unroll
+        for (int q = 0; q < LPW; ++q) j[q][0] = j[q][1] = 0;
+#pragma unroll
+        for (uint32_t st = 128; st; st >>= 1) {
+#pragma unroll
+            for (int q = 0; q < LPW; ++q) {
+                const uint32_t *w = win[wave][q];  // rows past nl hold stale keys: unused
+#pragma unroll
+                for (int k = 0; k < 2; ++k) j[q][k] += w[j[q][k] + st - 1] < cp[k] ? st : 0u;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < LPW; ++q) {
+            const int lv = wave + 4 * q;
+            if (lv >= nl) break;  // wave-uniform
+            const int i = c0 + lv;
+            const uint32_t base = s0[i - FT_L0];
+            const uint32_t *w = win[wave][q];
+            const bool aok = (arcbits >> q) & 1u;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t r = lane + 64 * k;
+                if (r >= rows || i <= glog[r]) continue;  // next peer: filled at write-back
+                uint32_t f = CX_NONE;
+                const uint32_t jj = j[q][k];
+                if (aok && jj < FT_W && w[jj] != cp[k]) {
+                    const uint32_t e = base + jj;
+                    f = e >= n ? e - n : e;
+                }
+                if (f == CX_NONE)  // tie on the key / past the window / no arc
+                    f = dir_successor(sv, idp[k] + ((u128)1 << i));
+                tile[r * FT_ROW + (i - FT_L0)] = f;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // searches done before the next chunk's keys
+    }
+    __syncthreads();
+    // write-back: 8 rows per pass, 16 B per thread, full 512-B rows
+    const int chunk = threadIdx.x & 31;
+    for (int r = threadIdx.x >> 5; r < (int)rows; r += 8) {
+        const uint32_t p = a + r;
+        const uint32_t nx = p + 1 == n ? 0u : p + 1;
+        const int g = glog[r];
+        uint4 o;
+        if (chunk * 4 + 3 <= g) {  // all four levels are the next peer
+            o = make_uint4(nx, nx, nx, nx);
+        } else {
+            uint32_t v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = chunk * 4 + c;
+                if (i <= g)
+                    v[c] = nx;
+                else if (i >= FT_L0)
+                    v[c] = tile[r * FT_ROW + (i - FT_L0)];
+                else  // a gap under 2^88 (clustered rings): exact search
+                    v[c] = dir_successor(sv, ld128(ring + p) + ((u128)1 << i));
+            }
+            o = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        reinterpret_cast<uint4 *>(F + (size_t)p * CX_FINGERS)[chunk] = o;
+    }
+}
+
+// Slice position of the streaming finger build: the expected span of a
+// window (FT_W gaps, 2^(135.6 - log2 n)) stays far below 2^(kb + 32), and
+// kb <= FT_L0 so every tile level is >= kb.
+int finger_key_shift(size_t n) {
+    int lg = 0;
+    while (((size_t)1 << lg) < n) ++lg;
+    const int kb = 108 - lg;
+    return kb > FT_L0 ? FT_L0 : (kb < 0 ? 0 : kb);
+}
+
+hipError_t ring_slice_build(const cell128 *ring, size_t n, int kb, uint32_t *key, hipStream_t s) {
+    k_ring_slice<<<cx_grid(n, 256), 256, 0, s>>>(ring, n, kb, key);
+    return hipGetLastError();
+}
+
+// ring_key (n ID slices, ring_slice_build at finger_key_shift(n)) selects the
+// streaming build for rings of 2^18 peers or more; smaller rings (whose
+// windows would span too much of the circle for 32-bit keys) take one
+// directory search per entry.
+size_t fingers_workspace_bytes(size_t n) {
+    const size_t nblk = (n + FT_P - 1) / FT_P;
+    return n + nblk + nblk * FT_COLS * sizeof(uint32_t) + 16;
+}
+
+hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32_t *ring_key,
+                         void *ws, uint32_t *F, hipStream_t s) {
+    const size_t n = sv.ev.n;
+    if (ring_key && ws && sv.dir && n >= ((size_t)1 << 18)) {
+        const uint32_t nblk = (uint32_t)((n + FT_P - 1) / FT_P);
+        uint32_t *S0 = static_cast<uint32_t *>(ws);
+        uint8_t *glog = reinterpret_cast<uint8_t *>(S0 + (size_t)nblk * FT_COLS);
+        uint8_t *lvl0 = glog + n;
+        k_fingers_plan<<<(nblk + 3) / 4, 256, 0, s>>>(sv, ring, glog, lvl0, S0, nblk);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        k_fingers_tile<<<nblk, 256, 0, s>>>(sv, ring, ring_key, finger_key_shift(n), glog, lvl0,
+                                            S0, F);
+        return hipGetLastError();
+    }
+    const size_t total = n * CX_FINGERS;
     if (sv.dir)
         k_fingers<true><<<cx_grid(total, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, ring, F);
     else

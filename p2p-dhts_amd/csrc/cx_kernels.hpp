@@ -65,7 +65,14 @@ hipError_t dir_build(const cell128 *ring, size_t n, int k, uint32_t *lo_tmp, uin
                      hipStream_t s);
 hipError_t successor(const SearchView &ev, const cell128 *keys, size_t q, uint32_t *owner,
                      hipStream_t s);
-hipError_t fingers_build(const SearchView &ev, const cell128 *ring, uint32_t *F, hipStream_t s);
+// Streaming build when ring_key (ID slices at finger_key_shift(n),
+// ring_slice_build) and ws (fingers_workspace_bytes) are given and the ring
+// has >= 2^18 peers, else one directory search per entry.
+size_t fingers_workspace_bytes(size_t n);
+int finger_key_shift(size_t n);
+hipError_t fingers_build(const SearchView &ev, const cell128 *ring, const uint32_t *ring_key,
+                         void *ws, uint32_t *F, hipStream_t s);
+hipError_t ring_slice_build(const cell128 *ring, size_t n, int kb, uint32_t *key, hipStream_t s);
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, const LitState &ls, bool literal, const uint32_t *src,
                  const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status,

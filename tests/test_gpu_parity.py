@@ -507,3 +507,27 @@ def test_uuid5_lengths_and_bytes(cx, O):
     for g, n in zip(O.ints_from_keys(got), names):
         k = O.lib().or_uuid5_dns(n, len(n))
         assert g == (k.lo | (k.hi << 64))
+
+
+@pytest.mark.parametrize("spread", [40, 100, 127])
+def test_fingers_streaming_build_clustered(cx, O, spread):
+    """The streaming finger build (ID-slice windows, k_fingers_tile; rings of
+    2^18 peers or more) with IDs packed so tightly that slices tie, windows
+    overflow and key ranges are exceeded: every entry bit-exact vs the
+    oracle's PopulateFingerTable restatement."""
+    ids = clustered_ring(O, (1 << 18) + 77, 0xF1 + spread, spread)
+    want = O.ring_build(ids)
+    assert len(want) >= 1 << 18
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    assert (ring.ids() == want).all()
+    assert (F == O.fingers(want)).all()
+
+
+def test_fingers_streaming_build_uniform_tail(cx, O):
+    """Ring size not a multiple of the 128-peer block, wrap at the last peer."""
+    ids = O.splitmix_keys(0xF2, (1 << 18) + 1234)
+    want = O.ring_build(ids)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    assert (F == O.fingers(want)).all()

@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Per-kernel averages of the PMC passes under a tools/pmc_kernel.sh output dir."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+out = sys.argv[1]
+acc = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            name = row.get("Kernel_Name", "?").split("(")[0]
+            acc[name][row["Counter_Name"]].append((row.get("Dispatch_Id"), float(row["Counter_Value"])))
+res = {}
+for k, ctrs in acc.items():
+    res[k] = {}
+    for c, vals in ctrs.items():
+        per = defaultdict(float)
+        for d, v in vals:
+            per[d] += v  # sum over XCD/SE instances of one dispatch
+        res[k][c] = sum(per.values()) / len(per)
+print(json.dumps(res, indent=1))
