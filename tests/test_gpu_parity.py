@@ -531,3 +531,39 @@ def test_fingers_streaming_build_uniform_tail(cx, O):
     ring = cx.Ring(ids)
     F = ring.build_fingers(copy_out=True)
     assert (F == O.fingers(want)).all()
+
+
+def test_misplaced_with_foreign_map_and_chained_churn(cx, O):
+    """cx_misplaced derives new successors from the churn's recorded old->new
+    map; a caller map that differs from it (here: one survivor treated as
+    departed) must take the two-search path, and a ring churned twice pairs
+    each scan with its own map.  All keys vs the oracle."""
+    n_old, q = 5000, 60000
+    ids = O.splitmix_keys(0xC5, n_old)
+    old = cx.Ring(ids)
+    want_old = O.ring_build(ids)
+    rng = np.random.default_rng(0xC6)
+    leaves = want_old[rng.choice(len(want_old), 300, replace=False)]
+    joins = O.splitmix_keys(0xC7, 300)
+    new, o2n = old.churn(joins, leaves)
+    want_new, want_o2n = O.churn(want_old, joins, leaves)
+    keys = O.splitmix_keys(0xC8, q)
+    for m in (o2n, o2n.copy()):  # the recorded map and an equal copy
+        got = old.misplaced(new, m, keys, 14)
+        want = O.misplaced(want_old, want_new, want_o2n, keys, 14)
+        for g, w in zip(got, want):
+            assert (g == w).all()
+    foreign = o2n.copy()
+    foreign[np.flatnonzero(foreign != O.NONE)[7]] = O.NONE
+    got = old.misplaced(new, foreign, keys, 14)
+    want = O.misplaced(want_old, want_new, foreign, keys, 14)
+    for g, w in zip(got, want):
+        assert (g == w).all()
+    # second churn: new -> newer; and the stale pairing (old, newer) is rejected
+    joins2 = O.splitmix_keys(0xC9, 200)
+    newer, o2n2 = new.churn(joins2, want_new[:50])
+    want_newer, want_o2n2 = O.churn(want_new, joins2, want_new[:50])
+    got = new.misplaced(newer, o2n2, keys, 14)
+    want = O.misplaced(want_new, want_newer, want_o2n2, keys, 14)
+    for g, w in zip(got, want):
+        assert (g == w).all()
