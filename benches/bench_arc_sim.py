@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Arc-sharded routing on ONE GPU with G simulated ranks (SURVEY 8e layout 2).
 
-G engine handles share one MI355X; each holds tree rows for its own arc only,
-and records are exchanged in-process exactly as chordx.arc.ArcRouter does over
+G engine handles share one MI355X; each holds the replicated top-level route
+planes and the lower planes of its own arc (+ halo) only (cx_arc_build), and
+records are exchanged in-process exactly as chordx.arc.ArcRouter does over
 RCCL.  Per round and rank we time the walk step and the bucketing on the GPU
 (HIP events) and count the records that would cross xGMI, so the per-GPU cost
 of an 8-GPU arc-sharded run can be read off one box:
 
   per-GPU compute  ~ max over ranks of (step + bucket) per round, summed
   per-GPU exchange ~ records out per rank per round x 32 B over 7 xGMI links
+  projected rate   = keys per rank / (compute + exchange)   (no overlap)
 
 Prints one JSON object (profiles/<round>/arc_sim.json).
 """
@@ -26,15 +28,16 @@ sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
 import torch  # noqa: E402
 
 import chordx  # noqa: E402
-from chordx.arc import MAX_ROUNDS, arc_bounds  # noqa: E402
+from chordx.arc import MAX_ROUNDS  # noqa: E402
 
 XGMI_LINK = 153e9  # B/s per link per direction (MI355X_MICROARCH.md)
 
 
-def run(G, N, Q, ids, reps):
+def run(G, N, Q, ids, reps, top):
     rings = [chordx.Ring(ids) for _ in range(G)]
     for g, r in enumerate(rings):
-        r.arc_build(*arc_bounds(r.n, G, g))
+        r.arc_build(G, g, top)
+    info = [r.arc_info() for r in rings]
     q = Q // G
     keys, srcs, outs = [], [], []
     for g in range(G):
@@ -48,7 +51,7 @@ def run(G, N, Q, ids, reps):
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     best = None
     for _ in range(reps):
-        recs = [rings[g].arc_seed(g, srcs[g], keys[g]) for g in range(G)]
+        recs = [None] * G  # first step straight from the lookups (cx_arc_start)
         per_round = []
         t0 = time.perf_counter()
         for rnd in range(MAX_ROUNDS):
@@ -58,12 +61,14 @@ def run(G, N, Q, ids, reps):
             for g in range(G):
                 a, b, c = ev(), ev(), ev()
                 a.record()
-                out = rings[g].arc_step(g, recs[g], *outs[g])
+                out = (rings[g].arc_start(g, srcs[g], keys[g], *outs[g]) if recs[g] is None
+                       else rings[g].arc_step(g, recs[g], *outs[g]))
                 b.record()
                 send, counts = rings[g].arc_bucket(G, out)
                 c.record()
                 torch.cuda.synchronize()
-                rows.append({"in": int(recs[g].shape[0]), "step_ms": a.elapsed_time(b),
+                rows.append({"in": int(keys[g].shape[0] if recs[g] is None else recs[g].shape[0]),
+                             "step_ms": a.elapsed_time(b),
                              "bucket_ms": b.elapsed_time(c),
                              "out_remote": int(sum(counts) - counts[g])})
                 total += sum(counts)
@@ -79,12 +84,16 @@ def run(G, N, Q, ids, reps):
         xg = sum(max(r["out_remote"] for r in rows) * 32 / (7 * XGMI_LINK) * 1e3
                  for rows in per_round)
         res = {"G": G, "keys_total": Q, "keys_per_rank": q, "rounds": len(per_round),
+               "top_levels": info[0][0], "local_rows_max": max(i[1] for i in info),
+               "route_plane_bytes_per_gpu_max": max(i[2] for i in info),
                "per_gpu_compute_ms": comp, "per_gpu_xgmi_ms_model": xg,
                "projected_lookups_per_s_per_gpu": q / ((comp + xg) * 1e-3),
                "sim_wall_s": wall,
                "records_in_per_round": [sum(r["in"] for r in rows) for rows in per_round],
                "round_max_ms": [max(r["step_ms"] + r["bucket_ms"] for r in rows)
-                                for rows in per_round]}
+                                for rows in per_round],
+               "round_max_step_ms": [max(r["step_ms"] for r in rows) for rows in per_round],
+               "round_max_bucket_ms": [max(r["bucket_ms"] for r in rows) for rows in per_round]}
         if best is None or comp < best["per_gpu_compute_ms"]:
             best = res
     del rings
@@ -98,6 +107,7 @@ def main():
     ap.add_argument("--keys-log2", type=int, default=25, help="keys in total over the G ranks")
     ap.add_argument("--groups", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--top-levels", type=int, default=0, help="0: library default")
     a = ap.parse_args()
     N, Q = 1 << a.peers_log2, 1 << a.keys_log2
     ids = torch.empty((N, 2), dtype=torch.int64, device="cuda")
@@ -120,7 +130,7 @@ def main():
     del ref
     torch.cuda.empty_cache()
     for G in [int(x) for x in a.groups.split(",")]:
-        out["arc"].append(run(G, N, Q, ids, a.reps))
+        out["arc"].append(run(G, N, Q, ids, a.reps, a.top_levels))
         print(json.dumps(out["arc"][-1]), file=sys.stderr, flush=True)
     print(json.dumps(out))
 

@@ -271,14 +271,19 @@ int cx_wire_handle(cx_wire *wire, const char *request, size_t len, char **respon
 void cx_wire_free(char *response);
 
 /* ---- arc-sharded routing (multi-GPU layout 2) -------------------
- * Each rank keeps the replicated sorted ring but the lookahead-tree rows of its
- * own arc of peers only, arc g of G = [g n / G, (g+1) n / G).  A lookup walks
- * on the rank that owns the row it needs next, as the reference's
- * GET_SUCC request travels to the peer it is forwarded to
- * (ChordPeer::ForwardRequest, chord_peer.cpp:185-211): one bulk-synchronous
- * step per exchange, in-flight lookups travel between ranks as 32-B records.
- * Owners, hops and statuses equal cx_route's on the replicated ring.
- * All arc buffers are device memory (CX_MEM_DEVICE). */
+ * Rank g of G owns the arc of peers [g n / G, (g+1) n / G).  Every rank keeps
+ * the replicated sorted ring (and its finger table) and the pattern-keyed
+ * route planes of the top levels [128 - T, 128) for ALL peers (T =
+ * top_levels); the planes below them it keeps only for its own arc plus a
+ * halo (the peers whose IDs lie within 2^(128 - T) before the arc).  A
+ * lookup walks on its origin rank while it needs replicated rows; the first
+ * time it needs a lower level it is within 2^(128 - T) of its key, so it
+ * travels once, as a 32-B WALK record, to the rank whose arc holds the key's
+ * owner -- the GET_SUCC request forwarded to the next peer
+ * (ChordPeer::ForwardRequest, chord_peer.cpp:185-211) -- finishes there, and
+ * its result travels home once (RESULT record).  Owners, hops and statuses
+ * equal cx_route's on the replicated ring.  All arc buffers are device memory
+ * (CX_MEM_DEVICE). */
 typedef struct cx_arc_rec {
     uint64_t w0, w1; /* key (lookups) / owner | status << 32 (results) */
     uint64_t qid;    /* origin rank << 40 | index at the origin */
@@ -287,22 +292,31 @@ typedef struct cx_arc_rec {
 } cx_arc_rec;
 enum { CX_ARC_NEW = 0, CX_ARC_RESULT = 1, CX_ARC_WALK = 2, CX_ARC_NONE = 3 };
 #define CX_ARC_MAX_RANKS 64
+#define CX_ARC_TOP_LEVELS 6 /* default replicated top levels (top_levels = 0) */
 
-/* Builds the tree rows of peers [lo, hi) by successor searches on the ring
- * (no full finger table).  Replaces this rank's share of the finger tables
- * (FingerTable::AdjustFingers, finger_table.h:143-160). */
-int cx_arc_build(cx_ring *ring, uint32_t lo, uint32_t hi);
+/* Builds rank `rank`'s planes of a `world`-rank layout (and the converged
+ * finger table if missing: the planes are derived from it, as the reference's
+ * fingers are, abstract_chord_peer.cpp:564-613). */
+int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels);
+/* Replicated top levels, local rows (arc + halo) and route-plane bytes. */
+int cx_arc_info(const cx_ring *ring, int *top_levels, uint64_t *local_rows,
+                uint64_t *table_bytes);
 
 /* Records of q lookups issued at peers src[i] by rank `rank` (kind NEW). */
 int cx_arc_seed(const cx_ring *ring, int rank, const uint32_t *src, const cx_u128 *keys,
                 size_t q, cx_arc_rec *out);
 
 /* One step on rank `rank`: every input record yields exactly one output record:
- * WALK (continue at the rank owning cur's row), RESULT (for a remote origin)
+ * WALK (continue on the rank of the key's arc), RESULT (for a remote origin)
  * or NONE (result written to owner/hops/status at qid's index: results for
  * this rank's lookups, and RESULT records coming home). */
 int cx_arc_step(const cx_ring *ring, int rank, const cx_arc_rec *in, size_t q, cx_arc_rec *out,
                 uint32_t *owner, uint8_t *hops, uint8_t *status);
+
+/* cx_arc_seed + the first cx_arc_step in one pass: the step reads the new
+ * lookups straight from src / keys (out: one record per lookup). */
+int cx_arc_start(const cx_ring *ring, int rank, const uint32_t *src, const cx_u128 *keys,
+                 size_t q, cx_arc_rec *out, uint32_t *owner, uint8_t *hops, uint8_t *status);
 
 /* Groups WALK/RESULT records by destination rank into `send` (NONE dropped);
  * counts[world] (host) receives the per-destination record counts. */

@@ -42,7 +42,8 @@ EXPORTS = (
     "cx_peer_state_upload", "cx_liveness_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
     "cx_uuid5_dns", "cx_fill_splitmix",
-    "cx_arc_build", "cx_arc_seed", "cx_arc_step", "cx_arc_bucket",
+    "cx_arc_build", "cx_arc_info", "cx_arc_seed", "cx_arc_start", "cx_arc_step",
+    "cx_arc_bucket",
     "cx_hex_parse", "cx_hex_format",
     "cx_ida_segments", "cx_ida_encode", "cx_ida_decode",
     "cx_wire_create", "cx_wire_destroy", "cx_wire_ring", "cx_wire_handle", "cx_wire_free",
@@ -50,6 +51,7 @@ EXPORTS = (
 
 CX_ARC_NEW, CX_ARC_RESULT, CX_ARC_WALK, CX_ARC_NONE = 0, 1, 2, 3
 CX_ARC_MAX_RANKS = 64
+CX_ARC_TOP_LEVELS = 6
 
 
 class ChordError(RuntimeError):
@@ -111,9 +113,12 @@ def lib() -> ctypes.CDLL:
         "cx_wire_handle": ([vp, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_void_p),
                             ctypes.POINTER(ctypes.c_size_t)], i),
         "cx_wire_free": ([vp], None),
-        "cx_arc_build": ([vp, ctypes.c_uint32, ctypes.c_uint32], i),
+        "cx_arc_build": ([vp, i, i, i], i),
+        "cx_arc_info": ([vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint64),
+                         ctypes.POINTER(ctypes.c_uint64)], i),
         "cx_arc_seed": ([vp, i, vp, vp, sz, vp], i),
         "cx_arc_step": ([vp, i, vp, sz, vp, vp, vp, vp], i),
+        "cx_arc_start": ([vp, i, vp, vp, sz, vp, vp, vp, vp], i),
         "cx_arc_bucket": ([vp, i, vp, sz, vp, vp], i),
     }
     for name, (args, res) in sig.items():

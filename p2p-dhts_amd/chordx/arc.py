@@ -1,23 +1,27 @@
 """Arc-sharded routing across ranks (layout 2).
 
-When a ring's lookahead-tree table (n x R x 64 B: 32 GiB at 2^24 peers,
-320 GiB at 2^27) outgrows one GPU, each rank keeps the replicated sorted ring
-(16 B per peer) but tree rows only for its own arc of peers,
-arc g of G = [g n / G, (g+1) n / G).  A lookup walks on the rank that owns the
-row it needs next -- the GET_SUCC request travelling to the peer it was
-forwarded to (ChordPeer::ForwardRequest, chord_peer.cpp:185-211) -- and comes
-home as a RESULT record when it ends.  Owners, hops and statuses equal the
-replicated-ring route's (tests/test_gpu_arc.py).
+Rank g of G owns the arc of peers [g n / G, (g+1) n / G).  Each rank keeps
+the replicated sorted ring, the pattern-keyed route planes of the top levels
+for all peers (replicated) and the planes below them only for its arc plus a
+small halo (cx_arc_build).  A lookup walks on its origin rank while its rows
+are replicated; the first time it needs a lower level it is close enough to
+its key that every later peer lies in the key's arc or that arc's halo, so it
+travels once -- the GET_SUCC request forwarded to the next peer
+(ChordPeer::ForwardRequest, chord_peer.cpp:185-211) -- finishes on the rank of
+its key's arc, and its result travels home once.  Owners, hops and statuses
+equal the replicated-ring route's (tests/test_gpu_arc.py).
 
 One bulk-synchronous round = step (walk every record as far as this rank's
-rows reach) -> bucket by destination -> exchange.  The exchange is a real
-data-path collective: one all_gather of the G x G count matrix (every rank
-learns its receive splits and the global in-flight total from the same call)
-and one all_to_all_single of the 32-B records.  With the "nccl" backend both
-run on RCCL over xGMI; tests drive the same code with "gloo" on CPU.
+rows reach) -> bucket by destination -> exchange: one all_gather of the G x G
+count matrix (every rank learns its receive splits and the global in-flight
+total from the same call) and one all_to_all_single of the 32-B records.  A
+lookup takes three rounds: origin step, arc step, result delivery.  With the
+"nccl" backend both collectives run on RCCL over xGMI; tests drive the same
+code with "gloo" on CPU.
 
-The engine is any object with arc_build / arc_seed / arc_step / arc_bucket
-(chordx.Ring on a GPU; tests/test_multiproc.py plugs in an oracle stand-in).
+The engine is any object with arc_build(world, rank) / arc_seed / arc_step /
+arc_bucket (chordx.Ring on a GPU; tests/test_multiproc.py plugs in an oracle
+stand-in).
 """
 from __future__ import annotations
 
@@ -49,9 +53,10 @@ class ArcRouter:
         self.group = group
         self.comm_device = comm_device  # device of the collective buffers
         self.lo, self.hi = arc_bounds(n, world, rank)
-        engine.arc_build(self.lo, self.hi)
+        engine.arc_build(world, rank)
         self.rounds = 0
         self.records_sent = 0
+        self._mat_host = None  # pinned landing buffer of the count matrix
 
     def _exchange(self, send, counts):
         """Returns (received records, global number of records in flight)."""
@@ -61,7 +66,17 @@ class ArcRouter:
         mine = torch.tensor(counts, dtype=torch.int64, device=dev)
         mat = torch.empty((self.world, self.world), dtype=torch.int64, device=dev)
         tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
-        m = mat.cpu()
+        if mat.is_cuda:
+            # the splits must reach the host (all_to_all_single takes lists):
+            # one async copy into a pinned buffer, then wait on that copy only
+            if self._mat_host is None:
+                self._mat_host = torch.empty((self.world, self.world), dtype=torch.int64,
+                                             pin_memory=True)
+            self._mat_host.copy_(mat, non_blocking=True)
+            torch.cuda.current_stream(mat.device).synchronize()
+            m = self._mat_host
+        else:
+            m = mat
         inflight = int(m.sum())
         recv_counts = [int(x) for x in m[:, self.rank]]
         if inflight == 0:
@@ -76,9 +91,13 @@ class ArcRouter:
         """Routes this rank's lookups (issued at peers src[i]); collective over
         the group.  Writes owner/hops/status at the lookups' indices and
         returns the number of rounds taken."""
-        recs = self.engine.arc_seed(self.rank, src, keys)
+        start = getattr(self.engine, "arc_start", None)
+        recs = None if start else self.engine.arc_seed(self.rank, src, keys)
         for rnd in range(1, MAX_ROUNDS + 1):
-            out = self.engine.arc_step(self.rank, recs, owner, hops, status)
+            if recs is None:  # first step straight from the lookups
+                out = start(self.rank, src, keys, owner, hops, status)
+            else:
+                out = self.engine.arc_step(self.rank, recs, owner, hops, status)
             send, counts = self.engine.arc_bucket(self.world, out)
             self.records_sent += int(sum(counts))
             recs, inflight = self._exchange(send, counts)

@@ -356,9 +356,16 @@ class Ring:
         return lists, count, mask, target
 
     # ---- arc-sharded routing (chordx.arc drives the exchange) -------------
-    def arc_build(self, lo: int, hi: int):
-        """Tree rows of peers [lo, hi) (this rank's arc), cx_arc_build."""
-        L.check(L.lib().cx_arc_build(self._h, lo, hi))
+    def arc_build(self, world: int, rank: int, top_levels: int = 0):
+        """Rank `rank`'s route planes of a `world`-rank arc layout (cx_arc_build):
+        replicated top levels, lower levels for its arc + halo."""
+        L.check(L.lib().cx_arc_build(self._h, world, rank, top_levels))
+
+    def arc_info(self):
+        """(replicated top levels, local rows, route-plane bytes)."""
+        t, r, b = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        L.check(L.lib().cx_arc_info(self._h, ctypes.byref(t), ctypes.byref(r), ctypes.byref(b)))
+        return t.value, r.value, b.value
 
     def _arc_stream(self):
         L.check(L.lib().cx_ring_set_stream(
@@ -374,6 +381,20 @@ class Ring:
         out = torch.empty((q, 4), dtype=torch.int64, device=keys.device)
         self._arc_stream()
         L.check(L.lib().cx_arc_seed(self._h, rank, _ptr(src), _ptr(keys), q, _ptr(out)))
+        return out
+
+    def arc_start(self, rank: int, src, keys, owner, hops, status=None):
+        """arc_seed + the first arc_step in one pass (cx_arc_start): outcome
+        records of this rank's new lookups."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        out = torch.empty((q, 4), dtype=torch.int64, device=keys.device)
+        self._arc_stream()
+        L.check(L.lib().cx_arc_start(self._h, rank, _ptr(src), _ptr(keys), q, _ptr(out),
+                                     _ptr(owner), _ptr(hops), _ptr(status)))
         return out
 
     def arc_step(self, rank: int, recs, owner, hops, status=None):

@@ -133,8 +133,12 @@ struct cx_ring {
     uint32_t *d_scratch = nullptr; // small device scratch (counts/flags), 1 KiB
     unsigned long long *d_stats = nullptr;  // route gather counters (cxi_route_counters)
     bool counting = false;
-    uint64_t *d_arc_tree = nullptr;   // tree rows of the arc [arc_lo, arc_hi) (arc mode)
-    uint32_t arc_lo = 0, arc_hi = 0;
+    // arc mode (cx_arc_build): [replicated top planes | planes below arc_Lh for
+    // the arc_M peers from arc_plo (the arc and its halo)] of the cz table
+    uint64_t *d_arc_tree = nullptr;
+    ArcBound *d_arc_bounds = nullptr;  // last peer ID of each non-empty arc
+    int arc_world = 0, arc_rank = -1, arc_Lh = 128, arc_nb = 0;
+    uint32_t arc_plo = 0, arc_M = 0;
 
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
     uint32_t *d_ring_key = nullptr; // ID slices [n] of the streaming finger build
@@ -271,6 +275,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_succs);
     (void)hipFree(r->d_scratch);
     (void)hipFree(r->d_arc_tree);
+    (void)hipFree(r->d_arc_bounds);
     (void)hipFree(r->d_stats);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
     delete r;
@@ -560,21 +565,11 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
     return finish_out(owner, dout, q, memkind, s);
 }
 
-int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
-    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    int rc = use_device(ring);
-    if (rc) return rc;
-    hipStream_t s = ring->stream;
-    const size_t cnt = ring->n * CX_FINGERS;
-    if (!ring->d_fingers) {
-        hipError_t e = hipMalloc(&ring->d_fingers, cnt * sizeof(uint32_t));
-        if (e != hipSuccess) {
-            ring->d_fingers = nullptr;
-            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
-        }
-    }
-    // streaming per-block window build (needs the directory and the top
-    // halves); CX_FINGERS_SEARCH=1 keeps the one-search-per-entry kernel (A/B)
+namespace {
+// The converged n x 128 finger table into ring->d_fingers (allocated).
+int build_fingers_table(cx_ring *ring, hipStream_t s) {
+    // streaming per-block window build (needs the directory and the ID
+    // slices); CX_FINGERS_SEARCH=1 keeps one search per entry (A/B)
     static const bool search_only = getenv("CX_FINGERS_SEARCH") != nullptr;
     SearchView fv = ring->sv();
     fv.dir = ring->d_dir;
@@ -591,6 +586,25 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
                               streaming ? fws.p : nullptr, ring->d_fingers, s));
     ring->fingers_converged = true;
+    ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
+    return CX_OK;
+}
+}  // namespace
+
+int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    const size_t cnt = ring->n * CX_FINGERS;
+    if (!ring->d_fingers) {
+        hipError_t e = hipMalloc(&ring->d_fingers, cnt * sizeof(uint32_t));
+        if (e != hipSuccess) {
+            ring->d_fingers = nullptr;
+            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
+        }
+    }
+    if ((rc = build_fingers_table(ring, s))) return rc;
     route_geometry(ring);
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
@@ -1245,34 +1259,116 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
 }
 
 // ---- arc-sharded routing --------------------------------------------------
-int cx_arc_build(cx_ring *ring, uint32_t lo, uint32_t hi) {
+int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(lo <= hi && hi <= ring->n, CX_E_INVALID, "arc must satisfy lo <= hi <= n");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(rank >= 0 && rank < world, CX_E_INVALID, "rank out of range");
+    CX_CHECK(top_levels >= 0 && top_levels <= (int)CX_FINGERS, CX_E_INVALID,
+             "top_levels must be in [0, 128]");
     int rc = use_device(ring);
     if (rc) return rc;
     hipStream_t s = ring->stream;
+    const size_t n = ring->n;
+    // the converged finger table (streaming build; no route table); one built
+    // here only to derive the planes is released afterwards (the walk finds
+    // exact below-table fingers by directory search)
+    const bool own_fingers = !ring->d_fingers || !ring->fingers_converged;
+    if (own_fingers) {
+        if (!ring->d_fingers &&
+            hipMalloc(&ring->d_fingers, n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
+            ring->d_fingers = nullptr;
+            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
+        }
+        if ((rc = build_fingers_table(ring, s))) return rc;
+    }
     route_geometry(ring);
     if (!ring->d_ring_ext) {
-        CX_HIP(hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)));
-        CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
+        CX_HIP(hipMalloc(&ring->d_ring_ext, (n + 1) * sizeof(cell128)));
+        CX_HIP(cxk::ring_ext_build(ring->d_ring, n, ring->d_ring_ext, s));
+    }
+    const int l0 = ring->rt_l0;
+    int Lh = (int)CX_FINGERS - (top_levels ? top_levels : CX_ARC_TOP_LEVELS);
+    if (Lh < l0) Lh = l0;
+    const uint32_t lo = (uint32_t)((uint64_t)rank * n / world);
+    const uint32_t hi = (uint32_t)((uint64_t)(rank + 1) * n / world);
+    // local rows: the arc and the peers with IDs within 2^Lh before its first
+    // (a walk that needs a row below Lh is within 2^Lh of its key)
+    uint32_t plo = lo, M = hi - lo;
+    if (world == 1) {
+        plo = 0;
+        M = (uint32_t)n;
+    } else if (hi > lo) {
+        cell128 prev;
+        CX_HIP(hipMemcpy(&prev, ring->d_ring + (lo == 0 ? n - 1 : lo - 1), sizeof(prev),
+                         hipMemcpyDeviceToHost));
+        const cell128 start = to_cell(to_u128(prev) - ((u128)1 << Lh) + 1);
+        cell128 *dk = reinterpret_cast<cell128 *>(ring->d_scratch + 192);
+        uint32_t *dout = ring->d_scratch + 188;
+        CX_HIP(hipMemcpyAsync(dk, &start, sizeof(start), hipMemcpyHostToDevice, s));
+        SearchView v = ring->sv();
+        v.dir = ring->d_dir;
+        CX_HIP(cxk::successor(v, dk, 1, dout, s));
+        CX_HIP(hipMemcpyAsync(&plo, dout, sizeof(plo), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        const uint64_t halo = ((uint64_t)lo + n - plo) % n;
+        if (halo + (hi - lo) >= n) {
+            plo = 0;
+            M = (uint32_t)n;
+        } else {
+            M = (uint32_t)(halo + (hi - lo));
+        }
     }
     (void)hipFree(ring->d_arc_tree);
     ring->d_arc_tree = nullptr;
-    ring->arc_lo = ring->arc_hi = 0;
-    const size_t rows = (size_t)(hi - lo) * ring->rt_R;
-    if (rows) {
-        if (hipMalloc(&ring->d_arc_tree, rows * 64) != hipSuccess) {
-            ring->d_arc_tree = nullptr;
-            return fail(CX_E_NOMEM, "hipMalloc of the arc tree rows failed");
-        }
+    ring->arc_world = 0;
+    const size_t top_ent = (size_t)((int)CX_FINGERS - Lh) * 2 * n;
+    const size_t low_ent = (size_t)(Lh - l0) * 2 * M;
+    if (hipMalloc(&ring->d_arc_tree, (top_ent + low_ent) * 64 + 64) != hipSuccess) {
+        ring->d_arc_tree = nullptr;
+        return fail(CX_E_NOMEM, "hipMalloc of the arc route planes failed");
     }
-    SearchView v = ring->sv();
-    v.dir = ring->d_dir;  // the arc build and walk always search the directory
-    CX_HIP(cxk::tree_build_arc(v, ring->d_ring, ring->n, lo, hi, ring->rt_l0, ring->rt_R,
-                               ring->pk_ib, ring->d_arc_tree, s));
-    ring->arc_lo = lo;
-    ring->arc_hi = hi;
+    CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
+    CX_HIP(cxk::cz_build_part(ring->d_fingers, ring->d_ring, n, Lh, (int)CX_FINGERS - Lh, 0,
+                              (uint32_t)n, ring->pk_ib, ring->d_arc_tree, ring->d_scratch, s));
+    CX_HIP(cxk::cz_build_part(ring->d_fingers, ring->d_ring, n, l0, Lh - l0, plo, M, ring->pk_ib,
+                              ring->d_arc_tree + top_ent * 8, ring->d_scratch, s));
+    // WALK destinations: the last peer ID of every non-empty arc, ascending
+    std::vector<ArcBound> b;
+    for (int g = 0; g < world; ++g) {
+        const uint64_t glo = (uint64_t)g * n / world, ghi = (uint64_t)(g + 1) * n / world;
+        if (ghi <= glo) continue;
+        cell128 id;
+        CX_HIP(hipMemcpy(&id, ring->d_ring + ghi - 1, sizeof(id), hipMemcpyDeviceToHost));
+        b.push_back(ArcBound{id.lo, id.hi, (uint32_t)g, 0});
+    }
+    (void)hipFree(ring->d_arc_bounds);
+    ring->d_arc_bounds = nullptr;
+    CX_HIP(hipMalloc(&ring->d_arc_bounds, b.size() * sizeof(ArcBound)));
+    CX_HIP(hipMemcpy(ring->d_arc_bounds, b.data(), b.size() * sizeof(ArcBound),
+                     hipMemcpyHostToDevice));
     CX_HIP(hipStreamSynchronize(s));
+    if (own_fingers) {
+        (void)hipFree(ring->d_fingers);
+        ring->d_fingers = nullptr;
+        ring->fingers_converged = false;
+    }
+    ring->arc_world = world;
+    ring->arc_rank = rank;
+    ring->arc_Lh = Lh;
+    ring->arc_plo = plo;
+    ring->arc_M = M;
+    ring->arc_nb = (int)b.size();
+    return CX_OK;
+}
+
+int cx_arc_info(const cx_ring *ring, int *top_levels, uint64_t *local_rows,
+                uint64_t *table_bytes) {
+    CX_CHECK(ring && top_levels && local_rows && table_bytes, CX_E_INVALID, "null argument");
+    CX_CHECK(ring->arc_world > 0, CX_E_STATE, "arc not built (cx_arc_build)");
+    *top_levels = (int)CX_FINGERS - ring->arc_Lh;
+    *local_rows = ring->arc_M;
+    *table_bytes = ((uint64_t)((int)CX_FINGERS - ring->arc_Lh) * 2 * ring->n +
+                    (uint64_t)(ring->arc_Lh - ring->rt_l0) * 2 * ring->arc_M) * 64;
     return CX_OK;
 }
 
@@ -1292,17 +1388,36 @@ int cx_arc_seed(const cx_ring *ring, int rank, const uint32_t *src, const cx_u12
 int cx_arc_step(const cx_ring *ring, int rank, const cx_arc_rec *in, size_t q, cx_arc_rec *out,
                 uint32_t *owner, uint8_t *hops, uint8_t *status) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(ring->d_ring_ext && (ring->d_arc_tree || ring->arc_lo == ring->arc_hi), CX_E_STATE,
-             "arc not built (cx_arc_build)");
+    CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(rank == ring->arc_rank, CX_E_INVALID, "rank differs from the one cx_arc_build used");
     CX_CHECK(rank >= 0 && rank < CX_ARC_MAX_RANKS, CX_E_INVALID, "rank out of range");
     CX_CHECK(q == 0 || (in && out && owner && hops), CX_E_INVALID, "null buffer");
     int rc = use_device(ring);
     if (rc) return rc;
     SearchView v = ring->sv();
+    v.dir = ring->d_dir;  // exact below-table fingers by directory search
+    CX_HIP(cxk::route_arc(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree, ring->rt_l0,
+                          ring->rt_R, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
+                          ring->arc_M, rank, reinterpret_cast<const ArcRec *>(in), nullptr,
+                          nullptr, q, reinterpret_cast<ArcRec *>(out), owner, hops, status,
+                          ring->stream));
+    return CX_OK;
+}
+
+int cx_arc_start(const cx_ring *ring, int rank, const uint32_t *src, const cx_u128 *keys,
+                 size_t q, cx_arc_rec *out, uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(rank == ring->arc_rank, CX_E_INVALID, "rank differs from the one cx_arc_build used");
+    CX_CHECK(q < (1ull << ARC_ORIGIN_SHIFT), CX_E_INVALID, "too many lookups for one rank");
+    CX_CHECK(q == 0 || (src && keys && out && owner && hops), CX_E_INVALID, "null buffer");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    SearchView v = ring->sv();
     v.dir = ring->d_dir;
     CX_HIP(cxk::route_arc(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree, ring->rt_l0,
-                          ring->rt_R, ring->pk_ib, v, ring->arc_lo, ring->arc_hi, rank,
-                          reinterpret_cast<const ArcRec *>(in), q,
+                          ring->rt_R, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo, ring->arc_M,
+                          rank, nullptr, src, reinterpret_cast<const cell128 *>(keys), q,
                           reinterpret_cast<ArcRec *>(out), owner, hops, status, ring->stream));
     return CX_OK;
 }
@@ -1313,13 +1428,15 @@ int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t
     CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
     CX_CHECK(q == 0 || (recs && send), CX_E_INVALID, "null buffer");
     CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many records for one step");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
     int rc = use_device(ring);
     if (rc) return rc;
     hipStream_t s = ring->stream;
     uint32_t *dcnt = ring->d_scratch, *dcur = ring->d_scratch + CX_ARC_MAX_RANKS;
     CX_HIP(hipMemsetAsync(dcnt, 0, CX_ARC_MAX_RANKS * sizeof(uint32_t), s));
-    CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->n, world, dcnt,
-                           nullptr, nullptr, s, false));
+    CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->d_arc_bounds,
+                           ring->arc_nb, world, dcnt, nullptr, nullptr, s, false));
     uint32_t hc[CX_ARC_MAX_RANKS], hcur[CX_ARC_MAX_RANKS];
     CX_HIP(hipMemcpyAsync(hc, dcnt, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
@@ -1331,8 +1448,9 @@ int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t
     }
     if (acc) {
         CX_HIP(hipMemcpyAsync(dcur, hcur, world * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->n, world,
-                               nullptr, dcur, reinterpret_cast<ArcRec *>(send), s, true));
+        CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->d_arc_bounds,
+                               ring->arc_nb, world, nullptr, dcur,
+                               reinterpret_cast<ArcRec *>(send), s, true));
         // hcur is a stack buffer: the copy must complete before we return
         CX_HIP(hipStreamSynchronize(s));
     }

@@ -1373,11 +1373,19 @@ struct PkCtx {
     u128 W;
     // variant 5 (cz): gap-code shift of a compressed node
     int gs;
-    // arc mode: only rows [lo, hi) are local; F is absent (fingers by search)
+    // arc mode (cz rows): levels >= Lh are replicated; below Lh only the M
+    // peers plo, plo + 1, ... (cyclic: the rank's arc and its halo) have rows
+    // and no finger table: exact below-table fingers by directory search
     bool arc;
-    uint32_t lo, hi;
+    int Lh;
+    uint32_t plo, M;
     SearchView sv;
 };
+
+__device__ __forceinline__ bool arc_row_local(const PkCtx &c, uint32_t cur) {
+    const uint32_t j = cur >= c.plo ? cur - c.plo : cur + c.n - c.plo;
+    return j < c.M;
+}
 
 // finger(p, i) = succ(id_p + 2^i) on the converged ring (k_fingers' rule).
 __device__ __forceinline__ uint32_t finger_of(const SearchView &sv, const cell128 *ring, uint32_t n,
@@ -1747,15 +1755,13 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
         }
         cs = -1;
         if (i >= c.l0) {
-            if (c.arc && (cur < c.lo || cur >= c.hi)) return 2;  // row lives on another rank
             mode = A_HOP;
             lvl = i;
             return 0;
         }
         // rare: below the table -> exact finger + exact ids
         const u128 idc = cex ? clo : ld128(c.ring + cur);
-        const uint32_t nxt = c.arc ? finger_of(c.sv, c.ring, c.n, cur, i, idc)
-                                   : c.F[(size_t)cur * CX_FINGERS + i];
+        const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
         const u128 idn = ld128(c.ring + nxt);
         ++h;
         if (key - idc <= idn - idc) {
@@ -1830,17 +1836,22 @@ __device__ __forceinline__ uint32_t cz_next(uint32_t n, uint32_t cur, int l, uin
     return (uint32_t)t;
 }
 
-__global__ void k_cz_build(const uint32_t *F, const cell128 *ring, uint32_t n, int l0, int R,
-                           int gs, uint4 *cz, uint32_t *esc) {
-    const size_t total = (size_t)n * R * 2;
+// Planes [lvl_base, lvl_base + nlev) of the table for the M peers p_first,
+// p_first + 1, ... (cyclic): the whole table (lvl_base = l0, nlev = R,
+// p_first = 0, M = n), or an arc rank's replicated top levels / local rows.
+__global__ void k_cz_build(const uint32_t *F, const cell128 *ring, uint32_t n, int lvl_base,
+                           int nlev, uint32_t p_first, uint32_t M, int gs, uint4 *cz,
+                           uint32_t *esc) {
+    const size_t total = (size_t)M * nlev * 2;
     uint32_t bad = 0;
     for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
          t += (size_t)gridDim.x * blockDim.x) {
-        // level-major: t = ((i - l0) * 2 + b) * n + p (see the walk's entry index)
-        const size_t plane = t / n;
-        const size_t p = t - plane * n;
+        // level-major: t = ((i - lvl_base) * 2 + b) * M + j (the walk's entry index)
+        const size_t plane = t / M;
+        const size_t j = t - plane * M;
+        const size_t p = (p_first + j) % n;
         const int b = (int)(plane & 1);
-        const int i = l0 + (int)(plane >> 1);
+        const int i = lvl_base + (int)(plane >> 1);
         uint32_t node[16], out[16];
         u128 nid[16];
         const u128 idp = ld128(ring + p);
@@ -1884,8 +1895,16 @@ __global__ void k_cz_build(const uint32_t *F, const cell128 *ring, uint32_t n, i
 
 hipError_t cz_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
                     uint64_t *cz, uint32_t *esc, hipStream_t s) {
-    k_cz_build<<<cx_grid(n * (size_t)R * 2, 256), 256, 0, s>>>(
-        F, ring, (uint32_t)n, l0, R, cz_shift(ib), reinterpret_cast<uint4 *>(cz), esc);
+    return cz_build_part(F, ring, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s);
+}
+
+hipError_t cz_build_part(const uint32_t *F, const cell128 *ring, size_t n, int lvl_base, int nlev,
+                         uint32_t p_first, uint32_t M, int ib, uint64_t *cz, uint32_t *esc,
+                         hipStream_t s) {
+    if (M == 0 || nlev <= 0) return hipSuccess;
+    k_cz_build<<<cx_grid((size_t)M * nlev * 2, 256), 256, 0, s>>>(
+        F, ring, (uint32_t)n, lvl_base, nlev, p_first, M, cz_shift(ib),
+        reinterpret_cast<uint4 *>(cz), esc);
     return hipGetLastError();
 }
 
@@ -1910,7 +1929,8 @@ __device__ __forceinline__ int cz_exact(const PkCtx &c, u128 key, u128 &clo, uin
                                         uint64_t &dmax, uint32_t &cur, uint32_t &h, int i,
                                         uint32_t &own, uint8_t &st, uint32_t *xc = nullptr) {
     if (xc) ++*xc;  // counter build only: one F gather + one ring gather
-    const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
+    const uint32_t nxt =
+        c.arc ? finger_of(c.sv, c.ring, c.n, cur, i, clo) : c.F[(size_t)cur * CX_FINGERS + i];
     const u128 idn = ld128(c.ring + nxt);
     ++h;
     if (key - clo <= idn - clo) {
@@ -1996,6 +2016,9 @@ __device__ __forceinline__ int cz_plan(const PkCtx &c, u128 key, u128 &clo, bool
         }
         cs = -1;
         if (i >= c.l0) {
+            // arc mode: a row below the replicated levels that this rank does
+            // not hold -> the lookup continues on the rank of its key's arc
+            if (c.arc && i < c.Lh && !arc_row_local(c, cur)) return 2;
             mode = A_HOP;
             lvl = i;
             rb = (int)((dmax >> (i - 1 - c.gs)) & 1);  // bit i-1 of d - 2^i
@@ -2017,8 +2040,9 @@ struct TreeIO {
     const uint4 *tree;
     int l0, R, ib;
     const uint32_t *F;
-    SearchView sv;
-    uint32_t lo, hi;
+    int Lh;              // arc mode: first replicated level
+    uint32_t plo, M;     // arc mode: local rows (cyclic peer range)
+    SearchView sv;       // arc mode: directory of the replicated ring
     const uint32_t *src;
     const cell128 *keys;
     const ArcRec *in;
@@ -2040,7 +2064,7 @@ template <bool ARC, bool CZ, bool STATS = false>
 __global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(CZ ? CZ_WAVES : 1)))
 void k_route_tree(TreeIO io) {
     constexpr int RW = CZ ? CZ_RES_WIN : RES_WIN;  // cz: smaller window, more waves per CU
-    static_assert(!(ARC && CZ), "arc mode walks variant-4 rows");
+    static_assert(!ARC || CZ, "arc mode walks pattern-keyed (cz) rows");
     __shared__ uint64_t res_all[ARC ? 1 : RT_BLOCK / 64][ARC ? 1 : RW];
     __shared__ uint4 ent_all[RT_BLOCK][4];       // each lane's current 64-B entry
     __shared__ uint64_t addr_all[RT_BLOCK];      // entry index + 1 wanted by each lane (0: none)
@@ -2068,8 +2092,9 @@ void k_route_tree(TreeIO io) {
     c.W = ((u128)1 << c.S) - 1;
     c.gs = cz_shift(ib);
     c.arc = ARC;
-    c.lo = io.lo;
-    c.hi = io.hi;
+    c.Lh = io.Lh;
+    c.plo = io.plo;
+    c.M = io.M;
     c.sv = io.sv;
     size_t head = base, flushed = base;
 
@@ -2126,17 +2151,17 @@ void k_route_tree(TreeIO io) {
                 (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
             if (bst == B_EMPTY && rank < avail) {
                 pq = head + rank;
-                if (ARC) {
+                if (ARC && io.in) {
                     const ArcRec r = io.in[pq];
                     pkey = ((u128)r.w1 << 64) | r.w0;
                     pqid = r.qid;
                     psrc = r.cur;
                     ph = r.hk & 0xFF;
                     pkind = (int)(r.hk >> 8);
-                } else {
+                } else {  // a new lookup (arc mode: issued on this rank)
                     pkey = ld128(io.keys + pq);
                     psrc = io.src[pq];
-                    pqid = pq;
+                    pqid = ARC ? ((uint64_t)io.self << ARC_ORIGIN_SHIFT) | pq : pq;
                     ph = 0;
                     pkind = ARC_NEW;
                 }
@@ -2155,9 +2180,18 @@ void k_route_tree(TreeIO io) {
             // ([level][b][peer]): a wave's first hops leave ~64 consecutive
             // source peers, mostly at the top level or two, so their entries
             // share DRAM pages and 128-B lines instead of lying 4 KiB apart.
-            const uint64_t e =
-                CZ ? (uint64_t)((lvl - l0) * 2 + rb) * n + cur
-                   : (uint64_t)(cur - io.lo) * (unsigned)R + (unsigned)(lvl - l0);
+            uint64_t e;
+            if (!CZ) {
+                e = (uint64_t)cur * (unsigned)R + (unsigned)(lvl - l0);
+            } else if (!ARC) {
+                e = (uint64_t)((lvl - l0) * 2 + rb) * n + cur;
+            } else if (lvl >= io.Lh) {  // replicated top planes, all peers
+                e = (uint64_t)((lvl - io.Lh) * 2 + rb) * n + cur;
+            } else {  // this rank's rows (arc + halo), after the top planes
+                const uint32_t j = cur >= io.plo ? cur - io.plo : cur + n - io.plo;
+                e = (uint64_t)(CX_FINGERS - io.Lh) * 2 * n +
+                    (uint64_t)((lvl - l0) * 2 + rb) * io.M + j;
+            }
             addr_all[threadIdx.x] = mode == A_HOP ? e + 1 : 0;
             if (STATS) {
                 n_g64 += mode == A_HOP;
@@ -2276,7 +2310,7 @@ void k_route_tree(TreeIO io) {
                              own, st, xcp)
                    : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
             if (r == 1) fin = true;
-            if (ARC && r == 2) {  // continue on the rank that owns cur's row
+            if (ARC && r == 2) {  // continue on the rank of the key's arc
                 ArcRec o;
                 o.w0 = (uint64_t)key;
                 o.w1 = (uint64_t)(key >> 64);
@@ -2399,8 +2433,6 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
     io.R = R;
     io.ib = ib;
     io.F = F;
-    io.lo = 0;
-    io.hi = (uint32_t)n;
     io.src = src;
     io.keys = keys;
     io.q = q;
@@ -2431,8 +2463,6 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
     io.R = R;
     io.ib = ib;
     io.F = F;
-    io.lo = 0;
-    io.hi = (uint32_t)n;
     io.src = src;
     io.keys = keys;
     io.q = q;
@@ -2455,66 +2485,35 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
 }
 
 // ---------------------------------------------------------------------------
-// Arc-sharded mode (SURVEY 8e layout 2): rows of the arc [lo, hi) only, built
-// by directory searches on the replicated ring (no full finger table).
+// Arc-sharded mode (SURVEY 8e layout 2), two phases per lookup.  Every rank
+// holds the replicated ring, the pattern-keyed (cz) planes of the top levels
+// [Lh, 128) for all peers, and the planes below Lh only for its arc of peers
+// plus a halo: the peers whose IDs lie within 2^Lh before the arc's first
+// peer.  Phase 1 walks on the origin rank while the rows it needs are
+// replicated; once the walk needs a level below Lh, d = key - id_cur < 2^Lh,
+// so cur and every later peer lie in (key - 2^Lh, key]: inside the arc of the
+// key's owner plus its halo.  The lookup travels there once (a WALK record)
+// and finishes; results travel home once (RESULT records).
 // ---------------------------------------------------------------------------
-__global__ void k_tree_build_arc(SearchView sv, const cell128 *ring, uint32_t n, uint32_t lo,
-                                 uint32_t hi, int l0, int R, int ib, uint64_t *tree) {
-    const size_t total = (size_t)(hi - lo) * R;
-    const int S = 64 + ib;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-         t += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = t / (unsigned)R;
-        const uint32_t p = lo + (uint32_t)r;
-        const int i = l0 + (int)(t - r * (unsigned)R);
-        const int par[8] = {-1, 0, 0, 1, 0, 1, 2, 3};
-        const int off[8] = {0, 1, 2, 2, 3, 3, 3, 3};
-        uint32_t f[8];
-        u128 id[8];
-        f[0] = finger_of(sv, ring, n, p, i, ld128(ring + p));
-        id[0] = ld128(ring + f[0]);
-#pragma unroll
-        for (int sl = 1; sl < 8; ++sl) {
-            const int lv = i - off[sl];
-            if (lv >= 0 && f[par[sl]] != CX_NONE) {
-                f[sl] = finger_of(sv, ring, n, f[par[sl]], lv, id[par[sl]]);
-                id[sl] = ld128(ring + f[sl]);
-            } else {
-                f[sl] = CX_NONE;
-                id[sl] = 0;
-            }
-        }
-        uint64_t *e = tree + t * 8;
-#pragma unroll
-        for (int sl = 0; sl < 8; ++sl)
-            e[sl] = f[sl] == CX_NONE ? ~0ull : (((uint64_t)(id[sl] >> S) << ib) | f[sl]);
-    }
-}
-
-hipError_t tree_build_arc(const SearchView &sv, const cell128 *ring, size_t n, uint32_t lo,
-                          uint32_t hi, int l0, int R, int ib, uint64_t *tree, hipStream_t s) {
-    if (hi <= lo) return hipSuccess;
-    k_tree_build_arc<<<cx_grid((size_t)(hi - lo) * R, 256), 256, 0, s>>>(sv, ring, (uint32_t)n,
-                                                                         lo, hi, l0, R, ib, tree);
-    return hipGetLastError();
-}
-
-hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *tree,
-                     int l0, int R, int ib, const SearchView &sv, uint32_t lo, uint32_t hi,
-                     int self, const ArcRec *in, size_t q, ArcRec *out, uint32_t *owner,
-                     uint8_t *hops, uint8_t *status, hipStream_t s) {
+hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                     int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo, uint32_t M,
+                     int self, const ArcRec *in, const uint32_t *src, const cell128 *keys, size_t q,
+                     ArcRec *out, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
     if (q == 0) return hipSuccess;
     TreeIO io = {};
+    io.src = src;  // in == nullptr: new lookups read straight from src / keys
+    io.keys = keys;
     io.ring_ext = ring_ext;
     io.ring = ring;
     io.n = (uint32_t)n;
-    io.tree = reinterpret_cast<const uint4 *>(tree);
+    io.tree = reinterpret_cast<const uint4 *>(cz);
     io.l0 = l0;
     io.R = R;
     io.ib = ib;
     io.sv = sv;
-    io.lo = lo;
-    io.hi = hi;
+    io.Lh = Lh;
+    io.plo = plo;
+    io.M = M;
     io.in = in;
     io.out = out;
     io.self = self;
@@ -2522,9 +2521,14 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
     io.owner = owner;
     io.hops = hops;
     io.status = status;
-    unsigned blocks;
-    tree_geometry(q, io.chunk, blocks);
-    k_route_tree<true, false><<<blocks, RT_BLOCK, 0, s>>>(io);
+    static const unsigned resident = resident_grid(k_route_tree<true, true>, RT_BLOCK);
+    size_t waves = (size_t)resident * (RT_BLOCK / 64);
+    const size_t small = (q + 1023) / 1024;
+    if (small < waves) waves = small ? small : 1;
+    io.chunk = (q + waves - 1) / waves;
+    waves = (q + io.chunk - 1) / io.chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
+    k_route_tree<true, true><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 
@@ -2551,55 +2555,86 @@ hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self
     return hipGetLastError();
 }
 
-// Destination rank of an outcome record: WALK -> owner of cur's row, RESULT
-// -> origin rank, NONE -> -1.  Arc g = [g n / G, (g+1) n / G).
-__device__ __forceinline__ int arc_dest(const ArcRec &r, uint32_t n, int G) {
+// Destination rank of an outcome record: WALK -> the rank whose arc holds the
+// owner of the record's key (bounds: the last peer ID of every non-empty arc,
+// ascending, with its rank), RESULT -> origin rank, NONE -> -1.
+__device__ __forceinline__ int arc_dest(const ArcRec &r, const ArcBound *bounds, int nb, int G) {
     const uint32_t kind = r.hk >> 8;
     if (kind == ARC_RESULT) {
         const uint64_t o = r.qid >> ARC_ORIGIN_SHIFT;
         return o < (uint64_t)G ? (int)o : -1;
     }
-    if ((kind != ARC_WALK && kind != ARC_NEW) || r.cur >= n) return -1;
-    int g = (int)(((uint64_t)r.cur * (uint64_t)G) / n);
-    if (g >= G) g = G - 1;
-    while (g > 0 && (uint32_t)(((uint64_t)g * n) / G) > r.cur) --g;
-    while (g + 1 < G && (uint32_t)(((uint64_t)(g + 1) * n) / G) <= r.cur) ++g;
-    return g;
+    if (kind != ARC_WALK || nb == 0) return -1;
+    const u128 k = ((u128)r.w1 << 64) | r.w0;
+    int lo = 0, hi = nb;  // first bound >= key; past the last one the owner wraps to arc 0
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (((u128)bounds[mid].hi << 64 | bounds[mid].lo) < k) lo = mid + 1;
+        else hi = mid;
+    }
+    return (int)bounds[lo == nb ? 0 : lo].rank;
 }
 
 // Bucket outcome records by destination: per-block LDS histograms, one global
 // atomic per (block, destination) to reserve ranges, LDS-local offsets.
 constexpr int ARC_MAX_RANKS = 64;
 
-__global__ void k_arc_count(const ArcRec *recs, size_t q, uint32_t n, int G, uint32_t *counts) {
+// Per-destination counts of one wave's records: one ballot per destination,
+// one LDS atomic per (wave, destination) present; returns the record's slot
+// among the block's records for its destination (base from the LDS counter).
+__device__ __forceinline__ uint32_t arc_wave_slots(int d, int G, uint32_t *h) {
+    const int lane = threadIdx.x & 63;
+    uint32_t slot = 0;
+    for (int j = 0; j < G; ++j) {
+        const uint64_t m = __ballot(d == j);
+        if (!m) continue;  // wave-uniform
+        const int leader = __builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&h[j], (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (d == j)
+            slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    return slot;
+}
+
+__global__ __launch_bounds__(256) void k_arc_count(const ArcRec *recs, size_t q,
+                                                   const ArcBound *bounds, int nb, int G,
+                                                   uint32_t *counts) {
     __shared__ uint32_t h[ARC_MAX_RANKS];
+    __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
     __syncthreads();
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const int d = arc_dest(recs[i], n, G);
-        if (d >= 0) atomicAdd(&h[d], 1u);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i0 = blockIdx.x * (size_t)blockDim.x; i0 < q; i0 += stride) {  // uniform trips
+        const size_t i = i0 + threadIdx.x;
+        const int d = i < q ? arc_dest(recs[i], sb, nb, G) : -1;
+        (void)arc_wave_slots(d, G, h);
     }
     __syncthreads();
     for (int j = threadIdx.x; j < G; j += blockDim.x)
         if (h[j]) atomicAdd(&counts[j], h[j]);
 }
 
-__global__ void k_arc_scatter(const ArcRec *recs, size_t q, uint32_t n, int G,
-                              uint32_t *cursor, ArcRec *send) {
+__global__ __launch_bounds__(256) void k_arc_scatter(const ArcRec *recs, size_t q,
+                                                     const ArcBound *bounds, int nb, int G,
+                                                     uint32_t *cursor, ArcRec *send) {
     __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
+    __shared__ ArcBound sb[ARC_MAX_RANKS];
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
     for (size_t b0 = (size_t)blockIdx.x * blockDim.x; b0 < q; b0 += (size_t)gridDim.x * blockDim.x) {
         for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
         __syncthreads();
         const size_t i = b0 + threadIdx.x;
         int d = -1;
-        uint32_t slot = 0;
         ArcRec r;
         if (i < q) {
             r = recs[i];
-            d = arc_dest(r, n, G);
-            if (d >= 0) slot = atomicAdd(&h[d], 1u);
+            d = arc_dest(r, sb, nb, G);
         }
+        const uint32_t slot = arc_wave_slots(d, G, h);
         __syncthreads();
         for (int j = threadIdx.x; j < G; j += blockDim.x)
             basep[j] = h[j] ? atomicAdd(&cursor[j], h[j]) : 0u;
@@ -2609,14 +2644,15 @@ __global__ void k_arc_scatter(const ArcRec *recs, size_t q, uint32_t n, int G,
     }
 }
 
-hipError_t arc_bucket(const ArcRec *recs, size_t q, size_t n, int G, uint32_t *counts_dev,
-                      uint32_t *cursor_dev, ArcRec *send, hipStream_t s, bool scatter) {
+hipError_t arc_bucket(const ArcRec *recs, size_t q, const ArcBound *bounds, int nb, int G,
+                      uint32_t *counts_dev, uint32_t *cursor_dev, ArcRec *send, hipStream_t s,
+                      bool scatter) {
     if (!scatter) {
-        if (q) k_arc_count<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, (uint32_t)n, G,
+        if (q) k_arc_count<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, bounds, nb, G,
                                                                  counts_dev);
         return hipGetLastError();
     }
-    if (q) k_arc_scatter<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, (uint32_t)n, G,
+    if (q) k_arc_scatter<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, bounds, nb, G,
                                                                cursor_dev, send);
     return hipGetLastError();
 }

@@ -25,6 +25,11 @@ struct alignas(16) ArcRec {
 };
 static_assert(sizeof(ArcRec) == 32, "ArcRec is 32 B");
 #define ARC_ORIGIN_SHIFT 40
+// Last peer ID of a non-empty arc and its rank (WALK destinations).
+struct ArcBound {
+    uint64_t lo, hi;
+    uint32_t rank, pad;
+};
 #define ARC_INDEX_MASK ((1ull << ARC_ORIGIN_SHIFT) - 1)
 enum { ARC_NEW = 0, ARC_RESULT = 1, ARC_WALK = 2, ARC_NONE = 3 };
 
@@ -109,16 +114,18 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
 // the walk's access pattern, over `bytes` of `table` (read only): entries/s.
 hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, double *rate,
                         hipStream_t s);
-hipError_t tree_build_arc(const SearchView &sv, const cell128 *ring, size_t n, uint32_t lo,
-                          uint32_t hi, int l0, int R, int ib, uint64_t *tree, hipStream_t s);
-hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *tree,
-                     int l0, int R, int ib, const SearchView &sv, uint32_t lo, uint32_t hi,
-                     int self, const ArcRec *in, size_t q, ArcRec *out, uint32_t *owner,
-                     uint8_t *hops, uint8_t *status, hipStream_t s);
+hipError_t cz_build_part(const uint32_t *F, const cell128 *ring, size_t n, int lvl_base, int nlev,
+                         uint32_t p_first, uint32_t M, int ib, uint64_t *cz, uint32_t *esc,
+                         hipStream_t s);
+hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                     int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo, uint32_t M,
+                     int self, const ArcRec *in, const uint32_t *src, const cell128 *keys, size_t q,
+                     ArcRec *out, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,
                     hipStream_t s);
-hipError_t arc_bucket(const ArcRec *recs, size_t q, size_t n, int G, uint32_t *counts_dev,
-                      uint32_t *cursor_dev, ArcRec *send, hipStream_t s, bool scatter);
+hipError_t arc_bucket(const ArcRec *recs, size_t q, const ArcBound *bounds, int nb, int G,
+                      uint32_t *counts_dev, uint32_t *cursor_dev, ArcRec *send, hipStream_t s,
+                      bool scatter);
 hipError_t nsucc(const SearchView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const SearchView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,

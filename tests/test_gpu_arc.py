@@ -17,27 +17,30 @@ def cx():
     return chordx
 
 
-def simulate(cx, ids_dev, G, srcs, keys, status=True):
+def simulate(cx, ids_dev, G, srcs, keys, status=True, top=0, fused=True):
     """Round loop of ArcRouter.route with G in-process 'ranks'."""
     import torch
     from chordx.arc import MAX_ROUNDS
     rings = [cx.Ring(ids_dev) for _ in range(G)]
     n = rings[0].n
     for g, r in enumerate(rings):
-        r.arc_build(g * n // G, (g + 1) * n // G)
+        r.arc_build(G, g, top)
     outs = []
     for g in range(G):
         q = keys[g].shape[0]
         outs.append((torch.full((q,), -7, dtype=torch.int32, device="cuda"),
                      torch.full((q,), 77, dtype=torch.uint8, device="cuda"),
                      torch.full((q,), 9, dtype=torch.uint8, device="cuda") if status else None))
-    recs = [rings[g].arc_seed(g, srcs[g], keys[g]) for g in range(G)]
+    # fused first step (cx_arc_start) or seed records + step, as ArcRouter may
+    recs = ([None] * G if fused else
+            [rings[g].arc_seed(g, srcs[g], keys[g]) for g in range(G)])
     rounds, sent = 0, 0
     for rounds in range(1, MAX_ROUNDS + 1):
         inbox = [[] for _ in range(G)]
         total = 0
         for g in range(G):
-            out = rings[g].arc_step(g, recs[g], *outs[g])
+            out = (rings[g].arc_start(g, srcs[g], keys[g], *outs[g]) if recs[g] is None
+                   else rings[g].arc_step(g, recs[g], *outs[g]))
             send, counts = rings[g].arc_bucket(G, out)
             total += sum(counts)
             for d, part in enumerate(torch.split(send, counts)):
@@ -72,7 +75,7 @@ def test_arc_route_equals_replicated(cx, O, n, G):
     import torch
     q = 4096
     ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C0 + n + G)
-    outs, rounds, sent = simulate(cx, ids_dev, G, srcs, keys)
+    outs, rounds, sent = simulate(cx, ids_dev, G, srcs, keys, fused=(n + G) % 2 == 0)
     for g in range(G):
         ow, hp, st = ring.route(srcs[g], keys[g])
         assert torch.equal(outs[g][0], ow), (n, G, g)
@@ -80,7 +83,7 @@ def test_arc_route_equals_replicated(cx, O, n, G):
         assert torch.equal(outs[g][2], st), (n, G, g)
     if G == 1:
         assert rounds == 1 and sent == 0
-    assert rounds <= 40
+    assert rounds <= 3  # origin step, arc step, result delivery
 
 
 def test_arc_route_matches_oracle(cx, O):
@@ -142,26 +145,34 @@ def test_arc_clustered_ring(cx, O):
 
 def test_arc_bucket_groups_by_destination(cx, O):
     """Bucket output: every WALK record lands in the block of the rank whose
-    arc holds its peer; RESULT records go to their origin; NONE dropped."""
+    arc holds its key's owner; RESULT records go to their origin; NONE
+    dropped."""
     import torch
     from chordx.arc import arc_of
     n, G = 1000, 5
-    ring = cx.Ring(torch.from_numpy(O.splitmix_keys(7, n).view(np.int64).copy()).cuda())
-    ring.arc_build(0, n // G)
+    ids = O.splitmix_keys(7, n)
+    ring = cx.Ring(torch.from_numpy(ids.view(np.int64).copy()).cuda())
+    ring.arc_build(G, 0)
+    R = O.ring_build(ids)
     q = 5000
     rng = np.random.default_rng(3)
     recs = np.zeros((q, 4), dtype=np.int64)
     kind = rng.integers(0, 4, q)
     kind[kind == 0] = 2
+    keys = O.splitmix_keys(11, q)
+    keys[:40] = R[rng.integers(0, n, 40)]  # keys equal to peer IDs (arc ends)
+    keys[40:45] = [[0, 0], [2**64 - 1, 2**64 - 1], R[-1], R[0], R[n // G - 1]]
+    owner = O.successor(R, keys)
     cur = rng.integers(0, n, q)
     origin = rng.integers(0, G, q)
+    recs[:, :2] = keys.view(np.int64)
     recs[:, 2] = (origin << 40) | np.arange(q)
     recs[:, 3] = (cur & 0xFFFFFFFF) | ((5 | (kind << 8)) << 32)
     send, counts = ring.arc_bucket(G, torch.from_numpy(recs).cuda())
     want = [0] * G
     dest = []
     for i in range(q):
-        d = -1 if kind[i] == 3 else (origin[i] if kind[i] == 1 else arc_of(int(cur[i]), n, G))
+        d = -1 if kind[i] == 3 else (origin[i] if kind[i] == 1 else arc_of(int(owner[i]), n, G))
         dest.append(d)
         if d >= 0:
             want[d] += 1
@@ -173,3 +184,18 @@ def test_arc_bucket_groups_by_destination(cx, O):
         idx = (blk[:, 2] & ((1 << 40) - 1)).tolist()
         assert sorted(idx) == sorted(i for i in range(q) if dest[i] == d)
         off += counts[d]
+
+
+@pytest.mark.parametrize("top", [1, 3, 6, 12])
+def test_arc_top_levels(cx, O, top):
+    """Fewer replicated levels mean larger halos (more local rows); every
+    split of the table gives the replicated route's answers."""
+    import torch
+    n, q, G = 20000, 3000, 4
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C3 + top)
+    outs, rounds, _ = simulate(cx, ids_dev, G, srcs, keys, top=top)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)
+        assert torch.equal(outs[g][2], st)
+    assert rounds <= 3

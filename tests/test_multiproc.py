@@ -79,8 +79,9 @@ class OracleArcEngine:
     def __init__(self, P, n):
         self.P, self.n = P, n
 
-    def arc_build(self, lo, hi):
-        self.lo, self.hi = lo, hi
+    def arc_build(self, world, rank):
+        from chordx.arc import arc_bounds
+        self.lo, self.hi = arc_bounds(self.n, world, rank)
 
     def arc_seed(self, rank, src, keys):
         import torch
