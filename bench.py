@@ -153,7 +153,7 @@ def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "sample": f"first {qa} keys of the rank-0 stream (of {len(keys_np)}) on {threads} "
                       f"threads ({dta:.1f} s), first {q1} on 1 thread ({dt1:.1f} s); "
-                      "oracle/chord_oracle.c or_route, -O3 -march=native",
+                      "oracle/chord_oracle.c or_route, gcc -O3 -march=x86-64-v3",
             "parity_on_sample": ok}
 
 

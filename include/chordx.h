@@ -111,6 +111,13 @@ int cx_ring_sync(const cx_ring *ring);
 int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *owner,
                  int memkind);
 
+/* GetPredecessor(key) (abstract_chord_peer.cpp:380-421) on the converged
+ * ring: the owner's predecessor, pred[i] = (owner(keys[i]) + n - 1) mod n --
+ * what StoredLocally's predecessor_, the successor-list shortcut and the
+ * forwarded GET_PRED all return there (a lone peer is its own predecessor). */
+int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *pred,
+                   int memkind);
+
 /* ---- a4/a6: fingers ----------------------------------------------------
  * Converged PopulateFingerTable (abstract_chord_peer.cpp:564-613): row p,
  * entry i = succ(GetNthRange(i).first) = succ(id_p + 2^i mod 2^128)
@@ -216,8 +223,12 @@ int cx_fill_splitmix(cx_u128 *out_device, size_t count, uint64_t seed, uint64_t 
 /* ---- hex codec of keys on the wire ----------------------
  * cx_hex_parse: ChordKey(hex, hashed = true) = uint256("0x" + s) (key.h:73-75)
  * for each string bytes[offsets[i] .. offsets[i+1]); digits of either case, no
- * prefix.  out = value mod 2^128 (the engine's ring value), ok[i] = 0 for an
- * empty string or a non-hex character (where boost's parse throws).
+ * prefix.  out = value mod 2^128 (the engine's ring value); ok[i] = 1 for a
+ * raw value < 2^128, 2 for a raw value >= 2^128 (33+ significant digits; the
+ * raw uint256 wraps mod 2^256 like Boost's unchecked cpp_int -- over 64 digits
+ * parity unpinned), 0 for an empty string or a non-hex character (where
+ * boost's parse throws).  The raw value only matters to InBetween's point
+ * test (key.h:108-113); cx_wire applies that corner (cx_wire.cpp wide_keys).
  * cx_hex_format: std::string(key) = IntToHexStr (key.h:41-47) -- lowercase,
  * no leading zeros, "0" for zero -- into out[32 i .. 32 i + len[i]), the rest of
  * each 32-byte slot zero.  Both run on the GPU. */

@@ -177,14 +177,16 @@ void or_nth_range(or_key id, int n, or_u256 *lb, or_u256 *ub) {
 }
 
 /* a5: FingerTable::Lookup, finger_table.h:115-130 -- linear first-match scan. */
-int or_finger_index(or_key id, or_key key) {
-    or_u256 v = u256_from128(k2u(key));
+static int finger_index_raw(or_key id, or_u256 v) {
     for (int i = 0; i < OR_FINGERS; ++i) {
         or_u256 lb, ub;
         or_nth_range(id, i, &lb, &ub);
         if (or_in_between(v, lb, ub, 1)) return i;
     }
     return -1; /* throw std::runtime_error("ChordKey not found") */
+}
+int or_finger_index(or_key id, or_key key) {
+    return finger_index_raw(id, u256_from128(k2u(key)));
 }
 
 /* ------------------------------------------------------------------------
@@ -254,6 +256,25 @@ void or_successor_batch(const or_key *ring, size_t n, const or_key *keys, size_t
     parallel_for(q, nthreads, succ_range, &c);
 }
 
+/* GetPredecessor, abstract_chord_peer.cpp:380-421, on the converged ring:
+ * predecessor_ of the key's owner (StoredLocally at the owner returns it,
+ * :388-390; the successor-list shortcut checks InBetween(pred_of_succ, succ),
+ * :394-401; a forwarded GET_PRED ends at the owner, :405-412); a lone peer
+ * has no predecessor set and returns itself (:383-385). */
+typedef struct { const or_key *ring; size_t n; const or_key *keys; uint32_t *out; } pred_ctx;
+static void pred_range(void *c, size_t b, size_t e) {
+    pred_ctx *s = (pred_ctx *)c;
+    for (size_t i = b; i < e; ++i) {
+        uint32_t o = or_successor(s->ring, s->n, s->keys[i]);
+        s->out[i] = s->n == 1 ? o : (o == 0 ? (uint32_t)(s->n - 1) : o - 1);
+    }
+}
+void or_predecessor_batch(const or_key *ring, size_t n, const or_key *keys, size_t q,
+                          uint32_t *pred, int nthreads) {
+    pred_ctx c = {ring, n, keys, pred};
+    parallel_for(q, nthreads, pred_range, &c);
+}
+
 /* ------------------------------------------------------------------------
  * a6: converged PopulateFingerTable, abstract_chord_peer.cpp:564-613.
  * Entry i of peer p = successor of GetNthRange(i).first.
@@ -315,9 +336,8 @@ static int succ_list_size(const or_peers *P, uint32_t p) {
 /* RemotePeerList::Lookup(key, succ = true), remote_peer_list.cpp:86-110:
  * first entry i with key in [previous, id_i] (InBetween inclusive, previous
  * starting at the list's starting key = the owner's id), else none. */
-static uint32_t succ_list_lookup(const or_peers *P, uint32_t p, or_key key) {
+static uint32_t succ_list_lookup(const or_peers *P, uint32_t p, or_u256 v) {
     or_u256 prev = u256_from128(k2u(P->ring[p]));
-    or_u256 v = u256_from128(k2u(key));
     const int sz = succ_list_size(P, p);
     for (int i = 0; i < sz; ++i) {
         uint32_t e = succ_entry(P, p, i);
@@ -331,7 +351,7 @@ static uint32_t succ_list_lookup(const or_peers *P, uint32_t p, or_key key) {
  * found entry if alive; the scan for a later living entry runs
  * `for (i = succ_ind; i % size < succ_ind; ++i)`, whose condition is false on
  * entry (succ_ind < size), so it never executes. */
-static uint32_t succ_list_lookup_living(const or_peers *P, uint32_t p, or_key key) {
+static uint32_t succ_list_lookup_living(const or_peers *P, uint32_t p, or_u256 key) {
     uint32_t s = succ_list_lookup(P, p, key);
     if (s == OR_NONE) return OR_NONE;
     if (peer_alive(P, s)) return s;
@@ -345,12 +365,17 @@ static uint32_t succ_list_lookup_living(const or_peers *P, uint32_t p, or_key ke
     return OR_NONE;
 }
 /* StoredLocally, abstract_chord_peer.cpp:720-725. */
-static int stored_locally(const or_peers *P, uint32_t p, or_key key) {
-    return or_in_between(u256_from128(k2u(key)), peer_min_key(P, p),
+static int stored_locally(const or_peers *P, uint32_t p, or_u256 key) {
+    return or_in_between(key, peer_min_key(P, p),
                          u256_from128(k2u(P->ring[p])), 1);
 }
 
-int or_route(const or_peers *P, uint32_t src, or_key key, uint32_t *owner, uint8_t *hops) {
+/* The walk on the key's raw uint256 value: GenericKey keeps uint256("0x"+s)
+ * unreduced (key.h:73-75), so a wire key of 33+ significant hex digits fails
+ * every InBetween point test (key.h:108-113) while the ranged tests reduce it
+ * mod 2^128 (key.h:116-118). */
+static int route_raw(const or_peers *P, uint32_t src, or_u256 key, uint32_t *owner,
+                     uint8_t *hops) {
     uint32_t cur = src;
     unsigned h = 0;
     for (;;) {
@@ -361,11 +386,13 @@ int or_route(const or_peers *P, uint32_t src, or_key key, uint32_t *owner, uint8
             return OR_Q_OK;
         }
         /* ChordPeer::ForwardRequest, chord_peer.cpp:185-211 */
-        int fi = or_finger_index(P->ring[cur], key);
-        if (fi < 0) { /* unreachable: key == id is always stored locally */
+        int fi = finger_index_raw(P->ring[cur], key);
+        if (fi < 0) { /* no range holds key == id (or, raw, id + 1): Lookup
+                       * throws "ChordKey not found" (finger_table.h:129);
+                       * unreachable for a key < 2^128, which its own id stores */
             *owner = OR_NONE;
             *hops = (uint8_t)h;
-            return OR_Q_HOPCAP;
+            return OR_Q_NOT_FOUND;
         }
         uint32_t nxt = P->F[(size_t)cur * OR_FINGERS + fi];
         if (nxt == OR_NONE) { /* the matching finger was never added: Lookup
@@ -411,6 +438,9 @@ int or_route(const or_peers *P, uint32_t src, or_key key, uint32_t *owner, uint8
         cur = nxt;
     }
 }
+int or_route(const or_peers *P, uint32_t src, or_key key, uint32_t *owner, uint8_t *hops) {
+    return route_raw(P, src, u256_from128(k2u(key)), owner, hops);
+}
 
 typedef struct {
     const or_peers *P; const uint32_t *src; const or_key *keys;
@@ -430,6 +460,16 @@ void or_route_batch(const or_peers *P, const uint32_t *src, const or_key *keys, 
                     uint32_t *owner, uint8_t *hops, uint8_t *status, int nthreads) {
     route_ctx c = {P, src, keys, owner, hops, status};
     parallel_for(q, nthreads, route_range, &c);
+}
+
+/* Raw-value walk: key i = hi[i]:lo[i] (bits 255..128 : 127..0). */
+void or_route_raw_batch(const or_peers *P, const uint32_t *src, const or_key *lo,
+                        const or_key *hi, size_t q, uint32_t *owner, uint8_t *hops,
+                        uint8_t *status) {
+    for (size_t i = 0; i < q; ++i) {
+        or_u256 v = {{lo[i].lo, lo[i].hi, hi[i].lo, hi[i].hi}};
+        status[i] = (uint8_t)route_raw(P, src[i], v, &owner[i], &hops[i]);
+    }
 }
 
 /* a10: GetNSuccessors, abstract_chord_peer.cpp:345-373. */

@@ -87,6 +87,10 @@ void or_fingers_rows(const or_key *ring, size_t n, size_t p0, size_t p1, uint32_
  * index, or -1 ("ChordKey not found"). */
 int or_finger_index(or_key id, or_key key);
 
+/* GetPredecessor (abstract_chord_peer.cpp:380-421) on the converged ring. */
+void or_predecessor_batch(const or_key *ring, size_t n, const or_key *keys, size_t q,
+                          uint32_t *pred, int nthreads);
+
 /* ---- a7-a9: routed lookup -------------------------------------------- */
 /* Per-peer state a ChordPeer carries into GetSuccessor/ForwardRequest.
  * min_keys == NULL -> converged min_key = ring[p-1]+1 (ring[p]+1 when n==1,
@@ -118,6 +122,10 @@ typedef struct {
 int or_route(const or_peers *P, uint32_t src, or_key key, uint32_t *owner, uint8_t *hops);
 void or_route_batch(const or_peers *P, const uint32_t *src, const or_key *keys, size_t q,
                     uint32_t *owner, uint8_t *hops, uint8_t *status, int nthreads);
+/* or_route on the raw uint256 key hi:lo (a wire key of 33-64 hex digits). */
+void or_route_raw_batch(const or_peers *P, const uint32_t *src, const or_key *lo,
+                        const or_key *hi, size_t q, uint32_t *owner, uint8_t *hops,
+                        uint8_t *status);
 
 /* ---- a10/a11: n successors ------------------------------------------- */
 /* GetNSuccessors (abstract_chord_peer.cpp:345-373): n routed lookups from src,

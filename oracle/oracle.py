@@ -170,10 +170,12 @@ def lib():
         L.or_ring_build.argtypes = [vp, sz, vp]
         L.or_successor_batch.argtypes = [vp, sz, vp, sz, vp, i]
         L.or_fingers_build.argtypes = [vp, sz, vp, i]
+        L.or_predecessor_batch.argtypes = [vp, sz, vp, sz, vp, i]
         L.or_fingers_rows.argtypes = [vp, sz, sz, sz, vp, i]
         L.or_finger_index.restype = i
         L.or_finger_index.argtypes = [_Key, _Key]
         L.or_route_batch.argtypes = [ctypes.POINTER(_Peers), vp, vp, sz, vp, vp, vp, i]
+        L.or_route_raw_batch.argtypes = [ctypes.POINTER(_Peers), vp, vp, vp, sz, vp, vp, vp]
         L.or_nsucc_batch.argtypes = [ctypes.POINTER(_Peers), vp, vp, sz, i, vp, vp, i]
         L.or_churn.restype = sz
         L.or_churn.argtypes = [vp, sz, vp, sz, vp, sz, vp, vp]
@@ -237,6 +239,14 @@ def successor(ring, keys, threads=None) -> np.ndarray:
     return out
 
 
+def predecessor(ring, keys, threads=None) -> np.ndarray:
+    ring, keys = _keys(ring), _keys(keys)
+    out = np.empty(len(keys), dtype=np.uint32)
+    lib().or_predecessor_batch(_p(ring), len(ring), _p(keys), len(keys), _p(out),
+                               threads or default_threads())
+    return out
+
+
 def fingers(ring, threads=None, rows=None) -> np.ndarray:
     ring = _keys(ring)
     n = len(ring)
@@ -282,6 +292,31 @@ def route(peers: Peers, src, keys, threads=None):
     status = np.empty(q, dtype=np.uint8)
     lib().or_route_batch(ctypes.byref(peers.s), _p(src), _p(keys), q, _p(owner), _p(hops),
                          _p(status), threads or default_threads())
+    return owner, hops, status
+
+
+def hex_value(s: str) -> int:
+    """GenericKey(s, hashed = true).value_ = uint256("0x" + s) (key.h:73-75) as
+    a Python int: Boost's unchecked 256-bit cpp_int keeps the value mod 2^256
+    (strings over 64 hex digits are parity unpinned: no reference fixture
+    holds one).  Raises ValueError where boost's parse throws."""
+    if not s or any(c not in "0123456789abcdefABCDEF" for c in s):
+        raise ValueError(f"not a hex key: {s!r}")
+    return int(s, 16) & ((1 << 256) - 1)
+
+
+def route_raw(peers: Peers, src, values):
+    """or_route on raw uint256 key values (Python ints < 2^256)."""
+    values = [int(v) for v in values]
+    lo = keys_from_ints([v & ((1 << 128) - 1) for v in values])
+    hi = keys_from_ints([v >> 128 for v in values])
+    src = np.ascontiguousarray(src, dtype=np.uint32)
+    q = len(values)
+    owner = np.empty(q, dtype=np.uint32)
+    hops = np.empty(q, dtype=np.uint8)
+    status = np.empty(q, dtype=np.uint8)
+    lib().or_route_raw_batch(ctypes.byref(peers.s), _p(src), _p(lo), _p(hi), q, _p(owner),
+                             _p(hops), _p(status))
     return owner, hops, status
 
 

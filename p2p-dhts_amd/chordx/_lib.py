@@ -38,7 +38,7 @@ EXPORTS = (
     "cx_version", "cx_last_error", "cx_device_count",
     "cx_ring_create", "cx_ring_destroy", "cx_ring_size", "cx_ring_ids",
     "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_use_own_stream", "cx_ring_sync",
-    "cx_successor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
+    "cx_successor", "cx_predecessor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
     "cx_peer_state_upload", "cx_liveness_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
     "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
     "cx_uuid5_dns", "cx_fill_splitmix",
@@ -88,6 +88,7 @@ def lib() -> ctypes.CDLL:
         "cx_ring_use_own_stream": ([vp], i),
         "cx_ring_sync": ([vp], i),
         "cx_successor": ([vp, vp, sz, vp, i], i),
+        "cx_predecessor": ([vp, vp, sz, vp, i], i),
         "cx_fingers_build": ([vp, vp, i], i),
         "cx_fingers_upload": ([vp, vp, i], i),
         "cx_fingers_device": ([vp, pp], i),

@@ -145,9 +145,15 @@ class DataBlock:
         self = cls.__new__(cls)
         self.n, self.m, self.p, self.device = n, m, p, device
         self.original = vals
-        f = encode([bytes((vals & 0xFF).astype(np.uint8))], n, m, p, device)[0] \
-            if vals.max(initial=0) < 256 else None
-        self.fragments = [(i + 1, f[i]) for i in range(n)] if f is not None else []
+        if vals.max(initial=0) >= 256:
+            # the reference re-encodes its int values (data_block.cpp:52-53);
+            # the GPU encoder takes bytes, and a value of 256 or more (only
+            # from fragments that were not encoded from bytes) has no byte
+            # form: refuse rather than return a wrong or empty fragment list
+            raise L.ChordError(L.CX_E_INVALID,
+                               "decoded value >= 256: cannot re-encode from bytes")
+        f = encode([bytes(vals.astype(np.uint8))], n, m, p, device)[0]
+        self.fragments = [(i + 1, f[i]) for i in range(n)]
         return self
 
     def decode(self) -> str:

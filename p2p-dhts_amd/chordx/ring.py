@@ -8,6 +8,7 @@ batched over keys and source peers:
   ---------------------------------------------  -----------------------------
   converged successor ring (Join/Stabilize)      Ring(ids)  (GPU radix sort)
   StoredLocally / owner of a key                 successor(keys)
+  GetPredecessor(key)                            predecessor(keys)
   PopulateFingerTable (converged)                build_fingers()
   EditNthFinger / AdjustFingers (hand edits)     upload_fingers(F)
   min_key_ / predecessor_ (white-box state)      upload_peer_state(...)
@@ -183,6 +184,16 @@ class Ring:
         mk = self._mem(keys, owner)
         L.check(L.lib().cx_successor(self._h, _ptr(keys), q, _ptr(owner), mk))
         return owner
+
+    def predecessor(self, keys, out=None):
+        """GetPredecessor(key) on the converged ring: the owner's predecessor."""
+        keys = self._prep_keys(keys)
+        q = keys.shape[0]
+        pred = out if out is not None else self._empty(keys, (q,), np.uint32, torch and torch.int32)
+        self._check_out([(pred, 4, "pred")], q)
+        mk = self._mem(keys, pred)
+        L.check(L.lib().cx_predecessor(self._h, _ptr(keys), q, _ptr(pred), mk))
+        return pred
 
     # ---- a4/a6 -----------------------------------------------------------
     def build_fingers(self, copy_out: bool = False):

@@ -591,6 +591,21 @@ int build_fingers_table(cx_ring *ring, hipStream_t s) {
 }
 }  // namespace
 
+int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *pred,
+                   int memkind) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    DBuf tk, to;
+    const cx_u128 *dk;
+    uint32_t *dout;
+    if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
+    if ((rc = stage_out(pred, q, memkind, to, &dout))) return rc;
+    CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    return finish_out(pred, dout, q, memkind, s);
+}
+
 int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     int rc = use_device(ring);

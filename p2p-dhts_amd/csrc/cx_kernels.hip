@@ -344,14 +344,18 @@ hipError_t eyt_build(const cell128 *sorted, size_t n, cell128 *E, hipStream_t s)
 // ===========================================================================
 constexpr int SUCC_BLOCK = 1024;
 
-template <bool DIR>
+// PRED: the owner's predecessor instead (converged GetPredecessor).
+template <bool DIR, bool PRED = false>
 __global__ __launch_bounds__(SUCC_BLOCK) void k_successor(SearchView sv, const cell128 *keys,
                                                           size_t q, uint32_t *owner) {
     __shared__ u128 lds[Searcher<DIR>::LDS];
     Searcher<DIR>::stage(sv, lds);
+    const uint32_t n = sv.ev.n;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
-         i += (size_t)gridDim.x * blockDim.x)
-        owner[i] = Searcher<DIR>::find(sv, lds, ld128(keys + i));
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = Searcher<DIR>::find(sv, lds, ld128(keys + i));
+        owner[i] = PRED ? (s == 0 ? n - 1 : s - 1) : s;
+    }
 }
 
 hipError_t successor(const SearchView &sv, const cell128 *keys, size_t q, uint32_t *owner,
@@ -361,6 +365,18 @@ hipError_t successor(const SearchView &sv, const cell128 *keys, size_t q, uint32
         k_successor<true><<<cx_grid(q, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, keys, q, owner);
     else
         k_successor<false><<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, keys, q, owner);
+    return hipGetLastError();
+}
+
+hipError_t predecessor(const SearchView &sv, const cell128 *keys, size_t q, uint32_t *pred,
+                       hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    if (sv.dir)
+        k_successor<true, true><<<cx_grid(q, SUCC_BLOCK, 2048), SUCC_BLOCK, 0, s>>>(sv, keys, q,
+                                                                                    pred);
+    else
+        k_successor<false, true><<<cx_grid(q, SUCC_BLOCK, 512), SUCC_BLOCK, 0, s>>>(sv, keys, q,
+                                                                                    pred);
     return hipGetLastError();
 }
 
@@ -3177,7 +3193,9 @@ hipError_t uuid5(const uint8_t *bytes, const uint64_t *offs, size_t count, cell1
 // Hex codec of keys on the wire.  Parse: ChordKey(hex, hashed = true) =
 // uint256("0x" + s) (key.h:73-75) -- hex digits of either case, no prefix;
 // the engine keeps the value mod 2^128 (what every ring comparison reads,
-// key.h:103-131).  Format: std::string(key) = IntToHexStr (key.h:41-47):
+// key.h:103-131) and flags ok = 2 when the raw uint256 (which wraps mod
+// 2^256, Boost's unchecked cpp_int) is >= 2^128, i.e. bits 128..255 of it
+// are not all zero.  Format: std::string(key) = IntToHexStr (key.h:41-47):
 // lowercase, no leading zeros, "0" for zero; one 32-byte slot per key.
 // ---------------------------------------------------------------------------
 __global__ void k_hex_parse(const uint8_t *bytes, const uint64_t *offs, size_t count,
@@ -3185,7 +3203,7 @@ __global__ void k_hex_parse(const uint8_t *bytes, const uint64_t *offs, size_t c
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
          i += (size_t)gridDim.x * blockDim.x) {
         const uint64_t o = offs[i], e = offs[i + 1];
-        u128 v = 0;
+        u128 v = 0, hi = 0;  // raw value = hi:v mod 2^256
         bool good = e > o;
         for (uint64_t k = o; k < e; ++k) {
             const uint32_t c = bytes[k];
@@ -3194,10 +3212,11 @@ __global__ void k_hex_parse(const uint8_t *bytes, const uint64_t *offs, size_t c
             else if (c >= 'a' && c <= 'f') d = c - 'a' + 10;
             else if (c >= 'A' && c <= 'F') d = c - 'A' + 10;
             else { good = false; d = 0; }
+            hi = (hi << 4) | (v >> 124);
             v = (v << 4) | d;
         }
         st128(out + i, good ? v : (u128)0);
-        ok[i] = good ? 1 : 0;
+        ok[i] = good ? (hi != 0 ? 2 : 1) : 0;
     }
 }
 

@@ -75,6 +75,8 @@ hipError_t successor(const SearchView &ev, const cell128 *keys, size_t q, uint32
 // has >= 2^18 peers, else one directory search per entry.
 size_t fingers_workspace_bytes(size_t n);
 int finger_key_shift(size_t n);
+hipError_t predecessor(const SearchView &ev, const cell128 *keys, size_t q, uint32_t *pred,
+                       hipStream_t s);
 hipError_t fingers_build(const SearchView &ev, const cell128 *ring, const uint32_t *ring_key,
                          void *ws, uint32_t *F, hipStream_t s);
 hipError_t ring_slice_build(const cell128 *ring, size_t n, int kb, uint32_t *key, hipStream_t s);

@@ -263,12 +263,14 @@ struct cx_wire {
     std::vector<int> port;
     std::vector<std::string> id_hex;   // std::string(id) of each peer
     std::vector<std::string> min_hex;  // std::string(pred.id + 1)
+    std::vector<cx_u128> ids;          // ring IDs, ascending
     std::unordered_map<std::string, uint32_t> index;  // "ip:port" -> ring index
 };
 
 namespace {
 
-// Parses hex key strings on the GPU; ok[i] = 0 for an invalid string.
+// Parses hex key strings on the GPU; ok[i] = 0 for an invalid string, 2 for
+// a raw value >= 2^128.
 int parse_keys(const cx_wire *w, const std::vector<const std::string *> &keys,
                std::vector<cx_u128> &out, std::vector<uint8_t> &ok) {
     std::vector<uint64_t> offs(keys.size() + 1, 0);
@@ -282,6 +284,69 @@ int parse_keys(const cx_wire *w, const std::vector<const std::string *> &keys,
     if (keys.empty()) return CX_OK;
     return cx_hex_parse(reinterpret_cast<const uint8_t *>(bytes.data()), offs.data(), keys.size(),
                         out.data(), ok.data(), CX_MEM_HOST, w->device);
+}
+
+inline bool u128_eq(cx_u128 a, cx_u128 b) { return a.lo == b.lo && a.hi == b.hi; }
+inline cx_u128 u128_inc(cx_u128 a) { return {a.lo + 1, a.hi + (a.lo == UINT64_MAX ? 1u : 0u)}; }
+
+const char *status_error(uint8_t st) {
+    // finger_table.h:129 / chord_peer.cpp:206
+    return st == CX_Q_NOT_FOUND ? "ChordKey not found" : "Lookup failed";
+}
+
+// Keys whose raw uint256 value is >= 2^128 (ok == 2).  The engine routes
+// m = value mod 2^128, which is what every ranged InBetween reads (key.h:
+// 116-118); only the point tests (lb == ub, key.h:108-113) see the raw value,
+// and it never equals a bound < 2^128.  On the converged ring two point tests
+// exist: StoredLocally at a peer whose min_key == id (its predecessor's ID is
+// id - 1), and finger 0's range [id+1, id+1] (finger_table.h:177-188).  So
+// with x = pred(owner) and m == x.id + 1 (n >= 2):
+//   * m == owner.id  -> x and the owner both fail: "ChordKey not found";
+//   * otherwise the walk fails at x iff it visits x.  The walk to m and the
+//     walk to m - 1 = x.id take the same fingers until a step whose distance
+//     m - cur is a power of two (that step jumps straight to the owner), so
+//     the walk to m visits x iff hops(m) == hops(x.id) + 1.  The second walk
+//     runs on the GPU for just these keys.
+// Every other wide key routes as m.  (oracle or_route_raw_batch is the
+// literal raw-value walk the wire tests compare against.)
+int wide_keys(const cx_wire *w, const std::vector<uint8_t> &ok,
+              const std::vector<cx_u128> &kv, const std::vector<uint32_t> &src,
+              std::vector<uint32_t> &owner, std::vector<uint8_t> &hops,
+              std::vector<uint8_t> &status) {
+    const size_t n = w->ids.size();
+    if (n < 2) return CX_OK;
+    std::vector<size_t> redo;
+    for (size_t i = 0; i < kv.size(); ++i) {
+        if (ok[i] != 2 || status[i] != CX_Q_OK) continue;
+        const uint32_t o = owner[i], x = (uint32_t)((o + n - 1) % n);
+        if (!u128_eq(u128_inc(w->ids[x]), kv[i])) continue;
+        if (u128_eq(w->ids[o], kv[i])) {
+            status[i] = CX_Q_NOT_FOUND;
+            owner[i] = CX_NONE;
+        } else {
+            redo.push_back(i);
+        }
+    }
+    if (redo.empty()) return CX_OK;
+    std::vector<cx_u128> k2(redo.size());
+    std::vector<uint32_t> s2(redo.size()), o2(redo.size());
+    std::vector<uint8_t> h2(redo.size()), st2(redo.size());
+    for (size_t j = 0; j < redo.size(); ++j) {
+        const size_t i = redo[j];
+        k2[j] = w->ids[(owner[i] + n - 1) % n];
+        s2[j] = src[i];
+    }
+    const int e = cx_route(w->ring, s2.data(), k2.data(), redo.size(), o2.data(), h2.data(),
+                           st2.data(), CX_MEM_HOST);
+    if (e != CX_OK) return e;
+    for (size_t j = 0; j < redo.size(); ++j) {
+        const size_t i = redo[j];
+        if (st2[j] == CX_Q_OK && hops[i] == h2[j] + 1) {
+            status[i] = CX_Q_NOT_FOUND;
+            owner[i] = CX_NONE;
+        }
+    }
+    return CX_OK;
 }
 
 void peer_fields(const cx_wire *w, uint32_t o, std::string &r) {
@@ -340,10 +405,11 @@ std::string handle(cx_wire *w, const JVal &req) {
     if (q && cx_route(w->ring, src.data(), kv.data(), q, owner.data(), hops.data(),
                       status.data(), CX_MEM_HOST) != CX_OK)
         return failure(last_error());
+    if (wide_keys(w, ok, kv, src, owner, hops, status) != CX_OK) return failure(last_error());
 
     if (!batch) {
         if (!ok[0]) return failure("invalid hex key: \"" + *keys[0] + "\"");
-        if (status[0] != CX_Q_OK) return failure("Lookup failed");  // chord_peer.cpp:206
+        if (status[0] != CX_Q_OK) return failure(status_error(status[0]));
         std::string r = "{";
         peer_fields(w, owner[0], r);
         r += ",\"SUCCESS\":true}";
@@ -356,7 +422,7 @@ std::string handle(cx_wire *w, const JVal &req) {
         if (!ok[i]) {
             r += failure("invalid hex key: \"" + *keys[i] + "\"");
         } else if (status[i] != CX_Q_OK) {
-            r += failure("Lookup failed");
+            r += failure(status_error(status[i]));
         } else {
             r += '{';
             r += "\"HOPS\":" + std::to_string(hops[i]) + ',';
@@ -408,7 +474,8 @@ int cx_wire_create(const char *const *addrs, size_t n, int device, cx_wire **out
             w->index[a] = idx[i];
         }
         // ID and MIN_KEY = pred.id + 1 of every peer, formatted by the GPU codec
-        std::vector<cx_u128> sorted(n), both(2 * n);
+        std::vector<cx_u128> &sorted = w->ids, both(2 * n);
+        sorted.assign(n, cx_u128{0, 0});
         if ((e = cx_ring_ids(w->ring, sorted.data(), CX_MEM_HOST))) return e;
         for (size_t i = 0; i < n; ++i) {
             const cx_u128 p = sorted[(i + n - 1) % n];

@@ -200,6 +200,22 @@ def get_succ():
     }
 
 
+def get_pred():
+    """ChordGetPred.* (chord_test.cpp:131-227) on converged rings."""
+    d = load("chord_tests/GetPredTest.json")
+    sl = d["GET_PRED_IN_SUCC_LIST"]
+    ft = d["GET_PRED_FROM_FINGER_TABLE"]
+    return {
+        "source": "chord_test.cpp:131-227 + GetPredTest.json",
+        # FromSuccList: 3-peer ring, key just below a peer's ID
+        "in_succ_list": {"peers": [uuid5_hex(peer_name(p)) for p in sl["PEERS"]],
+                         "key": sl["KEY_TO_LOOKUP"], "expected": sl["EXPECTED_PRED_ID"]},
+        # FromFingerTable: 2-peer ring, key just above a peer's ID (owner wraps)
+        "from_finger_table": {"peers": [uuid5_hex(peer_name(p)) for p in ft["PEERS"]],
+                              "key": ft["KEY_TO_LOOKUP"], "expected": ft["EXPECTED_PRED_ID"]},
+    }
+
+
 def global_maintenance():
     """DHashGlobalMaintenance.MisplacedKeys (dhash_test.cpp:123-149): n=2
     (SetIdaParams(2,1,257)); keys 0x50..00-08 inserted into TESTED_IND's db; after
@@ -294,6 +310,7 @@ def main():
         "node_failure": node_failure(),
         "update_succ": update_succ(),
         "get_succ": get_succ(),
+        "get_pred": get_pred(),
         "global_maintenance": global_maintenance(),
         "dhash_create_read": dhash_create_read(),
         "ida_values": ida_values(),

@@ -150,3 +150,18 @@ def test_device_buffers_large(ida, O):
     got = fr[:8].cpu().numpy().view(np.uint16)
     for i in range(8):
         assert (got[i] == want[i]).all()
+
+
+def test_from_fragments_value_256_refused(ida):
+    """Fragments that decode to a value of 256 (p = 257; not producible from
+    bytes) are refused explicitly instead of yielding an empty fragment list."""
+    import chordx
+    # fragments of the int vector [256, 1, 2, ...] built by the oracle's
+    # Vandermonde rows: E[i] . v mod 257 for each row i (matrix_math.cpp:88-101)
+    n, m, p = 14, 10, 257
+    v = np.array([256, 1, 2, 3, 4, 5, 6, 7, 8, 9], dtype=np.int64)
+    E = np.array([[pow(i + 1, j, p) for j in range(m)] for i in range(n)], dtype=np.int64)
+    frag = (E @ v) % p
+    frags = [(i + 1, np.array([frag[i]], dtype=np.uint16)) for i in range(m)]
+    with pytest.raises(chordx.ChordError):
+        ida.DataBlock.from_fragments(frags, n, m, p)

@@ -567,3 +567,35 @@ def test_misplaced_with_foreign_map_and_chained_churn(cx, O):
     want = O.misplaced(want_new, want_newer, want_o2n2, keys, 14)
     for g, w in zip(got, want):
         assert (g == w).all()
+
+
+def test_predecessor(cx, O, refvec):
+    """Batched GetPredecessor vs the oracle: reference fixtures, edge rings and
+    keys (IDs, +-1, 0, 2^128 - 1), N = 1, 2, 3."""
+    for case in ("in_succ_list", "from_finger_table"):
+        g = refvec["get_pred"][case]
+        ring = cx.Ring(O.keys_from_ints([H(x) for x in g["peers"]]))
+        names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
+        assert names[ring.predecessor(O.keys_from_ints([H(g["key"])]))[0]] == g["expected"]
+    for n, seed in ((1, 1), (2, 2), (3, 3), (1000, 4), (70001, 5)):
+        ids = edge_ring(O, n, seed)
+        want_ring = O.ring_build(ids)
+        ring = cx.Ring(ids)
+        keys = edge_keys(O, want_ring, seed + 100, 20000)
+        assert (ring.predecessor(keys) == O.predecessor(want_ring, keys)).all()
+
+
+def test_predecessor(cx, O, refvec):
+    """Batched GetPredecessor vs the oracle: reference fixtures, edge rings and
+    keys (IDs, +-1, 0, 2^128 - 1), N = 1, 2, 3."""
+    for case in ("in_succ_list", "from_finger_table"):
+        g = refvec["get_pred"][case]
+        ring = cx.Ring(O.keys_from_ints([H(x) for x in g["peers"]]))
+        names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
+        assert names[ring.predecessor(O.keys_from_ints([H(g["key"])]))[0]] == g["expected"]
+    for n, seed in ((1, 1), (2, 2), (3, 3), (1000, 4), (70001, 5)):
+        ids = edge_ring(O, n, seed)
+        want_ring = O.ring_build(ids)
+        ring = cx.Ring(ids)
+        keys = edge_keys(O, want_ring, seed + 100, 20000)
+        assert (ring.predecessor(keys) == O.predecessor(want_ring, keys)).all()

@@ -35,11 +35,14 @@ def test_hex_parse(wire, O):
     strs = [format(v, "x") for v in vals]
     strs += [format(v, "X") for v in vals[:100]]                # upper case
     strs += ["0" * 10 + format(v, "x") for v in vals[:100]]     # leading zeros
-    strs += ["1" + "0" * 32, "f" * 64, "abc" * 30]               # > 128 bits: low 128 kept
-    exp = vals + vals[:100] + vals[:100] + [0, MASK, int("abc" * 30, 16) & MASK]
+    wide = ["1" + "0" * 32, "f" * 64, "abc" * 30, "0" * 40 + "f" * 32, "0" * 31 + "1" + "0" * 32]
+    strs += wide                                                 # 33+ digits: raw value kept mod 2^256
+    exp = vals + vals[:100] + vals[:100] + [O.hex_value(x) & MASK for x in wide]
     out, ok = wire.hex_parse(strs)
-    assert ok.all()
     assert O.ints_from_keys(out) == exp
+    raw = [O.hex_value(x) for x in strs]
+    assert ok.tolist() == [2 if v >> 128 else 1 for v in raw]
+    assert ok[-5:].tolist() == [2, 2, 2, 1, 2]
     bad = ["", "0x12", "12g4", " 12", "-1", "1 "]
     out, ok = wire.hex_parse(bad + ["ab"])
     assert ok.tolist() == [0] * len(bad) + [1]
@@ -133,3 +136,36 @@ def test_wire_errors(wire):
     single = wire.Wire(["127.0.0.1:6000"])
     r = single.handle({"COMMAND": "GET_SUCC", "KEY": "5"})
     assert r["SUCCESS"] and r["MIN_KEY"] == format((int(r["ID"], 16) + 1) & MASK, "x")
+
+
+def test_get_succ_wide_keys(wire, O):
+    """Keys of 33-64 hex digits keep their raw uint256 value (key.h:73-75):
+    ranged InBetween tests reduce it mod 2^128, point tests (key.h:108-113) do
+    not.  Every key id(x) + 1 + 2^128 from every source, and random wide keys,
+    against the oracle's literal raw-value walk (or_route_raw_batch)."""
+    import chordx
+    names = [f"10.1.0.{i}:7000" for i in range(48)]
+    w = wire.Wire(names)
+    ids = [int(v[0]) | (int(v[1]) << 64) for v in chordx.uuid5_dns(names)]
+    ring = O.ring_build(O.keys_from_ints(ids))
+    ring_ints = O.ints_from_keys(ring)
+    name_of = {v: nm for v, nm in zip(ids, names)}
+    P = O.Peers(ring, O.fingers(ring))
+    n = len(ring)
+    rnd = random.Random(9)
+    vals = [(1 << 128) | ((x + 1) & MASK) for x in ring_ints]
+    vals += [(rnd.getrandbits(128) << 128) | ((x + 1) & MASK) for x in ring_ints[:8]]
+    vals += [rnd.getrandbits(256) | (1 << 255) for _ in range(16)]
+    vals += [(1 << 128) | x for x in ring_ints[:8]]                # == an ID: stored there
+    src = [s for s in range(n) for _ in vals]
+    allv = vals * n
+    wo, wh, ws = O.route_raw(P, src, allv)
+    assert (ws == 4).any() and (ws == 0).any()                     # both outcomes present
+    r = w.handle({"COMMAND": "GET_SUCC_BATCH", "KEYS": [format(v, "x") for v in allv],
+                  "SRCS": [name_of[ring_ints[s]] for s in src]})
+    assert r["SUCCESS"] is True
+    for j, x in enumerate(r["RESULTS"]):
+        if ws[j] == 0:
+            assert x["ID"] == format(ring_ints[wo[j]], "x") and x["HOPS"] == wh[j], j
+        else:
+            assert x == {"SUCCESS": False, "ERRORS": "ChordKey not found"}, (j, x)

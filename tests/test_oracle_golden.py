@@ -409,3 +409,21 @@ def test_lookup_living_scan_never_runs(O):
     P = O.Peers(ring, F, alive=alive, succs=succs, rule=1)
     owner, hops, status = O.route(P, [0], O.keys_from_ints([0x38 << 120]))
     assert status[0] == O.Q_FAILED and hops[0] == 0
+
+
+@pytest.mark.parametrize("case", ["in_succ_list", "from_finger_table"])
+def test_get_pred_fixture(O, refvec, case):
+    """ChordGetPred.FromSuccList / FromFingerTable (chord_test.cpp:154-209):
+    the converged ring's answer is the key owner's predecessor."""
+    g = refvec["get_pred"][case]
+    ring = _ring(O, [H(x) for x in g["peers"]])
+    ids = [format(v, "x") for v in O.ints_from_keys(ring)]
+    pred = O.predecessor(ring, O.keys_from_ints([H(g["key"])]))
+    assert ids[pred[0]] == g["expected"]
+
+
+def test_get_pred_lone_peer_is_itself(O):
+    """A lone peer has no predecessor set and answers itself
+    (abstract_chord_peer.cpp:383-385; ChordGetPred.LocalKey's one-peer ring)."""
+    ring = _ring(O, [0xfffffffffffffffffffffffffffffff])
+    assert (O.predecessor(ring, O.keys_from_ints([1 << 120, 0, 5])) == 0).all()
