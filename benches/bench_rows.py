@@ -9,7 +9,13 @@ BASELINE.json configs, one MI355X.  Prints one JSON object (profiles/<round>/row
 
 Kernel times are HIP events on the launch stream (torch's current stream, which
 the library enqueues on for device buffers); host-synchronous calls (ring
-build, churn) are wall-clock.  Inputs: splitmix seeds of SURVEY 8(d).
+build, churn, finger + route-table build) are wall-clock.  Inputs: splitmix
+seeds of SURVEY 8(d).
+
+Every row also carries a "cpu" leg (BASELINE.md:39-49): the oracle's C
+restatement (oracle/chord_oracle.c, gcc -O3) of the same operation on this
+host, on all usable cores and on one core, over a bounded sample of the same
+inputs (named in "sample"); each leg also checks the GPU output on its sample.
 """
 from __future__ import annotations
 
@@ -18,6 +24,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
 
@@ -25,7 +33,36 @@ import torch  # noqa: E402
 
 import chordx  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)
+
 HBM = 8.0e12
+CPU_BUDGET_S = float(os.environ.get("CX_ROWS_CPU_S", "6"))
+
+
+def cpu_leg(fn, total, unit, what, check=None):
+    """Times fn(count, threads) on a sample sized to ~CPU_BUDGET_S (2/3 on all
+    usable cores, 1/3 on one core).  Returns the cpu dict."""
+    from bench import cpu_model, host_threads
+    th = host_threads()
+    t0 = time.perf_counter()
+    fn(min(total, 1024), 1)
+    per = max((time.perf_counter() - t0) / min(total, 1024), 1e-9)
+    q1 = int(min(total, max(1024, CPU_BUDGET_S / 3 / per)))
+    t0 = time.perf_counter()
+    fn(q1, 1)
+    d1 = time.perf_counter() - t0
+    qa = int(min(total, max(q1, CPU_BUDGET_S * 2 / 3 * th / per)))
+    t0 = time.perf_counter()
+    r = fn(qa, th)
+    da = time.perf_counter() - t0
+    out = {"value": qa / da, "value_1core": q1 / d1, "unit": unit, "cores": th,
+           "kind": "port", "cpu_model": cpu_model(),
+           "sample": f"first {qa} of {total} {what} on {th} threads ({da:.1f} s), "
+                     f"first {q1} on 1 thread ({d1:.1f} s)"}
+    if check is not None:
+        out["parity_on_sample"] = bool(check(r, qa))
+    return out
 
 
 def ev_time(fn, reps=3):
@@ -58,6 +95,13 @@ def main():
         t = ev_time(lambda: ring.successor(keys))
         res[name] = {"s": t, "lookups_per_s": (1 << 20) / t,
                      "algo_GBps": (1 << 20) * 20 / t / 1e9}
+    import oracle as O
+    ring_np = ring.ids()
+    keys_np = keys.cpu().numpy().view(np.uint64)
+    succ_gpu = ring.successor(keys).cpu().numpy().view(np.uint32)
+    res["cpu"] = cpu_leg(lambda q, th: O.successor(ring_np, keys_np[:q], threads=th), 1 << 20,
+                         "lookups/s", "keys (binary search over the sorted ring)",
+                         lambda r, q: (r == succ_gpu[:q]).all())
     out["C2_exact_successor"] = res
     del ring, keys
 
@@ -77,7 +121,21 @@ def main():
     tr = ev_time(lambda: ring.route(src, keys, out=(owner, hops, status)))
     sh = int(hops.to(torch.int64).sum())
     algo = q * (25 + 64) + 128 * sh
-    out["C3"] = {"fingers_build_s_wall": tf,
+    ring_np = ring.ids()
+    F_gpu = ring.fingers_device().cpu().numpy().view(np.uint32)
+    cpu_f = cpu_leg(lambda q, th: O.fingers(ring_np, threads=th, rows=(0, q)), N3,
+                    "peers/s", "peers' 128-entry finger rows (PopulateFingerTable restated)",
+                    lambda r, q: (r == F_gpu[:q]).all())
+    P = O.Peers(ring_np, F_gpu)
+    src_np = src.cpu().numpy().view(np.uint32)
+    kq_np = keys.cpu().numpy().view(np.uint64)
+    own_np = owner.cpu().numpy().view(np.uint32)
+    hop_np = hops.cpu().numpy()
+    cpu_r = cpu_leg(lambda q, th: O.route(P, src_np[:q], kq_np[:q], threads=th), q,
+                    "lookups/s", "routed lookups (or_route, literal ForwardRequest walk)",
+                    lambda r, qq: (r[0] == own_np[:qq]).all() and (r[1] == hop_np[:qq]).all())
+    del P, F_gpu
+    out["C3"] = {"fingers_build_s_wall": tf, "cpu_fingers": cpu_f, "cpu_route": cpu_r,
                  "fingers_algo_GBps": N3 * 528 / tf / 1e9,
                  "route_s": tr, "route_lookups_per_s": q / tr, "mean_hops": sh / q,
                  "route_algo_frac_of_hbm": algo / tr / HBM,
@@ -91,7 +149,8 @@ def main():
     lists = torch.empty((q5, n), dtype=torch.int32, device="cuda")
     tl = ev_time(lambda: old.nsucc(keys, n), reps=2)
     joins = keys_dev(N5 // 100, 0x5EED0009)
-    pick = keys_dev(N5 // 100, 0x5EED0009, offset=1 << 40)[:, 0].remainder(N5)
+    # distinct leaving peers (odd stride mod 2^24): the new ring keeps 2^24 peers
+    pick = (torch.arange(N5 // 100, device="cuda", dtype=torch.int64) * 0x9E3779B1) % N5
     leaves = old.ids_device()[pick].contiguous()
     tcv = {}
     for cv in (0, 1, 1):  # re-sort, merge (twice: the first call warms allocations)
@@ -105,7 +164,30 @@ def main():
     tm = ev_time(lambda: old.misplaced(new, o2n, keys, n), reps=2)
     lists, count, mask, target = old.misplaced(new, o2n, keys, n)
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    new.build_fingers()
+    new.sync()
+    t_ready = time.perf_counter() - t0
+    old_np, new_np = old.ids(), new.ids()
+    o2n_np = o2n.cpu().numpy().view(np.uint32) if hasattr(o2n, "cpu") else np.asarray(o2n)
+    j_np = joins.cpu().numpy().view(np.uint64)
+    l_np = leaves.cpu().numpy().view(np.uint64)
+    t0 = time.perf_counter()
+    want_new, want_o2n = O.churn(old_np, j_np, l_np)
+    t_churn_cpu = time.perf_counter() - t0
+    k5 = keys.cpu().numpy().view(np.uint64)
+    lists_np = lists.cpu().numpy().view(np.uint32)
+    mask_np = mask.cpu().numpy()
+    cpu_m = cpu_leg(lambda qq, th: O.misplaced(old_np, new_np, o2n_np, k5[:qq], n, threads=th),
+                    q5, "keys/s", "keys (RunGlobalMaintenance restated, n = 14)",
+                    lambda r, qq: (r[0] == lists_np[:qq]).all() and (r[2] == mask_np[:qq]).all())
     out["C5"] = {"ring_old": N5, "ring_new": new.n, "keys": q5, "n": n,
+                 "route_ready_after_churn_s_wall": tc + t_ready,
+                 "new_fingers_and_route_table_s_wall": t_ready,
+                 "cpu_churn": {"value_s": t_churn_cpu, "cores": 1, "kind": "port",
+                               "identical": bool((want_new == new_np).all()
+                                                 and (want_o2n == o2n_np).all())},
+                 "cpu_misplaced": cpu_m,
                  "nsucc_s": tl, "nsucc_keys_per_s": q5 / tl,
                  "churn_s_wall": tc, "churn_resort_s_wall": tcv[0],
                  "misplaced_s": tm, "misplaced_keys_per_s": q5 / tm,

@@ -284,6 +284,22 @@ class Ring:
         L.check(f(self._h, lanes, hops, ctypes.byref(r)))
         return r.value
 
+    def route_table_hash(self, arc: bool = False) -> int:
+        """Internal: order-sensitive 64-bit hash of the built pattern-keyed
+        table (arc=True: this rank's arc planes), for A/B identity of builds."""
+        f = L.lib().cxi_route_table_hash
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        h = ctypes.c_uint64()
+        L.check(f(self._h, int(bool(arc)), ctypes.byref(h)))
+        return h.value
+
+    def set_table_build(self, v: int):
+        """Internal A/B switch for the route-table build's finger input:
+        0 = level planes (default), 1 = the row-major finger table."""
+        f = L.lib().cxi_set_table_build
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.check(f(self._h, v))
+
     def set_churn_variant(self, v: int):
         """Internal A/B switch: 0 = full re-sort, 1 = merge of sorted joins (default)."""
         f = L.lib().cxi_set_churn_variant

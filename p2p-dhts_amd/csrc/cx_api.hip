@@ -118,6 +118,7 @@ struct cx_ring {
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
     uint64_t *d_cz = nullptr;      // pattern-keyed window table [rt_R][2][n][8 x u64] (variant 5)
+    bool cz_rows = false;          // A/B: build from the row-major fingers, not level planes
     bool cz_valid = false;
     uint64_t cz_escapes = 0;       // nodes the compressed format could not represent
     int route_variant = -1;        // 0: finger+ring gathers, 1: route table, 2: packed table,
@@ -331,6 +332,25 @@ void route_geometry(cx_ring *r) {
     r->pk_ib = lg < 1 ? 1 : lg;
 }
 
+// Finger access for a route-table build over levels [lo - 5, 128): level
+// planes in `ft` when HBM allows (cxi_set_table_build(ring, 1) forces the
+// row-major table, for A/B), else the row-major table itself.
+hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
+                         hipStream_t s) {
+    fv = cxk::FingerView::rows(r->d_fingers);
+    hipError_t e0 = hi.alloc(r->n * sizeof(uint64_t));
+    if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
+    if (e0 != hipSuccess) return e0;
+    const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
+    if (r->cz_rows || ft.alloc((size_t)nl * r->n * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        return hipSuccess;
+    }
+    hipError_t e = cxk::fingers_levels(r->d_fingers, r->n, L, nl, ft.as<uint32_t>(), s);
+    if (e == hipSuccess) fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
+    return e;
+}
+
 // Builds (once per finger build) the table the selected route variant reads.
 // Without HBM for it the route falls back to variant 0 (finger + ring gathers).
 int ensure_route_table(cx_ring *r, hipStream_t s) {
@@ -342,13 +362,17 @@ int ensure_route_table(cx_ring *r, hipStream_t s) {
             if (r->route_variant < 0) r->cz_failed = true;  // automatic: use variant 4
         }
         if (r->d_cz) {
-            CX_HIP(hipMemsetAsync(r->d_scratch, 0, sizeof(uint32_t), s));
-            CX_HIP(cxk::cz_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib,
-                                 r->d_cz, r->d_scratch, s));
-            uint32_t esc = 0;
-            CX_HIP(hipMemcpyAsync(&esc, r->d_scratch, sizeof(esc), hipMemcpyDeviceToHost, s));
+            CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
+            DBuf ft, hi;
+            cxk::FingerView fv;
+            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, s));
+            CX_HIP(cxk::cz_build(fv, r->d_ring, hi.as<uint64_t>(), r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_cz,
+                                 r->d_scratch, s));
+            uint32_t esc[2] = {0, 0};
+            CX_HIP(hipMemcpyAsync(esc, r->d_scratch, sizeof(esc), hipMemcpyDeviceToHost, s));
             CX_HIP(hipStreamSynchronize(s));
-            r->cz_escapes = esc;
+            CX_CHECK(esc[1] == 0, CX_E_STATE, "route-table build met a finger out of range");
+            r->cz_escapes = esc[0];
             r->cz_valid = true;
         }
     }
@@ -1342,11 +1366,20 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
         ring->d_arc_tree = nullptr;
         return fail(CX_E_NOMEM, "hipMalloc of the arc route planes failed");
     }
-    CX_HIP(hipMemsetAsync(ring->d_scratch, 0, sizeof(uint32_t), s));
-    CX_HIP(cxk::cz_build_part(ring->d_fingers, ring->d_ring, n, Lh, (int)CX_FINGERS - Lh, 0,
-                              (uint32_t)n, ring->pk_ib, ring->d_arc_tree, ring->d_scratch, s));
-    CX_HIP(cxk::cz_build_part(ring->d_fingers, ring->d_ring, n, l0, Lh - l0, plo, M, ring->pk_ib,
-                              ring->d_arc_tree + top_ent * 8, ring->d_scratch, s));
+    CX_HIP(hipMemsetAsync(ring->d_scratch, 0, 2 * sizeof(uint32_t), s));
+    {
+        DBuf ft, hi;
+        cxk::FingerView fv;
+        CX_HIP(finger_planes(ring, l0, ft, fv, hi, s));
+        CX_HIP(cxk::cz_build_part(fv, ring->d_ring, hi.as<uint64_t>(), n, Lh, (int)CX_FINGERS - Lh, 0, (uint32_t)n,
+                                  ring->pk_ib, ring->d_arc_tree, ring->d_scratch, s));
+        CX_HIP(cxk::cz_build_part(fv, ring->d_ring, hi.as<uint64_t>(), n, l0, Lh - l0, plo, M, ring->pk_ib,
+                                  ring->d_arc_tree + top_ent * 8, ring->d_scratch, s));
+        uint32_t esc[2] = {0, 0};
+        CX_HIP(hipMemcpyAsync(esc, ring->d_scratch, sizeof(esc), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));  // ft and hi are freed at scope end
+        CX_CHECK(esc[1] == 0, CX_E_STATE, "route-table build met a finger out of range");
+    }
     // WALK destinations: the last peer ID of every non-empty arc, ascending
     std::vector<ArcBound> b;
     for (int g = 0; g < world; ++g) {
@@ -1547,6 +1580,44 @@ int cxi_gather_probe(const cx_ring *ring, int lanes, int hops, double *rate) {
     }
     CX_CHECK(t != nullptr, CX_E_STATE, "no route table built");
     CX_HIP(cxk::gather_probe(t, bytes, lanes, hops, rate, ring->stream));
+    return CX_OK;
+}
+
+// Hash of the route table the ring built (the pattern-keyed window table, or
+// the arc planes when arc mode is on): A/B identity of two builds.
+int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
+    CX_CHECK(ring && out, CX_E_INVALID, "null argument");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    const void *t = nullptr;
+    size_t bytes = 0;
+    if (arc) {
+        CX_CHECK(ring->arc_world > 0, CX_E_STATE, "arc mode is off");
+        t = ring->d_arc_tree;
+        bytes = ((size_t)((int)CX_FINGERS - ring->arc_Lh) * 2 * ring->n +
+                 (size_t)(ring->arc_Lh - ring->rt_l0) * 2 * ring->arc_M) * 64;
+    } else {
+        CX_CHECK(ring->cz_valid, CX_E_STATE, "no pattern-keyed table built");
+        t = ring->d_cz;
+        bytes = ring->n * (size_t)ring->rt_R * 128;
+    }
+    hipStream_t s = ring->stream;
+    DBuf acc;
+    CX_HIP(acc.alloc(sizeof(unsigned long long)));
+    CX_HIP(cxk::table_hash(t, bytes, acc.as<unsigned long long>(), s));
+    unsigned long long h = 0;
+    CX_HIP(hipMemcpyAsync(&h, acc.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    *out = h;
+    return CX_OK;
+}
+
+// Route-table build input: 0 = finger level planes (default), 1 = row-major
+// finger table.  Takes effect at the next finger build.
+int cxi_set_table_build(cx_ring *ring, int variant) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    ring->cz_rows = variant == 1;
     return CX_OK;
 }
 

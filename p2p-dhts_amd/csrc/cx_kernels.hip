@@ -1852,75 +1852,229 @@ __device__ __forceinline__ uint32_t cz_next(uint32_t n, uint32_t cur, int l, uin
     return (uint32_t)t;
 }
 
+// Level planes of the finger table: FT[(l - L) * n + p] = F[p][l] for
+// l in [L, L + nl).  The cz build's gathers F[x][l] come from lanes whose x
+// are neighbours (adjacent peers' fingers at one level are adjacent peers), so
+// in planes a wave's 64 gathers touch a few cache lines instead of 64 rows
+// 512 B apart.  One block = 64 peers: rows in (coalesced 4-B runs), LDS
+// transpose, plane segments out.
+__global__ void k_fingers_levels(const uint32_t *F, uint32_t n, int L, int nl, uint32_t *FT) {
+    __shared__ uint32_t t[CX_FINGERS][65];
+    const size_t p0 = (size_t)blockIdx.x * 64;
+    const int rows = (int)(n - p0 < 64 ? n - p0 : 64);
+    for (int k = threadIdx.x; k < rows * nl; k += blockDim.x) {
+        const int r = k / nl, c = k - r * nl;
+        t[c][r] = F[(p0 + r) * CX_FINGERS + L + c];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nl * 64; k += blockDim.x) {
+        const int c = k >> 6, r = k & 63;
+        if (r < rows) FT[(size_t)c * n + p0 + r] = t[c][r];
+    }
+}
+
+hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
+                          hipStream_t s) {
+    if (n == 0 || nl <= 0) return hipSuccess;
+    if (L < 0 || L + nl > CX_FINGERS) return hipErrorInvalidValue;
+    k_fingers_levels<<<(unsigned)((n + 63) / 64), 256, 0, s>>>(F, (uint32_t)n, L, nl, FT);
+    return hipGetLastError();
+}
+
+// High words of the ring IDs, packed (8 B per peer instead of 16 at a 16-B
+// stride): what the build's gap codes read.
+__global__ void k_ring_hi(const cell128 *ring, uint32_t n, uint64_t *hi) {
+    for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < n;
+         p += (size_t)gridDim.x * blockDim.x)
+        hi[p] = ring[p].hi;
+}
+
+hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_ring_hi<<<cx_grid(n, 256), 256, 0, s>>>(ring, (uint32_t)n, hi);
+    return hipGetLastError();
+}
+
+// cz_encode from the IDs' high words.  The gap code (xid - pid - 2^l) >> gs
+// with gs >= 64 and l >= 64 is (D - c) >> (gs - 64), D = xhi - phi - 2^(l-64)
+// (mod 2^64), c = the borrow out of the low words (0 or 1): when D has a set
+// bit below gs - 64 the borrow cannot reach bit gs - 64, and D alone decides.
+// Otherwise (about 2^-28 of encodes) the full IDs are read.
+__device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t par, uint64_t phi,
+                                                 int l, uint32_t x, uint64_t xhi,
+                                                 const cell128 *ring) {
+    // x, par < n < 2^30 and E(l) <= n/2: x - par - E lies in (-3n/2, n), so
+    // two conditional adds give the residue (no modulo)
+    int d = (int)x - (int)par - (int)cz_expect(n, l);
+    if (d < 0) d += (int)n;
+    if (d < 0) d += (int)n;
+    if (d > (int)(n / 2)) d -= (int)n;  // (-n/2, n/2]
+    const int sh = gs - 64;
+    const uint64_t D = xhi - phi - (1ull << (l - 64));
+    uint64_t code;
+    if (D & ((1ull << sh) - 1)) {
+        code = D >> sh;
+    } else {
+        const u128 full = ld128(ring + x) - ld128(ring + par) - ((u128)1 << l);
+        code = (uint64_t)(full >> gs);
+        if ((full >> gs) >> 64) code = ~0ull;
+    }
+    if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
+    return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
+}
+
 // Planes [lvl_base, lvl_base + nlev) of the table for the M peers p_first,
 // p_first + 1, ... (cyclic): the whole table (lvl_base = l0, nlev = R,
 // p_first = 0, M = n), or an arc rank's replicated top levels / local rows.
-__global__ void k_cz_build(const uint32_t *F, const cell128 *ring, uint32_t n, int lvl_base,
-                           int nlev, uint32_t p_first, uint32_t M, int gs, uint4 *cz,
-                           uint32_t *esc) {
-    const size_t total = (size_t)M * nlev * 2;
-    uint32_t bad = 0;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-         t += (size_t)gridDim.x * blockDim.x) {
-        // level-major: t = ((i - lvl_base) * 2 + b) * M + j (the walk's entry index)
-        const size_t plane = t / M;
-        const size_t j = t - plane * M;
-        const size_t p = (p_first + j) % n;
-        const int b = (int)(plane & 1);
-        const int i = lvl_base + (int)(plane >> 1);
-        uint32_t node[16], out[16];
-        u128 nid[16];
-        const u128 idp = ld128(ring + p);
-        uint32_t a = (uint32_t)p;
-        u128 aid = idp;
+// One lane per entry; a wave's 64 lanes are 64 consecutive peers of one
+// plane, whose fingers at a level are (nearly) consecutive peers too, so with
+// fingers in level planes (fv) and the IDs' packed high words (rh) each
+// gather instruction touches a few cache lines.  At 2^24 (2^30 entries):
+// 129 ms from row-major fingers, 62 ms from level planes, 56 ms with one
+// entry per lane in dispatch order (resident waves on a compact window of
+// rows, XCD-aware), 54 ms with streaming stores (profiles/r02/cz_build/).
+// The build is bound by its 5-deep dependent finger chain (SQ_WAIT_ANY 86 %
+// of wave cycles, 29 GB fetched + 64 GiB written = 1.7 TB/s); 6 or 8 waves
+// per SIMD (forced, with spills) are slower (60 / 71 ms); storing each 16-B
+// row as soon as its slots are known serialised the gathers behind the
+// stores (95 ms); a quad of lanes per entry (four columns of the slot square)
+// issued more, less coalesced gathers (97 ms).
+template <bool PLANES>
+__global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *ring,
+                                                  const uint64_t *rh, uint32_t n, int lvl_base,
+                                                  int nlev, uint32_t p_first, uint32_t M, int gs,
+                                                  uint4 *cz, uint32_t *esc) {
+    // grid.y = plane (i - lvl_base) * 2 + b; x strides over the plane's M rows
+    const uint32_t plane = blockIdx.y;
+    const int b = (int)(plane & 1);
+    const int i = lvl_base + (int)(plane >> 1);
+    // finger (x, l): level planes -> plane base (uniform) + x; rows -> x * 128 + l
+    auto fat = [&](uint32_t x, int l) -> uint32_t {
+        if (PLANES) return fv.F[(size_t)(l - fv.L) * fv.sl + x];
+        return fv.F[(size_t)x * CX_FINGERS + l];
+    };
+    // one entry per lane, no grid stride: the dispatcher walks blocks in
+    // order, so the resident waves hold a compact window of rows of one or two
+    // planes and their gathers (16 windows near p + E(l) per plane) stay in
+    // L2/MALL.  XCD-aware: hardware block b runs on XCD b % 8; it takes logical
+    // block (b % 8) * per + b / 8, so each XCD's L2 serves one contiguous run.
+    const uint32_t per = gridDim.x >> 3;
+    const uint32_t lb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    uint32_t bad = 0, oob = 0;
+    const uint32_t j = lb * blockDim.x + threadIdx.x;
+    if (j < M) {
+        // level-major: t = plane * M + j (the walk's entry index)
+        const size_t t = (size_t)plane * M + j;
+        uint64_t pw = (uint64_t)p_first + j;  // p_first < n, j < M <= n
+        if (pw >= n) pw -= n;
+        const uint32_t p = (uint32_t)pw;
+        uint32_t node[8], out[16];
+        uint64_t nh[8];
+        const uint64_t ph = rh[p];
+        uint32_t a = p;
+        uint64_t ah = ph;
         int al = i;
-        if (b) {
-            node[15] = F[p * CX_FINGERS + i];
-            nid[15] = ld128(ring + node[15]);
-            out[15] = cz_encode(n, gs, (uint32_t)p, idp, i, node[15], nid[15]);
-            a = node[15];
-            aid = nid[15];
+        if (b) {  // slot 15 = A = f(p, i); the window hangs off A' = f(A, i-1)
+            uint32_t A = fat(p, i);
+            if (A >= n) {
+                A = 0;
+                oob = 1;
+            }
+            const uint64_t Ah = rh[A];
+            out[15] = cz_encode_hi(n, gs, p, ph, i, A, Ah, ring);
+            a = A;
+            ah = Ah;
             al = i - 1;
         }
-        node[0] = F[(size_t)a * CX_FINGERS + al];
-        nid[0] = ld128(ring + node[0]);
-        out[0] = cz_encode(n, gs, a, aid, al, node[0], nid[0]);
+        node[0] = fat(a, al);
+        if (node[0] >= n) {
+            node[0] = 0;
+            oob = 1;
+        }
+        nh[0] = rh[node[0]];
+        out[0] = cz_encode_hi(n, gs, a, ah, al, node[0], nh[0], ring);
 #pragma unroll
-        for (int v = 1; v < 15; ++v) {
+        for (int v = 1; v < 16; ++v) {
             const int hb = 31 - __builtin_clz((unsigned)v);
             const int pv = v & ~(1 << hb);
             const int lv = i - 2 - hb;
-            node[v] = F[(size_t)node[pv] * CX_FINGERS + lv];
-            nid[v] = ld128(ring + node[v]);
-            out[v] = cz_encode(n, gs, node[pv], nid[pv], lv, node[v], nid[v]);
-        }
-        if (!b) {  // v = 15: parent 7, level i - 5
-            node[15] = F[(size_t)node[7] * CX_FINGERS + i - 5];
-            nid[15] = ld128(ring + node[15]);
-            out[15] = cz_encode(n, gs, node[7], nid[7], i - 5, node[15], nid[15]);
+            if (v == 15 && b) continue;  // slot 15 of a b = 1 entry is A (above)
+            uint32_t x = fat(node[pv], lv);
+            if (x >= n) {  // not a converged finger table: reported, never followed
+                x = 0;
+                oob = 1;
+            }
+            const uint64_t xh = rh[x];
+            out[v] = cz_encode_hi(n, gs, node[pv], nh[pv], lv, x, xh, ring);
+            if (v < 8) {
+                node[v] = x;
+                nh[v] = xh;
+            }
         }
 #pragma unroll
         for (int v = 0; v < 16; ++v) bad += out[v] == CZ_NONE;
         uint4 *e = cz + t * 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            e[k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
+        for (int k = 0; k < 4; ++k) {
+            // streaming store: the 64 GiB table must not evict the gathered
+            // finger planes and high words from L2 (56.5 -> 53.7 ms at 2^24)
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u w = {out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]};
+            __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(e + k));
+        }
     }
+    if (oob) atomicOr(esc + 1, 1u);
     if (bad) atomicAdd(esc, bad);
 }
 
-hipError_t cz_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
-                    uint64_t *cz, uint32_t *esc, hipStream_t s) {
-    return cz_build_part(F, ring, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s);
+hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
+                    int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s) {
+    return cz_build_part(fv, ring, rh, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s);
 }
 
-hipError_t cz_build_part(const uint32_t *F, const cell128 *ring, size_t n, int lvl_base, int nlev,
-                         uint32_t p_first, uint32_t M, int ib, uint64_t *cz, uint32_t *esc,
-                         hipStream_t s) {
+hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
+                         int lvl_base, int nlev, uint32_t p_first, uint32_t M, int ib,
+                         uint64_t *cz, uint32_t *esc, hipStream_t s) {
     if (M == 0 || nlev <= 0) return hipSuccess;
-    k_cz_build<<<cx_grid((size_t)M * nlev * 2, 256), 256, 0, s>>>(
-        F, ring, (uint32_t)n, lvl_base, nlev, p_first, M, cz_shift(ib),
-        reinterpret_cast<uint4 *>(cz), esc);
+    if (lvl_base - 5 < fv.L || lvl_base + nlev > fv.L + fv.nl) return hipErrorInvalidValue;
+    // the high-word gap codes need every level >= 64 and gs >= 64
+    if (lvl_base - 5 < 64 || cz_shift(ib) < 65) return hipErrorInvalidValue;
+    if (p_first >= n || M > n || nlev * 2 > 65535) return hipErrorInvalidValue;
+    const uint32_t per = (uint32_t)((M + 256 * 8 - 1) / (256 * 8));
+    const dim3 grid(per * 8, nlev * 2);
+    if (n >= (1u << 30)) return hipErrorInvalidValue;
+    const bool planes = fv.sx == 1;
+    if (!planes && (fv.sx != CX_FINGERS || fv.sl != 1 || fv.L != 0)) return hipErrorInvalidValue;
+    if (planes && fv.sl != n) return hipErrorInvalidValue;
+    if (planes)
+        k_cz_build<true><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first,
+                                              M, cz_shift(ib), reinterpret_cast<uint4 *>(cz), esc);
+    else
+        k_cz_build<false><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first,
+                                               M, cz_shift(ib), reinterpret_cast<uint4 *>(cz), esc);
+    return hipGetLastError();
+}
+
+// Order-sensitive hash of a table (A/B identity of two builds): sum over words
+// of splitmix(w ^ golden * (index + 1)), wrapping.
+__global__ void k_table_hash(const uint64_t *t, size_t words, unsigned long long *out) {
+    uint64_t acc = 0;
+    for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < words;
+         k += (size_t)gridDim.x * blockDim.x) {
+        uint64_t z = t[k] ^ (0x9E3779B97F4A7C15ull * (k + 1));
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        acc += z ^ (z >> 31);
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+hipError_t table_hash(const void *t, size_t bytes, unsigned long long *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(*out), s);
+    if (e != hipSuccess || bytes < 8) return e;
+    k_table_hash<<<cx_grid(bytes / 8, 256), 256, 0, s>>>(static_cast<const uint64_t *>(t),
+                                                         bytes / 8, out);
     return hipGetLastError();
 }
 

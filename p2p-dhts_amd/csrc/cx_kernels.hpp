@@ -106,8 +106,30 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
                       const uint64_t *tree, int l0, int R, int ib, const uint32_t *F,
                       const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
                       uint8_t *hops, uint8_t *status, hipStream_t s);
-hipError_t cz_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
-                    uint64_t *cz, uint32_t *esc, hipStream_t s);
+// Finger access for the route-table builds: F[x][l] = F[x * sx + (l - L) * sl]
+// for l in [L, L + nl): the row-major table (sx = 128, sl = 1, L = 0,
+// nl = 128) or level planes from fingers_levels (sx = 1, sl = n).
+struct FingerView {
+    const uint32_t *F;
+    size_t sx, sl;
+    int L, nl;
+    __host__ __device__ uint32_t at(uint32_t x, int l) const {
+        return F[(size_t)x * sx + (size_t)(l - L) * sl];
+    }
+    static FingerView rows(const uint32_t *F) { return FingerView{F, CX_FINGERS, 1, 0, CX_FINGERS}; }
+    static FingerView planes(const uint32_t *FT, size_t n, int L, int nl) {
+        return FingerView{FT, 1, n, L, nl};
+    }
+};
+// Order-sensitive 64-bit hash of `bytes` (multiple of 8) into *out (device).
+hipError_t table_hash(const void *t, size_t bytes, unsigned long long *out, hipStream_t s);
+hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
+                          hipStream_t s);
+// rh = the IDs' high words (ring_hi); the build needs l0 >= 69 and ib <= 51.
+// esc[0] += slots not representable; esc[1] |= 1 if a finger was out of range.
+hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s);
+hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
+                    int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s);
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
@@ -116,9 +138,9 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
 // the walk's access pattern, over `bytes` of `table` (read only): entries/s.
 hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, double *rate,
                         hipStream_t s);
-hipError_t cz_build_part(const uint32_t *F, const cell128 *ring, size_t n, int lvl_base, int nlev,
-                         uint32_t p_first, uint32_t M, int ib, uint64_t *cz, uint32_t *esc,
-                         hipStream_t s);
+hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
+                         int lvl_base, int nlev, uint32_t p_first, uint32_t M, int ib,
+                         uint64_t *cz, uint32_t *esc, hipStream_t s);
 hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                      int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo, uint32_t M,
                      int self, const ArcRec *in, const uint32_t *src, const cell128 *keys, size_t q,

@@ -599,3 +599,22 @@ def test_predecessor(cx, O, refvec):
         ring = cx.Ring(ids)
         keys = edge_keys(O, want_ring, seed + 100, 20000)
         assert (ring.predecessor(keys) == O.predecessor(want_ring, keys)).all()
+
+
+@pytest.mark.parametrize("lg", [12, 20])
+def test_route_table_from_level_planes_identical(lg):
+    """The pattern-keyed table built from finger level planes is bit-identical
+    to the one built from the row-major finger table."""
+    import torch
+
+    import chordx
+    ids = torch.empty((1 << lg, 2), dtype=torch.int64, device="cuda:0")
+    chordx.fill_splitmix(ids, 0x5EED0003 + lg)
+    ring = chordx.Ring(ids)
+    ring.build_fingers()
+    assert ring.route_info()[0] == 5
+    h_planes = ring.route_table_hash()
+    ring.set_table_build(1)
+    ring.build_fingers()
+    h_rows = ring.route_table_hash()
+    assert h_planes == h_rows and h_planes != 0
