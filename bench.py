@@ -355,6 +355,15 @@ def main():
     torch.cuda.synchronize(dev)
     eyt_ms = e0.elapsed_time(e1) / 3
     owner_eq = owner_eq and bool((succ_out == owner).all().item())
+    ring.set_search_variant(2)  # A/B: wave-cooperative 16-ary tree (ballot + popcount)
+    ring.successor(keys, out=succ_out)
+    e0.record(stream)
+    for _ in range(3):
+        ring.successor(keys, out=succ_out)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wave_ms = e0.elapsed_time(e1) / 3
+    owner_eq = owner_eq and bool((succ_out == owner).all().item())
     ring.set_search_variant(1)
     # A/B: the other route kernels on the same batch (bit-identical results)
     variant_ms = {}
@@ -436,6 +445,7 @@ def main():
             "route_owner_equals_successor": owner_eq,
             "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
             "exact_successor_eytzinger_lookups_per_s": Q / (eyt_ms * 1e-3),
+            "exact_successor_wave16_lookups_per_s": Q / (wave_ms * 1e-3),
             "route_variant_kernel_ms": variant_ms,
             "setup_s": {"ring_sort": t_ring, "fingers_build": t_fing},
         }

@@ -90,7 +90,7 @@ def main():
     ring = chordx.Ring(keys_dev(1 << 16, 0x5EED0001))
     keys = keys_dev(1 << 20, 0x5EED0002)
     res = {}
-    for v, name in ((1, "directory"), (0, "eytzinger")):
+    for v, name in ((1, "directory"), (0, "eytzinger"), (2, "wave16")):
         ring.set_search_variant(v)
         t = ev_time(lambda: ring.successor(keys))
         res[name] = {"s": t, "lookups_per_s": (1 << 20) / t,

@@ -307,7 +307,9 @@ class Ring:
         L.check(f(self._h, v))
 
     def set_search_variant(self, v: int):
-        """Internal A/B switch: 0 = Eytzinger (LDS top levels), 1 = bucket directory."""
+        """Internal A/B switch: 0 = Eytzinger (LDS top levels), 1 = bucket directory
+        (default), 2 = wave-cooperative 16-ary tree (ballot/popcount; successor
+        and predecessor only, the other searches keep the directory)."""
         f = L.lib().cxi_set_search_variant
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))

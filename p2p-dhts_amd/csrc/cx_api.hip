@@ -144,7 +144,9 @@ struct cx_ring {
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
     uint32_t *d_ring_key = nullptr; // ID slices [n] of the streaming finger build
     int dir_k = 1;
-    int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory
+    int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory,
+                                   // 2: wave-cooperative 16-ary tree (successor / predecessor)
+    cell128 *d_stree = nullptr;    // levels 1.. of the 16-ary tree (variant 2, lazy)
     int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
 
     EytView eyt() const {
@@ -157,7 +159,7 @@ struct cx_ring {
     SearchView sv() const {
         SearchView v;
         v.ev = eyt();
-        v.dir = (search_variant == 1) ? d_dir : nullptr;
+        v.dir = (search_variant != 0) ? d_dir : nullptr;
         v.k = dir_k;
         v.ring = d_ring;
         return v;
@@ -269,6 +271,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_pk);
     (void)hipFree(r->d_tree);
     (void)hipFree(r->d_cz);
+    (void)hipFree(r->d_stree);
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
@@ -574,6 +577,22 @@ int cx_ring_sync(const cx_ring *ring) {
     return CX_OK;
 }
 
+namespace {
+// The 16-ary tree's levels (search variant 2), built on first use.
+int stree_view(cx_ring *r, cxk::STreeView &st, hipStream_t s) {
+    st = cxk::stree_plan(r->d_ring, r->n, r->d_stree);
+    if (!r->d_stree && st.words) {
+        if (hipMalloc(&r->d_stree, st.words * sizeof(cell128)) != hipSuccess) {
+            r->d_stree = nullptr;
+            return fail(CX_E_NOMEM, "hipMalloc of the 16-ary search levels failed");
+        }
+        st = cxk::stree_plan(r->d_ring, r->n, r->d_stree);
+        CX_HIP(cxk::stree_build(st, s));
+    }
+    return CX_OK;
+}
+}  // namespace
+
 int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *owner,
                  int memkind) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
@@ -585,7 +604,13 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
     uint32_t *dout;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
     if ((rc = stage_out(owner, q, memkind, to, &dout))) return rc;
-    CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    if (ring->search_variant == 2) {
+        cxk::STreeView st;
+        if ((rc = stree_view(const_cast<cx_ring *>(ring), st, s))) return rc;
+        CX_HIP(cxk::successor_stree(st, reinterpret_cast<const cell128 *>(dk), q, dout, false, s));
+    } else {
+        CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    }
     return finish_out(owner, dout, q, memkind, s);
 }
 
@@ -626,7 +651,13 @@ int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t 
     uint32_t *dout;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
     if ((rc = stage_out(pred, q, memkind, to, &dout))) return rc;
-    CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    if (ring->search_variant == 2) {
+        cxk::STreeView st;
+        if ((rc = stree_view(const_cast<cx_ring *>(ring), st, s))) return rc;
+        CX_HIP(cxk::successor_stree(st, reinterpret_cast<const cell128 *>(dk), q, dout, true, s));
+    } else {
+        CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+    }
     return finish_out(pred, dout, q, memkind, s);
 }
 
@@ -1629,10 +1660,12 @@ int cxi_set_churn_variant(cx_ring *ring, int variant) {
     return CX_OK;
 }
 
-// 0 = Eytzinger search with LDS-staged top levels, 1 = bucket directory (default).
+// 0 = Eytzinger search with LDS-staged top levels, 1 = bucket directory (default),
+// 2 = wave-cooperative 16-ary tree for cx_successor / cx_predecessor (the
+// other searches keep the directory).
 int cxi_set_search_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
     ring->search_variant = variant;
     return CX_OK;
 }

@@ -380,6 +380,140 @@ hipError_t predecessor(const SearchView &sv, const cell128 *keys, size_t q, uint
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Search variant 2: wave-cooperative 16-ary search (static S+-tree over the
+// sorted ring).  Level 0 is the ring; level l >= 1 holds every 16^l-th ID,
+// S_l[j] = ring[j * 16^l], so block c of level l (16 consecutive entries) is
+// the 16 children separators under entry c of level l+1 and S_l[16c] =
+// S_{l+1}[c].  Sixteen lanes search one query: lane i loads entry 16c + i
+// (one coalesced 256-B block per query and level), compares it with the key
+// in 128 bits, and the wave's ballot, cut to the group's 16 bits and counted
+// (a sorted block gives a prefix mask, popcount = its length), names the child:
+// c <- 16c + cnt - 1 (cnt >= 1 below the top: the block's first entry is the
+// parent separator, < key).  At level 0 the count is #{ids < key} = the
+// successor index.  Four queries per wave instruction, U rounds interleaved
+// so U loads per lane are in flight per level.  Levels 1.. take n/15 IDs: at
+// 2^24 level 1 is 16 MiB (MALL-resident), levels 2-5 1 MiB and less (L2);
+// level 0 is the ring.
+// ---------------------------------------------------------------------------
+__global__ void k_stree_level(const cell128 *ring, uint32_t sz, int shift, cell128 *out) {
+    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < sz;
+         j += (size_t)gridDim.x * blockDim.x)
+        out[j] = ring[j << shift];
+}
+
+constexpr uint32_t ST_LDS = 4384;  // cells of staged top levels: 70 KB, 2 blocks of 1024 per CU
+constexpr int ST_BLOCK = 1024;
+
+STreeView stree_plan(const cell128 *ring, size_t n, cell128 *buf) {
+    STreeView v{};
+    v.lv[0] = ring;
+    v.sz[0] = (uint32_t)n;
+    int l = 0;
+    size_t off = 0;
+    while (v.sz[l] > 16 && l + 1 < CX_STREE_MAX) {
+        v.sz[l + 1] = (v.sz[l] + 15) / 16;
+        v.lv[l + 1] = buf ? buf + off : nullptr;
+        off += v.sz[l + 1];
+        ++l;
+    }
+    v.top = l;
+    v.words = off;
+    // stage the top levels in LDS while they fit (16 + 256 + 4096 cells at 2^24)
+    uint32_t used = 0;
+    v.lds_from = v.top + 1;
+    for (int k = v.top; k >= 1 && used + v.sz[k] <= ST_LDS; --k) {
+        v.lds_off[k] = used;
+        used += v.sz[k];
+        v.lds_from = k;
+    }
+    return v;
+}
+
+hipError_t stree_build(const STreeView &v, hipStream_t s) {
+    for (int l = 1; l <= v.top; ++l) {
+        k_stree_level<<<cx_grid(v.sz[l], 256), 256, 0, s>>>(v.lv[0], v.sz[l], 4 * l,
+                                                            const_cast<cell128 *>(v.lv[l]));
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+template <bool PRED, int U>
+__global__ __launch_bounds__(ST_BLOCK) void k_successor_stree(STreeView st, const cell128 *keys,
+                                                              size_t q, uint32_t *owner) {
+    __shared__ u128 lds[ST_LDS];
+    for (int l = st.lds_from; l <= st.top; ++l)
+        for (uint32_t k = threadIdx.x; k < st.sz[l]; k += blockDim.x)
+            lds[st.lds_off[l] + k] = ld128(st.lv[l] + k);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t n = st.sz[0];
+    const u128 inf = ~(u128)0;
+    for (size_t base = wave * 4 * U; base < q; base += nwaves * 4 * U) {
+        u128 x[U];
+        uint32_t c[U];
+        bool live[U], zero[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t qi = base + u * 4 + g;
+            live[u] = qi < q;
+            x[u] = live[u] ? ld128(keys + qi) : (u128)0;
+            c[u] = 0;
+            zero[u] = false;
+        }
+        for (int l = st.top; l >= 0; --l) {
+            const cell128 *L = st.lv[l];
+            const uint32_t sz = st.sz[l];
+            u128 k[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t idx = c[u] * 16 + li;
+                if (l >= st.lds_from)
+                    k[u] = idx < sz ? lds[st.lds_off[l] + idx] : inf;
+                else
+                    k[u] = idx < sz ? ld128(L + idx) : inf;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool lt = live[u] && k[u] < x[u];
+                const uint32_t m = (uint32_t)(__ballot(lt) >> (16 * g)) & 0xFFFFu;
+                const uint32_t cnt = __popc(m);
+                if (l > 0) {
+                    if (cnt == 0) zero[u] = true;  // key <= ring[0] (top level only)
+                    else if (!zero[u]) c[u] = c[u] * 16 + cnt - 1;
+                } else {
+                    c[u] = zero[u] ? 0 : c[u] * 16 + cnt;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t qi = base + u * 4 + g;
+            if (live[u] && li == 0) {
+                const uint32_t sidx = c[u] >= n ? 0u : c[u];
+                owner[qi] = PRED ? (sidx == 0 ? n - 1 : sidx - 1) : sidx;
+            }
+        }
+    }
+}
+
+hipError_t successor_stree(const STreeView &st, const cell128 *keys, size_t q, uint32_t *owner,
+                           bool pred, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    constexpr int U = 4;
+    const size_t waves = (q + 4 * U - 1) / (4 * U);
+    const unsigned blocks = cx_grid(waves * 64, ST_BLOCK, 512);  // 2 per CU (LDS)
+    if (pred)
+        k_successor_stree<true, U><<<blocks, ST_BLOCK, 0, s>>>(st, keys, q, owner);
+    else
+        k_successor_stree<false, U><<<blocks, ST_BLOCK, 0, s>>>(st, keys, q, owner);
+    return hipGetLastError();
+}
+
 // Directory build: lo[b] = first ring index whose ID is >= b << (128 - k).
 // Thread j fills the buckets (bucket(ring[j-1]), bucket(ring[j])]; thread n
 // fills the tail up to 2^k.

@@ -123,6 +123,20 @@ struct FingerView {
 };
 // Order-sensitive 64-bit hash of `bytes` (multiple of 8) into *out (device).
 hipError_t table_hash(const void *t, size_t bytes, unsigned long long *out, hipStream_t s);
+// Search variant 2: static 16-ary S+-tree over the ring (k_successor_stree).
+#define CX_STREE_MAX 10
+struct STreeView {
+    const cell128 *lv[CX_STREE_MAX];  // lv[0] = the ring; lv[l][j] = ring[j * 16^l]
+    uint32_t sz[CX_STREE_MAX];
+    int top;                          // sz[top] <= 16
+    size_t words;                     // cells of levels 1..top (buffer size)
+    int lds_from;                     // levels >= lds_from are staged in LDS
+    uint32_t lds_off[CX_STREE_MAX];   // their offsets there (cells)
+};
+STreeView stree_plan(const cell128 *ring, size_t n, cell128 *buf);
+hipError_t stree_build(const STreeView &v, hipStream_t s);
+hipError_t successor_stree(const STreeView &st, const cell128 *keys, size_t q, uint32_t *owner,
+                           bool pred, hipStream_t s);
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s);
 // rh = the IDs' high words (ring_hi); the build needs l0 >= 69 and ib <= 51.

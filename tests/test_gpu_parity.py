@@ -60,8 +60,8 @@ def test_ring_build_equal_high_bits(cx, O):
 
 
 # ---------------------------------------------------------------- a5/a7 successor
-@pytest.mark.parametrize("search", [0, 1])
-@pytest.mark.parametrize("n", [1, 2, 3, 8, 1000, 4095, 4096, 70000])
+@pytest.mark.parametrize("search", [0, 1, 2])
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 16, 17, 256, 257, 1000, 4095, 4096, 65537, 70000])
 def test_successor(cx, O, n, search):
     ids = edge_ring(O, n, 77 + n)
     ring = cx.Ring(ids)
@@ -72,7 +72,7 @@ def test_successor(cx, O, n, search):
     assert (got == O.successor(want_ring, keys)).all()
 
 
-@pytest.mark.parametrize("search", [0, 1])
+@pytest.mark.parametrize("search", [0, 1, 2])
 def test_successor_c2(cx, O, search):
     """Config C2: 2^16-peer ring, 2^20 uniform keys (seeds of SURVEY 8d)."""
     ids = O.splitmix_keys(0x5EED0001, 1 << 16)
@@ -569,34 +569,23 @@ def test_misplaced_with_foreign_map_and_chained_churn(cx, O):
         assert (g == w).all()
 
 
-def test_predecessor(cx, O, refvec):
+
+
+@pytest.mark.parametrize("search", [1, 2])
+def test_predecessor(cx, O, refvec, search):
     """Batched GetPredecessor vs the oracle: reference fixtures, edge rings and
     keys (IDs, +-1, 0, 2^128 - 1), N = 1, 2, 3."""
     for case in ("in_succ_list", "from_finger_table"):
         g = refvec["get_pred"][case]
         ring = cx.Ring(O.keys_from_ints([H(x) for x in g["peers"]]))
+        ring.set_search_variant(search)
         names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
         assert names[ring.predecessor(O.keys_from_ints([H(g["key"])]))[0]] == g["expected"]
     for n, seed in ((1, 1), (2, 2), (3, 3), (1000, 4), (70001, 5)):
         ids = edge_ring(O, n, seed)
         want_ring = O.ring_build(ids)
         ring = cx.Ring(ids)
-        keys = edge_keys(O, want_ring, seed + 100, 20000)
-        assert (ring.predecessor(keys) == O.predecessor(want_ring, keys)).all()
-
-
-def test_predecessor(cx, O, refvec):
-    """Batched GetPredecessor vs the oracle: reference fixtures, edge rings and
-    keys (IDs, +-1, 0, 2^128 - 1), N = 1, 2, 3."""
-    for case in ("in_succ_list", "from_finger_table"):
-        g = refvec["get_pred"][case]
-        ring = cx.Ring(O.keys_from_ints([H(x) for x in g["peers"]]))
-        names = [format(v, "x") for v in O.ints_from_keys(ring.ids())]
-        assert names[ring.predecessor(O.keys_from_ints([H(g["key"])]))[0]] == g["expected"]
-    for n, seed in ((1, 1), (2, 2), (3, 3), (1000, 4), (70001, 5)):
-        ids = edge_ring(O, n, seed)
-        want_ring = O.ring_build(ids)
-        ring = cx.Ring(ids)
+        ring.set_search_variant(search)
         keys = edge_keys(O, want_ring, seed + 100, 20000)
         assert (ring.predecessor(keys) == O.predecessor(want_ring, keys)).all()
 
