@@ -47,12 +47,13 @@ def main():
     t_churn, (new, o2n) = wall(lambda: old.churn(joins, leaves))
     out = {"log2_peers": lg, "ring_new": new.n, "old_fingers_and_table_s": t_old,
            "churn_s": t_churn}
-    for name, v in (("rows", 1), ("planes", 0), ("planes_again", 0)):
+    for name, v in (("rows", 1), ("planes_only", 2), ("planes", 0), ("planes_again", 0)):
         new.set_table_build(v)
         t, _ = wall(new.build_fingers)
         out[f"fingers_and_table_{name}_s"] = t
         out[f"hash_{name}"] = new.route_table_hash()
-    out["identical"] = out["hash_rows"] == out["hash_planes"] == out["hash_planes_again"]
+    out["identical"] = (out["hash_rows"] == out["hash_planes_only"] == out["hash_planes"]
+                        == out["hash_planes_again"])
     out["route_ready_after_churn_s"] = t_churn + out["fingers_and_table_planes_again_s"]
     keys = keys_dev(1 << 24, 0x5EED0008)
     src = (torch.arange(1 << 24, device="cuda", dtype=torch.int64) % new.n).to(torch.int32)

@@ -295,7 +295,8 @@ class Ring:
 
     def set_table_build(self, v: int):
         """Internal A/B switch for the route-table build's finger input:
-        0 = level planes (default), 1 = the row-major finger table."""
+        0 = level planes + two-hop planes (default), 1 = the row-major finger
+        table, 2 = level planes only."""
         f = L.lib().cxi_set_table_build
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))

@@ -118,7 +118,8 @@ struct cx_ring {
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
     uint64_t *d_cz = nullptr;      // pattern-keyed window table [rt_R][2][n][8 x u64] (variant 5)
-    bool cz_rows = false;          // A/B: build from the row-major fingers, not level planes
+    int table_build = 0;           // route-table build input: 0 level + two-hop planes,
+                                   // 1 row-major fingers, 2 level planes only (A/B)
     bool cz_valid = false;
     uint64_t cz_escapes = 0;       // nodes the compressed format could not represent
     int route_variant = -1;        // 0: finger+ring gathers, 1: route table, 2: packed table,
@@ -339,18 +340,24 @@ void route_geometry(cx_ring *r) {
 // planes in `ft` when HBM allows (cxi_set_table_build(ring, 1) forces the
 // row-major table, for A/B), else the row-major table itself.
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
-                         hipStream_t s) {
+                         DBuf &c2, hipStream_t s) {
     fv = cxk::FingerView::rows(r->d_fingers);
     hipError_t e0 = hi.alloc(r->n * sizeof(uint64_t));
     if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
     if (e0 != hipSuccess) return e0;
     const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
-    if (r->cz_rows || ft.alloc((size_t)nl * r->n * sizeof(uint32_t)) != hipSuccess) {
+    if (r->table_build == 1 || ft.alloc((size_t)nl * r->n * sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
         return hipSuccess;
     }
     hipError_t e = cxk::fingers_levels(r->d_fingers, r->n, L, nl, ft.as<uint32_t>(), s);
-    if (e == hipSuccess) fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
+    if (e != hipSuccess) return e;
+    fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
+    if (r->table_build == 0 && c2.alloc((size_t)(nl - 1) * r->n * sizeof(uint32_t)) == hipSuccess) {
+        e = cxk::fingers_pairs(ft.as<uint32_t>(), r->n, nl, c2.as<uint32_t>(), s);
+        if (e == hipSuccess) fv.C2 = c2.as<uint32_t>();
+    }
+    (void)hipGetLastError();
     return e;
 }
 
@@ -366,9 +373,9 @@ int ensure_route_table(cx_ring *r, hipStream_t s) {
         }
         if (r->d_cz) {
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
-            DBuf ft, hi;
+            DBuf ft, hi, c2;
             cxk::FingerView fv;
-            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, s));
+            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s));
             CX_HIP(cxk::cz_build(fv, r->d_ring, hi.as<uint64_t>(), r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_cz,
                                  r->d_scratch, s));
             uint32_t esc[2] = {0, 0};
@@ -1399,9 +1406,9 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     }
     CX_HIP(hipMemsetAsync(ring->d_scratch, 0, 2 * sizeof(uint32_t), s));
     {
-        DBuf ft, hi;
+        DBuf ft, hi, c2;
         cxk::FingerView fv;
-        CX_HIP(finger_planes(ring, l0, ft, fv, hi, s));
+        CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s));
         CX_HIP(cxk::cz_build_part(fv, ring->d_ring, hi.as<uint64_t>(), n, Lh, (int)CX_FINGERS - Lh, 0, (uint32_t)n,
                                   ring->pk_ib, ring->d_arc_tree, ring->d_scratch, s));
         CX_HIP(cxk::cz_build_part(fv, ring->d_ring, hi.as<uint64_t>(), n, l0, Lh - l0, plo, M, ring->pk_ib,
@@ -1643,12 +1650,13 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
     return CX_OK;
 }
 
-// Route-table build input: 0 = finger level planes (default), 1 = row-major
-// finger table.  Takes effect at the next finger build.
+// Route-table build input: 0 = finger level planes + two-hop planes (default),
+// 1 = row-major finger table, 2 = level planes only.  Takes effect at the next
+// finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
-    ring->cz_rows = variant == 1;
+    CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
+    ring->table_build = variant;
     return CX_OK;
 }
 

@@ -2007,6 +2007,26 @@ __global__ void k_fingers_levels(const uint32_t *F, uint32_t n, int L, int nl, u
     }
 }
 
+// Two-hop planes: C2[(l - L - 1) n + x] = F[F[x][l]][l - 1].  One gather per
+// entry into the plane below (adjacent x -> adjacent fingers: coalesced-ish).
+__global__ void k_fingers_pairs(const uint32_t *FT, uint32_t n, int nl, uint32_t *C2) {
+    const size_t total = (size_t)(nl - 1) * n;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        const size_t k = t / n;  // plane of level L + 1 + k
+        const size_t x = t - k * n;
+        const uint32_t y = FT[(k + 1) * n + x];
+        C2[t] = y < n ? FT[k * n + y] : CX_NONE;
+    }
+}
+
+hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hipStream_t s) {
+    if (n == 0 || nl < 2) return hipSuccess;
+    k_fingers_pairs<<<cx_grid((size_t)(nl - 1) * n, 256, 16384), 256, 0, s>>>(FT, (uint32_t)n, nl,
+                                                                               C2);
+    return hipGetLastError();
+}
+
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s) {
     if (n == 0 || nl <= 0) return hipSuccess;
@@ -2068,12 +2088,16 @@ __device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t pa
 // entry per lane in dispatch order (resident waves on a compact window of
 // rows, XCD-aware), 54 ms with streaming stores (profiles/r02/cz_build/).
 // The build is bound by its 5-deep dependent finger chain (SQ_WAIT_ANY 86 %
-// of wave cycles, 29 GB fetched + 64 GiB written = 1.7 TB/s); 6 or 8 waves
+// of wave cycles, 29 GB fetched + 64 GiB written = 1.7 TB/s).  MODE 2 takes
+// each consecutive level pair of a slot's path as one gather from two-hop
+// planes (chain 5 -> 3 gathers): 53.5 -> 47.9 ms, + 1.7 ms to build the
+// planes (profiles/r02/cz_build/kernel_stats_modes.csv).  6 or 8 waves
 // per SIMD (forced, with spills) are slower (60 / 71 ms); storing each 16-B
 // row as soon as its slots are known serialised the gathers behind the
 // stores (95 ms); a quad of lanes per entry (four columns of the slot square)
 // issued more, less coalesced gathers (97 ms).
-template <bool PLANES>
+// MODE 0: row-major fingers; 1: level planes; 2: level + two-hop planes.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *ring,
                                                   const uint64_t *rh, uint32_t n, int lvl_base,
                                                   int nlev, uint32_t p_first, uint32_t M, int gs,
@@ -2084,7 +2108,7 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
     const int i = lvl_base + (int)(plane >> 1);
     // finger (x, l): level planes -> plane base (uniform) + x; rows -> x * 128 + l
     auto fat = [&](uint32_t x, int l) -> uint32_t {
-        if (PLANES) return fv.F[(size_t)(l - fv.L) * fv.sl + x];
+        if (MODE != 0) return fv.F[(size_t)(l - fv.L) * fv.sl + x];
         return fv.F[(size_t)x * CX_FINGERS + l];
     };
     // one entry per lane, no grid stride: the dispatcher walks blocks in
@@ -2105,6 +2129,60 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
         uint32_t node[8], out[16];
         uint64_t nh[8];
         const uint64_t ph = rh[p];
+        if (MODE == 2) {
+            // two-hop planes cut the dependent chain from 5 gathers to 3:
+            // slot v's node = its levels' fingers in descending order, with
+            // each consecutive pair (l, l-1) taken as one C2 gather
+            auto c2 = [&](uint32_t x, int l) -> uint32_t {
+                return fv.C2[(size_t)(l - fv.L - 1) * fv.sl + x];
+            };
+            auto chk = [&](uint32_t x) -> uint32_t {
+                if (x >= n) {  // not a converged finger table: reported, never followed
+                    oob = 1;
+                    return 0u;
+                }
+                return x;
+            };
+            uint32_t nd[16], A = 0, a = p;
+            int al = i;
+            if (b) {  // slot 15 = A = f(p, i); the window hangs off A' = f(A, i-1) = C2(p, i)
+                A = chk(fat(p, i));
+                a = A;
+                al = i - 1;
+                nd[0] = chk(c2(p, i));
+            } else {
+                nd[0] = chk(fat(p, i));
+            }
+            // depth 2 (bit w <-> level i-2-w)
+            nd[1] = chk(fat(nd[0], i - 2));
+            nd[2] = chk(fat(nd[0], i - 3));
+            nd[3] = chk(c2(nd[0], i - 2));
+            nd[4] = chk(fat(nd[0], i - 4));
+            nd[6] = chk(c2(nd[0], i - 3));
+            nd[8] = chk(fat(nd[0], i - 5));
+            nd[12] = chk(c2(nd[0], i - 4));
+            // depth 3
+            nd[5] = chk(fat(nd[1], i - 4));
+            nd[7] = chk(fat(nd[3], i - 4));
+            nd[9] = chk(fat(nd[1], i - 5));
+            nd[10] = chk(fat(nd[2], i - 5));
+            nd[11] = chk(fat(nd[3], i - 5));
+            nd[13] = chk(c2(nd[1], i - 4));
+            nd[14] = chk(c2(nd[2], i - 4));
+            nd[15] = b ? A : chk(c2(nd[3], i - 4));
+            uint64_t hv[16];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) hv[v] = rh[nd[v]];
+            const uint64_t ah = b ? hv[15] : ph;
+            out[0] = cz_encode_hi(n, gs, a, ah, al, nd[0], hv[0], ring);
+#pragma unroll
+            for (int v = 1; v < 16; ++v) {
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pv = v & ~(1 << hb);
+                out[v] = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+            }
+            if (b) out[15] = cz_encode_hi(n, gs, p, ph, i, A, hv[15], ring);
+        } else {
         uint32_t a = p;
         uint64_t ah = ph;
         int al = i;
@@ -2145,6 +2223,7 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
                 nh[v] = xh;
             }
         }
+        }  // chained path
 #pragma unroll
         for (int v = 0; v < 16; ++v) bad += out[v] == CZ_NONE;
         uint4 *e = cz + t * 4;
@@ -2178,14 +2257,20 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     const dim3 grid(per * 8, nlev * 2);
     if (n >= (1u << 30)) return hipErrorInvalidValue;
     const bool planes = fv.sx == 1;
-    if (!planes && (fv.sx != CX_FINGERS || fv.sl != 1 || fv.L != 0)) return hipErrorInvalidValue;
+    if (!planes && (fv.sx != CX_FINGERS || fv.sl != 1 || fv.L != 0 || fv.C2))
+        return hipErrorInvalidValue;
     if (planes && fv.sl != n) return hipErrorInvalidValue;
-    if (planes)
-        k_cz_build<true><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first,
-                                              M, cz_shift(ib), reinterpret_cast<uint4 *>(cz), esc);
+    uint4 *out = reinterpret_cast<uint4 *>(cz);
+    const int gs = cz_shift(ib);
+    if (planes && fv.C2)
+        k_cz_build<2><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
+                                           gs, out, esc);
+    else if (planes)
+        k_cz_build<1><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
+                                           gs, out, esc);
     else
-        k_cz_build<false><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first,
-                                               M, cz_shift(ib), reinterpret_cast<uint4 *>(cz), esc);
+        k_cz_build<0><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
+                                           gs, out, esc);
     return hipGetLastError();
 }
 

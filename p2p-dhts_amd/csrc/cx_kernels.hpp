@@ -113,12 +113,17 @@ struct FingerView {
     const uint32_t *F;
     size_t sx, sl;
     int L, nl;
+    // planes only, optional: two-hop planes C2[(l - L - 1) * sl + x] =
+    // F[F[x][l]][l - 1] for l in (L, L + nl) (fingers_pairs)
+    const uint32_t *C2 = nullptr;
     __host__ __device__ uint32_t at(uint32_t x, int l) const {
         return F[(size_t)x * sx + (size_t)(l - L) * sl];
     }
-    static FingerView rows(const uint32_t *F) { return FingerView{F, CX_FINGERS, 1, 0, CX_FINGERS}; }
+    static FingerView rows(const uint32_t *F) {
+        return FingerView{F, CX_FINGERS, 1, 0, CX_FINGERS, nullptr};
+    }
     static FingerView planes(const uint32_t *FT, size_t n, int L, int nl) {
-        return FingerView{FT, 1, n, L, nl};
+        return FingerView{FT, 1, n, L, nl, nullptr};
     }
 };
 // Order-sensitive 64-bit hash of `bytes` (multiple of 8) into *out (device).
@@ -139,6 +144,8 @@ hipError_t successor_stree(const STreeView &st, const cell128 *keys, size_t q, u
                            bool pred, hipStream_t s);
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s);
+// C2 planes (nl - 1 of them) from the level planes FT.
+hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hipStream_t s);
 // rh = the IDs' high words (ring_hi); the build needs l0 >= 69 and ib <= 51.
 // esc[0] += slots not representable; esc[1] |= 1 if a finger was out of range.
 hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s);

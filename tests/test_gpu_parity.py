@@ -606,4 +606,7 @@ def test_route_table_from_level_planes_identical(lg):
     ring.set_table_build(1)
     ring.build_fingers()
     h_rows = ring.route_table_hash()
-    assert h_planes == h_rows and h_planes != 0
+    ring.set_table_build(2)
+    ring.build_fingers()
+    h_planes_only = ring.route_table_hash()
+    assert h_planes == h_rows == h_planes_only and h_planes != 0
