@@ -120,7 +120,12 @@ def main():
     status = torch.empty(q, dtype=torch.uint8, device="cuda")
     tr = ev_time(lambda: ring.route(src, keys, out=(owner, hops, status)))
     sh = int(hops.to(torch.int64).sum())
-    algo = q * (25 + 64) + 128 * sh
+    # bench.py's roofline model: 58 B of streams per lookup + 64 B per random
+    # gather the walk issued (counted by the counting build on the same batch)
+    ring.route_counters(True)
+    ring.route(src, keys, out=(owner, hops, status))
+    g64, r16, xc, _ = ring.route_counters(False)
+    algo = q * 58 + 64 * (g64 + r16 + 2 * xc)
     ring_np = ring.ids()
     F_gpu = ring.fingers_device().cpu().numpy().view(np.uint32)
     cpu_f = cpu_leg(lambda q, th: O.fingers(ring_np, threads=th, rows=(0, q)), N3,
@@ -138,7 +143,8 @@ def main():
     out["C3"] = {"fingers_build_s_wall": tf, "cpu_fingers": cpu_f, "cpu_route": cpu_r,
                  "fingers_algo_GBps": N3 * 528 / tf / 1e9,
                  "route_s": tr, "route_lookups_per_s": q / tr, "mean_hops": sh / q,
-                 "route_algo_frac_of_hbm": algo / tr / HBM,
+                 "route_algo_GBps": algo / tr / 1e9, "route_algo_frac_of_hbm": algo / tr / HBM,
+                 "route_gathers_per_lookup": (g64 + r16 + 2 * xc) / q,
                  "bad_status": int((status != 0).sum())}
     del ring, keys, src, owner, hops, status
 
@@ -152,6 +158,8 @@ def main():
     # distinct leaving peers (odd stride mod 2^24): the new ring keeps 2^24 peers
     pick = (torch.arange(N5 // 100, device="cuda", dtype=torch.int64) * 0x9E3779B1) % N5
     leaves = old.ids_device()[pick].contiguous()
+    old.build_fingers()  # the live ring is route-ready when membership changes
+    old.sync()
     tcv = {}
     for cv in (0, 1, 1):  # re-sort, merge (twice: the first call warms allocations)
         old.set_churn_variant(cv)
@@ -167,7 +175,15 @@ def main():
     t0 = time.perf_counter()
     new.build_fingers()
     new.sync()
-    t_ready = time.perf_counter() - t0
+    t_first = time.perf_counter() - t0  # fresh HBM for the new ring's 72 GiB of tables
+    # steady state: the previous epoch's ring is gone (its tables in the pool)
+    del new, o2n
+    t0 = time.perf_counter()
+    new, o2n = old.churn(joins, leaves)
+    new.build_fingers()
+    new.sync()
+    t_cycle = time.perf_counter() - t0
+    t_ready = t_cycle - tc
     old_np, new_np = old.ids(), new.ids()
     o2n_np = o2n.cpu().numpy().view(np.uint32) if hasattr(o2n, "cpu") else np.asarray(o2n)
     j_np = joins.cpu().numpy().view(np.uint64)
@@ -182,8 +198,9 @@ def main():
                     q5, "keys/s", "keys (RunGlobalMaintenance restated, n = 14)",
                     lambda r, qq: (r[0] == lists_np[:qq]).all() and (r[2] == mask_np[:qq]).all())
     out["C5"] = {"ring_old": N5, "ring_new": new.n, "keys": q5, "n": n,
-                 "route_ready_after_churn_s_wall": tc + t_ready,
+                 "route_ready_after_churn_s_wall": t_cycle,
                  "new_fingers_and_route_table_s_wall": t_ready,
+                 "first_fingers_and_route_table_s_wall_fresh_hbm": t_first,
                  "cpu_churn": {"value_s": t_churn_cpu, "cores": 1, "kind": "port",
                                "identical": bool((want_new == new_np).all()
                                                  and (want_o2n == o2n_np).all())},

@@ -35,6 +35,95 @@ int fail(int code, const std::string &msg) {
     } while (0)
 
 // RAII device allocation.
+// ---------------------------------------------------------------------------
+// Table pool.  A ring's large tables (finger table, route tables, arc planes:
+// >= 1 GiB each, 72 GiB per 2^24-peer replica) are not returned to the driver
+// when the ring is destroyed but kept, up to CX_POOL_CAP bytes per process,
+// for the next ring that asks for the same size on the same device: after a
+// membership change the new ring's tables reuse the old ring's HBM instead of
+// paying ~0.6 s of fresh page mappings for 72 GiB.  A failed hipMalloc trims
+// the pool and retries; cxi_pool_trim releases it.
+// ---------------------------------------------------------------------------
+namespace {
+struct PoolEnt {
+    int device;
+    size_t bytes;
+    void *p;
+};
+std::mutex g_pool_mu;
+std::vector<PoolEnt> g_pool;
+size_t g_pool_bytes = 0;
+constexpr size_t POOL_MIN = (size_t)1 << 30;
+constexpr size_t POOL_CAP = (size_t)96 << 30;
+
+void pool_trim_locked(int device) {
+    for (size_t k = 0; k < g_pool.size();) {
+        if (device < 0 || g_pool[k].device == device) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(g_pool[k].device);
+            (void)hipFree(g_pool[k].p);
+            (void)hipSetDevice(cur);
+            g_pool_bytes -= g_pool[k].bytes;
+            g_pool.erase(g_pool.begin() + k);
+        } else {
+            ++k;
+        }
+    }
+}
+
+// hipMalloc through the pool (current device).
+hipError_t table_alloc(void **p, size_t bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (bytes >= POOL_MIN) {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t k = 0; k < g_pool.size(); ++k)
+            if (g_pool[k].device == dev && g_pool[k].bytes == bytes) {
+                *p = g_pool[k].p;
+                g_pool_bytes -= bytes;
+                g_pool.erase(g_pool.begin() + k);
+                return hipSuccess;
+            }
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            pool_trim_locked(dev);
+        }
+        e = hipMalloc(p, bytes);
+    }
+    if (e != hipSuccess) *p = nullptr;
+    return e;
+}
+
+// Returns a table to the pool (or frees it).  The caller has synchronised
+// every stream that used it.
+void table_free(int device, void *p, size_t bytes) {
+    if (!p) return;
+    if (bytes >= POOL_MIN) {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        while (g_pool_bytes + bytes > POOL_CAP && !g_pool.empty()) {  // oldest first
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(g_pool.front().device);
+            (void)hipFree(g_pool.front().p);
+            (void)hipSetDevice(cur);
+            g_pool_bytes -= g_pool.front().bytes;
+            g_pool.erase(g_pool.begin());
+        }
+        if (g_pool_bytes + bytes <= POOL_CAP) {
+            g_pool.push_back(PoolEnt{device, bytes, p});
+            g_pool_bytes += bytes;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+}  // namespace
+
 struct DBuf {
     void *p = nullptr;
     ~DBuf() {
@@ -141,6 +230,7 @@ struct cx_ring {
     ArcBound *d_arc_bounds = nullptr;  // last peer ID of each non-empty arc
     int arc_world = 0, arc_rank = -1, arc_Lh = 128, arc_nb = 0;
     uint32_t arc_plo = 0, arc_M = 0;
+    size_t arc_bytes = 0;          // d_arc_tree allocation
 
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
     uint32_t *d_ring_key = nullptr; // ID slices [n] of the streaming finger build
@@ -267,11 +357,12 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_eyt);
     (void)hipFree(r->d_dir);
     (void)hipFree(r->d_ring_key);
-    (void)hipFree(r->d_fingers);
-    (void)hipFree(r->d_rt);
-    (void)hipFree(r->d_pk);
-    (void)hipFree(r->d_tree);
-    (void)hipFree(r->d_cz);
+    const size_t ent = r->n * (size_t)r->rt_R;
+    table_free(r->device, r->d_fingers, r->n * CX_FINGERS * sizeof(uint32_t));
+    table_free(r->device, r->d_rt, ent * sizeof(RtEntry));
+    table_free(r->device, r->d_pk, ent * 16);
+    table_free(r->device, r->d_tree, ent * 64);
+    table_free(r->device, r->d_cz, ent * 128);
     (void)hipFree(r->d_stree);
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
@@ -279,7 +370,7 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_alive);
     (void)hipFree(r->d_succs);
     (void)hipFree(r->d_scratch);
-    (void)hipFree(r->d_arc_tree);
+    table_free(r->device, r->d_arc_tree, r->arc_bytes);
     (void)hipFree(r->d_arc_bounds);
     (void)hipFree(r->d_stats);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
@@ -367,7 +458,7 @@ int ensure_route_table(cx_ring *r, hipStream_t s) {
     if (!r->fingers_converged || !r->d_ring_ext) return CX_OK;
     const size_t ent = r->n * (size_t)r->rt_R;
     if (r->variant() == 5 && !r->cz_valid) {
-        if (!r->d_cz && hipMalloc(&r->d_cz, ent * 128) != hipSuccess) {
+        if (!r->d_cz && table_alloc((void **)&r->d_cz, ent * 128) != hipSuccess) {
             r->d_cz = nullptr;
             if (r->route_variant < 0) r->cz_failed = true;  // automatic: use variant 4
         }
@@ -387,19 +478,21 @@ int ensure_route_table(cx_ring *r, hipStream_t s) {
         }
     }
     if (r->variant() == 1 && !r->rt_valid) {
-        if (!r->d_rt && hipMalloc(&r->d_rt, ent * sizeof(RtEntry)) != hipSuccess) r->d_rt = nullptr;
+        if (!r->d_rt && table_alloc((void **)&r->d_rt, ent * sizeof(RtEntry)) != hipSuccess)
+            r->d_rt = nullptr;
         if (r->d_rt) {
             CX_HIP(cxk::rt_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->d_rt, r->d_ring_ext, s));
             r->rt_valid = true;
         }
     } else if ((r->variant() == 2 || r->variant() == 3) && !r->pk_valid) {
-        if (!r->d_pk && hipMalloc(&r->d_pk, ent * 16) != hipSuccess) r->d_pk = nullptr;
+        if (!r->d_pk && table_alloc((void **)&r->d_pk, ent * 16) != hipSuccess) r->d_pk = nullptr;
         if (r->d_pk) {
             CX_HIP(cxk::pk_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_pk, s));
             r->pk_valid = true;
         }
     } else if (r->variant() == 4 && !r->tree_valid) {
-        if (!r->d_tree && hipMalloc(&r->d_tree, ent * 64) != hipSuccess) r->d_tree = nullptr;
+        if (!r->d_tree && table_alloc((void **)&r->d_tree, ent * 64) != hipSuccess)
+            r->d_tree = nullptr;
         if (r->d_tree) {
             CX_HIP(cxk::tree_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_tree, s));
             r->tree_valid = true;
@@ -675,7 +768,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     hipStream_t s = ring->stream;
     const size_t cnt = ring->n * CX_FINGERS;
     if (!ring->d_fingers) {
-        hipError_t e = hipMalloc(&ring->d_fingers, cnt * sizeof(uint32_t));
+        hipError_t e = table_alloc((void **)&ring->d_fingers, cnt * sizeof(uint32_t));
         if (e != hipSuccess) {
             ring->d_fingers = nullptr;
             return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
@@ -720,7 +813,7 @@ int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
     CX_HIP(hipMemcpyAsync(&bad, ring->d_scratch, sizeof(bad), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
     CX_CHECK(!bad, CX_E_INVALID, "finger entry is neither a ring index nor CX_NONE");
-    (void)hipFree(ring->d_fingers);
+    table_free(ring->device, ring->d_fingers, cnt * sizeof(uint32_t));
     ring->d_fingers = staged.as<uint32_t>();
     staged.release();
     ring->fingers_converged = false;
@@ -1352,7 +1445,7 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     const bool own_fingers = !ring->d_fingers || !ring->fingers_converged;
     if (own_fingers) {
         if (!ring->d_fingers &&
-            hipMalloc(&ring->d_fingers, n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
+            table_alloc((void **)&ring->d_fingers, n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
             ring->d_fingers = nullptr;
             return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
         }
@@ -1395,15 +1488,18 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
             M = (uint32_t)(halo + (hi - lo));
         }
     }
-    (void)hipFree(ring->d_arc_tree);
+    (void)hipStreamSynchronize(s);
+    table_free(ring->device, ring->d_arc_tree, ring->arc_bytes);
     ring->d_arc_tree = nullptr;
+    ring->arc_bytes = 0;
     ring->arc_world = 0;
     const size_t top_ent = (size_t)((int)CX_FINGERS - Lh) * 2 * n;
     const size_t low_ent = (size_t)(Lh - l0) * 2 * M;
-    if (hipMalloc(&ring->d_arc_tree, (top_ent + low_ent) * 64 + 64) != hipSuccess) {
+    if (table_alloc((void **)&ring->d_arc_tree, (top_ent + low_ent) * 64 + 64) != hipSuccess) {
         ring->d_arc_tree = nullptr;
         return fail(CX_E_NOMEM, "hipMalloc of the arc route planes failed");
     }
+    ring->arc_bytes = (top_ent + low_ent) * 64 + 64;
     CX_HIP(hipMemsetAsync(ring->d_scratch, 0, 2 * sizeof(uint32_t), s));
     {
         DBuf ft, hi, c2;
@@ -1434,7 +1530,7 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
                      hipMemcpyHostToDevice));
     CX_HIP(hipStreamSynchronize(s));
     if (own_fingers) {
-        (void)hipFree(ring->d_fingers);
+        table_free(ring->device, ring->d_fingers, ring->n * CX_FINGERS * sizeof(uint32_t));
         ring->d_fingers = nullptr;
         ring->fingers_converged = false;
     }
@@ -1657,6 +1753,13 @@ int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
     ring->table_build = variant;
+    return CX_OK;
+}
+
+// Releases every pooled table (all devices).
+int cxi_pool_trim(void) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    pool_trim_locked(-1);
     return CX_OK;
 }
 
