@@ -13,6 +13,8 @@
 //     (finger_table.h:102-141)
 //   AbstractChordPeer::GetSuccessor(key)             Ring::GetSuccessor(src, key) -> {owner, hops}
 //     (abstract_chord_peer.cpp:318-330)
+//   AbstractChordPeer::GetPredecessor(key)           Ring::GetPredecessor(key)
+//     (abstract_chord_peer.cpp:380-421)
 //   AbstractChordPeer::GetNSuccessors(key, n)        Ring::GetNSuccessors(key, n)
 //     (abstract_chord_peer.cpp:345-373)
 //   DHashPeer::Create's replica check                Ring::CheckReplicas(n, m)
@@ -152,6 +154,16 @@ public:
         return out;
     }
     uint32_t Owner(const Key &key) const { return Successors({key})[0]; }
+
+    // GetPredecessor on the converged ring (abstract_chord_peer.cpp:380-421):
+    // the predecessor of each key's owner (a lone peer answers itself).
+    std::vector<uint32_t> GetPredecessors(const std::vector<Key> &keys) const {
+        std::vector<cx_u128> k = pack(keys);
+        std::vector<uint32_t> out(keys.size());
+        check(cx_predecessor(h_, k.data(), k.size(), out.data(), CX_MEM_HOST));
+        return out;
+    }
+    uint32_t GetPredecessor(const Key &key) const { return GetPredecessors({key})[0]; }
 
     void PopulateFingerTable() { check(cx_fingers_build(h_, nullptr, CX_MEM_HOST)); }
 

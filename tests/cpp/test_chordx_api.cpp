@@ -83,6 +83,20 @@ TEST(ChordGetSucc, FromFingerTable) {
     EXPECT_EQ(l.hops, 1);
 }
 
+// ChordGetPred.InSuccList / FromFingerTable (chord_test.cpp:131-227,
+// GetPredTest.json): the converged answer, batched.
+TEST(ChordGetPred, Fixtures) {
+    Ring a({Key::FromHex("8fcd40610a285f29ad7168be553d20db"),
+            Key::FromHex("f7ad227bcc0f55b3b15927475dd5a053"),
+            Key::FromHex("67cd3c64a95a51229cf89ec7a252772a")});
+    EXPECT_EQ(a.Ids()[a.GetPredecessor(Key::FromHex("67cd3c64a95a51229cf89ec7a2527729"))].Str(),
+              std::string("f7ad227bcc0f55b3b15927475dd5a053"));
+    Ring b({Key::FromHex("459a8765538b59a2b2a046143026ed56"),
+            Key::FromHex("3b74d34668f5258974b09b496fa4bb0")});
+    EXPECT_EQ(b.Ids()[b.GetPredecessor(Key::FromHex("459a8765538b59a2b2a046143026ed57"))].Str(),
+              std::string("459a8765538b59a2b2a046143026ed56"));
+}
+
 TEST(ChordGetSucc, FromPredecessor) {
     Ring ring({Key::FromHex("61b23792c54457c5ac5b7a95b35722db"), Key::FromHex("f56febc96cfa5a6f8469b933a76dd0e0")});
     std::vector<uint32_t> F = ring.FingerTable();
