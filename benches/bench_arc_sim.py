@@ -33,7 +33,7 @@ from chordx.arc import MAX_ROUNDS  # noqa: E402
 XGMI_LINK = 153e9  # B/s per link per direction (MI355X_MICROARCH.md)
 
 
-def run(G, N, Q, ids, reps, top):
+def run(G, N, Q, ids, reps, top, key_first):
     rings = [chordx.Ring(ids) for _ in range(G)]
     for g, r in enumerate(rings):
         r.arc_build(G, g, top)
@@ -51,7 +51,9 @@ def run(G, N, Q, ids, reps, top):
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     best = None
     for _ in range(reps):
-        recs = [None] * G  # first step straight from the lookups (cx_arc_start)
+        # origin mode: first step straight from the lookups (cx_arc_start);
+        # key_first: seed records, sent ahead by key in round 1 (no origin walk)
+        recs = [None] * G
         per_round = []
         t0 = time.perf_counter()
         for rnd in range(MAX_ROUNDS):
@@ -61,11 +63,18 @@ def run(G, N, Q, ids, reps, top):
             for g in range(G):
                 a, b, c = ev(), ev(), ev()
                 a.record()
-                out = (rings[g].arc_start(g, srcs[g], keys[g], *outs[g]) if recs[g] is None
-                       else rings[g].arc_step(g, recs[g], *outs[g]))
-                b.record()
-                send, counts = rings[g].arc_bucket(G, out)
-                c.record()
+                if key_first and rnd == 0:  # fused seed + bucket (cx_arc_send_ahead)
+                    b.record()
+                    send, counts = rings[g].arc_send_ahead(G, g, srcs[g], keys[g])
+                    c.record()
+                else:
+                    if recs[g] is None:
+                        out = rings[g].arc_start(g, srcs[g], keys[g], *outs[g])
+                    else:
+                        out = rings[g].arc_step(g, recs[g], *outs[g])
+                    b.record()
+                    send, counts = rings[g].arc_bucket(G, out)
+                    c.record()
                 torch.cuda.synchronize()
                 rows.append({"in": int(keys[g].shape[0] if recs[g] is None else recs[g].shape[0]),
                              "step_ms": a.elapsed_time(b),
@@ -83,7 +92,7 @@ def run(G, N, Q, ids, reps, top):
         comp = sum(max(r["step_ms"] + r["bucket_ms"] for r in rows) for rows in per_round)
         xg = sum(max(r["out_remote"] for r in rows) * 32 / (7 * XGMI_LINK) * 1e3
                  for rows in per_round)
-        res = {"G": G, "keys_total": Q, "keys_per_rank": q, "rounds": len(per_round),
+        res = {"G": G, "mode": "key_first" if key_first else "origin_walk", "keys_total": Q, "keys_per_rank": q, "rounds": len(per_round),
                "top_levels": info[0][0], "local_rows_max": max(i[1] for i in info),
                "route_plane_bytes_per_gpu_max": max(i[2] for i in info),
                "per_gpu_compute_ms": comp, "per_gpu_xgmi_ms_model": xg,
@@ -108,6 +117,7 @@ def main():
     ap.add_argument("--groups", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--top-levels", type=int, default=0, help="0: library default")
+    ap.add_argument("--modes", default="key_first,origin_walk")
     a = ap.parse_args()
     N, Q = 1 << a.peers_log2, 1 << a.keys_log2
     ids = torch.empty((N, 2), dtype=torch.int64, device="cuda")
@@ -130,8 +140,9 @@ def main():
     del ref
     torch.cuda.empty_cache()
     for G in [int(x) for x in a.groups.split(",")]:
-        out["arc"].append(run(G, N, Q, ids, a.reps, a.top_levels))
-        print(json.dumps(out["arc"][-1]), file=sys.stderr, flush=True)
+        for mode in a.modes.split(","):
+            out["arc"].append(run(G, N, Q, ids, a.reps, a.top_levels, mode == "key_first"))
+            print(json.dumps(out["arc"][-1]), file=sys.stderr, flush=True)
     print(json.dumps(out))
 
 

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Lean headline-kernel timer for A/B work: C4 per GPU (2^24-peer ring, 2^25
+keys, src = q mod N), default route kernel, HIP events over `reps` launches
+after warm-up, repeated `rounds` times (min and median reported); checks owner
+== successor.  Prints one JSON line.
+    python benches/bench_route.py [reps] [rounds]
+"""
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
+
+import torch  # noqa: E402
+
+import chordx  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    N, Q = 1 << 24, 1 << 25
+    ids = torch.empty((N, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(ids, 0x5EED0005)
+    ring = chordx.Ring(ids)
+    del ids
+    ring.build_fingers()
+    keys = torch.empty((Q, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(keys, 0x5EED0006)
+    src = (torch.arange(Q, device="cuda", dtype=torch.int64) % N).to(torch.int32)
+    owner = torch.empty(Q, dtype=torch.int32, device="cuda")
+    hops = torch.empty(Q, dtype=torch.uint8, device="cuda")
+    status = torch.empty(Q, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        ring.route(src, keys, out=(owner, hops, status))
+    ms = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(reps):
+            ring.route(src, keys, out=(owner, hops, status))
+        b.record(s)
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b) / reps)
+    ok = bool((owner == ring.successor(keys)).all()) and int((status != 0).sum()) == 0
+    print(json.dumps({"lib": os.path.basename(os.environ.get("CHORDX_LIB", "default")),
+                      "ms_min": min(ms), "ms_median": statistics.median(ms),
+                      "lookups_per_s": Q / (min(ms) * 1e-3), "probe": ring.gather_probe(),
+                      "owner_ok": ok, "mean_hops": float(hops.double().mean())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -329,10 +329,16 @@ int cx_arc_step(const cx_ring *ring, int rank, const cx_arc_rec *in, size_t q, c
 int cx_arc_start(const cx_ring *ring, int rank, const uint32_t *src, const cx_u128 *keys,
                  size_t q, cx_arc_rec *out, uint32_t *owner, uint8_t *hops, uint8_t *status);
 
-/* Groups WALK/RESULT records by destination rank into `send` (NONE dropped);
- * counts[world] (host) receives the per-destination record counts. */
+/* Groups WALK/RESULT records (and NEW ones, by key) by destination rank into
+ * `send` (NONE dropped); counts[world] (host) receives the per-destination
+ * record counts. */
 int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t q,
                   cx_arc_rec *send, uint64_t *counts);
+/* Lookups sent ahead by key (no origin walk): cx_arc_seed + cx_arc_bucket in
+ * one pass, the NEW records built on the fly; the rank of the key's arc walks
+ * them from their sources (cx_arc_step). */
+int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *src,
+                      const cx_u128 *keys, size_t q, cx_arc_rec *send, uint64_t *counts);
 
 #ifdef __cplusplus
 }

@@ -56,6 +56,7 @@ class ArcRouter:
         engine.arc_build(world, rank)
         self.rounds = 0
         self.records_sent = 0
+        self.key_first = True
         self._mat_host = None  # pinned landing buffer of the count matrix
 
     def _exchange(self, send, counts):
@@ -87,18 +88,34 @@ class ArcRouter:
                                 input_split_sizes=list(counts), group=self.group)
         return (recv.to(send.device) if recv.device != send.device else recv), inflight
 
-    def route(self, src, keys, owner, hops, status=None) -> int:
+    def route(self, src, keys, owner, hops, status=None, key_first=None) -> int:
         """Routes this rank's lookups (issued at peers src[i]); collective over
         the group.  Writes owner/hops/status at the lookups' indices and
-        returns the number of rounds taken."""
+        returns the number of rounds taken.
+
+        key_first (default self.key_first): the origin does not walk; every
+        NEW lookup goes straight to the rank whose arc holds its key's owner,
+        which walks it from its source over the replicated top planes and its
+        own lower planes (a walk that needs a lower level is within 2^Lh of its
+        key, i.e. in that arc or its halo).  Otherwise the origin walks the top
+        levels first (cx_arc_start) and forwards a WALK record."""
+        kf = self.key_first if key_first is None else key_first
         start = getattr(self.engine, "arc_start", None)
-        recs = None if start else self.engine.arc_seed(self.rank, src, keys)
+        ahead = getattr(self.engine, "arc_send_ahead", None)
+        recs = None if (start and not kf) or (kf and ahead) else \
+            self.engine.arc_seed(self.rank, src, keys)
         for rnd in range(1, MAX_ROUNDS + 1):
-            if recs is None:  # first step straight from the lookups
-                out = start(self.rank, src, keys, owner, hops, status)
+            if kf and rnd == 1:  # send the lookups ahead by key
+                if ahead:
+                    send, counts = ahead(self.world, self.rank, src, keys)
+                else:
+                    send, counts = self.engine.arc_bucket(self.world, recs)
             else:
-                out = self.engine.arc_step(self.rank, recs, owner, hops, status)
-            send, counts = self.engine.arc_bucket(self.world, out)
+                if recs is None:  # first step straight from the lookups
+                    out = start(self.rank, src, keys, owner, hops, status)
+                else:
+                    out = self.engine.arc_step(self.rank, recs, owner, hops, status)
+                send, counts = self.engine.arc_bucket(self.world, out)
             self.records_sent += int(sum(counts))
             recs, inflight = self._exchange(send, counts)
             if inflight == 0:

@@ -436,6 +436,21 @@ class Ring:
                                     _ptr(hops), _ptr(status)))
         return out
 
+    def arc_send_ahead(self, world: int, rank: int, src, keys):
+        """(send, counts): this rank's new lookups as NEW records grouped by the
+        rank of their key's arc (cx_arc_send_ahead; no origin walk)."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        send = torch.empty((q, 4), dtype=torch.int64, device=keys.device)
+        counts = np.zeros(world, dtype=np.uint64)
+        self._arc_stream()
+        L.check(L.lib().cx_arc_send_ahead(self._h, world, rank, _ptr(src), _ptr(keys), q,
+                                          _ptr(send), _ptr(counts)))
+        return send[: int(counts.sum())], [int(c) for c in counts]
+
     def arc_bucket(self, world: int, recs):
         """(send, counts): records grouped by destination rank, NONE dropped."""
         q = recs.shape[0]

@@ -1617,25 +1617,43 @@ int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t
     hipStream_t s = ring->stream;
     uint32_t *dcnt = ring->d_scratch, *dcur = ring->d_scratch + CX_ARC_MAX_RANKS;
     CX_HIP(hipMemsetAsync(dcnt, 0, CX_ARC_MAX_RANKS * sizeof(uint32_t), s));
+    // count -> device-side cursors -> scatter, one host synchronisation (the
+    // counts the caller needs for the exchange)
     CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->d_arc_bounds,
-                           ring->arc_nb, world, dcnt, nullptr, nullptr, s, false));
-    uint32_t hc[CX_ARC_MAX_RANKS], hcur[CX_ARC_MAX_RANKS];
+                           ring->arc_nb, world, dcnt, dcur, nullptr, s, false));
+    CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->d_arc_bounds,
+                           ring->arc_nb, world, nullptr, dcur, reinterpret_cast<ArcRec *>(send), s,
+                           true));
+    uint32_t hc[CX_ARC_MAX_RANKS];
     CX_HIP(hipMemcpyAsync(hc, dcnt, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
-    uint32_t acc = 0;
-    for (int g = 0; g < world; ++g) {
-        hcur[g] = acc;
-        acc += hc[g];
-        counts[g] = hc[g];
-    }
-    if (acc) {
-        CX_HIP(hipMemcpyAsync(dcur, hcur, world * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        CX_HIP(cxk::arc_bucket(reinterpret_cast<const ArcRec *>(recs), q, ring->d_arc_bounds,
-                               ring->arc_nb, world, nullptr, dcur,
-                               reinterpret_cast<ArcRec *>(send), s, true));
-        // hcur is a stack buffer: the copy must complete before we return
-        CX_HIP(hipStreamSynchronize(s));
-    }
+    for (int g = 0; g < world; ++g) counts[g] = hc[g];
+    return CX_OK;
+}
+
+int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *src,
+                      const cx_u128 *keys, size_t q, cx_arc_rec *send, uint64_t *counts) {
+    CX_CHECK(ring && counts, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(rank >= 0 && rank < world, CX_E_INVALID, "rank out of range");
+    CX_CHECK(q == 0 || (src && keys && send), CX_E_INVALID, "null buffer");
+    CX_CHECK(q < (1ull << ARC_ORIGIN_SHIFT), CX_E_INVALID, "too many lookups for one rank");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    uint32_t *dcnt = ring->d_scratch, *dcur = ring->d_scratch + CX_ARC_MAX_RANKS;
+    const cell128 *k = reinterpret_cast<const cell128 *>(keys);
+    CX_HIP(hipMemsetAsync(dcnt, 0, CX_ARC_MAX_RANKS * sizeof(uint32_t), s));
+    CX_HIP(cxk::arc_bucket_seed(src, k, rank, q, ring->d_arc_bounds, ring->arc_nb, world, dcnt,
+                                dcur, nullptr, s, false));
+    CX_HIP(cxk::arc_bucket_seed(src, k, rank, q, ring->d_arc_bounds, ring->arc_nb, world,
+                                nullptr, dcur, reinterpret_cast<ArcRec *>(send), s, true));
+    uint32_t hc[CX_ARC_MAX_RANKS];
+    CX_HIP(hipMemcpyAsync(hc, dcnt, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    for (int g = 0; g < world; ++g) counts[g] = hc[g];
     return CX_OK;
 }
 

@@ -2953,7 +2953,9 @@ __device__ __forceinline__ int arc_dest(const ArcRec &r, const ArcBound *bounds,
         const uint64_t o = r.qid >> ARC_ORIGIN_SHIFT;
         return o < (uint64_t)G ? (int)o : -1;
     }
-    if (kind != ARC_WALK || nb == 0) return -1;
+    // WALK records, and NEW lookups sent ahead by key (ArcRouter key_first):
+    // the rank whose arc holds the key's owner
+    if ((kind != ARC_WALK && kind != ARC_NEW) || nb == 0) return -1;
     const u128 k = ((u128)r.w1 << 64) | r.w0;
     int lo = 0, hi = nb;  // first bound >= key; past the last one the owner wraps to arc 0
     while (lo < hi) {
@@ -2967,6 +2969,27 @@ __device__ __forceinline__ int arc_dest(const ArcRec &r, const ArcBound *bounds,
 // Bucket outcome records by destination: per-block LDS histograms, one global
 // atomic per (block, destination) to reserve ranges, LDS-local offsets.
 constexpr int ARC_MAX_RANKS = 64;
+
+// Records to bucket: stored ones, or (SEED) NEW lookups synthesised from the
+// caller's src / keys as k_arc_seed writes them (no seed array in HBM).
+template <bool SEED>
+struct ArcIn {
+    const ArcRec *recs;
+    const uint32_t *src;
+    const cell128 *keys;
+    int self;
+    __device__ __forceinline__ ArcRec get(size_t i) const {
+        if (!SEED) return recs[i];
+        const u128 k = ld128(keys + i);
+        ArcRec r;
+        r.w0 = (uint64_t)k;
+        r.w1 = (uint64_t)(k >> 64);
+        r.qid = ((uint64_t)self << ARC_ORIGIN_SHIFT) | i;
+        r.cur = src[i];
+        r.hk = ARC_NEW << 8;
+        return r;
+    }
+};
 
 // Per-destination counts of one wave's records: one ballot per destination,
 // one LDS atomic per (wave, destination) present; returns the record's slot
@@ -2988,7 +3011,8 @@ __device__ __forceinline__ uint32_t arc_wave_slots(int d, int G, uint32_t *h) {
     return slot;
 }
 
-__global__ __launch_bounds__(256) void k_arc_count(const ArcRec *recs, size_t q,
+template <bool SEED>
+__global__ __launch_bounds__(256) void k_arc_count(ArcIn<SEED> in, size_t q,
                                                    const ArcBound *bounds, int nb, int G,
                                                    uint32_t *counts) {
     __shared__ uint32_t h[ARC_MAX_RANKS];
@@ -2999,7 +3023,7 @@ __global__ __launch_bounds__(256) void k_arc_count(const ArcRec *recs, size_t q,
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i0 = blockIdx.x * (size_t)blockDim.x; i0 < q; i0 += stride) {  // uniform trips
         const size_t i = i0 + threadIdx.x;
-        const int d = i < q ? arc_dest(recs[i], sb, nb, G) : -1;
+        const int d = i < q ? arc_dest(in.get(i), sb, nb, G) : -1;
         (void)arc_wave_slots(d, G, h);
     }
     __syncthreads();
@@ -3007,43 +3031,86 @@ __global__ __launch_bounds__(256) void k_arc_count(const ArcRec *recs, size_t q,
         if (h[j]) atomicAdd(&counts[j], h[j]);
 }
 
-__global__ __launch_bounds__(256) void k_arc_scatter(const ArcRec *recs, size_t q,
+// Four records per thread per pass (1024 per block): the block's slot
+// reservation (LDS histogram, one global atomic per destination, three
+// barriers) is paid once per 1024 records instead of once per 256.
+constexpr int ARC_SCAT_R = 4;
+
+template <bool SEED>
+__global__ __launch_bounds__(256) void k_arc_scatter(ArcIn<SEED> in, size_t q,
                                                      const ArcBound *bounds, int nb, int G,
                                                      uint32_t *cursor, ArcRec *send) {
     __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
-    for (size_t b0 = (size_t)blockIdx.x * blockDim.x; b0 < q; b0 += (size_t)gridDim.x * blockDim.x) {
+    const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
+    for (size_t b0 = (size_t)blockIdx.x * per; b0 < q; b0 += (size_t)gridDim.x * per) {
         for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
         __syncthreads();
-        const size_t i = b0 + threadIdx.x;
-        int d = -1;
-        ArcRec r;
-        if (i < q) {
-            r = recs[i];
-            d = arc_dest(r, sb, nb, G);
+        ArcRec r[ARC_SCAT_R];
+        int d[ARC_SCAT_R];
+        uint32_t slot[ARC_SCAT_R];
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) {
+            const size_t i = b0 + (size_t)k * blockDim.x + threadIdx.x;
+            d[k] = -1;
+            if (i < q) {
+                r[k] = in.get(i);
+                d[k] = arc_dest(r[k], sb, nb, G);
+            }
         }
-        const uint32_t slot = arc_wave_slots(d, G, h);
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
         __syncthreads();
         for (int j = threadIdx.x; j < G; j += blockDim.x)
             basep[j] = h[j] ? atomicAdd(&cursor[j], h[j]) : 0u;
         __syncthreads();
-        if (d >= 0) send[basep[d] + slot] = r;
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k)
+            if (d[k] >= 0) send[basep[d[k]] + slot[k]] = r[k];
         __syncthreads();
     }
+}
+
+// cursor[g] = exclusive prefix sum of counts (one wave).
+__global__ void k_arc_offsets(const uint32_t *counts, int G, uint32_t *cursor) {
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int g = 0; g < G; ++g) {
+            cursor[g] = acc;
+            acc += counts[g];
+        }
+    }
+}
+
+template <bool SEED>
+static hipError_t arc_bucket_in(const ArcIn<SEED> &in, size_t q, const ArcBound *bounds, int nb,
+                                int G, uint32_t *counts_dev, uint32_t *cursor_dev, ArcRec *send,
+                                hipStream_t s, bool scatter) {
+    if (!scatter) {  // counts, and the scatter cursors from them (device side)
+        if (q) k_arc_count<SEED><<<cx_grid(q, 256, 2048), 256, 0, s>>>(in, q, bounds, nb, G,
+                                                                       counts_dev);
+        if (cursor_dev) k_arc_offsets<<<1, 64, 0, s>>>(counts_dev, G, cursor_dev);
+        return hipGetLastError();
+    }
+    if (q)
+        k_arc_scatter<SEED><<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0,
+                              s>>>(in, q, bounds, nb, G, cursor_dev, send);
+    return hipGetLastError();
 }
 
 hipError_t arc_bucket(const ArcRec *recs, size_t q, const ArcBound *bounds, int nb, int G,
                       uint32_t *counts_dev, uint32_t *cursor_dev, ArcRec *send, hipStream_t s,
                       bool scatter) {
-    if (!scatter) {
-        if (q) k_arc_count<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, bounds, nb, G,
-                                                                 counts_dev);
-        return hipGetLastError();
-    }
-    if (q) k_arc_scatter<<<cx_grid(q, 256, 2048), 256, 0, s>>>(recs, q, bounds, nb, G,
-                                                               cursor_dev, send);
-    return hipGetLastError();
+    return arc_bucket_in(ArcIn<false>{recs, nullptr, nullptr, 0}, q, bounds, nb, G, counts_dev,
+                         cursor_dev, send, s, scatter);
+}
+
+hipError_t arc_bucket_seed(const uint32_t *src, const cell128 *keys, int self, size_t q,
+                           const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
+                           uint32_t *cursor_dev, ArcRec *send, hipStream_t s, bool scatter) {
+    return arc_bucket_in(ArcIn<true>{nullptr, src, keys, self}, q, bounds, nb, G, counts_dev,
+                         cursor_dev, send, s, scatter);
 }
 
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,

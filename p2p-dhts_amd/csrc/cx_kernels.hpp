@@ -171,6 +171,11 @@ hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self
 hipError_t arc_bucket(const ArcRec *recs, size_t q, const ArcBound *bounds, int nb, int G,
                       uint32_t *counts_dev, uint32_t *cursor_dev, ArcRec *send, hipStream_t s,
                       bool scatter);
+// arc_bucket of the NEW records arc_seed would write for (src, keys), without
+// writing them (lookups sent ahead by key).
+hipError_t arc_bucket_seed(const uint32_t *src, const cell128 *keys, int self, size_t q,
+                           const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
+                           uint32_t *cursor_dev, ArcRec *send, hipStream_t s, bool scatter);
 hipError_t nsucc(const SearchView &ev, const cell128 *keys, size_t q, int n, uint32_t *lists,
                  uint8_t *count, hipStream_t s);
 hipError_t mark_leaves(const SearchView &ev, const cell128 *ring, const cell128 *leaves, size_t nl,

@@ -17,7 +17,7 @@ def cx():
     return chordx
 
 
-def simulate(cx, ids_dev, G, srcs, keys, status=True, top=0, fused=True):
+def simulate(cx, ids_dev, G, srcs, keys, status=True, top=0, fused=True, key_first=False):
     """Round loop of ArcRouter.route with G in-process 'ranks'."""
     import torch
     from chordx.arc import MAX_ROUNDS
@@ -32,16 +32,21 @@ def simulate(cx, ids_dev, G, srcs, keys, status=True, top=0, fused=True):
                      torch.full((q,), 77, dtype=torch.uint8, device="cuda"),
                      torch.full((q,), 9, dtype=torch.uint8, device="cuda") if status else None))
     # fused first step (cx_arc_start) or seed records + step, as ArcRouter may
-    recs = ([None] * G if fused else
+    # (key_first: the seed records are sent ahead by key, no origin walk)
+    recs = ([None] * G if fused and not key_first else
             [rings[g].arc_seed(g, srcs[g], keys[g]) for g in range(G)])
     rounds, sent = 0, 0
     for rounds in range(1, MAX_ROUNDS + 1):
         inbox = [[] for _ in range(G)]
         total = 0
         for g in range(G):
-            out = (rings[g].arc_start(g, srcs[g], keys[g], *outs[g]) if recs[g] is None
-                   else rings[g].arc_step(g, recs[g], *outs[g]))
-            send, counts = rings[g].arc_bucket(G, out)
+            if key_first and rounds == 1:  # odd G: fused send-ahead, even: seed + bucket
+                send, counts = (rings[g].arc_send_ahead(G, g, srcs[g], keys[g]) if G % 2
+                                else rings[g].arc_bucket(G, recs[g]))
+            else:
+                out = (rings[g].arc_start(g, srcs[g], keys[g], *outs[g]) if recs[g] is None
+                       else rings[g].arc_step(g, recs[g], *outs[g]))
+                send, counts = rings[g].arc_bucket(G, out)
             total += sum(counts)
             for d, part in enumerate(torch.split(send, counts)):
                 inbox[d].append(part)
@@ -69,21 +74,23 @@ def _setup(cx, O, torch, n, q, G, seed):
     return ids_dev, ring, srcs, keys
 
 
+@pytest.mark.parametrize("key_first", [False, True])
 @pytest.mark.parametrize("n,G", [(5000, 1), (5000, 2), (5000, 3), (5000, 8), (1 << 16, 8),
                                  (70001, 5), (2, 2), (1, 1), (3, 4)])
-def test_arc_route_equals_replicated(cx, O, n, G):
+def test_arc_route_equals_replicated(cx, O, n, G, key_first):
     import torch
     q = 4096
     ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C0 + n + G)
-    outs, rounds, sent = simulate(cx, ids_dev, G, srcs, keys, fused=(n + G) % 2 == 0)
+    outs, rounds, sent = simulate(cx, ids_dev, G, srcs, keys, fused=(n + G) % 2 == 0,
+                                  key_first=key_first)
     for g in range(G):
         ow, hp, st = ring.route(srcs[g], keys[g])
         assert torch.equal(outs[g][0], ow), (n, G, g)
         assert torch.equal(outs[g][1], hp), (n, G, g)
         assert torch.equal(outs[g][2], st), (n, G, g)
-    if G == 1:
-        assert rounds == 1 and sent == 0
-    assert rounds <= 3  # origin step, arc step, result delivery
+    if G == 1:  # key_first: the lookups are "sent" to this rank, then walked
+        assert (rounds, sent) == ((2, q) if key_first else (1, 0))
+    assert rounds <= 3  # origin step (or send-ahead), arc step, result delivery
 
 
 def test_arc_route_matches_oracle(cx, O):
@@ -186,14 +193,15 @@ def test_arc_bucket_groups_by_destination(cx, O):
         off += counts[d]
 
 
+@pytest.mark.parametrize("key_first", [False, True])
 @pytest.mark.parametrize("top", [1, 3, 6, 12])
-def test_arc_top_levels(cx, O, top):
+def test_arc_top_levels(cx, O, top, key_first):
     """Fewer replicated levels mean larger halos (more local rows); every
     split of the table gives the replicated route's answers."""
     import torch
     n, q, G = 20000, 3000, 4
     ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2C3 + top)
-    outs, rounds, _ = simulate(cx, ids_dev, G, srcs, keys, top=top)
+    outs, rounds, _ = simulate(cx, ids_dev, G, srcs, keys, top=top, key_first=key_first)
     for g in range(G):
         ow, hp, st = ring.route(srcs[g], keys[g])
         assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)

@@ -131,6 +131,7 @@ class OracleArcEngine:
 
     def arc_bucket(self, world, recs):
         import torch
+        import oracle as O
         from chordx.arc import arc_of
         r = recs.numpy()
         dest = []
@@ -140,6 +141,9 @@ class OracleArcEngine:
                 dest.append(int(row[2]) >> 40)
             elif kind == 2:
                 dest.append(arc_of(int(row[3]) & 0xFFFFFFFF, self.n, world))
+            elif kind == 0:  # a lookup sent ahead by key: the arc of its owner
+                o = int(O.successor(self.P.ring, row[:2].view(np.uint64).reshape(1, 2))[0])
+                dest.append(arc_of(o, self.n, world))
             else:
                 dest.append(-1)
         dest = np.array(dest, dtype=np.int64)
@@ -149,7 +153,7 @@ class OracleArcEngine:
         return torch.from_numpy(r[order].copy()), counts
 
 
-def _arc_worker(rank, world, port, per_rank, out):
+def _arc_worker(rank, world, port, per_rank, out, key_first=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import sys
@@ -171,20 +175,22 @@ def _arc_worker(rank, world, port, per_rank, out):
     hops = torch.zeros(per_rank, dtype=torch.uint8)
     status = torch.full((per_rank,), 7, dtype=torch.uint8)
     router = ArcRouter(OracleArcEngine(P, len(ring)), len(ring), rank, world)
-    rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status)
+    rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status,
+                          key_first=key_first)
     out[rank] = (owner.numpy().view(np.uint32).tolist(), hops.tolist(), status.tolist(), rounds,
                  router.records_sent)
     tdist.destroy_process_group()
 
 
+@pytest.mark.parametrize("key_first", [True, False])
 @pytest.mark.parametrize("world", [2, 3])
-def test_arc_router_protocol_gloo(world):
+def test_arc_router_protocol_gloo(world, key_first):
     import oracle as O
     per_rank = 700
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out, key_first),
+                       nprocs=world, join=True, start_method="spawn")
     ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
     P = O.Peers(ring, O.fingers(ring))
     for r in range(world):

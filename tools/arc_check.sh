@@ -10,5 +10,5 @@ python3 -c "
 import json,sys
 d=json.load(open('$OUT/arc_sim.json'))
 print('replicated_ms', d['replicated_route_ms'])
-for a in d['arc']: print(a['G'], a['rounds'], round(a['per_gpu_compute_ms'],3), round(a['per_gpu_xgmi_ms_model'],3), '%.3g'%a['projected_lookups_per_s_per_gpu'], a['records_in_per_round'], a['route_plane_bytes_per_gpu_max']>>30, 'GiB')
+for a in d['arc']: print(a['G'], a.get('mode'), a['rounds'], round(a['per_gpu_compute_ms'],3), round(a['per_gpu_xgmi_ms_model'],3), '%.3g'%a['projected_lookups_per_s_per_gpu'], a['records_in_per_round'], a['route_plane_bytes_per_gpu_max']>>30, 'GiB')
 "
