@@ -787,7 +787,10 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
             }
             o = make_uint4(v[0], v[1], v[2], v[3]);
         }
-        reinterpret_cast<uint4 *>(F + (size_t)p * CX_FINGERS)[chunk] = o;
+        // streaming store: 8 GiB of rows nobody re-reads soon from L2
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u ov = {o.x, o.y, o.z, o.w};
+        __builtin_nontemporal_store(ov, reinterpret_cast<v4u *>(F + (size_t)p * CX_FINGERS) + chunk);
     }
 }
 
