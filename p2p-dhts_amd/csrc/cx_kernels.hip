@@ -3142,14 +3142,25 @@ template <class T>
 __device__ __forceinline__ void flush_rows(const T *stage, T *out, size_t base, int cnt, int w) {
     const int total = cnt * w;
     T *dst = out + base * (size_t)w;
-    for (int t = threadIdx.x; t < total; t += blockDim.x) dst[t] = stage[t];
+    int t0 = 0;
+    if (sizeof(T) == 4 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        // 16-B streaming stores for the bulk (rows are written once, read by
+        // the caller later): the block's range is contiguous and LDS-staged
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const int nv = total >> 2;
+        const v4u *sv = reinterpret_cast<const v4u *>(stage);
+        v4u *dv = reinterpret_cast<v4u *>(dst);
+        for (int t = threadIdx.x; t < nv; t += blockDim.x) __builtin_nontemporal_store(sv[t], dv + t);
+        t0 = nv << 2;
+    }
+    for (int t = t0 + threadIdx.x; t < total; t += blockDim.x) dst[t] = stage[t];
 }
 
 template <bool DIR>
 __global__ __launch_bounds__(ROW_BLOCK) void k_nsucc(SearchView sv, const cell128 *keys, size_t q,
                                                      int nlist, uint32_t *lists, uint8_t *count) {
     __shared__ u128 lds[Searcher<DIR>::LDS];
-    __shared__ uint32_t stage[ROW_BLOCK * CX_MAX_NSUCC];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[ROW_BLOCK * CX_MAX_NSUCC];
     Searcher<DIR>::stage(sv, lds);
     const uint32_t n = sv.ev.n;
     const int nn = (uint32_t)nlist < n ? nlist : (int)n;
@@ -3336,7 +3347,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                                                          uint16_t *mask, uint8_t *target) {
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
-    __shared__ uint32_t stage_l[ROW_BLOCK * CX_MAX_NSUCC];
+    __shared__ __attribute__((aligned(16))) uint32_t stage_l[ROW_BLOCK * CX_MAX_NSUCC];
     __shared__ uint8_t stage_t[ROW_BLOCK * CX_MAX_NSUCC];
     Searcher<DIR>::stage(sv_new, lds_new);
     if (CHURN) Searcher<DIR>::stage(sv_old, lds_old);
