@@ -139,7 +139,24 @@ def main():
     cpu_r = cpu_leg(lambda q, th: O.route(P, src_np[:q], kq_np[:q], threads=th), q,
                     "lookups/s", "routed lookups (or_route, literal ForwardRequest walk)",
                     lambda r, qq: (r[0] == own_np[:qq]).all() and (r[1] == hop_np[:qq]).all())
-    del P, F_gpu
+    # a9: the literal walk with dead peers (every 100th peer dead, converged
+    # 8-entry successor lists, DHash forwarding rule), same keys and sources
+    alive = np.ones(N3, dtype=np.uint8)
+    alive[::100] = 0
+    ring.upload_liveness(alive=alive, ns=8, rule=chordx.CX_FWD_DHASH)
+    tlit = ev_time(lambda: ring.route(src, keys, out=(owner, hops, status)))
+    st_lit = status.cpu().numpy()
+    own_l, hop_l = owner.cpu().numpy().view(np.uint32), hops.cpu().numpy()
+    PL = O.Peers(ring_np, F_gpu, alive=alive, ns=8, rule=O.FWD_DHASH)
+    cpu_lit = cpu_leg(lambda q, th: O.route(PL, src_np[:q], kq_np[:q], threads=th), q,
+                      "lookups/s", "routed lookups with 1 % dead peers (or_route, DHash rule)",
+                      lambda r, qq: (r[0] == own_l[:qq]).all() and (r[1] == hop_l[:qq]).all()
+                      and (r[2] == st_lit[:qq]).all())
+    a9 = {"route_s": tlit, "lookups_per_s": q / tlit, "dead_fraction": 0.01,
+          "status_counts": {str(k): int((st_lit == k).sum()) for k in np.unique(st_lit)},
+          "cpu": cpu_lit}
+    del P, PL, F_gpu
+    out["C3_a9_dead_peers"] = a9
     out["C3"] = {"fingers_build_s_wall": tf, "cpu_fingers": cpu_f, "cpu_route": cpu_r,
                  "fingers_algo_GBps": N3 * 528 / tf / 1e9,
                  "route_s": tr, "route_lookups_per_s": q / tr, "mean_hops": sh / q,

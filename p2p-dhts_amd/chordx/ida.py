@@ -32,6 +32,21 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _need(t, esize: int, name: str, numel: int, dev):
+    """Device-tensor argument check: element size, contiguity, size, device
+    (the kernels read and write these through raw pointers)."""
+    if not _is_dev(t):
+        raise TypeError(f"{name}: expected a device tensor like the others")
+    if t.element_size() != esize:
+        raise TypeError(f"{name}: expected {esize}-byte elements, got {t.dtype}")
+    if not t.is_contiguous():
+        raise TypeError(f"{name}: must be contiguous")
+    if t.numel() < numel:
+        raise TypeError(f"{name}: needs {numel} elements, has {t.numel()}")
+    if t.device != dev:
+        raise TypeError(f"{name}: on {t.device}, expected {dev}")
+
+
 def segments(lengths, m: int) -> np.ndarray:
     """seg_offsets (blocks + 1,) uint64: prefix sums of ceil(len / m)."""
     offs = np.zeros(len(lengths) + 1, dtype=np.uint64)
@@ -46,6 +61,9 @@ def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0, seg_offsets=N
     (numpy, or torch device tensors).  Returns (frags uint16, seg_offsets);
     pass seg_offsets (same memory kind) to skip computing them."""
     blocks = offsets.shape[0] - 1
+    if _is_dev(data):
+        _need(data, 1, "data", 0, data.device)
+        _need(offsets, 8, "offsets", blocks + 1, data.device)
     if seg_offsets is None:
         off_h = offsets.cpu().numpy() if _is_dev(offsets) else np.asarray(offsets, np.uint64)
         seg = np.zeros(blocks + 1, dtype=np.uint64)
@@ -54,8 +72,11 @@ def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0, seg_offsets=N
         seg_offsets = torch.from_numpy(seg.astype(np.int64)).to(offsets.device) \
             if _is_dev(offsets) else seg
     if _is_dev(data):
+        total = int(seg_offsets[-1])
+        _need(seg_offsets, 8, "seg_offsets", blocks + 1, data.device)
         frags = out if out is not None else torch.empty(
-            max(int(seg_offsets[-1]) * n, 1), dtype=torch.int16, device=data.device)
+            max(total * n, 1), dtype=torch.int16, device=data.device)
+        _need(frags, 2, "out", total * n, data.device)
         mk = L.CX_MEM_DEVICE
     else:
         data = np.ascontiguousarray(data, dtype=np.uint8)
@@ -73,11 +94,17 @@ def decode_flat(frags, seg_offsets, indices, m=10, p=257, device: int = 0, total
     device tensors, pass total (= seg_offsets[-1]) to avoid reading it back."""
     blocks = seg_offsets.shape[0] - 1
     if _is_dev(frags):
+        dev = frags.device
+        total = int(seg_offsets[-1].item()) if total is None else int(total)
+        _need(frags, 2, "frags", total * m, dev)
+        _need(seg_offsets, 8, "seg_offsets", blocks + 1, dev)
+        _need(indices, 1, "indices", blocks * m, dev)
         if out is None:
-            total = (int(seg_offsets[-1].item()) if total is None else int(total)) * m
-            out = (torch.empty(max(total, 1), dtype=torch.int16, device=frags.device),
-                   torch.empty(max(blocks, 1), dtype=torch.int64, device=frags.device))
+            out = (torch.empty(max(total * m, 1), dtype=torch.int16, device=dev),
+                   torch.empty(max(blocks, 1), dtype=torch.int64, device=dev))
         out, ln = out
+        _need(out, 2, "out", total * m, dev)
+        _need(ln, 8, "out_len", blocks, dev)
         mk = L.CX_MEM_DEVICE
     else:
         frags = np.ascontiguousarray(frags, dtype=np.uint16)

@@ -165,3 +165,28 @@ def test_from_fragments_value_256_refused(ida):
     frags = [(i + 1, np.array([frag[i]], dtype=np.uint16)) for i in range(m)]
     with pytest.raises(chordx.ChordError):
         ida.DataBlock.from_fragments(frags, n, m, p)
+
+
+def test_device_arguments_checked(ida):
+    """Device tensors of the wrong element size, too small or on another
+    device are refused before any pointer reaches the kernels."""
+    import torch
+    nb, bl = 16, 100
+    data = torch.randint(0, 256, (nb * bl,), dtype=torch.uint8, device="cuda")
+    offs = torch.arange(0, nb * bl + 1, bl, dtype=torch.int64, device="cuda")
+    frags, seg = ida.encode_flat(data, offs)
+    S = (bl + 9) // 10
+    rows = frags.view(nb, 14, S)[:, :10, :].contiguous().view(-1)
+    idx = torch.arange(1, 11, dtype=torch.uint8, device="cuda").repeat(nb)
+    with pytest.raises(TypeError):
+        ida.decode_flat(rows, seg, idx.to(torch.int32))        # 4-byte indices
+    with pytest.raises(TypeError):
+        ida.decode_flat(rows[: rows.numel() // 2], seg, idx)    # too few fragment values
+    with pytest.raises(TypeError):
+        ida.encode_flat(data, offs.to(torch.int32))             # 4-byte offsets
+    bad_out = (torch.empty(1, dtype=torch.int16, device="cuda"),
+               torch.empty(nb, dtype=torch.int64, device="cuda"))
+    with pytest.raises(TypeError):
+        ida.decode_flat(rows, seg, idx, out=bad_out)            # output too small
+    out, ln = ida.decode_flat(rows, seg, idx)                   # the valid call still works
+    assert bool((ln == bl).all())
