@@ -2104,9 +2104,24 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *ring,
                                                   const uint64_t *rh, uint32_t n, int lvl_base,
                                                   int nlev, uint32_t p_first, uint32_t M, int gs,
-                                                  uint4 *cz, uint32_t *esc) {
-    // grid.y = plane (i - lvl_base) * 2 + b; x strides over the plane's M rows
-    const uint32_t plane = blockIdx.y;
+                                                  uint4 *cz, uint32_t *esc, uint32_t K) {
+    // K = 0: grid.y = plane (i - lvl_base) * 2 + b, x over the plane's rows
+    // (plane after plane).  K > 0: 1-D grid in chunks of K row-blocks: every
+    // plane of a chunk of rows is dispatched before the next chunk, so planes
+    // whose gathers land near the same rows (the lower levels, small E(l))
+    // share them in L2/MALL.
+    uint32_t plane, lb;
+    if (K == 0) {
+        plane = blockIdx.y;
+        const uint32_t per = gridDim.x >> 3;
+        lb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    } else {
+        const uint32_t P = (uint32_t)nlev * 2, B = blockIdx.x;
+        const uint32_t chunk = B / (K * P), rem = B - chunk * K * P;
+        plane = rem / K;
+        const uint32_t sub = rem - plane * K;  // XCD sub % 8 takes a contiguous run
+        lb = chunk * K + (sub & 7) * (K >> 3) + (sub >> 3);
+    }
     const int b = (int)(plane & 1);
     const int i = lvl_base + (int)(plane >> 1);
     // finger (x, l): level planes -> plane base (uniform) + x; rows -> x * 128 + l
@@ -2119,8 +2134,6 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
     // planes and their gathers (16 windows near p + E(l) per plane) stay in
     // L2/MALL.  XCD-aware: hardware block b runs on XCD b % 8; it takes logical
     // block (b % 8) * per + b / 8, so each XCD's L2 serves one contiguous run.
-    const uint32_t per = gridDim.x >> 3;
-    const uint32_t lb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     uint32_t bad = 0, oob = 0;
     const uint32_t j = lb * blockDim.x + threadIdx.x;
     if (j < M) {
@@ -2256,8 +2269,23 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     // the high-word gap codes need every level >= 64 and gs >= 64
     if (lvl_base - 5 < 64 || cz_shift(ib) < 65) return hipErrorInvalidValue;
     if (p_first >= n || M > n || nlev * 2 > 65535) return hipErrorInvalidValue;
+    // row-blocks per chunk: 16 (4096 rows x all planes, ~1000 blocks: about one
+    // resident round); CX_CZ_CHUNK overrides for A/B (0 = plane after plane).
+    // At 2^24 with two-hop planes: 48.5 ms plane order, 44.1 / 37.6 / 41.7 /
+    // 39.8 / 38.3 ms for 8 / 16 / 24 / 32 / 64 (profiles/r02/cz_build/).
+    static const uint32_t K = [] {
+        const char *e = getenv("CX_CZ_CHUNK");
+        const int v = e ? atoi(e) : 16;
+        return (uint32_t)(v > 0 ? (v + 7) / 8 * 8 : 0);
+    }();
     const uint32_t per = (uint32_t)((M + 256 * 8 - 1) / (256 * 8));
-    const dim3 grid(per * 8, nlev * 2);
+    dim3 grid(per * 8, nlev * 2);
+    if (K) {
+        const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + K - 1) / K;
+        const uint64_t blocks = chunks * K * (uint64_t)nlev * 2;
+        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+        grid = dim3((unsigned)blocks, 1);
+    }
     if (n >= (1u << 30)) return hipErrorInvalidValue;
     const bool planes = fv.sx == 1;
     if (!planes && (fv.sx != CX_FINGERS || fv.sl != 1 || fv.L != 0 || fv.C2))
@@ -2267,13 +2295,13 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     const int gs = cz_shift(ib);
     if (planes && fv.C2)
         k_cz_build<2><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
-                                           gs, out, esc);
+                                           gs, out, esc, K);
     else if (planes)
         k_cz_build<1><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
-                                           gs, out, esc);
+                                           gs, out, esc, K);
     else
         k_cz_build<0><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
-                                           gs, out, esc);
+                                           gs, out, esc, K);
     return hipGetLastError();
 }
 
