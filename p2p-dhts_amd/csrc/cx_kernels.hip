@@ -2100,11 +2100,13 @@ __device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t pa
 // stores (95 ms); a quad of lanes per entry (four columns of the slot square)
 // issued more, less coalesced gathers (97 ms).
 // MODE 0: row-major fingers; 1: level planes; 2: level + two-hop planes.
-template <int MODE>
+// STORE bit 0: streaming (non-temporal) stores; bit 1: through LDS, whole lines.
+template <int MODE, int STORE = 1>
 __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *ring,
                                                   const uint64_t *rh, uint32_t n, int lvl_base,
                                                   int nlev, uint32_t p_first, uint32_t M, int gs,
                                                   uint4 *cz, uint32_t *esc, uint32_t K) {
+    __shared__ uint4 cz_stage[(STORE & 2) ? 256 * 4 : 1];
     // K = 0: grid.y = plane (i - lvl_base) * 2 + b, x over the plane's rows
     // (plane after plane).  K > 0: 1-D grid in chunks of K row-blocks: every
     // plane of a chunk of rows is dispatched before the next chunk, so planes
@@ -2136,13 +2138,14 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
     // block (b % 8) * per + b / 8, so each XCD's L2 serves one contiguous run.
     uint32_t bad = 0, oob = 0;
     const uint32_t j = lb * blockDim.x + threadIdx.x;
+    uint32_t out[16];
     if (j < M) {
         // level-major: t = plane * M + j (the walk's entry index)
         const size_t t = (size_t)plane * M + j;
         uint64_t pw = (uint64_t)p_first + j;  // p_first < n, j < M <= n
         if (pw >= n) pw -= n;
         const uint32_t p = (uint32_t)pw;
-        uint32_t node[8], out[16];
+        uint32_t node[8];
         uint64_t nh[8];
         const uint64_t ph = rh[p];
         if (MODE == 2) {
@@ -2242,14 +2245,46 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
         }  // chained path
 #pragma unroll
         for (int v = 0; v < 16; ++v) bad += out[v] == CZ_NONE;
-        uint4 *e = cz + t * 4;
+        if (!(STORE & 2)) {
+            uint4 *e = cz + t * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                const v4u w = {out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]};
+                if (STORE & 1)
+                    __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(e + k));
+                else
+                    *reinterpret_cast<v4u *>(e + k) = w;
+            }
+        }
+    }
+    if (STORE & 2) {
+        // the wave's 64 entries (4 KiB, contiguous: one plane, consecutive
+        // rows) leave through LDS as 4 stores of 1 KiB each, so every store
+        // instruction writes whole lines instead of 16 B of 64 lines
+        const int lane = threadIdx.x & 63;
+        uint4 *ws = cz_stage + (threadIdx.x >> 6) * 256;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            ws[lane * 4 + k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t j0 = lb * blockDim.x + (threadIdx.x & ~63u);  // the wave's first row
+        const size_t t0 = (size_t)plane * M + j0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            // streaming store: the 64 GiB table must not evict the gathered
-            // finger planes and high words from L2 (56.5 -> 53.7 ms at 2^24)
-            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            const v4u w = {out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]};
-            __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(e + k));
+            const int c = k * 64 + lane;  // 16-B chunk of the wave's 4 KiB
+            if (j0 + (c >> 2) < M) {
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                const uint4 u = ws[c];
+                const v4u w = {u.x, u.y, u.z, u.w};
+                v4u *dst = reinterpret_cast<v4u *>(cz + t0 * 4) + c;
+                if (STORE & 1)
+                    __builtin_nontemporal_store(w, dst);
+                else
+                    *dst = w;
+            }
         }
     }
     if (oob) atomicOr(esc + 1, 1u);
@@ -2293,7 +2328,25 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     if (planes && fv.sl != n) return hipErrorInvalidValue;
     uint4 *out = reinterpret_cast<uint4 *>(cz);
     const int gs = cz_shift(ib);
-    if (planes && fv.C2)
+    // stores: whole lines through LDS, streaming (3, default); CX_CZ_STORE A/B at
+    // 2^24: 37.7 ms direct plain, 37-41 ms direct streaming (16 B of 64 lines
+    // per instruction: WRITE_SIZE 1.44 x the table), 33.4 ms via LDS plain,
+    // 31.8 ms via LDS streaming (profiles/r02/cz_build/store_ab/)
+    static const int store = [] {
+        const char *e = getenv("CX_CZ_STORE");
+        return e ? (atoi(e) & 3) : 3;
+    }();
+    if (planes && fv.C2 && store != 1) {
+        if (store == 0)
+            k_cz_build<2, 0><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
+                                                  p_first, M, gs, out, esc, K);
+        else if (store == 2)
+            k_cz_build<2, 2><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
+                                                  p_first, M, gs, out, esc, K);
+        else
+            k_cz_build<2, 3><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
+                                                  p_first, M, gs, out, esc, K);
+    } else if (planes && fv.C2)
         k_cz_build<2><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
                                            gs, out, esc, K);
     else if (planes)
