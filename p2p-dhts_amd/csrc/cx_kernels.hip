@@ -2006,7 +2006,7 @@ __global__ void k_fingers_levels(const uint32_t *F, uint32_t n, int L, int nl, u
     __syncthreads();
     for (int k = threadIdx.x; k < nl * 64; k += blockDim.x) {
         const int c = k >> 6, r = k & 63;
-        if (r < rows) FT[(size_t)c * n + p0 + r] = t[c][r];
+        if (r < rows) __builtin_nontemporal_store(t[c][r], FT + (size_t)c * n + p0 + r);
     }
 }
 
@@ -2019,7 +2019,7 @@ __global__ void k_fingers_pairs(const uint32_t *FT, uint32_t n, int nl, uint32_t
         const size_t k = t / n;  // plane of level L + 1 + k
         const size_t x = t - k * n;
         const uint32_t y = FT[(k + 1) * n + x];
-        C2[t] = y < n ? FT[k * n + y] : CX_NONE;
+        __builtin_nontemporal_store(y < n ? FT[k * n + y] : CX_NONE, C2 + t);
     }
 }
 
