@@ -126,21 +126,40 @@ void table_free(int device, void *p, size_t bytes) {
 
 struct DBuf {
     void *p = nullptr;
-    ~DBuf() {
-        if (p) (void)hipFree(p);
+    size_t pooled = 0;  // > 0: a table-pool block of this size (build temporaries >= 1 GiB)
+    ~DBuf() { drop(); }
+    void drop() {
+        if (!p) return;
+        if (pooled) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            table_free(dev, p, pooled);
+        } else {
+            (void)hipFree(p);
+        }
+        p = nullptr;
+        pooled = 0;
     }
     hipError_t alloc(size_t bytes) {
-        if (p) (void)hipFree(p);
-        p = nullptr;
+        drop();
         return hipMalloc(&p, bytes ? bytes : 16);
+    }
+    // through the table pool: build temporaries of the same size recur every
+    // membership epoch (the caller synchronises before the buffer is dropped)
+    hipError_t alloc_pooled(size_t bytes) {
+        drop();
+        hipError_t e = table_alloc(&p, bytes ? bytes : 16);
+        if (e == hipSuccess) pooled = bytes ? bytes : 16;
+        return e;
     }
     template <class T>
     T *as() const {
         return static_cast<T *>(p);
     }
-    void *release() {
+    void *release() {  // ownership to the caller (hipMalloc'd buffers only)
         void *r = p;
         p = nullptr;
+        pooled = 0;
         return r;
     }
 };
@@ -431,21 +450,28 @@ void route_geometry(cx_ring *r) {
 // planes in `ft` when HBM allows (cxi_set_table_build(ring, 1) forces the
 // row-major table, for A/B), else the row-major table itself.
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
-                         DBuf &c2, hipStream_t s) {
+                         DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     fv = cxk::FingerView::rows(r->d_fingers);
     hipError_t e0 = hi.alloc(r->n * sizeof(uint64_t));
     if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
     if (e0 != hipSuccess) return e0;
     const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
-    if (r->table_build == 1 || ft.alloc((size_t)nl * r->n * sizeof(uint32_t)) != hipSuccess) {
-        (void)hipGetLastError();
-        return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (ft_pre && r->table_build != 1) {  // written by the finger build itself
+        fv = cxk::FingerView::planes(ft_pre, r->n, L, nl);
+    } else {
+        if (r->table_build == 1 ||
+            ft.alloc_pooled((size_t)nl * r->n * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            return hipSuccess;
+        }
+        e = cxk::fingers_levels(r->d_fingers, r->n, L, nl, ft.as<uint32_t>(), s);
+        if (e != hipSuccess) return e;
+        fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
-    hipError_t e = cxk::fingers_levels(r->d_fingers, r->n, L, nl, ft.as<uint32_t>(), s);
-    if (e != hipSuccess) return e;
-    fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
-    if (r->table_build == 0 && c2.alloc((size_t)(nl - 1) * r->n * sizeof(uint32_t)) == hipSuccess) {
-        e = cxk::fingers_pairs(ft.as<uint32_t>(), r->n, nl, c2.as<uint32_t>(), s);
+    if (r->table_build == 0 &&
+        c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t)) == hipSuccess) {
+        e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) fv.C2 = c2.as<uint32_t>();
     }
     (void)hipGetLastError();
@@ -454,7 +480,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
 
 // Builds (once per finger build) the table the selected route variant reads.
 // Without HBM for it the route falls back to variant 0 (finger + ring gathers).
-int ensure_route_table(cx_ring *r, hipStream_t s) {
+int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     if (!r->fingers_converged || !r->d_ring_ext) return CX_OK;
     const size_t ent = r->n * (size_t)r->rt_R;
     if (r->variant() == 5 && !r->cz_valid) {
@@ -466,7 +492,7 @@ int ensure_route_table(cx_ring *r, hipStream_t s) {
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
             DBuf ft, hi, c2;
             cxk::FingerView fv;
-            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s));
+            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre));
             CX_HIP(cxk::cz_build(fv, r->d_ring, hi.as<uint64_t>(), r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_cz,
                                  r->d_scratch, s));
             uint32_t esc[2] = {0, 0};
@@ -716,7 +742,8 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
 
 namespace {
 // The converged n x 128 finger table into ring->d_fingers (allocated).
-int build_fingers_table(cx_ring *ring, hipStream_t s) {
+int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, int ft_l = 0,
+                        bool *ft_done = nullptr) {
     // streaming per-block window build (needs the directory and the ID
     // slices); CX_FINGERS_SEARCH=1 keeps one search per entry (A/B)
     static const bool search_only = getenv("CX_FINGERS_SEARCH") != nullptr;
@@ -733,7 +760,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s) {
     const bool streaming = !search_only && ring->d_ring_key &&
                            fws.alloc(cxk::fingers_workspace_bytes(ring->n)) == hipSuccess;
     CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
-                              streaming ? fws.p : nullptr, ring->d_fingers, s));
+                              streaming ? fws.p : nullptr, ring->d_fingers, s, ft, ft_l, ft_done));
     ring->fingers_converged = true;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
     return CX_OK;
@@ -774,15 +801,26 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
             return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
         }
     }
-    if ((rc = build_fingers_table(ring, s))) return rc;
     route_geometry(ring);
+    // the default route table reads the fingers as level planes: the streaming
+    // finger build writes them alongside the rows (no transpose pass)
+    DBuf ft_pre;
+    bool ft_done = false;
+    const int ft_l = ring->rt_l0 - 5;
+    if (ring->variant() == 5 && ring->table_build == 0 && ft_l >= 64 &&
+        ft_pre.alloc_pooled((size_t)(CX_FINGERS - ft_l) * ring->n * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        ft_pre.p = nullptr;
+    }
+    if ((rc = build_fingers_table(ring, s, ft_pre.as<uint32_t>(), ft_l, &ft_done))) return rc;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
     if (ring->d_ring_ext) CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
     // the default route kernel's table is built now (outside any timed query)
-    if (int rc2 = ensure_route_table(ring, s)) return rc2;
+    if (int rc2 = ensure_route_table(ring, s, ft_done ? ft_pre.as<uint32_t>() : nullptr))
+        return rc2;
     if (fingers_out) {
         const hipMemcpyKind kind =
             memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;

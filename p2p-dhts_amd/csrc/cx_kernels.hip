@@ -644,7 +644,8 @@ __global__ __launch_bounds__(256) void k_fingers_plan(SearchView sv, const cell1
 __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell128 *ring,
                                                       const uint32_t *ring_key, int kb,
                                                       const uint8_t *glog_g, const uint8_t *lvl0_g,
-                                                      const uint32_t *S0, uint32_t *F) {
+                                                      const uint32_t *S0, uint32_t *F,
+                                                      uint32_t *FT, int Lft) {
     constexpr int LPW = FT_CH / 4;    // levels per wave per chunk
     constexpr int EPL = FT_W / 64;    // window elements per lane per level
     static_assert(EPL * 64 == FT_W && LPW * 4 == FT_CH, "window geometry");
@@ -792,6 +793,23 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
         const v4u ov = {o.x, o.y, o.z, o.w};
         __builtin_nontemporal_store(ov, reinterpret_cast<v4u *>(F + (size_t)p * CX_FINGERS) + chunk);
     }
+    // optional: the level planes FT[(l - Lft) n + p] = F[p][l] for l >= Lft
+    // (>= FT_L0) that the route-table build reads, straight from the tile --
+    // 512 contiguous bytes per level and block instead of a transpose pass
+    // over the finger table
+    if (FT) {
+        const uint32_t n_ = n;
+        const int nlev = CX_FINGERS - Lft;
+        for (int k = threadIdx.x; k < nlev * FT_P; k += blockDim.x) {
+            const int c = k / FT_P, r = k - c * FT_P;
+            if (r >= (int)rows) continue;
+            const int i = Lft + c;
+            const uint32_t p = a + r;
+            const uint32_t v = i <= glog[r] ? (p + 1 == n_ ? 0u : p + 1)
+                                             : tile[r * FT_ROW + (i - FT_L0)];
+            __builtin_nontemporal_store(v, FT + (size_t)c * n_ + p);
+        }
+    }
 }
 
 // Slice position of the streaming finger build: the expected span of a
@@ -819,8 +837,10 @@ size_t fingers_workspace_bytes(size_t n) {
 }
 
 hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32_t *ring_key,
-                         void *ws, uint32_t *F, hipStream_t s) {
+                         void *ws, uint32_t *F, hipStream_t s, uint32_t *FT, int Lft,
+                         bool *planes_done) {
     const size_t n = sv.ev.n;
+    if (planes_done) *planes_done = false;
     if (ring_key && ws && sv.dir && n >= ((size_t)1 << 18)) {
         const uint32_t nblk = (uint32_t)((n + FT_P - 1) / FT_P);
         uint32_t *S0 = static_cast<uint32_t *>(ws);
@@ -829,8 +849,11 @@ hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32
         k_fingers_plan<<<(nblk + 3) / 4, 256, 0, s>>>(sv, ring, glog, lvl0, S0, nblk);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+        // planes straight from the tile when every plane level is a tile level
+        const bool planes = FT && Lft >= FT_L0 && Lft < CX_FINGERS;
         k_fingers_tile<<<nblk, 256, 0, s>>>(sv, ring, ring_key, finger_key_shift(n), glog, lvl0,
-                                            S0, F);
+                                            S0, F, planes ? FT : nullptr, Lft);
+        if (planes_done) *planes_done = planes;
         return hipGetLastError();
     }
     const size_t total = n * CX_FINGERS;

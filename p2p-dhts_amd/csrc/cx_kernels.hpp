@@ -77,8 +77,9 @@ size_t fingers_workspace_bytes(size_t n);
 int finger_key_shift(size_t n);
 hipError_t predecessor(const SearchView &ev, const cell128 *keys, size_t q, uint32_t *pred,
                        hipStream_t s);
-hipError_t fingers_build(const SearchView &ev, const cell128 *ring, const uint32_t *ring_key,
-                         void *ws, uint32_t *F, hipStream_t s);
+hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32_t *ring_key,
+                         void *ws, uint32_t *F, hipStream_t s, uint32_t *FT = nullptr,
+                         int Lft = 0, bool *planes_done = nullptr);
 hipError_t ring_slice_build(const cell128 *ring, size_t n, int kb, uint32_t *key, hipStream_t s);
 hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128 *min_keys,
                  const uint32_t *preds, const LitState &ls, bool literal, const uint32_t *src,
