@@ -37,7 +37,8 @@ int fail(int code, const std::string &msg) {
 // RAII device allocation.
 // ---------------------------------------------------------------------------
 // Table pool.  A ring's large tables (finger table, route tables, arc planes:
-// >= 1 GiB each, 72 GiB per 2^24-peer replica) are not returned to the driver
+// 72 GiB per 2^24-peer replica) and the builds' large temporaries (>= 16 MiB)
+// are not returned to the driver
 // when the ring is destroyed but kept, up to CX_POOL_CAP bytes per process,
 // for the next ring that asks for the same size on the same device: after a
 // membership change the new ring's tables reuse the old ring's HBM instead of
@@ -53,7 +54,7 @@ struct PoolEnt {
 std::mutex g_pool_mu;
 std::vector<PoolEnt> g_pool;
 size_t g_pool_bytes = 0;
-constexpr size_t POOL_MIN = (size_t)1 << 30;
+constexpr size_t POOL_MIN = (size_t)16 << 20;
 constexpr size_t POOL_CAP = (size_t)96 << 30;
 
 void pool_trim_locked(int device) {
@@ -452,7 +453,7 @@ void route_geometry(cx_ring *r) {
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
                          DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     fv = cxk::FingerView::rows(r->d_fingers);
-    hipError_t e0 = hi.alloc(r->n * sizeof(uint64_t));
+    hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t));
     if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
     if (e0 != hipSuccess) return e0;
     const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
@@ -758,7 +759,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
     }
     DBuf fws;
     const bool streaming = !search_only && ring->d_ring_key &&
-                           fws.alloc(cxk::fingers_workspace_bytes(ring->n)) == hipSuccess;
+                           fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n)) == hipSuccess;
     CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
                               streaming ? fws.p : nullptr, ring->d_fingers, s, ft, ft_l, ft_done));
     ring->fingers_converged = true;
