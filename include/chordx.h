@@ -307,7 +307,10 @@ enum { CX_ARC_NEW = 0, CX_ARC_RESULT = 1, CX_ARC_WALK = 2, CX_ARC_NONE = 3 };
 
 /* Builds rank `rank`'s planes of a `world`-rank layout (and the converged
  * finger table if missing: the planes are derived from it, as the reference's
- * fingers are, abstract_chord_peer.cpp:564-613). */
+ * fingers are, abstract_chord_peer.cpp:564-613).  Arc routing walks the
+ * converged ring: after cx_fingers_upload, cx_peer_state_upload or
+ * cx_liveness_upload the arc calls fail with CX_E_STATE (cx_route honours
+ * that state). */
 int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels);
 /* Replicated top levels, local rows (arc + halo) and route-plane bytes. */
 int cx_arc_info(const cx_ring *ring, int *top_levels, uint64_t *local_rows,

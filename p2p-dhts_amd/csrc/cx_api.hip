@@ -276,6 +276,9 @@ struct cx_ring {
         return v;
     }
     bool literal() const { return !fingers_converged || d_min_keys || d_preds || liveness; }
+    // hand-edited state (peer state or liveness uploads): only cx_route's
+    // literal walk honours it
+    bool edited() const { return d_min_keys || d_preds || liveness; }
     LitState lit() const {
         LitState l;
         l.alive = d_alive;
@@ -1481,7 +1484,12 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     // the converged finger table (streaming build; no route table); one built
     // here only to derive the planes is released afterwards (the walk finds
     // exact below-table fingers by directory search)
-    const bool own_fingers = !ring->d_fingers || !ring->fingers_converged;
+    // arc routing walks the converged table: refuse state it would ignore
+    CX_CHECK(!ring->edited(), CX_E_STATE,
+             "arc routing walks the converged ring; peer-state / liveness uploads need cx_route");
+    CX_CHECK(!ring->d_fingers || ring->fingers_converged, CX_E_STATE,
+             "arc routing walks the converged ring; uploaded fingers need cx_route");
+    const bool own_fingers = !ring->d_fingers;
     if (own_fingers) {
         if (!ring->d_fingers &&
             table_alloc((void **)&ring->d_fingers, n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
@@ -1610,6 +1618,7 @@ int cx_arc_step(const cx_ring *ring, int rank, const cx_arc_rec *in, size_t q, c
                 uint32_t *owner, uint8_t *hops, uint8_t *status) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
     CX_CHECK(rank == ring->arc_rank, CX_E_INVALID, "rank differs from the one cx_arc_build used");
     CX_CHECK(rank >= 0 && rank < CX_ARC_MAX_RANKS, CX_E_INVALID, "rank out of range");
     CX_CHECK(q == 0 || (in && out && owner && hops), CX_E_INVALID, "null buffer");
@@ -1629,6 +1638,7 @@ int cx_arc_start(const cx_ring *ring, int rank, const uint32_t *src, const cx_u1
                  size_t q, cx_arc_rec *out, uint32_t *owner, uint8_t *hops, uint8_t *status) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
     CX_CHECK(rank == ring->arc_rank, CX_E_INVALID, "rank differs from the one cx_arc_build used");
     CX_CHECK(q < (1ull << ARC_ORIGIN_SHIFT), CX_E_INVALID, "too many lookups for one rank");
     CX_CHECK(q == 0 || (src && keys && out && owner && hops), CX_E_INVALID, "null buffer");
@@ -1679,6 +1689,7 @@ int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *
     CX_CHECK(q < (1ull << ARC_ORIGIN_SHIFT), CX_E_INVALID, "too many lookups for one rank");
     CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
              "arc not built for this world size (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
     int rc = use_device(ring);
     if (rc) return rc;
     hipStream_t s = ring->stream;

@@ -207,3 +207,30 @@ def test_arc_top_levels(cx, O, top, key_first):
         assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)
         assert torch.equal(outs[g][2], st)
     assert rounds <= 3
+
+
+def test_arc_refuses_hand_edited_state(cx, O):
+    """Arc routing walks the converged ring; liveness / uploaded state that it
+    would ignore is refused (cx_route's literal walk honours it)."""
+    import torch
+    ids = O.splitmix_keys(0xA2C9, 3000)
+    ids_dev = torch.from_numpy(ids.view(np.int64).copy()).cuda()
+    r = cx.Ring(ids_dev)
+    alive = np.ones(r.n, dtype=np.uint8)
+    alive[5] = 0
+    r.upload_liveness(alive=alive, ns=4)
+    with pytest.raises(cx.ChordError):
+        r.arc_build(2, 0)
+    r2 = cx.Ring(ids_dev)
+    r2.build_fingers()
+    F = r2.fingers_device().cpu().numpy().view(np.uint32).copy()
+    r2.upload_fingers(F)  # hand-edited (even if equal): not converged any more
+    with pytest.raises(cx.ChordError):
+        r2.arc_build(2, 0)
+    r3 = cx.Ring(ids_dev)
+    r3.arc_build(2, 1)
+    r3.upload_liveness(alive=alive, ns=4)
+    src = torch.zeros(4, dtype=torch.int32, device="cuda")
+    keys = torch.zeros((4, 2), dtype=torch.int64, device="cuda")
+    with pytest.raises(cx.ChordError):
+        r3.arc_send_ahead(2, 1, src, keys)
