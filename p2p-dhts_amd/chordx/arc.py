@@ -56,7 +56,9 @@ class ArcRouter:
         engine.arc_build(world, rank)
         self.rounds = 0
         self.records_sent = 0
-        self.key_first = True
+        # key-first routing (no origin walk) pays off once lookups cross ranks;
+        # a single rank walks them in place
+        self.key_first = world > 1
         self._mat_host = None  # pinned landing buffer of the count matrix
 
     def _exchange(self, send, counts):
