@@ -11,7 +11,16 @@ travels once -- the GET_SUCC request forwarded to the next peer
 its key's arc, and its result travels home once.  Owners, hops and statuses
 equal the replicated-ring route's (tests/test_gpu_arc.py).
 
-One bulk-synchronous round = step (walk every record as far as this rank's
+Default protocol ("soa", engines with arc_partition): the lookups go straight
+to the rank whose arc holds their key's owner as two arrays -- keys (16 B) and
+sources (4 B) -- in one all_to_all each; that rank walks them from their
+sources over the replicated top planes and its own rows and answers in
+receive order, 8 B per lookup; the answers come back with the splits swapped
+and land in send order, where the origin scatters them through the
+permutation it kept.  One count exchange, three all_to_alls, no origin or
+index crossing xGMI, no re-bucketing of results.
+
+Record protocol ("records", origin walk or key-first): one bulk-synchronous round = step (walk every record as far as this rank's
 rows reach) -> bucket by destination -> exchange: one all_gather of the G x G
 count matrix (every rank learns its receive splits and the global in-flight
 total from the same call) and one all_to_all_single of the 32-B records.  A
@@ -90,7 +99,49 @@ class ArcRouter:
                                 input_split_sizes=list(counts), group=self.group)
         return (recv.to(send.device) if recv.device != send.device else recv), inflight
 
-    def route(self, src, keys, owner, hops, status=None, key_first=None) -> int:
+    def _splits(self, counts, dev):
+        """Receive splits of this rank (column of the all-gathered G x G count
+        matrix), through one pinned async copy."""
+        mine = torch.tensor(counts, dtype=torch.int64, device=dev)
+        mat = torch.empty((self.world, self.world), dtype=torch.int64, device=dev)
+        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
+        if mat.is_cuda:
+            if self._mat_host is None:
+                self._mat_host = torch.empty((self.world, self.world), dtype=torch.int64,
+                                             pin_memory=True)
+            self._mat_host.copy_(mat, non_blocking=True)
+            torch.cuda.current_stream(mat.device).synchronize()
+            mat = self._mat_host
+        return [int(x) for x in mat[:, self.rank]]
+
+    def _a2a(self, t, out_splits, in_splits, dev):
+        s = t.to(dev) if t.device != torch.device(dev) else t
+        out = torch.empty((sum(out_splits),) + tuple(s.shape[1:]), dtype=s.dtype, device=dev)
+        tdist.all_to_all_single(out, s.contiguous(), output_split_sizes=out_splits,
+                                input_split_sizes=in_splits, group=self.group)
+        return out.to(t.device) if out.device != t.device else out
+
+    def route_soa(self, src, keys, owner, hops, status=None) -> int:
+        """Key-first routing in structure-of-arrays form (module docstring);
+        returns the number of exchange rounds (1 on a single rank, else 2)."""
+        eng = self.engine
+        if self.world == 1:
+            eng.arc_deliver(eng.arc_route(src, keys), None, owner, hops, status)
+            self.rounds = 1
+            return 1
+        skeys, ssrc, perm, counts = eng.arc_partition(self.world, src, keys)
+        dev = self.comm_device if self.comm_device is not None else skeys.device
+        recv = self._splits(counts, dev)
+        rkeys = self._a2a(skeys, recv, counts, dev)
+        rsrc = self._a2a(ssrc, recv, counts, dev)
+        res = eng.arc_route(rsrc, rkeys)
+        back = self._a2a(res, counts, recv, dev)
+        eng.arc_deliver(back, perm, owner, hops, status)
+        self.records_sent += int(sum(counts))
+        self.rounds = 2
+        return 2
+
+    def route(self, src, keys, owner, hops, status=None, key_first=None, protocol=None) -> int:
         """Routes this rank's lookups (issued at peers src[i]); collective over
         the group.  Writes owner/hops/status at the lookups' indices and
         returns the number of rounds taken.
@@ -101,6 +152,13 @@ class ArcRouter:
         own lower planes (a walk that needs a lower level is within 2^Lh of its
         key, i.e. in that arc or its halo).  Otherwise the origin walks the top
         levels first (cx_arc_start) and forwards a WALK record."""
+        if protocol is None:
+            protocol = "soa" if (hasattr(self.engine, "arc_partition") and
+                                 (key_first is None or key_first)) else "records"
+        if protocol == "soa":
+            return self.route_soa(src, keys, owner, hops, status)
+        if protocol != "records":
+            raise ValueError("protocol must be 'soa' or 'records'")
         kf = self.key_first if key_first is None else key_first
         start = getattr(self.engine, "arc_start", None)
         ahead = getattr(self.engine, "arc_send_ahead", None)

@@ -451,6 +451,57 @@ class Ring:
                                           _ptr(send), _ptr(counts)))
         return send[: int(counts.sum())], [int(c) for c in counts]
 
+    def arc_partition(self, world: int, src, keys):
+        """(send_keys, send_src, perm, counts): this rank's lookups grouped by
+        the rank of their key's arc (cx_arc_partition).  send_keys / send_src
+        are exchanged; perm (send slot -> lookup index) stays here."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        skeys = torch.empty((q, 2), dtype=torch.int64, device=keys.device)
+        ssrc = torch.empty(q, dtype=torch.int32, device=keys.device)
+        perm = torch.empty(q, dtype=torch.int32, device=keys.device)
+        counts = np.zeros(world, dtype=np.uint64)
+        self._arc_stream()
+        L.check(L.lib().cx_arc_partition(self._h, world, _ptr(src), _ptr(keys), q, _ptr(skeys),
+                                         _ptr(ssrc), _ptr(perm), _ptr(counts)))
+        return skeys, ssrc, perm, [int(c) for c in counts]
+
+    def arc_route(self, src, keys, res=None):
+        """Packed results (int64: owner | hops << 32 | status << 40 | 1 << 63)
+        of lookups received from every rank, in input order (cx_arc_route)."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        if res is None:
+            res = torch.empty(q, dtype=torch.int64, device=keys.device)
+        elif not (_is_dev(res) and res.element_size() == 8 and res.numel() == q
+                  and res.is_contiguous()):
+            raise TypeError("res must be a contiguous 8-byte device tensor of q elements")
+        self._arc_stream()
+        L.check(L.lib().cx_arc_route(self._h, _ptr(src), _ptr(keys), q, _ptr(res)))
+        return res
+
+    def arc_deliver(self, res, perm, owner, hops, status=None):
+        """Scatter returned results (send order) to owner/hops/status through
+        perm (None: identity) (cx_arc_deliver)."""
+        q = res.shape[0]
+        if not (_is_dev(res) and res.element_size() == 8 and res.is_contiguous()):
+            raise TypeError("res must be a contiguous 8-byte device tensor")
+        if perm is not None and not (_is_dev(perm) and perm.element_size() == 4
+                                     and perm.is_contiguous() and perm.numel() == q):
+            raise TypeError("perm must be a contiguous 4-byte device tensor of len(res)")
+        for t, w, name in ((owner, 4, "owner"), (hops, 1, "hops"), (status, 1, "status")):
+            if t is not None and not (_is_dev(t) and t.element_size() == w and t.numel() >= q):
+                raise TypeError(f"{name}: device tensor of {w}-byte elements, >= q")
+        self._arc_stream()
+        L.check(L.lib().cx_arc_deliver(self._h, _ptr(res), _ptr(perm) if perm is not None
+                                       else None, q, _ptr(owner), _ptr(hops), _ptr(status)))
+
     def arc_bucket(self, world: int, recs):
         """(send, counts): records grouped by destination rank, NONE dropped."""
         q = recs.shape[0]

@@ -1707,6 +1707,59 @@ int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *
     return CX_OK;
 }
 
+int cx_arc_partition(const cx_ring *ring, int world, const uint32_t *src, const cx_u128 *keys,
+                     size_t q, cx_u128 *send_keys, uint32_t *send_src, uint32_t *perm,
+                     uint64_t *counts) {
+    CX_CHECK(ring && counts, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(q == 0 || (src && keys && send_keys && send_src && perm), CX_E_INVALID,
+             "null buffer");
+    CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many lookups for one rank");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    uint32_t *dcnt = ring->d_scratch, *dcur = ring->d_scratch + CX_ARC_MAX_RANKS;
+    CX_HIP(hipMemsetAsync(dcnt, 0, CX_ARC_MAX_RANKS * sizeof(uint32_t), s));
+    CX_HIP(cxk::arc_partition(src, reinterpret_cast<const cell128 *>(keys), q, ring->d_arc_bounds,
+                              ring->arc_nb, world, dcnt, dcur,
+                              reinterpret_cast<cell128 *>(send_keys), send_src, perm, s));
+    uint32_t hc[CX_ARC_MAX_RANKS];
+    CX_HIP(hipMemcpyAsync(hc, dcnt, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    for (int g = 0; g < world; ++g) counts[g] = hc[g];
+    return CX_OK;
+}
+
+int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
+                 uint64_t *res) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    CX_CHECK(q == 0 || (src && keys && res), CX_E_INVALID, "null buffer");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    SearchView v = ring->sv();
+    v.dir = ring->d_dir;  // exact below-table fingers by directory search
+    CX_HIP(cxk::route_arc_kf(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
+                             ring->rt_l0, ring->rt_R, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
+                             ring->arc_M, src, reinterpret_cast<const cell128 *>(keys), q, res,
+                             ring->stream));
+    return CX_OK;
+}
+
+int cx_arc_deliver(const cx_ring *ring, const uint64_t *res, const uint32_t *perm, size_t q,
+                   uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(q == 0 || (res && owner && hops), CX_E_INVALID, "null buffer");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    CX_HIP(cxk::arc_deliver(res, perm, q, owner, hops, status, ring->stream));
+    return CX_OK;
+}
+
 // ---- internal (not part of chordx.h): error reporting for cx_wire.cpp
 int cxi_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
 

@@ -1983,6 +1983,7 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
 // interval, and an undecided one fetches the exact IDs (A_FIXC / A_FIXT).
 // ---------------------------------------------------------------------------
 constexpr uint32_t CZ_NONE = 0xFFFFFFFFu;
+constexpr uint8_t CX_QI_ARC_MISS = 0xFE;  // key-first arc walk left the rank's rows (never on a correct layout)
 constexpr int CZ_RES_WIN = 256;  // 26 KB of LDS per 256-lane block: 6 blocks per CU
 constexpr int CZ_WAVES = 5;      // waves per SIMD the VGPR budget allows (88 VGPRs; 6 spills)
 
@@ -2548,6 +2549,7 @@ struct TreeIO {
     uint32_t *owner;
     uint8_t *hops;
     uint8_t *status;
+    uint64_t *res_out;   // key-first arc walk: packed results in input order
     // STATS build only: [0] 64-B table gathers, [1] exact 16-B ring gathers,
     // [2] exact hops (one F + one ring gather each), [3] lookups started
     unsigned long long *stats;
@@ -2556,22 +2558,29 @@ struct TreeIO {
 // STATS: the same walk, additionally counting the random gathers it issues
 // (bench.py's algorithmic-bytes model and request-rate roofline); the timed
 // kernel is the STATS = false instantiation.
-template <bool ARC, bool CZ, bool STATS = false>
+// KF (key-first arc walk): arc-mode tables (replicated top planes + this
+// rank's rows), replicated-mode I/O: lookups (src, keys) in, one packed result
+// per lookup out in input order (io.res_out).  Every lookup finishes here
+// (records were sent to the rank of their key's arc); a row that is not local
+// would be a layout bug and reports CX_QI_ARC_MISS.
+template <bool ARC, bool CZ, bool STATS = false, bool KF = false>
 __global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(CZ ? CZ_WAVES : 1)))
 void k_route_tree(TreeIO io) {
     constexpr int RW = CZ ? CZ_RES_WIN : RES_WIN;  // cz: smaller window, more waves per CU
     static_assert(!ARC || CZ, "arc mode walks pattern-keyed (cz) rows");
-    __shared__ uint64_t res_all[ARC ? 1 : RT_BLOCK / 64][ARC ? 1 : RW];
+    static_assert(!KF || ARC, "key-first walks arc tables");
+    constexpr bool RIO = !ARC || KF;  // results staged per wave, written in input order
+    __shared__ uint64_t res_all[RIO ? RT_BLOCK / 64 : 1][RIO ? RW : 1];
     __shared__ uint4 ent_all[RT_BLOCK][4];       // each lane's current 64-B entry
     __shared__ uint64_t addr_all[RT_BLOCK];      // entry index + 1 wanted by each lane (0: none)
     const uint32_t n = io.n;
     const int l0 = io.l0, R = io.R, ib = io.ib;
     const int lane = threadIdx.x & 63;
     const int quad0 = threadIdx.x & ~3, qs = threadIdx.x & 3;
-    uint64_t *res = res_all[ARC ? 0 : (threadIdx.x >> 6)];
+    uint64_t *res = res_all[RIO ? (threadIdx.x >> 6) : 0];
     const uint64_t *ent = reinterpret_cast<const uint64_t *>(ent_all[threadIdx.x]);
     const uint32_t *ent32 = reinterpret_cast<const uint32_t *>(ent_all[threadIdx.x]);
-    if (!ARC)
+    if (RIO)
         for (int j = lane; j < RW; j += 64) res[j] = 0;
     const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
     const size_t base = wave * io.chunk;
@@ -2612,7 +2621,7 @@ void k_route_tree(TreeIO io) {
 
     // outcome of a finished query (ARC: local delivery or a result record)
     auto deliver = [&](size_t idx, uint64_t id, uint32_t o, uint32_t hh, uint8_t stt) {
-        if (!ARC) {
+        if (RIO) {
             res[idx & (RW - 1)] = pack_res(o, hh, stt);
         } else {
             ArcRec r;
@@ -2640,14 +2649,14 @@ void k_route_tree(TreeIO io) {
         // ---- refill slot B ----
         {
             size_t lim = end;
-            if (!ARC && flushed + RW < end) lim = flushed + RW;
+            if (RIO && flushed + RW < end) lim = flushed + RW;
             const size_t avail = lim > head ? lim - head : 0;
             const uint64_t want = __ballot(bst == B_EMPTY);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
             if (bst == B_EMPTY && rank < avail) {
                 pq = head + rank;
-                if (ARC && io.in) {
+                if (ARC && !KF && io.in) {
                     const ArcRec r = io.in[pq];
                     pkey = ((u128)r.w1 << 64) | r.w0;
                     pqid = r.qid;
@@ -2657,7 +2666,7 @@ void k_route_tree(TreeIO io) {
                 } else {  // a new lookup (arc mode: issued on this rank)
                     pkey = ld128(io.keys + pq);
                     psrc = io.src[pq];
-                    pqid = ARC ? ((uint64_t)io.self << ARC_ORIGIN_SHIFT) | pq : pq;
+                    pqid = (ARC && !KF) ? ((uint64_t)io.self << ARC_ORIGIN_SHIFT) | pq : pq;
                     ph = 0;
                     pkind = ARC_NEW;
                 }
@@ -2667,7 +2676,7 @@ void k_route_tree(TreeIO io) {
             head += took < avail ? took : avail;
         }
         if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end &&
-            (ARC || flushed >= end))  // every staged result written
+            (!RIO || flushed >= end))  // every staged result written
             break;
 
         // ---- memory round ----
@@ -2806,7 +2815,11 @@ void k_route_tree(TreeIO io) {
                              own, st, xcp)
                    : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
             if (r == 1) fin = true;
-            if (ARC && r == 2) {  // continue on the rank of the key's arc
+            if (KF && r == 2) {
+                fin = true;
+                own = CX_NONE;
+                st = CX_QI_ARC_MISS;
+            } else if (ARC && r == 2) {  // continue on the rank of the key's arc
                 ArcRec o;
                 o.w0 = (uint64_t)key;
                 o.w1 = (uint64_t)(key >> 64);
@@ -2856,7 +2869,11 @@ void k_route_tree(TreeIO io) {
                                     ri, ent32, own, st, xcp)
                           : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own,
                                       st);
-                if (ARC && done == 2) {
+                if (KF && done == 2) {
+                    own = CX_NONE;
+                    st = CX_QI_ARC_MISS;
+                    done = 1;
+                } else if (ARC && done == 2) {
                     ArcRec o;
                     o.w0 = (uint64_t)key;
                     o.w1 = (uint64_t)(key >> 64);
@@ -2875,7 +2892,7 @@ void k_route_tree(TreeIO io) {
         }
 
         // ---- flush complete 64-result segments (replicated mode) ----
-        if (!ARC) {
+        if (RIO) {
             for (int it = 0; it < 2; ++it) {
                 if (flushed >= end) break;
                 const size_t idx = flushed + lane;
@@ -2883,9 +2900,13 @@ void k_route_tree(TreeIO io) {
                 const uint64_t v = inr ? res[idx & (RW - 1)] : 0ull;
                 if (__ballot(!inr || (v >> 63)) != ~0ull) break;
                 if (inr) {
-                    io.owner[idx] = (uint32_t)v;
-                    io.hops[idx] = (uint8_t)(v >> 32);
-                    if (io.status) io.status[idx] = (uint8_t)(v >> 40);
+                    if (KF) {
+                        __builtin_nontemporal_store(v, io.res_out + idx);
+                    } else {
+                        io.owner[idx] = (uint32_t)v;
+                        io.hops[idx] = (uint8_t)(v >> 32);
+                        if (io.status) io.status[idx] = (uint8_t)(v >> 40);
+                    }
                     res[idx & (RW - 1)] = 0;
                 }
                 flushed += 64;
@@ -3025,6 +3046,42 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
     k_route_tree<true, true><<<blocks, RT_BLOCK, 0, s>>>(io);
+    return hipGetLastError();
+}
+
+// Key-first arc walk (k_route_tree<true, true, false, true>): lookups received
+// from every rank, walked from their sources over the replicated top planes
+// and this rank's rows; packed results (owner | hops << 32 | status << 40 |
+// 1 << 63) in input order.
+hipError_t route_arc_kf(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                        int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo,
+                        uint32_t M, const uint32_t *src, const cell128 *keys, size_t q,
+                        uint64_t *res, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    TreeIO io = {};
+    io.src = src;
+    io.keys = keys;
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.tree = reinterpret_cast<const uint4 *>(cz);
+    io.l0 = l0;
+    io.R = R;
+    io.ib = ib;
+    io.sv = sv;
+    io.Lh = Lh;
+    io.plo = plo;
+    io.M = M;
+    io.q = q;
+    io.res_out = res;
+    static const unsigned resident = resident_grid(k_route_tree<true, true, false, true>, RT_BLOCK);
+    size_t waves = (size_t)resident * (RT_BLOCK / 64);
+    const size_t small = (q + 1023) / 1024;
+    if (small < waves) waves = small ? small : 1;
+    io.chunk = (q + waves - 1) / waves;
+    waves = (q + io.chunk - 1) / io.chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
+    k_route_tree<true, true, false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 
@@ -3179,6 +3236,66 @@ __global__ __launch_bounds__(256) void k_arc_scatter(ArcIn<SEED> in, size_t q,
     }
 }
 
+// Key-first partition, structure of arrays: this rank's lookups grouped by the
+// rank of their key's arc, as the exchange sends them -- keys (16 B), sources
+// (4 B) and, kept at the origin, the lookup index of every send slot (perm).
+// Results come back in send order (the arc rank answers its receive buffer in
+// order and the return exchange swaps the splits), so no record carries an
+// origin or an index across xGMI.
+__global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t q,
+                                                         const ArcBound *bounds, int nb, int G,
+                                                         uint32_t *cursor, cell128 *skeys,
+                                                         uint32_t *ssrc, uint32_t *perm) {
+    __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
+    __shared__ ArcBound sb[ARC_MAX_RANKS];
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
+    const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
+    for (size_t b0 = (size_t)blockIdx.x * per; b0 < q; b0 += (size_t)gridDim.x * per) {
+        for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+        __syncthreads();
+        ArcRec r[ARC_SCAT_R];
+        int d[ARC_SCAT_R];
+        uint32_t slot[ARC_SCAT_R];
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) {
+            const size_t i = b0 + (size_t)k * blockDim.x + threadIdx.x;
+            d[k] = -1;
+            if (i < q) {
+                r[k] = in.get(i);
+                d[k] = arc_dest(r[k], sb, nb, G);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
+        __syncthreads();
+        for (int j = threadIdx.x; j < G; j += blockDim.x)
+            basep[j] = h[j] ? atomicAdd(&cursor[j], h[j]) : 0u;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k)
+            if (d[k] >= 0) {
+                const uint32_t o = basep[d[k]] + slot[k];
+                skeys[o] = cell128{r[k].w0, r[k].w1};
+                ssrc[o] = r[k].cur;
+                perm[o] = (uint32_t)(r[k].qid & ARC_INDEX_MASK);
+            }
+        __syncthreads();
+    }
+}
+
+// Results back at the origin: res[j] answers the lookup in send slot j.
+__global__ void k_arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q,
+                              uint32_t *owner, uint8_t *hops, uint8_t *status) {
+    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < q;
+         j += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t v = res[j];
+        const size_t i = perm ? perm[j] : j;
+        owner[i] = (uint32_t)v;
+        hops[i] = (uint8_t)(v >> 32);
+        if (status) status[i] = (uint8_t)(v >> 40);
+    }
+}
+
 // cursor[g] = exclusive prefix sum of counts (one wave).
 __global__ void k_arc_offsets(const uint32_t *counts, int G, uint32_t *cursor) {
     if (threadIdx.x == 0) {
@@ -3203,6 +3320,25 @@ static hipError_t arc_bucket_in(const ArcIn<SEED> &in, size_t q, const ArcBound 
     if (q)
         k_arc_scatter<SEED><<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0,
                               s>>>(in, q, bounds, nb, G, cursor_dev, send);
+    return hipGetLastError();
+}
+
+hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
+                         const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
+                         uint32_t *cursor_dev, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
+                         hipStream_t s) {
+    const ArcIn<true> in{nullptr, src, keys, 0};
+    hipError_t e = arc_bucket_in(in, q, bounds, nb, G, counts_dev, cursor_dev, nullptr, s, false);
+    if (e != hipSuccess || q == 0) return e;
+    k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
+        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm);
+    return hipGetLastError();
+}
+
+hipError_t arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q, uint32_t *owner,
+                       uint8_t *hops, uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    k_arc_deliver<<<cx_grid(q, 256, 8192), 256, 0, s>>>(res, perm, q, owner, hops, status);
     return hipGetLastError();
 }
 

@@ -167,6 +167,17 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
                      int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo, uint32_t M,
                      int self, const ArcRec *in, const uint32_t *src, const cell128 *keys, size_t q,
                      ArcRec *out, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
+// Key-first SoA protocol (cx_arc_partition / cx_arc_route / cx_arc_deliver).
+hipError_t route_arc_kf(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                        int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo,
+                        uint32_t M, const uint32_t *src, const cell128 *keys, size_t q,
+                        uint64_t *res, hipStream_t s);
+hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
+                         const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
+                         uint32_t *cursor_dev, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
+                         hipStream_t s);
+hipError_t arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q, uint32_t *owner,
+                       uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,
                     hipStream_t s);
 hipError_t arc_bucket(const ArcRec *recs, size_t q, const ArcBound *bounds, int nb, int G,

@@ -234,3 +234,103 @@ def test_arc_refuses_hand_edited_state(cx, O):
     keys = torch.zeros((4, 2), dtype=torch.int64, device="cuda")
     with pytest.raises(cx.ChordError):
         r3.arc_send_ahead(2, 1, src, keys)
+
+
+# ---------------------------------------------------------------------------
+# Structure-of-arrays key-first protocol (ArcRouter.route_soa): partition by
+# the key's arc, walk in receive order, answers back in send order.
+# ---------------------------------------------------------------------------
+def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0):
+    import torch
+    rings = [cx.Ring(ids_dev) for _ in range(G)]
+    for g, r in enumerate(rings):
+        r.arc_build(G, g, top)
+    outs = []
+    for g in range(G):
+        q = keys[g].shape[0]
+        outs.append((torch.full((q,), -7, dtype=torch.int32, device="cuda"),
+                     torch.full((q,), 77, dtype=torch.uint8, device="cuda"),
+                     torch.full((q,), 9, dtype=torch.uint8, device="cuda") if status else None))
+    if G == 1:
+        rings[0].arc_deliver(rings[0].arc_route(srcs[0], keys[0]), None, *outs[0])
+        torch.cuda.synchronize()
+        return outs, 0
+    parts = [rings[g].arc_partition(G, srcs[g], keys[g]) for g in range(G)]
+    for g, (sk, ss, perm, counts) in enumerate(parts):
+        assert sum(counts) == keys[g].shape[0]
+        assert torch.equal(torch.sort(perm.long()).values,
+                           torch.arange(keys[g].shape[0], device="cuda"))
+    ks = [torch.split(p[0], p[3]) for p in parts]
+    ss = [torch.split(p[1], p[3]) for p in parts]
+    back = [[None] * G for _ in range(G)]
+    for d in range(G):
+        rk = torch.cat([ks[g][d] for g in range(G)])
+        rs = torch.cat([ss[g][d] for g in range(G)])
+        res = rings[d].arc_route(rs, rk)
+        for g, part in enumerate(torch.split(res, [parts[g][3][d] for g in range(G)])):
+            back[g][d] = part
+    sent = 0
+    for g in range(G):
+        rings[g].arc_deliver(torch.cat(back[g]), parts[g][2], *outs[g])
+        sent += sum(parts[g][3]) - parts[g][3][g]
+    torch.cuda.synchronize()
+    return outs, sent
+
+
+@pytest.mark.parametrize("n,G", [(5000, 1), (5000, 2), (5000, 3), (5000, 8), (1 << 16, 8),
+                                 (70001, 5), (2, 2), (1, 1), (3, 4)])
+def test_arc_soa_equals_replicated(cx, O, n, G):
+    import torch
+    q = 4096
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2D0 + n + G)
+    outs, sent = simulate_soa(cx, ids_dev, G, srcs, keys)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow), (n, G, g)
+        assert torch.equal(outs[g][1], hp), (n, G, g)
+        assert torch.equal(outs[g][2], st), (n, G, g)
+    if G > 1 and n > 100:
+        assert sent > 0
+
+
+@pytest.mark.parametrize("top", [1, 3, 6, 12])
+def test_arc_soa_top_levels_and_bad_sources(cx, O, top):
+    import torch
+    n, q, G = 20000, 3000, 4
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2D3 + top)
+    srcs[1][::7] = n + 5
+    srcs[2][::11] = -1
+    outs, _ = simulate_soa(cx, ids_dev, G, srcs, keys, top=top)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)
+        assert torch.equal(outs[g][2], st)
+    assert int((outs[1][2] == cx.CX_Q_BADPEER).sum()) == len(range(0, q, 7))
+    outs2, _ = simulate_soa(cx, ids_dev, G, srcs, keys, status=False, top=top)
+    for g in range(G):
+        assert torch.equal(outs2[g][0], outs[g][0]) and torch.equal(outs2[g][1], outs[g][1])
+
+
+def test_arc_soa_matches_oracle_clustered(cx, O):
+    """Clustered IDs (exact-ID fallbacks) and the oracle's literal walk."""
+    import torch
+    base = 0x1234_5678_9ABC_DEF0 << 64
+    vals = [base + i * 977 for i in range(3000)] + [(1 << 127) + i for i in range(50)]
+    ids = O.keys_from_ints(vals)
+    ids_dev = torch.from_numpy(ids.view(np.int64).copy()).cuda()
+    G, q = 3, 3000
+    srcs, keys = [], []
+    for g in range(G):
+        kv = [base + (i * 7919 + g) * 131 for i in range(q // 2)]
+        kv += O.ints_from_keys(O.splitmix_keys(0xC1 + g, q - len(kv)))
+        keys.append(torch.from_numpy(O.keys_from_ints(kv).view(np.int64).copy()).cuda())
+        srcs.append(torch.from_numpy((np.arange(q) * 13 % len(vals)).astype(np.int32)).cuda())
+    outs, _ = simulate_soa(cx, ids_dev, G, srcs, keys)
+    R = O.ring_build(ids)
+    P = O.Peers(R, O.fingers(R))
+    for g in range(G):
+        ow, hp, st = O.route(P, srcs[g].cpu().numpy().astype(np.uint32),
+                             keys[g].cpu().numpy().view(np.uint64).reshape(-1, 2))
+        assert (outs[g][0].cpu().numpy().view(np.uint32) == ow).all()
+        assert (outs[g][1].cpu().numpy() == hp).all()
+        assert (outs[g][2].cpu().numpy() == st).all()

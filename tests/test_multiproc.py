@@ -129,6 +129,40 @@ class OracleArcEngine:
                 out[i, 3] = o | ((hh | (1 << 8)) << 32)
         return torch.from_numpy(out)
 
+    # --- structure-of-arrays key-first protocol (ArcRouter.route_soa) ---
+    def arc_partition(self, world, src, keys):
+        import torch
+        import oracle as O
+        from chordx.arc import arc_of
+        k = keys.numpy().view(np.uint64).reshape(-1, 2)
+        own = O.successor(self.P.ring, k)
+        dest = np.array([arc_of(int(o), self.n, world) for o in own], dtype=np.int64)
+        perm = np.argsort(dest, kind="stable")
+        counts = [int((dest == d).sum()) for d in range(world)]
+        return (keys[torch.from_numpy(perm)].contiguous(), src[torch.from_numpy(perm)].contiguous(),
+                torch.from_numpy(perm.astype(np.int32)), counts)
+
+    def arc_route(self, src, keys):
+        import torch
+        import oracle as O
+        k = keys.numpy().view(np.uint64).reshape(-1, 2)
+        ow, hp, st = O.route(self.P, src.numpy().astype(np.uint32), k)
+        own = np.asarray(ow, dtype=np.uint64)
+        # every lookup sent here ends in this rank's arc (or fails at its source)
+        assert all(st[j] != 0 or self.lo <= int(own[j]) < self.hi for j in range(len(own)))
+        v = own | (np.asarray(hp, np.uint64) << 32) | (np.asarray(st, np.uint64) << 40)
+        return torch.from_numpy((v | np.uint64(1 << 63)).view(np.int64))
+
+    def arc_deliver(self, res, perm, owner, hops, status):
+        v = res.numpy().view(np.uint64)
+        idx = np.arange(len(v)) if perm is None else perm.numpy()
+        for j, i in enumerate(idx):
+            o = int(v[j]) & 0xFFFFFFFF
+            owner[int(i)] = o if o < (1 << 31) else o - (1 << 32)
+            hops[int(i)] = (int(v[j]) >> 32) & 0xFF
+            if status is not None:
+                status[int(i)] = (int(v[j]) >> 40) & 0xFF
+
     def arc_bucket(self, world, recs):
         import torch
         import oracle as O
@@ -153,7 +187,7 @@ class OracleArcEngine:
         return torch.from_numpy(r[order].copy()), counts
 
 
-def _arc_worker(rank, world, port, per_rank, out, key_first=True):
+def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="records"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import sys
@@ -176,20 +210,22 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True):
     status = torch.full((per_rank,), 7, dtype=torch.uint8)
     router = ArcRouter(OracleArcEngine(P, len(ring)), len(ring), rank, world)
     rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status,
-                          key_first=key_first)
+                          key_first=key_first, protocol=protocol)
     out[rank] = (owner.numpy().view(np.uint32).tolist(), hops.tolist(), status.tolist(), rounds,
                  router.records_sent)
     tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("key_first", [True, False])
+@pytest.mark.parametrize("key_first,protocol", [(True, "records"), (False, "records"),
+                                               (True, "soa")])
 @pytest.mark.parametrize("world", [2, 3])
-def test_arc_router_protocol_gloo(world, key_first):
+def test_arc_router_protocol_gloo(world, key_first, protocol):
     import oracle as O
     per_rank = 700
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out, key_first),
+    mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out, key_first,
+                                          protocol),
                        nprocs=world, join=True, start_method="spawn")
     ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
     P = O.Peers(ring, O.fingers(ring))
@@ -199,7 +235,8 @@ def test_arc_router_protocol_gloo(world, key_first):
         ow, hp, st = O.route(P, src, keys)
         assert out[r][0] == ow.tolist() and out[r][1] == hp.tolist()
         assert out[r][2] == st.tolist()
-        assert out[r][3] == 3           # walk -> result -> home, then drained
+        # records: walk -> result -> home, then drained; soa: there and back
+        assert out[r][3] == (3 if protocol == "records" else 2)
         assert out[r][4] > 0            # records crossed ranks
 
 
