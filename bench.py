@@ -176,13 +176,16 @@ def dry_run(args):
 
 def main_arc(args):
     """Arc-sharded layout (SURVEY 8e layout 2): ring IDs generated in shares
-    and all-gathered (RCCL), tree rows per arc, lookups exchanged as 32-B
-    records by all_to_all every round until none is in flight."""
+    and all-gathered (RCCL), route planes per arc, lookups sent to their key's
+    arc and answered in the key-first structure-of-arrays protocol
+    (ArcRouter.route_soa: 20 B out, 8 B back per lookup, pipelined pieces)."""
     from chordx.arc import ArcRouter
     world, rank, local = dist.env_rank()
+    local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks share a GPU
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
-    dist.init("nccl", dev)
+    backend = os.environ.get("CX_DIST_BACKEND", "nccl")
+    dist.init(backend, dev)
     N = 1 << args.peers_log2
     Q = 1 << args.keys_log2
     lo, hi = rank * N // world, (rank + 1) * N // world
@@ -191,13 +194,16 @@ def main_arc(args):
     assert N % world == 0
     chordx.fill_splitmix(share, SEED_RING, offset=lo)
     if world > 1:
-        ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
-        torch.distributed.all_gather_into_tensor(ids, share)
+        cd = torch.device("cpu") if backend == "gloo" else dev
+        ids = torch.empty((N, 2), dtype=torch.int64, device=cd)
+        torch.distributed.all_gather_into_tensor(ids, share.to(cd))
+        ids = ids.to(dev)
     else:
         ids = share
     ring = chordx.Ring(ids, device=local)
     del ids, share
-    router = ArcRouter(ring, ring.n, rank, world)
+    router = ArcRouter(ring, ring.n, rank, world,
+                       comm_device="cpu" if backend == "gloo" else None)
     torch.cuda.synchronize(dev)
     t_setup = time.perf_counter() - t0
     keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
@@ -223,6 +229,8 @@ def main_arc(args):
     bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
     sent = dist.sum_over_ranks(router.records_sent, world, dev)
     sum_hops = dist.sum_over_ranks(int(hops.to(torch.int64).sum().item()), world, dev)
+    succ = ring.successor(keys)  # exact successor (directory search) of every key
+    mismatch = dist.sum_over_ranks(int((succ != owner).sum().item()), world, dev)
     if rank == 0:
         total = world * Q * args.steps
         line = {
@@ -242,11 +250,13 @@ def main_arc(args):
             "config": {"workload": "C4 finger-routed lookups with hop counts, arc-sharded: "
                                    f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step",
                        "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
-                       "parallelism": f"arc-sharded tree rows x{world}, records by all_to_all"},
+                       "parallelism": f"arc-sharded route planes x{world}, key-first SoA "
+                                      "all_to_all (20 B out, 8 B back per lookup)"},
             "rounds_per_step": rounds,
             "records_exchanged_per_lookup": sent / (world * Q * args.steps),
             "mean_hops": sum_hops / (world * Q),
             "bad_status": bad,
+            "route_owner_equals_successor": mismatch == 0,
             "setup_s": t_setup,
         }
         print(json.dumps(line), flush=True)

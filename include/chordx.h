@@ -343,20 +343,20 @@ int cx_arc_bucket(const cx_ring *ring, int world, const cx_arc_rec *recs, size_t
 int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *src,
                       const cx_u128 *keys, size_t q, cx_arc_rec *send, uint64_t *counts);
 
-/* ---- key-first exchange, structure of arrays (the default multi-GPU path) --
+/* ---- key-first exchange, structure of arrays (the default arc protocol) -----
  * One batch = two all-to-all exchanges (ForwardRequest's GET_SUCC sent to the
  * key's arc, chord_peer.cpp:185-211, and its reply):
  *   1. cx_arc_partition on every rank: its lookups grouped by the rank of the
  *      key's arc -> send_keys / send_src (exchanged: 20 B per lookup), perm
- *      (kept: the lookup index of every send slot), counts[world] (host);
+ *      (kept: perm[i] = the send slot of lookup i), counts[world] (host);
  *   2. cx_arc_route on every rank over what it received (in receive order):
  *      res[j] = owner | hops << 32 | status << 40 | 1 << 63 for lookup j,
  *      walked from its source over the replicated top planes and the rank's
  *      own rows (a walk that needs a lower level is within 2^(128 - T) of its
  *      key: in the key's arc or its halo);
  *   3. res goes back with the splits swapped (8 B per lookup) and lands in
- *      send order; cx_arc_deliver scatters it to owner / hops / status
- *      through perm (perm == NULL: identity, the single-rank case).
+ *      send order; cx_arc_deliver writes owner / hops / status of lookup i
+ *      from res[perm[i]] (perm == NULL: identity, the single-rank case).
  * Owners, hops and statuses equal cx_route's on the replicated ring.  Device
  * buffers; perm, send_* sized q. */
 int cx_arc_partition(const cx_ring *ring, int world, const uint32_t *src, const cx_u128 *keys,

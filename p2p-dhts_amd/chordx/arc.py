@@ -69,6 +69,7 @@ class ArcRouter:
         # a single rank walks them in place
         self.key_first = world > 1
         self._mat_host = None  # pinned landing buffer of the count matrix
+        self.chunks = None     # route_soa pipeline depth (None: by batch size)
 
     def _exchange(self, send, counts):
         """Returns (received records, global number of records in flight)."""
@@ -81,7 +82,7 @@ class ArcRouter:
         if mat.is_cuda:
             # the splits must reach the host (all_to_all_single takes lists):
             # one async copy into a pinned buffer, then wait on that copy only
-            if self._mat_host is None:
+            if self._mat_host is None or self._mat_host.shape != mat.shape:
                 self._mat_host = torch.empty((self.world, self.world), dtype=torch.int64,
                                              pin_memory=True)
             self._mat_host.copy_(mat, non_blocking=True)
@@ -99,45 +100,75 @@ class ArcRouter:
                                 input_split_sizes=list(counts), group=self.group)
         return (recv.to(send.device) if recv.device != send.device else recv), inflight
 
-    def _splits(self, counts, dev):
-        """Receive splits of this rank (column of the all-gathered G x G count
-        matrix), through one pinned async copy."""
-        mine = torch.tensor(counts, dtype=torch.int64, device=dev)
-        mat = torch.empty((self.world, self.world), dtype=torch.int64, device=dev)
-        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
-        if mat.is_cuda:
-            if self._mat_host is None:
-                self._mat_host = torch.empty((self.world, self.world), dtype=torch.int64,
-                                             pin_memory=True)
-            self._mat_host.copy_(mat, non_blocking=True)
-            torch.cuda.current_stream(mat.device).synchronize()
-            mat = self._mat_host
-        return [int(x) for x in mat[:, self.rank]]
-
     def _a2a(self, t, out_splits, in_splits, dev):
+        """Asynchronous all_to_all_single: (output, work)."""
         s = t.to(dev) if t.device != torch.device(dev) else t
         out = torch.empty((sum(out_splits),) + tuple(s.shape[1:]), dtype=s.dtype, device=dev)
-        tdist.all_to_all_single(out, s.contiguous(), output_split_sizes=out_splits,
-                                input_split_sizes=in_splits, group=self.group)
-        return out.to(t.device) if out.device != t.device else out
+        work = tdist.all_to_all_single(out, s.contiguous(), output_split_sizes=out_splits,
+                                       input_split_sizes=in_splits, group=self.group,
+                                       async_op=True)
+        return out, work
 
-    def route_soa(self, src, keys, owner, hops, status=None) -> int:
+    @staticmethod
+    def _land(t, work, like):
+        work.wait()  # the current stream waits for the collective
+        return t.to(like.device) if t.device != like.device else t
+
+    def route_soa(self, src, keys, owner, hops, status=None, chunks=None) -> int:
         """Key-first routing in structure-of-arrays form (module docstring);
-        returns the number of exchange rounds (1 on a single rank, else 2)."""
+        returns the number of exchange rounds (1 on a single rank, else 2).
+
+        The batch is cut into `chunks` pieces (default: one per 2^22 lookups,
+        at most 4), partitioned up front; one all_gather carries every
+        piece's counts.  Piece c + 1's lookups travel while piece c is walked,
+        and piece c's answers travel back while piece c + 1 is walked (the
+        collectives run on RCCL's stream, the walks on the current stream)."""
         eng = self.engine
         if self.world == 1:
             eng.arc_deliver(eng.arc_route(src, keys), None, owner, hops, status)
             self.rounds = 1
             return 1
-        skeys, ssrc, perm, counts = eng.arc_partition(self.world, src, keys)
-        dev = self.comm_device if self.comm_device is not None else skeys.device
-        recv = self._splits(counts, dev)
-        rkeys = self._a2a(skeys, recv, counts, dev)
-        rsrc = self._a2a(ssrc, recv, counts, dev)
-        res = eng.arc_route(rsrc, rkeys)
-        back = self._a2a(res, counts, recv, dev)
-        eng.arc_deliver(back, perm, owner, hops, status)
-        self.records_sent += int(sum(counts))
+        q = int(keys.shape[0])
+        k = chunks if chunks is not None else self.chunks
+        if k is None:
+            k = max(1, min(4, q >> 22))
+        k = max(1, min(int(k), max(q, 1)))
+        cut = [c * q // k for c in range(k + 1)]
+        parts = [eng.arc_partition(self.world, src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]])
+                 for c in range(k)]
+        dev = self.comm_device if self.comm_device is not None else parts[0][0].device
+        G = self.world
+        mine = torch.tensor([x for p in parts for x in p[3]], dtype=torch.int64, device=dev)
+        mat = torch.empty((G, k * G), dtype=torch.int64, device=dev)
+        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
+        if mat.is_cuda:
+            if self._mat_host is None or self._mat_host.shape != mat.shape:
+                self._mat_host = torch.empty(mat.shape, dtype=torch.int64, pin_memory=True)
+            self._mat_host.copy_(mat, non_blocking=True)
+            torch.cuda.current_stream(mat.device).synchronize()
+            mat = self._mat_host
+        recv = [[int(mat[r, c * G + self.rank]) for r in range(G)] for c in range(k)]
+
+        def send(c):
+            sk, ss, _, cnt = parts[c]
+            return self._a2a(sk, recv[c], cnt, dev), self._a2a(ss, recv[c], cnt, dev)
+
+        inflight = send(0)
+        backs = []
+        for c in range(k):
+            (rk, wk), (rs, ws) = inflight
+            rk = self._land(rk, wk, parts[c][0])
+            rs = self._land(rs, ws, parts[c][1])
+            if c + 1 < k:
+                inflight = send(c + 1)
+            res = eng.arc_route(rs, rk)
+            backs.append(self._a2a(res, parts[c][3], recv[c], dev))
+        for c in range(k):
+            back = self._land(backs[c][0], backs[c][1], parts[c][2])
+            sl = slice(cut[c], cut[c + 1])
+            eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
+                            status[sl] if status is not None else None)
+            self.records_sent += int(sum(parts[c][3]))
         self.rounds = 2
         return 2
 

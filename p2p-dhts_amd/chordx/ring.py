@@ -454,7 +454,7 @@ class Ring:
     def arc_partition(self, world: int, src, keys):
         """(send_keys, send_src, perm, counts): this rank's lookups grouped by
         the rank of their key's arc (cx_arc_partition).  send_keys / send_src
-        are exchanged; perm (send slot -> lookup index) stays here."""
+        are exchanged; perm (lookup index -> send slot) stays here."""
         keys = self._prep_keys(keys)
         src = self._prep_u32(src, "src", keys.shape[0])
         if not (_is_dev(keys) and _is_dev(src)):
@@ -487,8 +487,8 @@ class Ring:
         return res
 
     def arc_deliver(self, res, perm, owner, hops, status=None):
-        """Scatter returned results (send order) to owner/hops/status through
-        perm (None: identity) (cx_arc_deliver)."""
+        """owner/hops/status of lookup i from the returned results (send
+        order) at perm[i] (None: identity) (cx_arc_deliver)."""
         q = res.shape[0]
         if not (_is_dev(res) and res.element_size() == 8 and res.is_contiguous()):
             raise TypeError("res must be a contiguous 8-byte device tensor")

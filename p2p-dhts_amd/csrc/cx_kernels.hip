@@ -3238,14 +3238,14 @@ __global__ __launch_bounds__(256) void k_arc_scatter(ArcIn<SEED> in, size_t q,
 
 // Key-first partition, structure of arrays: this rank's lookups grouped by the
 // rank of their key's arc, as the exchange sends them -- keys (16 B), sources
-// (4 B) and, kept at the origin, the lookup index of every send slot (perm).
-// Results come back in send order (the arc rank answers its receive buffer in
-// order and the return exchange swaps the splits), so no record carries an
-// origin or an index across xGMI.
+// (4 B) -- and, kept at the origin, the send slot of every lookup (slot[i],
+// written in lookup order: coalesced).  Results come back in send order (the
+// arc rank answers its receive buffer in order and the return exchange swaps
+// the splits), so no record carries an origin or an index across xGMI.
 __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t q,
                                                          const ArcBound *bounds, int nb, int G,
                                                          uint32_t *cursor, cell128 *skeys,
-                                                         uint32_t *ssrc, uint32_t *perm) {
+                                                         uint32_t *ssrc, uint32_t *slot_of) {
     __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
@@ -3277,19 +3277,20 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
                 const uint32_t o = basep[d[k]] + slot[k];
                 skeys[o] = cell128{r[k].w0, r[k].w1};
                 ssrc[o] = r[k].cur;
-                perm[o] = (uint32_t)(r[k].qid & ARC_INDEX_MASK);
+                slot_of[r[k].qid & ARC_INDEX_MASK] = o;
             }
         __syncthreads();
     }
 }
 
-// Results back at the origin: res[j] answers the lookup in send slot j.
-__global__ void k_arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q,
+// Results back at the origin: res[j] answers the lookup in send slot j; lookup
+// i reads res[slot_of[i]] (an 8-B gather) and its outputs are written in
+// lookup order (coalesced, no scattered byte stores).
+__global__ void k_arc_deliver(const uint64_t *res, const uint32_t *slot_of, size_t q,
                               uint32_t *owner, uint8_t *hops, uint8_t *status) {
-    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < q;
-         j += (size_t)gridDim.x * blockDim.x) {
-        const uint64_t v = res[j];
-        const size_t i = perm ? perm[j] : j;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t v = res[slot_of ? slot_of[i] : i];
         owner[i] = (uint32_t)v;
         hops[i] = (uint8_t)(v >> 32);
         if (status) status[i] = (uint8_t)(v >> 40);

@@ -137,10 +137,13 @@ class OracleArcEngine:
         k = keys.numpy().view(np.uint64).reshape(-1, 2)
         own = O.successor(self.P.ring, k)
         dest = np.array([arc_of(int(o), self.n, world) for o in own], dtype=np.int64)
-        perm = np.argsort(dest, kind="stable")
+        order = np.argsort(dest, kind="stable")  # send slot -> lookup
+        slot = np.empty_like(order)
+        slot[order] = np.arange(len(order))       # lookup -> send slot
         counts = [int((dest == d).sum()) for d in range(world)]
-        return (keys[torch.from_numpy(perm)].contiguous(), src[torch.from_numpy(perm)].contiguous(),
-                torch.from_numpy(perm.astype(np.int32)), counts)
+        return (keys[torch.from_numpy(order)].contiguous(),
+                src[torch.from_numpy(order)].contiguous(),
+                torch.from_numpy(slot.astype(np.int32)), counts)
 
     def arc_route(self, src, keys):
         import torch
@@ -155,13 +158,14 @@ class OracleArcEngine:
 
     def arc_deliver(self, res, perm, owner, hops, status):
         v = res.numpy().view(np.uint64)
-        idx = np.arange(len(v)) if perm is None else perm.numpy()
-        for j, i in enumerate(idx):
-            o = int(v[j]) & 0xFFFFFFFF
-            owner[int(i)] = o if o < (1 << 31) else o - (1 << 32)
-            hops[int(i)] = (int(v[j]) >> 32) & 0xFF
+        slot = np.arange(len(v)) if perm is None else perm.numpy()
+        for i, j in enumerate(slot):
+            w = int(v[int(j)])
+            o = w & 0xFFFFFFFF
+            owner[i] = o if o < (1 << 31) else o - (1 << 32)
+            hops[i] = (w >> 32) & 0xFF
             if status is not None:
-                status[int(i)] = (int(v[j]) >> 40) & 0xFF
+                status[i] = (w >> 40) & 0xFF
 
     def arc_bucket(self, world, recs):
         import torch
@@ -187,7 +191,8 @@ class OracleArcEngine:
         return torch.from_numpy(r[order].copy()), counts
 
 
-def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="records"):
+def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="records",
+                chunks=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import sys
@@ -209,6 +214,7 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="reco
     hops = torch.zeros(per_rank, dtype=torch.uint8)
     status = torch.full((per_rank,), 7, dtype=torch.uint8)
     router = ArcRouter(OracleArcEngine(P, len(ring)), len(ring), rank, world)
+    router.chunks = chunks
     rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status,
                           key_first=key_first, protocol=protocol)
     out[rank] = (owner.numpy().view(np.uint32).tolist(), hops.tolist(), status.tolist(), rounds,
@@ -216,16 +222,16 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="reco
     tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("key_first,protocol", [(True, "records"), (False, "records"),
-                                               (True, "soa")])
+@pytest.mark.parametrize("key_first,protocol,chunks", [
+    (True, "records", None), (False, "records", None), (True, "soa", None), (True, "soa", 3)])
 @pytest.mark.parametrize("world", [2, 3])
-def test_arc_router_protocol_gloo(world, key_first, protocol):
+def test_arc_router_protocol_gloo(world, key_first, protocol, chunks):
     import oracle as O
     per_rank = 700
     mgr = mp.Manager()
     out = mgr.dict()
     mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out, key_first,
-                                          protocol),
+                                          protocol, chunks),
                        nprocs=world, join=True, start_method="spawn")
     ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
     P = O.Peers(ring, O.fingers(ring))
