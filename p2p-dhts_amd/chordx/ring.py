@@ -315,6 +315,13 @@ class Ring:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))
 
+    def set_misplaced_variant(self, v: int):
+        """Internal A/B switch for cx_misplaced on a ring from cx_churn: 0 = two
+        searches + the old_to_new window per key, 1 = churn directory (default)."""
+        f = L.lib().cxi_set_misplaced_variant
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.check(f(self._h, v))
+
     # ---- a7-a9 -----------------------------------------------------------
     def route(self, src, keys, out=None):
         """GetSuccessor(key) issued at peer src: (owner, hops, status)."""

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <initializer_list>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -259,6 +260,16 @@ struct cx_ring {
                                    // 2: wave-cooperative 16-ary tree (successor / predecessor)
     cell128 *d_stree = nullptr;    // levels 1.. of the 16-ary tree (variant 2, lazy)
     int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
+    uint64_t serial = 0;           // process-unique handle number
+    // cx_churn result: the parent's serial and the old_to_new it returned; the
+    // churn directory (misplaced scan) is built from them on first use
+    uint64_t churn_parent = 0;
+    uint32_t *d_o2n_canon = nullptr;
+    size_t o2n_canon_n = 0;
+    uint4 *d_cdir = nullptr;       // [2^cdir_kb][2] (ChurnDir)
+    int cdir_kb = 0;
+    size_t cdir_bytes = 0;
+    int misplaced_variant = 1;     // 0: two searches + old_to_new window, 1: churn directory
 
     EytView eyt() const {
         EytView v;
@@ -362,6 +373,8 @@ int alloc_ring(int device, cx_ring **out) {
         return fail(CX_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
     r->stream = r->own_stream;
+    static std::atomic<uint64_t> next_serial{1};
+    r->serial = next_serial++;
     e = hipMalloc(&r->d_scratch, 1024);
     if (e != hipSuccess) {
         (void)hipStreamDestroy(r->own_stream);
@@ -396,6 +409,8 @@ void free_ring(cx_ring *r) {
     table_free(r->device, r->d_arc_tree, r->arc_bytes);
     (void)hipFree(r->d_arc_bounds);
     (void)hipFree(r->d_stats);
+    (void)hipFree(r->d_o2n_canon);
+    table_free(r->device, r->d_cdir, r->cdir_bytes);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
     delete r;
 }
@@ -1062,6 +1077,7 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
             if (e) return e;
             r->search_variant = old_ring->search_variant;
             r->churn_variant = old_ring->churn_variant;
+            r->misplaced_variant = old_ring->misplaced_variant;
             if ((e = build_search(r, s))) return e;
             if (old_to_new) {
                 const hipMemcpyKind kind =
@@ -1069,6 +1085,10 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
                 CX_HIP(hipMemcpyAsync(old_to_new, o2n.p, n_old * sizeof(uint32_t), kind, s));
             }
             CX_HIP(hipStreamSynchronize(s));
+            r->churn_parent = old_ring->serial;
+            r->o2n_canon_n = n_old;
+            r->d_o2n_canon = o2n.as<uint32_t>();
+            o2n.release();
             return CX_OK;
         }
         CX_HIP(gone.alloc(n_old));
@@ -1110,6 +1130,7 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         ringbuf.release();
         r->search_variant = old_ring->search_variant;
         r->churn_variant = old_ring->churn_variant;
+        r->misplaced_variant = old_ring->misplaced_variant;
         {
             int e2 = build_search(r, s);
             if (e2) return e2;
@@ -1120,6 +1141,10 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
             CX_HIP(hipMemcpyAsync(old_to_new, o2n.p, n_old * sizeof(uint32_t), kind, s));
         }
         CX_HIP(hipStreamSynchronize(s));
+        r->churn_parent = old_ring->serial;
+        r->o2n_canon_n = n_old;
+        r->d_o2n_canon = o2n.as<uint32_t>();
+        o2n.release();
         return CX_OK;
     }();
     if (rc) {
@@ -1151,8 +1176,49 @@ int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_
     if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
     if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
     if ((rc = stage_out(target, q * (size_t)n, memkind, tt, &dt))) return rc;
+    // churn directory: the new ring came from cx_churn(old_ring) and the
+    // caller's mapping equals the one it returned (checked on the device)
+    cxk::ChurnDirArgs cda{};
+    const bool cd_ok = q && new_ring->misplaced_variant == 1 &&
+                       new_ring->churn_parent == old_ring->serial && new_ring->d_o2n_canon &&
+                       new_ring->o2n_canon_n == old_ring->n && old_ring->n >= 32 &&
+                       new_ring->n >= 32 && old_ring->d_dir && new_ring->d_dir &&
+                       old_ring->search_variant != 0 && new_ring->search_variant != 0;
+    if (cd_ok) {
+        cx_ring *nr = const_cast<cx_ring *>(new_ring);
+        if (!nr->d_cdir) {
+            const size_t Mmax = old_ring->n + new_ring->n;
+            int kb = 1;
+            while (((size_t)1 << kb) < Mmax) ++kb;  // >= 2^kb / 2 >= the merged size
+            const size_t bytes = ((size_t)1 << kb) * 32;
+            DBuf ws, lo, sw;
+            CX_HIP(ws.alloc_pooled(cxk::churn_dir_workspace_bytes(old_ring->n, new_ring->n)));
+            CX_HIP(lo.alloc((((size_t)1 << kb) + 1) * sizeof(uint32_t)));
+            CX_HIP(sw.alloc(cxk::scan_workspace_words(Mmax + 1) * sizeof(uint32_t)));
+            void *cdp = nullptr;
+            CX_CHECK(table_alloc(&cdp, bytes) == hipSuccess, CX_E_NOMEM,
+                     "hipMalloc of the churn directory failed");
+            uint32_t M = 0;
+            hipError_t e = cxk::churn_dir_build(old_ring->sv(), new_ring->sv(), nr->d_o2n_canon,
+                                                kb, ws.p, lo.as<uint32_t>(),
+                                                static_cast<uint4 *>(cdp), sw.as<uint32_t>(), &M,
+                                                s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) {
+                table_free(nr->device, cdp, bytes);
+                return fail(CX_E_HIP, std::string("churn directory: ") + hipGetErrorString(e));
+            }
+            nr->d_cdir = static_cast<uint4 *>(cdp);
+            nr->cdir_kb = kb;
+            nr->cdir_bytes = bytes;
+        }
+        uint32_t *ok = new_ring->d_scratch + 250;
+        CX_HIP(cxk::churn_dir_same(d_o2n, new_ring->d_o2n_canon, old_ring->n, ok, s));
+        cda = cxk::ChurnDirArgs{new_ring->d_cdir, new_ring->cdir_kb, ok};
+    }
     CX_HIP(cxk::misplaced_churn(old_ring->sv(), new_ring->sv(), d_o2n,
-                                reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, dm, dt, s));
+                                reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, dm, dt,
+                                cd_ok ? &cda : nullptr, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(new_lists, dl, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
         CX_HIP(hipMemcpyAsync(count, dc, q, hipMemcpyDeviceToHost, s));
@@ -1899,6 +1965,17 @@ int cxi_set_search_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
     ring->search_variant = variant;
+    return CX_OK;
+}
+
+// Misplaced scan after cx_churn: 0 = two directory searches + the old_to_new
+// window per key, 1 = churn directory (default; one 32-B gather per key,
+// built on first use from the rings and cx_churn's mapping).  Set on the NEW
+// ring (rings from cx_churn inherit the parent's setting).
+int cxi_set_misplaced_variant(cx_ring *ring, int variant) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    ring->misplaced_variant = variant;
     return CX_OK;
 }
 

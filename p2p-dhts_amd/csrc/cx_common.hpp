@@ -127,6 +127,26 @@ struct SearchView {
     const cell128 *ring;
 };
 
+// Number of ring IDs < x (the unwrapped successor index, n if x is past the
+// last ID).
+__device__ __forceinline__ uint32_t dir_lower_bound(const SearchView &sv, u128 x) {
+    const int k = sv.k;
+    const uint4 e = sv.dir[(size_t)(uint64_t)(x >> (128 - k))];
+    const uint32_t lo = e.x, hi = e.y;
+    if (lo == hi) return hi;
+    const uint64_t frac = ((uint64_t)e.w << 32) | e.z;
+    const uint64_t xf = (uint64_t)(x >> (64 - k));  // ID bits [64-k, 128-k)
+    if (xf < frac) return lo;
+    if (xf > frac && hi - lo == 1) return hi;
+    uint32_t a = (xf > frac) ? lo + 1 : lo, z = hi;
+    while (a < z) {
+        const uint32_t m = a + (z - a) / 2;
+        if (ld128(sv.ring + m) < x) a = m + 1;
+        else z = m;
+    }
+    return a;
+}
+
 __device__ __forceinline__ uint32_t dir_successor(const SearchView &sv, u128 x) {
     const uint32_t n = sv.ev.n;
     const int k = sv.k;

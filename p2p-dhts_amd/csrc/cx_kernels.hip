@@ -3575,17 +3575,109 @@ hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Churn directory (misplaced scan after cx_churn).  The merged ring = old ring
+// U joining peers in ID order; merged entry m is tagged 1 (departed old peer),
+// 2 (joiner) or 3 (survivor).  For a key whose first merged entry at or after
+// it is m: the old successor is so(m) = #old entries before m, the new one
+// sn(m) = #new entries before m, and the old n-window's holders follow from
+// the tags after m -- a survivor at old rank j holds new rank r = #new entries
+// from m before it, a departed one is CX_NONE (dhash_peer.cpp:322-328 on the
+// mapping cx_churn returns).  Bucket b (top kb bits, load factor <= 1/2) is
+// one 32-B entry: {hint0 | so_b | sn_b}, {tags of m_b .. m_b + 31 | hint1 |
+// cnt} with m_b = the bucket's first merged entry, hint = ID bits
+// [64 - kb, 128 - kb) (hint1's low two bits hold cnt = entries in the bucket,
+// capped at 3).  One 32-B gather replaces two directory searches and the
+// 64-B window of old_to_new entries; keys it cannot settle (a third entry in
+// the bucket, an equal hint, a window with too many joiners) take the
+// two-search path.
+// ---------------------------------------------------------------------------
+struct ChurnDir {
+    const uint4 *cd;          // [2^kb][2]
+    int kb;
+    const cell128 *ring_old, *ring_new;
+    const uint32_t *ok;       // device flag: old_to_new equals cx_churn's mapping
+};
+
+// 1 = settled (so, sn, has, mis set), 0 = take the search path.
+__device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, uint32_t n_old,
+                                         uint32_t n_new, int no, int nn, uint32_t &so,
+                                         uint32_t &sn, uint32_t &has, uint32_t &mis) {
+    const size_t b = (size_t)(uint64_t)(key >> (128 - c.kb));
+    const uint4 A = c.cd[2 * b], B = c.cd[2 * b + 1];
+    const uint64_t xf = (uint64_t)(key >> (64 - c.kb));
+    const uint64_t h0 = ((uint64_t)A.y << 32) | A.x;
+    uint64_t tg = ((uint64_t)B.y << 32) | B.x;
+    const uint64_t h1c = ((uint64_t)B.w << 32) | B.z;
+    const int cnt = (int)(h1c & 3);
+    uint32_t o = A.z, w = A.w;  // so / sn at the bucket's first merged entry
+    int t = 0;
+    if (cnt >= 1) {
+        if (xf == h0) {  // exact compare with the first entry's ID
+            const u128 id = (tg & 1) ? ld128(c.ring_old + o) : ld128(c.ring_new + w);
+            t = key > id;
+        } else {
+            t = xf > h0;
+        }
+        if (t) {
+            o += (uint32_t)(tg & 1);
+            w += (uint32_t)((tg >> 1) & 1);
+            if (o >= n_old) o -= n_old;
+            if (w >= n_new) w -= n_new;
+            tg >>= 2;
+            if (cnt >= 2) {
+                int t2;
+                if ((xf >> 2) == (h1c >> 2)) {
+                    const u128 id = (tg & 1) ? ld128(c.ring_old + o) : ld128(c.ring_new + w);
+                    t2 = key > id;
+                } else {
+                    t2 = (xf >> 2) > (h1c >> 2);
+                }
+                if (t2) {
+                    if (cnt == 3) return 0;  // a third entry may precede the key
+                    o += (uint32_t)(tg & 1);
+                    w += (uint32_t)((tg >> 1) & 1);
+                    if (o >= n_old) o -= n_old;
+                    if (w >= n_new) w -= n_new;
+                    tg >>= 2;
+                }
+            }
+        }
+    }
+    so = o;
+    sn = w;
+    uint32_t j = 0, r = 0, hs = 0, ms = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t g = (uint32_t)(tg >> (2 * k)) & 3u;
+        if ((int)j < no) {
+            if (g == 3u) {
+                if ((int)r < nn) hs |= 1u << r;
+                else ms |= 1u << j;
+            }
+            j += g & 1u;
+            r += g >> 1;
+        }
+    }
+    if ((int)j < no) return 0;  // window ran out of tags (shifted-in zeros)
+    has = hs;
+    mis = ms;
+    return 1;
+}
+
 // Misplaced scan core.  Holder ranks j in order; `has` = mask of new-list ranks
 // already holding the key; membership of a holder in the new window is
 // (holder - s_new) mod n_new < nn.  Rows (new list, targets) are staged in LDS
-// per block of 256 consecutive keys and written coalesced.
-template <bool CHURN, bool DIR>
+// per block of 256 consecutive keys and written coalesced.  CD: the churn
+// directory settles most keys in one gather (cd_lookup) when *cd.ok.
+template <bool CHURN, bool DIR, bool CD = false>
 __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, SearchView sv_old,
                                                          const uint32_t *old_to_new,
                                                          const uint32_t *holders, int nh,
                                                          const cell128 *keys, size_t q, int nlist,
                                                          uint32_t *new_lists, uint8_t *count,
-                                                         uint16_t *mask, uint8_t *target) {
+                                                         uint16_t *mask, uint8_t *target,
+                                                         ChurnDir cd) {
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
     __shared__ __attribute__((aligned(16))) uint32_t stage_l[ROW_BLOCK * CX_MAX_NSUCC];
@@ -3599,20 +3691,80 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
     const int nslots = CHURN ? nlist : nh;
     const uint32_t full = (nn >= 32) ? 0xFFFFFFFFu : ((1u << nn) - 1u);
     const bool o2n_al = CHURN && ((uintptr_t)old_to_new & 15) == 0;
+    const bool use_cd = CD && *cd.ok;  // wave-uniform
     static_assert(CX_MAX_NSUCC <= 17, "five 16-B o2n loads cover 17 entries");
     for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q;
          base += (size_t)gridDim.x * ROW_BLOCK) {
         const size_t i = base + threadIdx.x;
         const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
         if (i < q) {
-            // Both searches are issued together: deriving the new successor from
-            // a verified old->new mapping saves a search for ~98 % of keys but
-            // serialises it behind the old one for the rest, and with 64 lanes a
-            // wave almost always holds one of those (measured 7 % slower).
             const u128 key = ld128(keys + i);
-            const uint32_t sn = Searcher<DIR>::find(sv_new, lds_new, key);
-            uint32_t so = 0;
-            if (CHURN) so = Searcher<DIR>::find(sv_old, lds_old, key);
+            uint32_t sn = 0, so = 0, has = 0, m = 0;
+            const bool settled =
+                use_cd && cd_lookup(cd, key, n_old, n_new, no, nn, so, sn, has, m);
+            if (!settled) {
+                // Both searches are issued together: deriving the new successor
+                // from a verified old->new mapping saves a search for ~98 % of
+                // keys but serialises it behind the old one for the rest, and
+                // with 64 lanes a wave almost always holds one of those
+                // (measured 7 % slower).
+                sn = Searcher<DIR>::find(sv_new, lds_new, key);
+                if (CHURN) so = Searcher<DIR>::find(sv_old, lds_old, key);
+                // holders: old n-window mapped to the new ring, or the caller's list
+                uint32_t hv[CX_MAX_NSUCC];
+                // the old window's o2n entries are contiguous: five aligned 16-B
+                // loads cover [so, so + no) for no <= 17 (one request each instead
+                // of one dword request per entry); the window may not wrap or pass
+                // the end
+                const uint32_t ob = so & ~3u;
+                const bool wide = CHURN && o2n_al && (size_t)ob + 20 <= n_old;
+                if (wide) {
+                    const uint4 *w4 = reinterpret_cast<const uint4 *>(old_to_new + ob);
+                    uint32_t w[20];
+#pragma unroll
+                    for (int t = 0; t < 5; ++t) {
+                        const uint4 x = w4[t];
+                        w[4 * t] = x.x;
+                        w[4 * t + 1] = x.y;
+                        w[4 * t + 2] = x.z;
+                        w[4 * t + 3] = x.w;
+                    }
+                    const uint32_t sh = so & 3u;
+#pragma unroll
+                    for (int j = 0; j < CX_MAX_NSUCC; ++j)
+                        hv[j] = j >= no ? CX_NONE
+                                        : (sh == 0 ? w[j] : sh == 1 ? w[j + 1] : sh == 2 ? w[j + 2]
+                                                                               : w[j + 3]);
+                }
+#pragma unroll
+                for (int j = 0; j < CX_MAX_NSUCC; ++j) {
+                    if (wide) break;
+                    uint32_t hj = CX_NONE;
+                    if (j < no) {
+                        if (CHURN) {
+                            uint32_t o = so + (uint32_t)j;
+                            if (o >= n_old) o -= n_old;
+                            hj = old_to_new[o];
+                        } else {
+                            hj = holders[i * (size_t)nh + j];
+                        }
+                    }
+                    hv[j] = hj;
+                }
+                // pass 1: which new-list ranks already hold the key, and which
+                // holders are misplaced: any value but CX_NONE is a holder; one
+                // that is not a ring index is never in the new list (oracle
+                // misplaced_one)
+#pragma unroll
+                for (int j = 0; j < CX_MAX_NSUCC; ++j) {
+                    const uint32_t hj = hv[j];
+                    if (hj == CX_NONE) continue;
+                    const uint32_t r = hj >= n_new ? 0xFFFFFFFFu
+                                                   : (hj >= sn ? hj - sn : hj + n_new - sn);
+                    if (r < (uint32_t)nn) has |= 1u << r;
+                    else if (j < nslots) m |= 1u << j;
+                }
+            }
             uint32_t *l = stage_l + threadIdx.x * nlist;
             for (int j = 0; j < nlist; ++j) {
                 uint32_t v = sn + (uint32_t)j;
@@ -3620,76 +3772,18 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                 l[j] = j < nn ? v : CX_NONE;
             }
             count[i] = (uint8_t)nn;
-            // holders: old n-window mapped to the new ring, or the caller's list
-            uint32_t hv[CX_MAX_NSUCC];
-            // the old window's o2n entries are contiguous: five aligned 16-B loads
-            // cover [so, so + no) for no <= 17 (one request each instead of one
-            // dword request per entry); the window may not wrap or pass the end
-            const uint32_t ob = so & ~3u;
-            const bool wide = CHURN && o2n_al && (size_t)ob + 20 <= n_old;
-            if (wide) {
-                const uint4 *w4 = reinterpret_cast<const uint4 *>(old_to_new + ob);
-                uint32_t w[20];
-#pragma unroll
-                for (int t = 0; t < 5; ++t) {
-                    const uint4 x = w4[t];
-                    w[4 * t] = x.x;
-                    w[4 * t + 1] = x.y;
-                    w[4 * t + 2] = x.z;
-                    w[4 * t + 3] = x.w;
-                }
-                const uint32_t sh = so & 3u;
-#pragma unroll
-                for (int j = 0; j < CX_MAX_NSUCC; ++j)
-                    hv[j] = j >= no ? CX_NONE
-                                    : (sh == 0 ? w[j] : sh == 1 ? w[j + 1] : sh == 2 ? w[j + 2]
-                                                                           : w[j + 3]);
-            }
-#pragma unroll
-            for (int j = 0; j < CX_MAX_NSUCC; ++j) {
-                if (wide) break;
-                uint32_t hj = CX_NONE;
-                if (j < no) {
-                    if (CHURN) {
-                        uint32_t o = so + (uint32_t)j;
-                        if (o >= n_old) o -= n_old;
-                        hj = old_to_new[o];
-                    } else {
-                        hj = holders[i * (size_t)nh + j];
-                    }
-                }
-                hv[j] = hj;
-            }
-            // pass 1: which new-list ranks already hold the key
-            uint32_t has = 0;
-#pragma unroll
-            for (int j = 0; j < CX_MAX_NSUCC; ++j) {
-                const uint32_t hj = hv[j];
-                if (hj >= n_new) continue;  // CX_NONE (empty / departed) or invalid
-                const uint32_t r = hj >= sn ? hj - sn : hj + n_new - sn;
-                if (r < (uint32_t)nn) has |= 1u << r;
-            }
             // pass 2: misplaced holders in rank order take the first lacking rank
-            uint32_t m = 0;
             uint8_t *tg = stage_t + threadIdx.x * nslots;
 #pragma unroll
             for (int j = 0; j < CX_MAX_NSUCC; ++j) {
                 if (j >= nslots) break;
                 uint8_t t = 0xFF;
-                const uint32_t hj = hv[j];
-                // any value but CX_NONE is a holder; one that is not a ring index
-                // is never in the new list (oracle misplaced_one)
-                if (hj != CX_NONE) {
-                    const uint32_t r = hj >= n_new ? 0xFFFFFFFFu
-                                                   : (hj >= sn ? hj - sn : hj + n_new - sn);
-                    if (r >= (uint32_t)nn) {
-                        m |= 1u << j;
-                        const uint32_t free_ranks = ~has & full;
-                        if (free_ranks) {
-                            const int rr = __builtin_ctz(free_ranks);
-                            has |= 1u << rr;
-                            t = (uint8_t)rr;
-                        }
+                if ((m >> j) & 1u) {
+                    const uint32_t free_ranks = ~has & full;
+                    if (free_ranks) {
+                        const int rr = __builtin_ctz(free_ranks);
+                        has |= 1u << rr;
+                        t = (uint8_t)rr;
                     }
                 }
                 tg[j] = t;
@@ -3706,14 +3800,166 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
 hipError_t misplaced_churn(const SearchView &sv_old, const SearchView &sv_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
-                           hipStream_t s) {
+                           const ChurnDirArgs *cda, hipStream_t s) {
     if (q == 0) return hipSuccess;
-    if (sv_new.dir && sv_old.dir)
+    ChurnDir cd = {};
+    if (cda) cd = ChurnDir{cda->cd, cda->kb, sv_old.ring, sv_new.ring, cda->ok};
+    if (cda && sv_new.dir && sv_old.dir)
+        k_misplaced<true, true, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd);
+    else if (sv_new.dir && sv_old.dir)
         k_misplaced<true, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target);
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd);
     else
         k_misplaced<true, false><<<cx_grid(q, ROW_BLOCK, 256), ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target);
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd);
+    return hipGetLastError();
+}
+
+// ---- churn directory build (see ChurnDir) ----------------------------------
+// dflag[o] = old peer o departed; jflag[p] = new peer p joined (no old peer
+// maps to it).  Both arrays carry a trailing 0 so their exclusive scans end in
+// the totals.
+__global__ void k_cd_flags(const uint32_t *o2n, uint32_t n_old, uint32_t n_new, uint32_t *dflag,
+                           uint32_t *jflag) {
+    for (size_t o = blockIdx.x * (size_t)blockDim.x + threadIdx.x; o < n_old;
+         o += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t u = o2n[o];
+        dflag[o] = u == CX_NONE;
+        if (u < n_new) jflag[u] = 0;
+    }
+}
+
+// Merged entry of old peer o: survivor u = o2n[o] sits at u + (departed
+// before o); a departed one at (#new IDs below it) + (departed before o).
+__global__ void k_cd_place_old(SearchView sv_new, const cell128 *ring_old, const uint32_t *o2n,
+                               const uint32_t *dex, uint32_t n_old, uint32_t n_new,
+                               cell128 *mid, uint32_t *mso, uint32_t *msn, uint8_t *mtag) {
+    for (size_t o = blockIdx.x * (size_t)blockDim.x + threadIdx.x; o < n_old;
+         o += (size_t)gridDim.x * blockDim.x) {
+        const u128 id = ld128(ring_old + o);
+        const uint32_t u = o2n[o];
+        uint32_t c = u, tag = 3;
+        if (u == CX_NONE) {
+            c = dir_lower_bound(sv_new, id);
+            tag = 1;
+        }
+        const size_t m = (size_t)c + dex[o];
+        st128(mid + m, id);
+        mso[m] = (uint32_t)o;
+        msn[m] = c == n_new ? 0u : c;
+        mtag[m] = (uint8_t)tag;
+    }
+}
+
+// Merged entry of joiner p: p + (departed old peers below its ID).
+__global__ void k_cd_place_join(SearchView sv_old, const cell128 *ring_new, const uint32_t *jex,
+                                uint32_t n_old, uint32_t n_new, cell128 *mid, uint32_t *mso,
+                                uint32_t *msn, uint8_t *mtag) {
+    for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < n_new;
+         p += (size_t)gridDim.x * blockDim.x) {
+        if (jex[p + 1] == jex[p]) continue;  // survivor: placed from the old side
+        const u128 id = ld128(ring_new + p);
+        const uint32_t c = dir_lower_bound(sv_old, id);  // old IDs below it
+        const size_t m = (size_t)p + c - (p - jex[p]);
+        st128(mid + m, id);
+        mso[m] = c == n_old ? 0u : c;
+        msn[m] = (uint32_t)p;
+        mtag[m] = 2;
+    }
+}
+
+// lo[b] = first merged entry whose bucket is >= b (k_dir_lo on the merged IDs).
+__global__ void k_cd_lo(const cell128 *mid, uint32_t M, int kb, uint32_t *lo) {
+    const size_t nb = (size_t)1 << kb;
+    for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j <= M;
+         j += (size_t)gridDim.x * blockDim.x) {
+        const long long pb = j == 0 ? -1 : (long long)(uint64_t)(ld128(mid + j - 1) >> (128 - kb));
+        const long long cb = j == M ? (long long)nb : (long long)(uint64_t)(ld128(mid + j) >> (128 - kb));
+        for (long long b = pb + 1; b <= cb; ++b) lo[b] = (uint32_t)j;
+    }
+}
+
+__global__ void k_cd_pack(const cell128 *mid, const uint32_t *mso, const uint32_t *msn,
+                          const uint8_t *mtag, const uint32_t *lo, uint32_t M, int kb, uint4 *cd) {
+    const size_t nb = (size_t)1 << kb;
+    for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b < nb;
+         b += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t a = lo[b], z = lo[b + 1];
+        const uint32_t cnt = z - a < 3 ? z - a : 3;
+        const uint32_t m0 = a < M ? a : 0;
+        const uint64_t h0 = cnt >= 1 ? (uint64_t)(ld128(mid + a) >> (64 - kb)) : 0;
+        const uint64_t h1 = cnt >= 2 ? (uint64_t)(ld128(mid + a + 1) >> (64 - kb)) : 0;
+        uint64_t tags = 0;
+        uint32_t m = m0;
+        for (int j = 0; j < 32; ++j) {
+            tags |= (uint64_t)mtag[m] << (2 * j);
+            if (++m == M) m = 0;
+        }
+        const uint64_t h1c = (h1 & ~3ull) | cnt;
+        cd[2 * b] = make_uint4((uint32_t)h0, (uint32_t)(h0 >> 32), mso[m0], msn[m0]);
+        cd[2 * b + 1] = make_uint4((uint32_t)tags, (uint32_t)(tags >> 32), (uint32_t)h1c,
+                                   (uint32_t)(h1c >> 32));
+    }
+}
+
+// Compares a caller's old_to_new with cx_churn's (ok = 1 iff equal).
+__global__ void k_cd_same(const uint32_t *a, const uint32_t *b, size_t n, uint32_t *ok) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        if (a[i] != b[i]) *ok = 0;
+}
+
+size_t churn_dir_workspace_bytes(size_t n_old, size_t n_new) {
+    const size_t M = n_old + n_new;  // upper bound of the merged size
+    return ((n_old + 1) + (n_new + 1)) * 4 + M * (16 + 4 + 4 + 1) + 64 * 6;
+}
+
+hipError_t churn_dir_build(const SearchView &sv_old, const SearchView &sv_new,
+                           const uint32_t *o2n, int kb, void *ws, uint32_t *lo, uint4 *cd,
+                           uint32_t *scan_ws, uint32_t *M_out, hipStream_t s) {
+    const uint32_t n_old = sv_old.ev.n, n_new = sv_new.ev.n;
+    const size_t Mcap = (size_t)n_old + n_new;
+    char *w = static_cast<char *>(ws);
+    auto carve = [&](size_t bytes) {
+        char *r = w;
+        w += (bytes + 63) & ~(size_t)63;
+        return r;
+    };
+    uint32_t *dflag = reinterpret_cast<uint32_t *>(carve((n_old + 1) * 4));
+    uint32_t *jflag = reinterpret_cast<uint32_t *>(carve((n_new + 1) * 4));
+    cell128 *mid = reinterpret_cast<cell128 *>(carve(Mcap * 16));
+    uint32_t *mso = reinterpret_cast<uint32_t *>(carve(Mcap * 4));
+    uint32_t *msn = reinterpret_cast<uint32_t *>(carve(Mcap * 4));
+    uint8_t *mtag = reinterpret_cast<uint8_t *>(carve(Mcap));
+    hipError_t e = fill_u32(jflag, n_new, 1u, s);
+    if (e == hipSuccess) e = hipMemsetAsync(jflag + n_new, 0, 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(dflag + n_old, 0, 4, s);
+    if (e != hipSuccess) return e;
+    k_cd_flags<<<cx_grid(n_old, 256), 256, 0, s>>>(o2n, n_old, n_new, dflag, jflag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = exclusive_scan(dflag, (size_t)n_old + 1, scan_ws, s)) != hipSuccess) return e;
+    if ((e = exclusive_scan(jflag, (size_t)n_new + 1, scan_ws, s)) != hipSuccess) return e;
+    uint32_t D = 0;
+    if ((e = hipMemcpyAsync(&D, dflag + n_old, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint32_t M = n_new + D;
+    *M_out = M;
+    k_cd_place_old<<<cx_grid(n_old, 256), 256, 0, s>>>(sv_new, sv_old.ring, o2n, dflag, n_old,
+                                                      n_new, mid, mso, msn, mtag);
+    k_cd_place_join<<<cx_grid(n_new, 256), 256, 0, s>>>(sv_old, sv_new.ring, jflag, n_old, n_new,
+                                                       mid, mso, msn, mtag);
+    k_cd_lo<<<cx_grid((size_t)M + 1, 256), 256, 0, s>>>(mid, M, kb, lo);
+    k_cd_pack<<<cx_grid((size_t)1 << kb, 256), 256, 0, s>>>(mid, mso, msn, mtag, lo, M, kb, cd);
+    return hipGetLastError();
+}
+
+hipError_t churn_dir_same(const uint32_t *a, const uint32_t *b, size_t n, uint32_t *ok,
+                          hipStream_t s) {
+    hipError_t e = fill_u32(ok, 1, 1u, s);
+    if (e != hipSuccess || n == 0) return e;
+    k_cd_same<<<cx_grid(n, 256, 4096), 256, 0, s>>>(a, b, n, ok);
     return hipGetLastError();
 }
 
@@ -3723,10 +3969,10 @@ hipError_t misplaced_holders(const SearchView &sv, const uint32_t *holders, int 
     if (q == 0) return hipSuccess;
     if (sv.dir)
         k_misplaced<false, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
-            sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target);
+            sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target, ChurnDir{});
     else
         k_misplaced<false, false><<<cx_grid(q, ROW_BLOCK, 512), ROW_BLOCK, 0, s>>>(
-            sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target);
+            sv, sv, nullptr, holders, nh, keys, q, n, lists, count, mask, target, ChurnDir{});
     return hipGetLastError();
 }
 

@@ -200,10 +200,25 @@ hipError_t merge_join_pos(const SearchView &sv, const cell128 *ring, size_t n,
 hipError_t merge_scatter(const cell128 *ring, size_t n, const uint32_t *SG, const uint32_t *SA,
                          const cell128 *J, size_t nj, const uint32_t *pos, const uint32_t *kidx,
                          cell128 *out, uint32_t *o2n, hipStream_t s);
+// Churn directory of (old ring, new ring, cx_churn's old_to_new): 2^kb
+// buckets x 32 B (k_misplaced's one-gather path).  ok: device flag, nonzero
+// when the caller's old_to_new equals the one the directory was built from.
+struct ChurnDirArgs {
+    const uint4 *cd;
+    int kb;
+    const uint32_t *ok;
+};
 hipError_t misplaced_churn(const SearchView &ev_old, const SearchView &ev_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
-                           hipStream_t s);
+                           const ChurnDirArgs *cda, hipStream_t s);
+size_t churn_dir_workspace_bytes(size_t n_old, size_t n_new);
+// lo: 2^kb + 1 words; scan_ws: scan_workspace_words(max(n_old, n_new) + 1).
+hipError_t churn_dir_build(const SearchView &sv_old, const SearchView &sv_new,
+                           const uint32_t *o2n, int kb, void *ws, uint32_t *lo, uint4 *cd,
+                           uint32_t *scan_ws, uint32_t *M_out, hipStream_t s);
+hipError_t churn_dir_same(const uint32_t *a, const uint32_t *b, size_t n, uint32_t *ok,
+                          hipStream_t s);
 hipError_t misplaced_holders(const SearchView &ev, const uint32_t *holders, int nh,
                              const cell128 *keys, size_t q, int n, uint32_t *lists,
                              uint8_t *count, uint16_t *mask, uint8_t *target, hipStream_t s);

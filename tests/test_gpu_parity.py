@@ -610,3 +610,94 @@ def test_route_table_from_level_planes_identical(lg):
     ring.build_fingers()
     h_planes_only = ring.route_table_hash()
     assert h_planes == h_rows == h_planes_only and h_planes != 0
+
+
+# ------------------------------------------------- a12 churn directory (fast path)
+def _churn_cases(O):
+    """(old IDs, joins, leaves) exercising the churn directory's corners."""
+    rng = np.random.default_rng(99)
+    out = []
+    ids = O.splitmix_keys(5150, 20000)
+    R = O.ring_build(ids)
+    out.append(("uniform_1pct", ids, O.splitmix_keys(5151, 200),
+                R[rng.choice(20000, 200, replace=False)]))
+    # joiners packed right after old peers: windows with many joiners, buckets
+    # holding 3+ merged entries, equal hints (IDs differing in the low bits)
+    v = O.ints_from_keys(R)
+    dense = [v[i] + 1 + j for i in range(0, 20000, 97) for j in range(20)]
+    out.append(("dense_joins", ids, O.keys_from_ints(dense),
+                R[rng.choice(20000, 3000, replace=False)]))
+    # clustered ring: every ID in one narrow band (a handful of buckets)
+    base = 0x0FED_CBA9_8765_4321 << 64
+    cl = O.keys_from_ints([base + i * 131 for i in range(4000)] + [(1 << 127) + i for i in range(40)])
+    out.append(("clustered", cl, O.keys_from_ints([base + i * 131 + 7 for i in range(0, 4000, 3)]),
+                cl[rng.choice(4040, 500, replace=False)]))
+    # heavy churn: half the ring leaves, as many join
+    out.append(("half", ids, O.splitmix_keys(5152, 10000),
+                R[rng.choice(20000, 10000, replace=False)]))
+    # small rings straddling the 32-peer threshold of the directory path
+    s = O.splitmix_keys(5153, 40)
+    Rs = O.ring_build(s)
+    out.append(("small", s, O.splitmix_keys(5154, 3), Rs[:9]))
+    return out
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_misplaced_churn_directory(cx, O, case):
+    """cx_misplaced on a ring from cx_churn with cx_churn's mapping takes the
+    churn directory (one gather per key); it must equal the two-search path
+    and the oracle on keys at and next to every old, new, joining and
+    departed ID, for both list lengths and a caller copy of the mapping."""
+    name, ids, joins, leaves = _churn_cases(O)[case]
+    old = cx.Ring(ids)
+    want_old = O.ring_build(ids)
+    new, o2n = old.churn(joins, leaves)
+    want_new, want_o2n = O.churn(want_old, joins, leaves)
+    assert (o2n == want_o2n).all()
+    rng = np.random.default_rng(case)
+    vals = O.ints_from_keys(O.splitmix_keys(600 + case, 30000))
+    for arr in (want_old, want_new, joins, leaves):
+        a = O.ints_from_keys(arr)
+        for x in (a if len(a) <= 3000 else [a[i] for i in rng.choice(len(a), 3000, replace=False)]):
+            vals += [x, (x + 1) % (1 << 128), (x - 1) % (1 << 128)]
+    vals += [0, 1, MAX, MAX - 1]
+    keys = O.keys_from_ints(vals)
+    for n in (1, 5, 14, 16):
+        got = old.misplaced(new, o2n.copy(), keys, n)
+        new.set_misplaced_variant(0)
+        two = old.misplaced(new, o2n, keys, n)
+        new.set_misplaced_variant(1)
+        exp = O.misplaced(want_old, want_new, want_o2n, keys, n)
+        for a, b, c in zip(got, two, exp):
+            assert (a == c).all(), (name, n)
+            assert (b == c).all(), (name, n)
+
+
+def test_misplaced_churn_directory_device_and_foreign_parent(cx, O):
+    """Device buffers through the directory path; a ring churned from a
+    different parent (or a mapping that differs in one entry) takes the
+    two-search path and still matches the oracle."""
+    import torch
+    ids = O.splitmix_keys(5160, 5000)
+    want_old = O.ring_build(ids)
+    old = cx.Ring(ids)
+    joins = O.splitmix_keys(5161, 60)
+    leaves = want_old[np.random.default_rng(5).choice(5000, 60, replace=False)]
+    new, o2n = old.churn(joins, leaves)
+    want_new, want_o2n = O.churn(want_old, joins, leaves)
+    keys = edge_keys(O, want_new, 79, 20000)
+    exp = O.misplaced(want_old, want_new, want_o2n, keys, 14)
+    kd = torch.from_numpy(keys.view(np.int64).copy()).cuda()
+    od = torch.from_numpy(o2n.view(np.int32).copy()).cuda()
+    got = old.misplaced(new, od, kd, 14)
+    for a, b in zip(got, exp):
+        assert (a.cpu().numpy().view(b.dtype).reshape(b.shape) == b).all()
+    other = cx.Ring(ids)   # same IDs, not new's parent
+    got = other.misplaced(new, o2n, keys, 14)
+    for a, b in zip(got, exp):
+        assert (a == b).all()
+    bent = o2n.copy()
+    bent[17] = 0xFFFFFFFF
+    got = old.misplaced(new, bent, keys, 14)
+    for a, b in zip(got, O.misplaced(want_old, want_new, bent, keys, 14)):
+        assert (a == b).all()
