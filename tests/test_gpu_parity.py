@@ -612,6 +612,41 @@ def test_route_table_from_level_planes_identical(lg):
     assert h_planes == h_rows == h_planes_only and h_planes != 0
 
 
+@pytest.mark.parametrize("kind", ["small", "mixed", "clustered"])
+def test_route_table_builds_edge_rings(cx, O, kind):
+    """The default route-table build (level + two-hop planes) equals the
+    level-planes-only build on small rings, rings mixing a dense cluster with
+    uniform IDs, and a dense cluster alone (escapes equal too), and routes
+    through it equal the oracle."""
+    rng = np.random.default_rng(len(kind))
+    if kind == "small":
+        ids = O.splitmix_keys(0xB0, 200)
+    else:
+        base = 0x3C3C_5A5A_0F0F_1234 << 64
+        m = 1500 if kind == "mixed" else 6000
+        vals = [base + i * 7919 for i in range(m)]
+        if kind == "mixed":
+            vals += O.ints_from_keys(O.splitmix_keys(0xB1, 6000))
+        ids = O.keys_from_ints(vals)
+    ring = cx.Ring(ids)
+    ring.build_fingers()
+    assert ring.route_info()[0] == 5
+    h0, e0 = ring.route_table_hash(), ring.route_info()[1]
+    ring.set_table_build(2)
+    ring.build_fingers()
+    h2, e2 = ring.route_table_hash(), ring.route_info()[1]
+    assert h0 == h2 and e0 == e2 and h0 != 0
+    ring.set_table_build(0)
+    ring.build_fingers()
+    want = O.ring_build(ids)
+    keys = edge_keys(O, want, 0xB2, 5000)
+    src = rng.integers(0, len(want), len(keys)).astype(np.uint32)
+    got = ring.route(src, keys)
+    exp = O.route(O.Peers(want, O.fingers(want)), src, keys)
+    for a, b in zip(got, exp):
+        assert (a == b).all()
+
+
 # ------------------------------------------------- a12 churn directory (fast path)
 def _churn_cases(O):
     """(old IDs, joins, leaves) exercising the churn directory's corners."""
