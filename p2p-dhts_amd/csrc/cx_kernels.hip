@@ -2084,12 +2084,20 @@ hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s) {
 __device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t par, uint64_t phi,
                                                  int l, uint32_t x, uint64_t xhi,
                                                  const cell128 *ring) {
-    // x, par < n < 2^30 and E(l) <= n/2: x - par - E lies in (-3n/2, n), so
-    // two conditional adds give the residue (no modulo)
+    // x, par < n < 2^30 and E(l) <= n/2: x - par - E lies in (-3n/2, n).  The
+    // stored advance is its residue in [h + 1 - n, h] (h = n / 2); when the raw
+    // difference already lies there and in the 16-bit field's range -- every
+    // slot but those whose hop wraps the ring's end -- it is the residue, else
+    // two conditional adds and a subtract give it (no modulo)
     int d = (int)x - (int)par - (int)cz_expect(n, l);
-    if (d < 0) d += (int)n;
-    if (d < 0) d += (int)n;
-    if (d > (int)(n / 2)) d -= (int)n;  // (-n/2, n/2]
+    const int h = (int)(n / 2);
+    const int lo = h + 1 - (int)n > -32768 ? h + 1 - (int)n : -32768;  // uniform
+    const int hi = h < 32766 ? h : 32766;
+    if ((uint32_t)(d - lo) > (uint32_t)(hi - lo)) {
+        if (d < 0) d += (int)n;
+        if (d < 0) d += (int)n;
+        if (d > h) d -= (int)n;  // [h + 1 - n, h]
+    }
     const int sh = gs - 64;
     const uint64_t D = xhi - phi - (1ull << (l - 64));
     uint64_t code;
