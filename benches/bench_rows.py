@@ -233,6 +233,70 @@ def main():
     del old, new, keys, lists, count, mask, target, joins, leaves, pick, o2n
     torch.cuda.empty_cache()
 
+    # ---------------- f1 UUIDv5 IDs, f3 hex codec (device buffers) ----------------
+    import ctypes
+    import uuid
+    from chordx import _lib as LL
+    lib = chordx.lib()
+    vp = ctypes.c_void_p
+    nq = 1 << 22
+    names = [f"127.0.0.1:{5000 + i}" if i % 2 else f"key{i}" for i in range(nq)]
+    enc = "".join(names).encode()
+    offs = np.zeros(nq + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in names])
+    d_bytes = torch.from_numpy(np.frombuffer(enc, dtype=np.uint8).copy()).cuda()
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_ids = torch.empty((nq, 2), dtype=torch.int64, device="cuda")
+    uu = lambda: LL.check(lib.cx_uuid5_dns(vp(d_bytes.data_ptr()), vp(d_offs.data_ptr()), nq,  # noqa: E731
+                                           vp(d_ids.data_ptr()), LL.CX_MEM_DEVICE, 0))
+    t_uuid = ev_time(uu)
+    ids_np = d_ids.cpu().numpy().view(np.uint64)
+    want = [uuid.uuid5(uuid.NAMESPACE_DNS, x).int for x in names[:4096]]
+    ok_uuid = all(int(ids_np[i, 1]) << 64 | int(ids_np[i, 0]) == want[i] for i in range(4096))
+    t0 = time.perf_counter()
+    m1 = 200000
+    for x in names[:m1]:
+        uuid.uuid5(uuid.NAMESPACE_DNS, x)
+    cpu_uuid = m1 / (time.perf_counter() - t0)
+    # hex: format 2^24 keys to text, parse the text back (round trip on the GPU)
+    nh = 1 << 24
+    hk = keys_dev(nh, 0x5EED000A)
+    txt = torch.empty((nh, 32), dtype=torch.uint8, device="cuda")
+    ln = torch.empty(nh, dtype=torch.uint8, device="cuda")
+    fm = lambda: LL.check(lib.cx_hex_format(vp(hk.data_ptr()), nh, vp(txt.data_ptr()),  # noqa: E731
+                                            vp(ln.data_ptr()), LL.CX_MEM_DEVICE, 0))
+    t_fmt = ev_time(fm)
+    back = torch.empty((nh, 2), dtype=torch.int64, device="cuda")
+    okb = torch.empty(nh, dtype=torch.uint8, device="cuda")
+    # the strings (each slot's first len bytes), packed as the parser takes them
+    packed_offs = torch.empty(nh + 1, dtype=torch.int64, device="cuda")
+    packed_offs[0] = 0
+    packed_offs[1:] = torch.cumsum(ln.to(torch.int64), 0)
+    sel = (torch.arange(32, device="cuda")[None, :] < ln[:, None].to(torch.int64))
+    packed = txt[sel].contiguous()
+    pa = lambda: LL.check(lib.cx_hex_parse(vp(packed.data_ptr()), vp(packed_offs.data_ptr()), nh,  # noqa: E731
+                                           vp(back.data_ptr()), vp(okb.data_ptr()),
+                                           LL.CX_MEM_DEVICE, 0))
+    t_parse = ev_time(pa)
+    rt_ok = bool(torch.equal(back, hk)) and bool((okb == 1).all())
+    t0 = time.perf_counter()
+    hk_np = hk[:200000].cpu().numpy().view(np.uint64)
+    for lo, hi in hk_np:
+        int(format((int(hi) << 64) | int(lo), "x"), 16)
+    cpu_hex = 200000 / (time.perf_counter() - t0)
+    out["f1_uuid5_f3_hex"] = {
+        "uuid5_names": nq, "uuid5_s": t_uuid, "uuid5_names_per_s": nq / t_uuid,
+        "uuid5_matches_python_uuid5_on_4096": ok_uuid,
+        "cpu_uuid5": {"value": cpu_uuid, "unit": "names/s", "cores": 1, "kind": "python stdlib",
+                      "sample": f"first {m1} names, uuid.uuid5 (DNS namespace)"},
+        "hex_keys": nh, "hex_format_s": t_fmt, "hex_format_keys_per_s": nh / t_fmt,
+        "hex_parse_s": t_parse, "hex_parse_keys_per_s": nh / t_parse,
+        "hex_round_trip_identical": rt_ok,
+        "cpu_hex_round_trip": {"value": cpu_hex, "unit": "keys/s", "cores": 1,
+                               "kind": "python format/int", "sample": "first 200000 keys"}}
+    del d_bytes, d_offs, d_ids, hk, txt, ln, back, okb, packed, packed_offs, sel
+    torch.cuda.empty_cache()
+
     # ---------------- IDA (DHash payload coding, 14/10/257) ----------------
     from chordx import ida
     res = {}
