@@ -56,6 +56,23 @@ def segments(lengths, m: int) -> np.ndarray:
     return seg
 
 
+def _on_default_stream(t):
+    """The IDA entry points run on the device's null stream: when the caller
+    works on another (non-blocking) torch stream, its pending writes to the
+    inputs are waited for before the call (and _after_call orders the
+    outputs back), so no kernel reads a buffer another stream is filling."""
+    cur = torch.cuda.current_stream(t.device)
+    if cur.cuda_stream != 0:
+        cur.synchronize()
+        return False
+    return True
+
+
+def _after_call(t, was_default):
+    if not was_default:
+        torch.cuda.synchronize(t.device)
+
+
 def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0, seg_offsets=None, out=None):
     """Raw batched encode.  data: uint8 bytes, offsets: (blocks + 1,) uint64
     (numpy, or torch device tensors).  Returns (frags uint16, seg_offsets);
@@ -78,6 +95,7 @@ def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0, seg_offsets=N
             max(total * n, 1), dtype=torch.int16, device=data.device)
         _need(frags, 2, "out", total * n, data.device)
         mk = L.CX_MEM_DEVICE
+        dflt = _on_default_stream(data)
     else:
         data = np.ascontiguousarray(data, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -85,6 +103,8 @@ def encode_flat(data, offsets, n=14, m=10, p=257, device: int = 0, seg_offsets=N
         mk = L.CX_MEM_HOST
     L.check(L.lib().cx_ida_encode(_ptr(data), _ptr(offsets), _ptr(seg_offsets), blocks, n, m,
                                   p, _ptr(frags), mk, device))
+    if mk == L.CX_MEM_DEVICE:
+        _after_call(data, dflt)
     return frags, seg_offsets
 
 
@@ -106,6 +126,7 @@ def decode_flat(frags, seg_offsets, indices, m=10, p=257, device: int = 0, total
         _need(out, 2, "out", total * m, dev)
         _need(ln, 8, "out_len", blocks, dev)
         mk = L.CX_MEM_DEVICE
+        dflt = _on_default_stream(frags)
     else:
         frags = np.ascontiguousarray(frags, dtype=np.uint16)
         seg_offsets = np.ascontiguousarray(seg_offsets, dtype=np.uint64)
@@ -115,6 +136,8 @@ def decode_flat(frags, seg_offsets, indices, m=10, p=257, device: int = 0, total
         mk = L.CX_MEM_HOST
     L.check(L.lib().cx_ida_decode(_ptr(frags), _ptr(seg_offsets), _ptr(indices), blocks, m, p,
                                   _ptr(out), _ptr(ln), mk, device))
+    if mk == L.CX_MEM_DEVICE:
+        _after_call(frags, dflt)
     return out, ln
 
 

@@ -152,6 +152,28 @@ def test_device_buffers_large(ida, O):
         assert (got[i] == want[i]).all()
 
 
+def test_device_buffers_on_a_side_stream(ida, O):
+    """Inputs produced and outputs consumed on a non-default (non-blocking)
+    torch stream: the wrappers order the null-stream IDA calls against it."""
+    import torch
+    nb, bl = 1 << 12, 1000
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        g = torch.Generator(device="cuda").manual_seed(9)
+        data = torch.randint(0, 256, (nb * bl,), dtype=torch.uint8, device="cuda", generator=g)
+        offs = torch.arange(0, nb * bl + 1, bl, dtype=torch.int64, device="cuda")
+        frags, seg = ida.encode_flat(data, offs)
+        S = (bl + 9) // 10
+        keep = torch.tensor([1, 2, 3, 4, 5, 7, 8, 10, 12, 13], device="cuda")
+        rows = frags.view(nb, 14, S)[:, keep, :].contiguous().view(-1)
+        idx = (keep + 1).to(torch.uint8).repeat(nb).contiguous()
+        out, ln = ida.decode_flat(rows, seg, idx, total=nb * S)
+        ok = bool((out.view(nb, S * 10)[:, :bl].to(torch.int32) ==
+                   data.view(nb, bl).to(torch.int32)).all())
+    side.synchronize()
+    assert ok
+
+
 def test_from_fragments_value_256_refused(ida):
     """Fragments that decode to a value of 256 (p = 257; not producible from
     bytes) are refused explicitly instead of yielding an empty fragment list."""
