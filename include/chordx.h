@@ -294,7 +294,10 @@ void cx_wire_free(char *response);
  * (ChordPeer::ForwardRequest, chord_peer.cpp:185-211) -- finishes there, and
  * its result travels home once (RESULT record).  Owners, hops and statuses
  * equal cx_route's on the replicated ring.  All arc buffers are device memory
- * (CX_MEM_DEVICE). */
+ * (CX_MEM_DEVICE).  This record protocol (origin walk or key-first, three
+ * rounds) is kept for A/B; the default exchange is the key-first structure-of-
+ * arrays protocol at the end of this header (cx_arc_partition / route /
+ * deliver: two all-to-alls, 20 B out and 8 B back per lookup). */
 typedef struct cx_arc_rec {
     uint64_t w0, w1; /* key (lookups) / owner | status << 32 (results) */
     uint64_t qid;    /* origin rank << 40 | index at the origin */
