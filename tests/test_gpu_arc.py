@@ -278,7 +278,7 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0):
 
 
 @pytest.mark.parametrize("n,G", [(5000, 1), (5000, 2), (5000, 3), (5000, 8), (1 << 16, 8),
-                                 (70001, 5), (2, 2), (1, 1), (3, 4)])
+                                 (70001, 5), (2, 2), (1, 1), (3, 4), (20000, 16), (9000, 33)])
 def test_arc_soa_equals_replicated(cx, O, n, G):
     import torch
     q = 4096
