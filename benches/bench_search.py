@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Exact successor search variants (rows a5/a7): bucket directory (default),
-Eytzinger with LDS top levels, wave-cooperative 16-ary tree -- kernel time by
+Eytzinger with LDS top levels, wave-cooperative 16-ary tree, wave-cooperative
+Eytzinger (16 lanes a query, ballot over four levels) -- kernel time by
 HIP events on the launch stream, at C2 (2^16 ring, 2^20 keys) and C4 sizes
 (2^24 ring, 2^25 keys); every variant's output is compared with the default.
     python benches/bench_search.py
@@ -45,7 +46,7 @@ def main():
         res = torch.empty(1 << lq, dtype=torch.int32, device="cuda")
         ref = None
         row = {}
-        for v, vn in ((1, "directory"), (0, "eytzinger"), (2, "wave16")):
+        for v, vn in ((1, "directory"), (0, "eytzinger"), (2, "wave16"), (3, "eyt_wave16")):
             ring.set_search_variant(v)
             ms = timed(lambda: ring.successor(keys, out=res))
             same = True if ref is None else bool((res == ref).all())

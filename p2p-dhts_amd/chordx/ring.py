@@ -309,8 +309,10 @@ class Ring:
 
     def set_search_variant(self, v: int):
         """Internal A/B switch: 0 = Eytzinger (LDS top levels), 1 = bucket directory
-        (default), 2 = wave-cooperative 16-ary tree (ballot/popcount; successor
-        and predecessor only, the other searches keep the directory)."""
+        (default), 2 = wave-cooperative 16-ary tree (ballot/popcount), 3 =
+        wave-cooperative Eytzinger (16 lanes a query, four levels per ballot);
+        2 and 3 serve successor and predecessor only, the other searches keep
+        the directory."""
         f = L.lib().cxi_set_search_variant
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))

@@ -259,6 +259,7 @@ struct cx_ring {
     int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory,
                                    // 2: wave-cooperative 16-ary tree (successor / predecessor)
     cell128 *d_stree = nullptr;    // levels 1.. of the 16-ary tree (variant 2, lazy)
+    uint32_t *d_eyt_rank = nullptr; // Eytzinger node -> sorted index (variant 3, lazy)
     int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
     uint64_t serial = 0;           // process-unique handle number
     // cx_churn result: the parent's serial and the old_to_new it returned; the
@@ -400,6 +401,7 @@ void free_ring(cx_ring *r) {
     table_free(r->device, r->d_tree, ent * 64);
     table_free(r->device, r->d_cz, ent * 128);
     (void)hipFree(r->d_stree);
+    (void)hipFree(r->d_eyt_rank);
     (void)hipFree(r->d_ring_ext);
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
@@ -724,6 +726,14 @@ int cx_ring_sync(const cx_ring *ring) {
 
 namespace {
 // The 16-ary tree's levels (search variant 2), built on first use.
+// BFS -> sorted index table of the Eytzinger copy (search variant 3), lazy.
+int eyt_rank_view(cx_ring *r, hipStream_t s) {
+    if (r->d_eyt_rank) return CX_OK;
+    CX_HIP(hipMalloc(&r->d_eyt_rank, (r->n + 1) * sizeof(uint32_t)));
+    CX_HIP(cxk::eyt_rank_build(r->n, r->d_eyt_rank, s));
+    return CX_OK;
+}
+
 int stree_view(cx_ring *r, cxk::STreeView &st, hipStream_t s) {
     st = cxk::stree_plan(r->d_ring, r->n, r->d_stree);
     if (!r->d_stree && st.words) {
@@ -753,6 +763,10 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
         cxk::STreeView st;
         if ((rc = stree_view(const_cast<cx_ring *>(ring), st, s))) return rc;
         CX_HIP(cxk::successor_stree(st, reinterpret_cast<const cell128 *>(dk), q, dout, false, s));
+    } else if (ring->search_variant == 3) {
+        if ((rc = eyt_rank_view(const_cast<cx_ring *>(ring), s))) return rc;
+        CX_HIP(cxk::successor_eyt16(ring->eyt(), ring->d_eyt_rank,
+                                    reinterpret_cast<const cell128 *>(dk), q, dout, false, s));
     } else {
         CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     }
@@ -801,6 +815,10 @@ int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t 
         cxk::STreeView st;
         if ((rc = stree_view(const_cast<cx_ring *>(ring), st, s))) return rc;
         CX_HIP(cxk::successor_stree(st, reinterpret_cast<const cell128 *>(dk), q, dout, true, s));
+    } else if (ring->search_variant == 3) {
+        if ((rc = eyt_rank_view(const_cast<cx_ring *>(ring), s))) return rc;
+        CX_HIP(cxk::successor_eyt16(ring->eyt(), ring->d_eyt_rank,
+                                    reinterpret_cast<const cell128 *>(dk), q, dout, true, s));
     } else {
         CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     }
@@ -1959,11 +1977,12 @@ int cxi_set_churn_variant(cx_ring *ring, int variant) {
 }
 
 // 0 = Eytzinger search with LDS-staged top levels, 1 = bucket directory (default),
-// 2 = wave-cooperative 16-ary tree for cx_successor / cx_predecessor (the
-// other searches keep the directory).
+// 2 = wave-cooperative 16-ary tree, 3 = wave-cooperative Eytzinger (16 lanes a
+// query, four levels per ballot) for cx_successor / cx_predecessor (variants
+// 2 and 3: the other searches keep the directory).
 int cxi_set_search_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
+    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0, 1, 2 or 3");
     ring->search_variant = variant;
     return CX_OK;
 }

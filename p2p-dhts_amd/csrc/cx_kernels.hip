@@ -514,6 +514,125 @@ hipError_t successor_stree(const STreeView &st, const cell128 *keys, size_t q, u
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Search variant 3: wave-cooperative search of the Eytzinger layout itself
+// (north_star's "Eytzinger-layout successor search whose top levels are
+// staged in LDS, with wavefront-cooperative 128-bit compares using
+// ballot/ctz").  Sixteen lanes take one query; a step covers four levels of
+// the BFS tree below node k: lane j = 2^t - 1 + o (t < 4, o < 2^t) loads node
+// k 2^t + o (the level's nodes are contiguous: 1, 2, 4 and 8 cells), compares
+// it with the key in 128 bits, and the group's 16-bit ballot mask is walked
+// from the root lane -- lane j's children are lanes 2j + 1 and 2j + 2 -- with
+// one bit test per level; the last node on the path that is >= the key is the
+// successor, mapped to its sorted index by a BFS -> sorted table (4 B per
+// peer, built on first use) instead of summing subtree sizes per lane.  The top
+// CX_LDS_LEVELS levels come from LDS, so at 2^24 three of the six steps gather
+// from HBM (vs twelve dependent gathers per lane for variant 0).
+// ---------------------------------------------------------------------------
+template <bool PRED, int U>
+__global__ __launch_bounds__(256) void k_successor_eyt16(EytView ev, const uint32_t *rank,
+                                                         const cell128 *keys, size_t q,
+                                                         uint32_t *owner) {
+    __shared__ u128 lds[CX_LDS_NODES];
+    eyt_stage_lds(ev, lds);
+    const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+    const int lt_t = 31 - __builtin_clz((unsigned)(li + 1));  // level of lane li in the subtree
+    const uint32_t lt_o = (uint32_t)(li + 1) - (1u << lt_t);
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t n = ev.n;
+    for (size_t base = wave * 4 * U; base < q; base += nwaves * 4 * U) {
+        u128 x[U];
+        uint64_t k[U], lb[U];
+        bool live[U], run[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t qi = base + u * 4 + g;
+            live[u] = qi < q;
+            x[u] = live[u] ? ld128(keys + qi) : (u128)0;
+            k[u] = 1;
+            lb[u] = 0;  // BFS index of the last node >= key on the path (0: none)
+            run[u] = live[u];
+        }
+        for (;;) {
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < U; ++u) any |= run[u];
+            if (__ballot(any) == 0) break;  // wave-uniform
+            u128 e[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t node = (k[u] << lt_t) + lt_o;
+                e[u] = ~(u128)0;
+                if (run[u] && li < 15 && node <= n)
+                    e[u] = node <= CX_LDS_NODES ? lds[node - 1] : ld128(ev.E + node);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool lt = run[u] && li < 15 && e[u] < x[u];
+                const uint32_t m = (uint32_t)(__ballot(lt) >> (16 * g)) & 0xFFFFu;
+                if (!run[u]) continue;
+                // walk the four levels from the root lane (uniform in the group):
+                // bit j of m says "node of lane j < key" -> go right
+                uint32_t j = 0, o = 0;
+                const uint64_t kk = k[u];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint64_t node = (kk << t) + o;
+                    if (node > n) {  // the descent left the tree: done
+                        run[u] = false;
+                        break;
+                    }
+                    const uint32_t b = (m >> j) & 1u;
+                    if (!b) lb[u] = node;
+                    j = 2 * j + 1 + b;
+                    o = 2 * o + b;
+                }
+                if (run[u]) {
+                    k[u] = (kk << 4) + o;  // 16 k + the path's four bits
+                    if (k[u] > n) run[u] = false;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t qi = base + u * 4 + g;
+            if (live[u] && li == 0) {
+                // successor = the last node on the path that is >= key; its
+                // sorted index from the BFS -> sorted table; none: wrap to 0
+                const uint32_t sidx = lb[u] ? rank[lb[u]] : 0u;
+                owner[qi] = PRED ? (sidx == 0 ? n - 1 : sidx - 1) : sidx;
+            }
+        }
+    }
+}
+
+// rank[k] = sorted index of Eytzinger node k (k = 1..n).
+__global__ void k_eyt_rank(uint32_t n, int h, uint32_t *rank) {
+    for (size_t k = 1 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; k <= n;
+         k += (size_t)gridDim.x * blockDim.x)
+        rank[k] = eyt_rank(k, n, h);
+}
+
+hipError_t eyt_rank_build(size_t n, uint32_t *rank, hipStream_t s) {
+    const int h = 63 - __builtin_clzll((unsigned long long)n);
+    k_eyt_rank<<<cx_grid(n, 256), 256, 0, s>>>((uint32_t)n, h, rank);
+    return hipGetLastError();
+}
+
+hipError_t successor_eyt16(const EytView &ev, const uint32_t *rank, const cell128 *keys, size_t q,
+                           uint32_t *owner, bool pred, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    constexpr int U = 4;
+    const size_t waves = (q + 4 * U - 1) / (4 * U);
+    const unsigned blocks = cx_grid(waves * 64, 256, 512);  // 2 per CU (64 KiB of LDS)
+    if (pred)
+        k_successor_eyt16<true, U><<<blocks, 256, 0, s>>>(ev, rank, keys, q, owner);
+    else
+        k_successor_eyt16<false, U><<<blocks, 256, 0, s>>>(ev, rank, keys, q, owner);
+    return hipGetLastError();
+}
+
 // Directory build: lo[b] = first ring index whose ID is >= b << (128 - k).
 // Thread j fills the buckets (bucket(ring[j-1]), bucket(ring[j])]; thread n
 // fills the tail up to 2^k.

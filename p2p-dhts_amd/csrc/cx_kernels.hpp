@@ -143,6 +143,11 @@ STreeView stree_plan(const cell128 *ring, size_t n, cell128 *buf);
 hipError_t stree_build(const STreeView &v, hipStream_t s);
 hipError_t successor_stree(const STreeView &st, const cell128 *keys, size_t q, uint32_t *owner,
                            bool pred, hipStream_t s);
+// Search variant 3: sixteen lanes per query over the Eytzinger copy, four
+// levels per step (ballot of the subtree's 15 compares).
+hipError_t eyt_rank_build(size_t n, uint32_t *rank, hipStream_t s);
+hipError_t successor_eyt16(const EytView &ev, const uint32_t *rank, const cell128 *keys, size_t q,
+                           uint32_t *owner, bool pred, hipStream_t s);
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s);
 // C2 planes (nl - 1 of them) from the level planes FT.

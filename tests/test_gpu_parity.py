@@ -60,7 +60,7 @@ def test_ring_build_equal_high_bits(cx, O):
 
 
 # ---------------------------------------------------------------- a5/a7 successor
-@pytest.mark.parametrize("search", [0, 1, 2])
+@pytest.mark.parametrize("search", [0, 1, 2, 3])
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 16, 17, 256, 257, 1000, 4095, 4096, 65537, 70000])
 def test_successor(cx, O, n, search):
     ids = edge_ring(O, n, 77 + n)
@@ -72,7 +72,7 @@ def test_successor(cx, O, n, search):
     assert (got == O.successor(want_ring, keys)).all()
 
 
-@pytest.mark.parametrize("search", [0, 1, 2])
+@pytest.mark.parametrize("search", [0, 1, 2, 3])
 def test_successor_c2(cx, O, search):
     """Config C2: 2^16-peer ring, 2^20 uniform keys (seeds of SURVEY 8d)."""
     ids = O.splitmix_keys(0x5EED0001, 1 << 16)
@@ -571,7 +571,7 @@ def test_misplaced_with_foreign_map_and_chained_churn(cx, O):
 
 
 
-@pytest.mark.parametrize("search", [1, 2])
+@pytest.mark.parametrize("search", [1, 2, 3])
 def test_predecessor(cx, O, refvec, search):
     """Batched GetPredecessor vs the oracle: reference fixtures, edge rings and
     keys (IDs, +-1, 0, 2^128 - 1), N = 1, 2, 3."""
