@@ -4,6 +4,8 @@ keys, src = q mod N), default route kernel, HIP events over `reps` launches
 after warm-up, repeated `rounds` times (min and median reported); checks owner
 == successor.  Prints one JSON line.
     python benches/bench_route.py [reps] [rounds]
+CX_SRC=random draws each lookup's source peer uniformly instead (splitmix,
+seed 0x5EED000A): the first hops of a wave no longer leave adjacent peers.
 """
 import json
 import os
@@ -29,7 +31,14 @@ def main():
     ring.build_fingers()
     keys = torch.empty((Q, 2), dtype=torch.int64, device="cuda")
     chordx.fill_splitmix(keys, 0x5EED0006)
-    src = (torch.arange(Q, device="cuda", dtype=torch.int64) % N).to(torch.int32)
+    src_kind = os.environ.get("CX_SRC", "mod")
+    if src_kind == "random":
+        r = torch.empty((Q, 2), dtype=torch.int64, device="cuda")
+        chordx.fill_splitmix(r, 0x5EED000A)
+        src = (r[:, 0] & 0x7FFFFFFFFFFFFFFF).remainder(N).to(torch.int32)
+        del r
+    else:
+        src = (torch.arange(Q, device="cuda", dtype=torch.int64) % N).to(torch.int32)
     owner = torch.empty(Q, dtype=torch.int32, device="cuda")
     hops = torch.empty(Q, dtype=torch.uint8, device="cuda")
     status = torch.empty(Q, dtype=torch.uint8, device="cuda")
@@ -47,6 +56,7 @@ def main():
         ms.append(a.elapsed_time(b) / reps)
     ok = bool((owner == ring.successor(keys)).all()) and int((status != 0).sum()) == 0
     print(json.dumps({"lib": os.path.basename(os.environ.get("CHORDX_LIB", "default")),
+                      "src": src_kind,
                       "ms_min": min(ms), "ms_median": statistics.median(ms),
                       "lookups_per_s": Q / (min(ms) * 1e-3), "probe": ring.gather_probe(),
                       "owner_ok": ok, "mean_hops": float(hops.double().mean())}), flush=True)
