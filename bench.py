@@ -49,6 +49,7 @@ from chordx import dist  # noqa: E402
 
 SEED_RING = 0x5EED0005
 SEED_KEYS = 0x5EED0006
+SEED_RANDOM_SRC = 0x5EED000A  # A/B field only: uniformly random source peers
 HBM_PEAK = 8.0e12  # B/s per MI355X (MI355X_MICROARCH.md, HBM3E spec)
 # Bytes the walk must move per lookup in streams: key 16 + source 4 +
 # (pred, self) ID pair 32 + owner 4 + hops 1 + status 1.
@@ -387,6 +388,22 @@ def main():
         torch.cuda.synchronize(dev)
         variant_ms[v] = e0.elapsed_time(e1) / 3
     ring.set_route_variant(-1)
+    # A/B: the same keys from uniformly random source peers (C4 fixes src = q mod N,
+    # whose wave-adjacent sources share lines on the first gathers); owners must not change
+    rsrc = torch.empty((Q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(rsrc, SEED_RANDOM_SRC, offset=q0)
+    rsrc = (rsrc[:, 0] & 0x7FFFFFFFFFFFFFFF).remainder(ring.n).to(torch.int32)
+    rout = (torch.empty_like(owner), torch.empty_like(hops), torch.empty_like(status))
+    ring.route(rsrc, keys, out=rout)  # own buffers: owner/hops stay the timed run's
+    e0.record(stream)
+    for _ in range(3):
+        ring.route(rsrc, keys, out=rout)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    rsrc_ms = e0.elapsed_time(e1) / 3
+    owner_eq = owner_eq and bool((succ_out == rout[0]).all().item())
+    rsrc_bad = int((rout[2] != 0).sum().item())
+    del rsrc, rout
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -457,6 +474,10 @@ def main():
             "exact_successor_eytzinger_lookups_per_s": Q / (eyt_ms * 1e-3),
             "exact_successor_wave16_lookups_per_s": Q / (wave_ms * 1e-3),
             "route_variant_kernel_ms": variant_ms,
+            "route_random_src": {"kernel_ms": rsrc_ms, "lookups_per_s": Q / (rsrc_ms * 1e-3),
+                                 "bad_status": rsrc_bad,
+                                 "note": "same keys and kernel, src uniform in [0, N) "
+                                         "(splitmix 0x5EED000A) instead of q mod N"},
             "setup_s": {"ring_sort": t_ring, "fingers_build": t_fing},
         }
         print(json.dumps(line), flush=True)
