@@ -1,13 +1,25 @@
 #!/usr/bin/env python3
 """Headline benchmark: finger-routed successor lookups with hop counts on a
-2^24-peer Chord ring (BASELINE.json metric, config C4 per GPU).
+2^24-peer Chord ring (BASELINE.json metric, config C4).
 
 One step = one cx_route launch over this rank's batch of keys resident in HBM
-(the converged m=128 finger table, ring and Eytzinger copy are built before the
-timed region).  Weak scaling: every rank holds a replica of the ring and routes
-its own slice of the global key stream (keys[q] = splitmix(seed, q), src[q] =
-q mod N), so the data path has no collective; the barrier and the max-over-ranks
-timing are the only cross-rank traffic.
+(the converged m=128 finger table, ring and route table are built before the
+timed region).  Every rank generates its share of the ring IDs and one
+all_gather (RCCL over xGMI) replicates them; every rank then holds a replica of
+the ring and routes its own slice of the global key stream (keys[q] =
+splitmix(seed, q), src[q] = q mod N): weak scaling, no collective in the timed
+data path, the barrier and the max-over-ranks timing are the only cross-rank
+traffic.  After the timed region the same run measures, on every rank:
+
+  arc      C4 as BASELINE.json states it -- the ring sharded by key arc, each
+           rank holding route rows for its arc only, lookups exchanged with
+           all_to_all-v (chordx.arc.ArcRouter, key-first SoA protocol) -- timed
+           over the same number of steps on the same keys, results compared
+           with the replicated route;
+  churn    1 % joins + 1 % leaves of the bench ring (seed 0x5EED0009) ->
+           route-ready (merge churn + fingers + route table), cold (fresh HBM)
+           then warm (table pool), with the two tables' hashes compared;
+  cpu      the reference-faithful CPU walk (oracle/, rank 0, every world size).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -15,14 +27,14 @@ timing are the only cross-rank traffic.
 With --gpus N > 1 and no torch.distributed environment, bench.py starts
 `torch.distributed.run --nproc-per-node N` itself as a child process (before
 anything touches the GPU) and exits with its status; rank 0 of the child job
-prints the line.  Rank 0 prints ONE JSON line.
+prints the ONE JSON line.
 
-Roofline (per launch of the timed route kernel): `achieved` counts the bytes
-the walk must move -- its streams (key, source, (pred, self) pair, owner, hops,
-status) plus one 64-B granule per random gather it actually issues (window-table
-entries, exact ring IDs, finger entries), counted by the counting build of the
-same kernel on the same batch -- over the kernel time from HIP events on the
-launch stream.  SURVEY 8(d)'s reference-work model (128 B per hop) is reported
+Roofline (whole node): `achieved` = the algorithmic bytes of the timed route
+kernel summed over ranks -- its streams (key, source, (pred, self) pair,
+owner, hops, status) plus one 64-B granule per random gather it actually
+issues, counted by the counting build of the same kernel on the same batch --
+over the slowest rank's kernel time (HIP events on the launch stream); `peak`
+= 8 TB/s x N.  SURVEY 8(d)'s reference-work model (128 B per hop) is reported
 separately as `reference_work_model`: it prices hops the window table resolves
 without a gather and is not a byte count of this kernel.
 """
@@ -47,8 +59,10 @@ import torch  # noqa: E402
 import chordx  # noqa: E402
 from chordx import dist  # noqa: E402
 
+METRIC = "successor lookups/sec (whole node) + % HBM roofline, 2^24-peer ring, 1/2/4/8 GPUs"
 SEED_RING = 0x5EED0005
 SEED_KEYS = 0x5EED0006
+SEED_CHURN = 0x5EED0009    # C5's churn batch seed
 SEED_RANDOM_SRC = 0x5EED000A  # A/B field only: uniformly random source peers
 HBM_PEAK = 8.0e12  # B/s per MI355X (MI355X_MICROARCH.md, HBM3E spec)
 # Bytes the walk must move per lookup in streams: key 16 + source 4 +
@@ -70,10 +84,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target wall time of the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-arc", action="store_true", help="skip the arc-sharded sub-record")
+    ap.add_argument("--no-churn", action="store_true", help="skip the churn -> route-ready leg")
     ap.add_argument("--mode", choices=("replicated", "arc"), default="replicated",
-                    help="replicated: every rank holds the whole tree table and routes its "
-                         "own keys (default); arc: each rank holds tree rows for its arc only "
-                         "and lookups travel between ranks (chordx.arc)")
+                    help="replicated: every rank holds the whole route table and routes its "
+                         "own keys (default; the arc layout is still measured as the `arc` "
+                         "sub-record); arc: the arc-sharded layout is the headline value")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_route.json"))
     return ap.parse_args()
 
@@ -125,16 +141,17 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
+def cpu_baseline(ring_np, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s, world):
     """Literal restatement (oracle/chord_oracle.c or_route: linear 128-entry
     InBetween scan per hop, StoredLocally, ForwardRequest substitution) timed on
-    this host's cores over a bounded sample of the same key stream (about
+    this host's cores over a bounded sample of rank 0's key stream (about
     2/3 of budget_s on all usable cores, 1/3 on one core); also checks the
-    GPU's owner/hops on the sample."""
+    GPU's owner/hops on the sample (gpu_owner None: no GPU outputs, dry run).
+    Run on rank 0 after the timed region at every world size: the CPU path is
+    one host's, so it is reported next to the whole-node GPU value."""
     import oracle as O
 
     threads = host_threads()
-    ring_np = ring.ids()
     P = O.Peers(ring_np, F_host)
 
     def timed(q, th):
@@ -148,39 +165,190 @@ def cpu_baseline(ring, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s):
     _, dt1 = timed(q1, 1)
     qa = int(min(len(keys_np), max(q1, budget_s * 2 / 3 * threads / max(per1, 1e-9))))
     (wo, wh, ws), dta = timed(qa, threads)
-    ok = bool((wo == gpu_owner[:qa]).all() and (wh == gpu_hops[:qa]).all() and (ws == 0).all())
+    ok = None
+    if gpu_owner is not None:
+        ok = bool((wo == gpu_owner[:qa]).all() and (wh == gpu_hops[:qa]).all() and (ws == 0).all())
     return {"value": qa / dta, "unit": "lookups/s", "cores": threads, "kind": "port",
             "value_1core": q1 / dt1,
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "n_gpus_beside": world,
             "sample": f"first {qa} keys of the rank-0 stream (of {len(keys_np)}) on {threads} "
                       f"threads ({dta:.1f} s), first {q1} on 1 thread ({dt1:.1f} s); "
                       "oracle/chord_oracle.c or_route, gcc -O3 -march=x86-64-v3",
             "parity_on_sample": ok}
 
 
+def whole_node_roofline(algo_bytes, kern_ms, world, dev):
+    """Sum over ranks of the kernel's algorithmic bytes per launch over the
+    slowest rank's kernel time, against N x 8 TB/s."""
+    total = dist.sum_over_ranks(int(algo_bytes), world, dev)
+    ms = dist.max_over_ranks(float(kern_ms), world, dev)
+    achieved = total / (ms * 1e-3) if ms > 0 else 0.0
+    peak = HBM_PEAK * world
+    return {"bound": "hbm", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GB/s",
+            "frac": achieved / peak, "algo_bytes_per_launch": total, "kernel_ms": ms,
+            "n_gpus": world}
+
+
+def line_base(args, world, value, dt_max, config, dtype="u128"):
+    return {"metric": METRIC, "value": value, "unit": "lookups/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt_max * 1e3 / max(1, args.steps), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic",
+            "config": config}
+
+
 def dry_run(args):
-    """CX_BENCH_DRYRUN=1: the launch / rendezvous / timing / reporting flow
-    without a GPU (CPU tests of the N > 1 path over gloo)."""
+    """CX_BENCH_DRYRUN=1: the launch / rendezvous / timing / reduction /
+    reporting flow without a GPU (CPU tests of the N > 1 path over gloo): a
+    2^12-peer ring, the whole-node roofline reduction fed with zero bytes, and
+    the CPU baseline on rank 0 at every world size, as in the GPU run."""
     world, rank, _ = dist.env_rank()
     dist.init("gloo")
     dist.barrier(world)
     t0 = time.perf_counter()
     dist.barrier(world)
     dt_max = dist.max_over_ranks(time.perf_counter() - t0, world)
+    roof = whole_node_roofline(0, 1.0, world, None)
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        import oracle as O
+        ring_np = O.ring_build(O.splitmix_keys(SEED_RING, 1 << 12))
+        F = O.fingers(ring_np, threads=2)
+        keys_np = O.splitmix_keys(SEED_KEYS, 1 << 14)
+        src_np = (np.arange(1 << 14) % len(ring_np)).astype(np.uint32)
+        cpu = cpu_baseline(ring_np, F, keys_np, src_np, None, None, args.cpu_seconds, world)
+    dist.barrier(world)
     if rank == 0:
-        print(json.dumps({"metric": "dry run", "value": 0.0, "n_gpus": world,
-                          "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": dt_max * 1e3 / max(1, args.steps)}), flush=True)
+        line = line_base(args, world, 0.0, dt_max, {"workload": "dry run"})
+        line.update({"metric": "dry run", "roofline": roof, "cpu_baseline": cpu,
+                     "arc": {"skipped": "dry run: no GPU"}})
+        print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
-def main_arc(args):
-    """Arc-sharded layout (SURVEY 8e layout 2): ring IDs generated in shares
-    and all-gathered (RCCL), route planes per arc, lookups sent to their key's
-    arc and answered in the key-first structure-of-arrays protocol
-    (ArcRouter.route_soa: 20 B out, 8 B back per lookup, pipelined pieces)."""
+def setup_ring(args, world, rank, dev, backend):
+    """Ring IDs generated in shares and all-gathered, then the ring handle."""
+    N = 1 << args.peers_log2
+    assert N % world == 0
+    lo = rank * N // world
+    share = torch.empty((N // world, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(share, SEED_RING, offset=lo)
+    t0 = time.perf_counter()
+    ids = dist.gather_ids(share, world, backend)
+    torch.cuda.synchronize(dev)
+    t_gather = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ring = chordx.Ring(ids, device=dev.index or 0)
+    torch.cuda.synchronize(dev)
+    return ring, t_gather, time.perf_counter() - t0
+
+
+def time_steps(fn, steps, world, dev):
+    """Exactly `steps` calls bracketed by barrier + synchronize on both sides;
+    (wall seconds of this rank, max over ranks)."""
+    dist.barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    dist.barrier(world)
+    dt = time.perf_counter() - t0
+    return dt, dist.max_over_ranks(dt, world, dev)
+
+
+def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backend):
+    """C4 as BASELINE.json states it: arc-sharded route planes and lookups
+    exchanged with all_to_all-v, over the same keys and steps as the headline;
+    owners/hops/statuses must equal the replicated route's."""
     from chordx.arc import ArcRouter
+    Q = keys.shape[0]
+    t0 = time.perf_counter()
+    router = ArcRouter(ring, ring.n, rank, world,
+                       comm_device="cpu" if backend == "gloo" else None)
+    torch.cuda.synchronize(dev)
+    t_build = time.perf_counter() - t0
+    top, rows, plane_bytes = ring.arc_info()
+    owner = torch.empty(Q, dtype=torch.int32, device=dev)
+    hops = torch.empty(Q, dtype=torch.uint8, device=dev)
+    status = torch.empty(Q, dtype=torch.uint8, device=dev)
+    for _ in range(args.warmup):
+        router.route(src, keys, owner, hops, status)
+    torch.cuda.synchronize(dev)
+    router.records_sent = 0
+    _, dt_max = time_steps(lambda: router.route(src, keys, owner, hops, status), args.steps,
+                           world, dev)
+    sent = dist.sum_over_ranks(router.records_sent, world, dev)
+    same = bool((owner == owner_ref).all().item()) and bool((hops == hops_ref).all().item()) \
+        and int((status != 0).sum().item()) == 0
+    same = dist.all_over_ranks(same, world, dev)
+    total = world * Q * args.steps
+    return {"value": total / dt_max, "unit": "lookups/s", "ms_per_step": dt_max * 1e3 / args.steps,
+            "per_gpu_lookups_per_s": total / dt_max / world,
+            "records_exchanged_per_lookup": sent / total,
+            "rounds_per_step": router.rounds,
+            "equals_replicated_route": same,
+            "top_levels_replicated": top, "local_rows": rows,
+            "route_plane_bytes_per_gpu": plane_bytes, "build_s": t_build,
+            "layout": f"ring IDs all-gathered; arc-sharded route planes x{world} (top {top} "
+                      "levels replicated, lower levels for the arc + halo); key-first SoA "
+                      "all_to_all-v (20 B out, 8 B back per remote lookup), pipelined pieces",
+            "note": "owner, hops and status of every lookup equal the replicated route's "
+                    "(checked on every rank)"}
+
+
+def churn_leg(ring, dev):
+    """1 % joins + 1 % leaves of the bench ring -> route-ready, twice: cold (the
+    new ring's 72 GiB of tables are fresh HBM) and warm (the table pool hands
+    back the first new ring's blocks, as every later membership epoch gets)."""
+    N = ring.n
+    nj = N // 100
+    joins = torch.empty((nj, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(joins, SEED_CHURN)
+    # distinct leaving peers (an odd stride is a bijection mod 2^k)
+    pick = (torch.arange(nj, device=dev, dtype=torch.int64) * 0x9E3779B1) % N
+    leaves = ring.ids_device()[pick].contiguous()
+    out = {}
+    hashes = []
+    for phase in ("cold", "warm"):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        new, _ = ring.churn(joins, leaves)
+        new.sync()
+        t1 = time.perf_counter()
+        new.build_fingers()
+        new.sync()
+        t2 = time.perf_counter()
+        hashes.append(new.route_table_hash())
+        out[phase] = {"route_ready_ms": (t2 - t0) * 1e3, "churn_ms": (t1 - t0) * 1e3,
+                      "fingers_and_table_ms": (t2 - t1) * 1e3}
+        if phase == "warm":
+            q = 1 << 22
+            keys = torch.empty((q, 2), dtype=torch.int64, device=dev)
+            chordx.fill_splitmix(keys, SEED_KEYS + 0x100)
+            src = (torch.arange(q, device=dev, dtype=torch.int64) % new.n).to(torch.int32)
+            o, h, s = new.route(src, keys)
+            out["new_ring_route_equals_successor"] = bool((o == new.successor(keys)).all().item()) \
+                and int((s != 0).sum().item()) == 0
+            out["new_ring_peers"] = new.n
+        new.close()
+        del new
+    out["table_hash_equal"] = hashes[0] == hashes[1]
+    out["route_ready_ms"] = {"cold": out["cold"]["route_ready_ms"],
+                             "warm": out["warm"]["route_ready_ms"]}
+    out["workload"] = (f"cx_churn of the bench ring: {nj} joins (splitmix 0x5EED0009) + {nj} "
+                       "leaves (distinct peers), then cx_fingers_build (fingers + route table)")
+    out["note"] = ("cold = fresh hipMalloc'd HBM for the new ring's fingers (8 GiB) and route "
+                   "table (64 GiB at 2^24): first-touch page mapping dominates, as in "
+                   "setup_s.fingers_build; warm = the table pool returns the previous epoch's "
+                   "blocks (the steady state of a membership epoch)")
+    return out
+
+
+def main_arc(args):
+    """--mode arc: the arc-sharded layout (SURVEY 8e layout 2) is the headline."""
     world, rank, local = dist.env_rank()
     local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks share a GPU
     torch.cuda.set_device(local)
@@ -189,28 +357,15 @@ def main_arc(args):
     dist.init(backend, dev)
     N = 1 << args.peers_log2
     Q = 1 << args.keys_log2
-    lo, hi = rank * N // world, (rank + 1) * N // world
-    t0 = time.perf_counter()
-    share = torch.empty((N // world, 2), dtype=torch.int64, device=dev)
-    assert N % world == 0
-    chordx.fill_splitmix(share, SEED_RING, offset=lo)
-    if world > 1:
-        cd = torch.device("cpu") if backend == "gloo" else dev
-        ids = torch.empty((N, 2), dtype=torch.int64, device=cd)
-        torch.distributed.all_gather_into_tensor(ids, share.to(cd))
-        ids = ids.to(dev)
-    else:
-        ids = share
-    ring = chordx.Ring(ids, device=local)
-    del ids, share
-    router = ArcRouter(ring, ring.n, rank, world,
-                       comm_device="cpu" if backend == "gloo" else None)
-    torch.cuda.synchronize(dev)
-    t_setup = time.perf_counter() - t0
+    ring, t_gather, t_ring = setup_ring(args, world, rank, dev, backend)
     keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
     q0, q1 = dist.shard(rank, Q)
     chordx.fill_splitmix(keys, SEED_KEYS, offset=q0)
     src = (torch.arange(q0, q1, device=dev, dtype=torch.int64) % ring.n).to(torch.int32)
+    succ = ring.successor(keys)
+    from chordx.arc import ArcRouter
+    router = ArcRouter(ring, ring.n, rank, world,
+                       comm_device="cpu" if backend == "gloo" else None)
     owner = torch.empty(Q, dtype=torch.int32, device=dev)
     hops = torch.empty(Q, dtype=torch.uint8, device=dev)
     status = torch.empty(Q, dtype=torch.uint8, device=dev)
@@ -218,48 +373,25 @@ def main_arc(args):
         router.route(src, keys, owner, hops, status)
     torch.cuda.synchronize(dev)
     router.records_sent = 0
-    dist.barrier(world)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rounds = router.route(src, keys, owner, hops, status)
-    torch.cuda.synchronize(dev)
-    dist.barrier(world)
-    dt = time.perf_counter() - t0
-    dt_max = dist.max_over_ranks(dt, world, dev)
+    _, dt_max = time_steps(lambda: router.route(src, keys, owner, hops, status), args.steps,
+                           world, dev)
     bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
     sent = dist.sum_over_ranks(router.records_sent, world, dev)
     sum_hops = dist.sum_over_ranks(int(hops.to(torch.int64).sum().item()), world, dev)
-    succ = ring.successor(keys)  # exact successor (directory search) of every key
     mismatch = dist.sum_over_ranks(int((succ != owner).sum().item()), world, dev)
     if rank == 0:
         total = world * Q * args.steps
-        line = {
-            "metric": "successor lookups/sec (whole node) + % HBM roofline, 2^24-peer ring, "
-                      "1/2/4/8 GPUs",
-            "value": total / dt_max,
-            "unit": "lookups/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": dt_max * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u128",
-            "data": "synthetic",
-            "config": {"workload": "C4 finger-routed lookups with hop counts, arc-sharded: "
-                                   f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step",
-                       "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
-                       "parallelism": f"arc-sharded route planes x{world}, key-first SoA "
-                                      "all_to_all (20 B out, 8 B back per lookup)"},
-            "rounds_per_step": rounds,
-            "records_exchanged_per_lookup": sent / (world * Q * args.steps),
-            "mean_hops": sum_hops / (world * Q),
-            "bad_status": bad,
-            "route_owner_equals_successor": mismatch == 0,
-            "setup_s": t_setup,
-        }
+        line = line_base(args, world, total / dt_max, dt_max, {
+            "workload": "C4 finger-routed lookups with hop counts, arc-sharded: "
+                        f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step",
+            "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
+            "parallelism": f"arc-sharded route planes x{world}, key-first SoA "
+                           "all_to_all (20 B out, 8 B back per lookup)"})
+        line.update({"rounds_per_step": router.rounds,
+                     "records_exchanged_per_lookup": sent / total,
+                     "mean_hops": sum_hops / (world * Q), "bad_status": bad,
+                     "route_owner_equals_successor": mismatch == 0,
+                     "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring}})
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -280,28 +412,25 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
-    dist.init(os.environ.get("CX_DIST_BACKEND", "nccl"), dev)
+    backend = os.environ.get("CX_DIST_BACKEND", "nccl")
+    dist.init(backend, dev)
     N = 1 << args.peers_log2
     Q = 1 << args.keys_log2
 
-    # ---- setup (untimed): ring, Eytzinger copy, converged finger table ----
-    ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
-    chordx.fill_splitmix(ids, SEED_RING)
-    t0 = time.perf_counter()
-    ring = chordx.Ring(ids, device=local)
-    torch.cuda.synchronize(dev)
-    t_ring = time.perf_counter() - t0
-    del ids
+    # ---- setup (untimed): replicated ring, converged finger + route tables ----
+    ring, t_gather, t_ring = setup_ring(args, world, rank, dev, backend)
     t0 = time.perf_counter()
     ring.build_fingers()
     ring.sync()
     t_fing = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ring.build_fingers()  # same tables again: their HBM is now mapped
+    ring.sync()
+    t_fing_warm = time.perf_counter() - t0
     keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
     q0, q1 = dist.shard(rank, Q)
     chordx.fill_splitmix(keys, SEED_KEYS, offset=q0)
-    gq = torch.arange(q0, q1, device=dev, dtype=torch.int64)
-    src = (gq % ring.n).to(torch.int32)
-    del gq
+    src = (torch.arange(q0, q1, device=dev, dtype=torch.int64) % ring.n).to(torch.int32)
     owner = torch.empty(Q, dtype=torch.int32, device=dev)
     hops = torch.empty(Q, dtype=torch.uint8, device=dev)
     status = torch.empty(Q, dtype=torch.uint8, device=dev)
@@ -332,89 +461,73 @@ def main():
     dt_max = dist.max_over_ranks(dt, world, dev)
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # one cx_route launch per step
 
-    # ---- results ----
+    # ---- results (all reduced over ranks) ----
     bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
-    sum_hops = int(hops.to(torch.int64).sum().item())
-    # gathers the walk issues on this batch: the counting build of the same
-    # kernel, run once after the timed region (same inputs, same outputs)
-    ring.route_counters(True)
-    ring.route(src, keys, out=out)
-    g64, r16, xc, nq = ring.route_counters(False)
-    gathers = g64 + r16 + 2 * xc
-    algo_bytes = Q * BYTES_STREAM + GRANULE * gathers
-    achieved = algo_bytes / (kern_ms * 1e-3)
-    ref_bytes = Q * (REF_STREAM + REF_SRC) + REF_HOP * sum_hops
-    probe = ring.gather_probe()  # request-rate ceiling on this table, this box, this run
-    # exact-successor rate on the same keys (row a5, C2 kernel at C4 size)
-    succ_out = torch.empty(Q, dtype=torch.int32, device=dev)
-    ring.successor(keys, out=succ_out)
-    torch.cuda.synchronize(dev)
+    sum_hops = dist.sum_over_ranks(int(hops.to(torch.int64).sum().item()), world, dev)
+    succ = torch.empty(Q, dtype=torch.int32, device=dev)
+    ring.successor(keys, out=succ)  # exact successor (directory search) of every key
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(3):
-        ring.successor(keys, out=succ_out)
+        ring.successor(keys, out=succ)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     succ_ms = e0.elapsed_time(e1) / 3
-    owner_eq = bool((succ_out == owner).all().item())
-    ring.set_search_variant(0)  # A/B: Eytzinger search with LDS top levels
-    ring.successor(keys, out=succ_out)
-    e0.record(stream)
-    for _ in range(3):
-        ring.successor(keys, out=succ_out)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    eyt_ms = e0.elapsed_time(e1) / 3
-    owner_eq = owner_eq and bool((succ_out == owner).all().item())
-    ring.set_search_variant(2)  # A/B: wave-cooperative 16-ary tree (ballot + popcount)
-    ring.successor(keys, out=succ_out)
-    e0.record(stream)
-    for _ in range(3):
-        ring.successor(keys, out=succ_out)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    wave_ms = e0.elapsed_time(e1) / 3
-    owner_eq = owner_eq and bool((succ_out == owner).all().item())
-    ring.set_search_variant(1)
-    # A/B: the other route kernels on the same batch (bit-identical results)
-    variant_ms = {}
-    for v in (0, 1, 2, 3, 4, 5):
-        ring.set_route_variant(v)
-        ring.route(src, keys, out=out)
-        e0.record(stream)
-        for _ in range(3):
-            ring.route(src, keys, out=out)
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        variant_ms[v] = e0.elapsed_time(e1) / 3
-    ring.set_route_variant(-1)
+    owner_eq = dist.all_over_ranks(bool((succ == owner).all().item()), world, dev)
+    # gathers the walk issues on this batch: the counting build of the same
+    # kernel, run once after the timed region (same inputs, same outputs)
+    ref = (owner.clone(), hops.clone())
+    ring.route_counters(True)
+    ring.route(src, keys, out=out)
+    g64, r16, xc, nq = ring.route_counters(False)
+    counting_same = bool((owner == ref[0]).all().item()) and bool((hops == ref[1]).all().item())
+    gathers = g64 + r16 + 2 * xc
+    algo_bytes = Q * BYTES_STREAM + GRANULE * gathers
+    roof = whole_node_roofline(algo_bytes, kern_ms, world, dev)
+    ref_bytes = dist.sum_over_ranks(Q * (REF_STREAM + REF_SRC), world, dev) + REF_HOP * sum_hops
+    probe = ring.gather_probe()  # request-rate ceiling on this table, this box, this run
     # A/B: the same keys from uniformly random source peers (C4 fixes src = q mod N,
     # whose wave-adjacent sources share lines on the first gathers); owners must not change
     rsrc = torch.empty((Q, 2), dtype=torch.int64, device=dev)
     chordx.fill_splitmix(rsrc, SEED_RANDOM_SRC, offset=q0)
     rsrc = (rsrc[:, 0] & 0x7FFFFFFFFFFFFFFF).remainder(ring.n).to(torch.int32)
     rout = (torch.empty_like(owner), torch.empty_like(hops), torch.empty_like(status))
-    ring.route(rsrc, keys, out=rout)  # own buffers: owner/hops stay the timed run's
+    ring.route(rsrc, keys, out=rout)
     e0.record(stream)
     for _ in range(3):
         ring.route(rsrc, keys, out=rout)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     rsrc_ms = e0.elapsed_time(e1) / 3
-    owner_eq = owner_eq and bool((succ_out == rout[0]).all().item())
+    owner_eq = dist.all_over_ranks(owner_eq and bool((succ == rout[0]).all().item()), world, dev)
     rsrc_bad = int((rout[2] != 0).sum().item())
     del rsrc, rout
 
+    # ---- churn -> route-ready (f2), cold then warm ----
+    churn = None
+    if not args.no_churn:
+        churn = churn_leg(ring, dev)
+        chordx.pool_trim()  # the new rings' blocks are not needed by the arc leg
+        churn["route_ready_ms_max_over_ranks"] = {
+            k: dist.max_over_ranks(v, world, dev) for k, v in churn["route_ready_ms"].items()}
+        churn["table_hash_equal"] = dist.all_over_ranks(churn["table_hash_equal"], world, dev)
+
+    # ---- arc-sharded C4 (all_to_all-v) on the same keys and steps ----
+    arc = None
+    if not args.no_arc:
+        arc = arc_leg(args, ring, src, keys, owner, hops, world, rank, dev, backend)
+
+    # ---- CPU baseline: rank 0, every world size, after the timed region ----
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
         F_host[:] = ring.fingers_device().cpu().numpy().view(np.uint32)
-        cs = Q  # the sample is sized by --cpu-seconds inside cpu_baseline
-        cpu = cpu_baseline(ring, F_host, keys[:cs].cpu().numpy().view(np.uint64),
-                           src[:cs].cpu().numpy().view(np.uint32),
-                           owner[:cs].cpu().numpy().view(np.uint32),
-                           hops[:cs].cpu().numpy(), args.cpu_seconds)
+        cpu = cpu_baseline(ring.ids(), F_host, keys.cpu().numpy().view(np.uint64),
+                           src.cpu().numpy().view(np.uint32),
+                           owner.cpu().numpy().view(np.uint32), hops.cpu().numpy(),
+                           args.cpu_seconds, world)
         del F_host
+    dist.barrier(world)
 
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -425,61 +538,62 @@ def main():
     req = gathers / (kern_ms * 1e-3)
     gather = {"requests_per_s": req, "ceiling": probe, "frac": req / probe,
               "gathers_per_lookup": gathers / Q, "table_gathers": g64, "exact_id_gathers": r16,
-              "exact_hops": xc,
+              "exact_hops": xc, "rank": 0,
               "note": "random 64-B requests the walk issued (counting build, same batch) per "
                       "second of kernel time, vs dependent quad-cooperative 64-B gathers/s "
-                      "measured on the same route table in this run"}
+                      "measured on the same route table in this run (rank 0)"}
 
     if rank == 0:
         total = world * Q * args.steps
-        line = {
-            "metric": "successor lookups/sec (whole node) + % HBM roofline, 2^24-peer ring, "
-                      "1/2/4/8 GPUs",
-            "value": total / dt_max,
-            "unit": "lookups/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": dt_max * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u128",
-            "data": "synthetic",
-            "config": {"workload": "C4 finger-routed lookups with hop counts (per GPU): "
-                                   f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step, "
-                                   "src = q mod N, splitmix seeds 0x5EED0005/0x5EED0006",
-                       "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
-                       "parallelism": f"replicated ring, keys sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "kernel": kernel_name, "kernel_ms": kern_ms,
-                         "algo_bytes_per_launch": algo_bytes,
-                         "algo_model": f"{BYTES_STREAM} B streams per lookup + {GRANULE} B per "
-                                       "random gather issued (counted)"},
+        line = line_base(args, world, total / dt_max, dt_max, {
+            "workload": "C4 finger-routed lookups with hop counts (per GPU): "
+                        f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step, "
+                        "src = q mod N, splitmix seeds 0x5EED0005/0x5EED0006",
+            "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
+            "parallelism": f"ring IDs all-gathered, replicated route tables, keys sharded "
+                           f"x{world} (arc-sharded all_to_all-v layout: `arc`)"})
+        roof.update({
+            "traffic": None if traffic is None else traffic * world,
+            "traffic_note": "PMC FETCH_SIZE + WRITE_SIZE per launch on one GPU "
+                            "(profiles/traffic_route.json) x N",
+            "kernel": kernel_name,
+            "per_gpu": {"achieved": algo_bytes / (kern_ms * 1e-3) / 1e9,
+                        "frac": algo_bytes / (kern_ms * 1e-3) / HBM_PEAK,
+                        "kernel_ms": kern_ms, "algo_bytes_per_launch": algo_bytes,
+                        "traffic": traffic, "rank": 0},
+            "algo_model": f"{BYTES_STREAM} B streams per lookup + {GRANULE} B per random "
+                          "gather issued (counted), summed over ranks"})
+        line.update({
+            "roofline": roof,
             "reference_work_model": {"bytes_per_launch": ref_bytes,
-                                     "GBps": ref_bytes / (kern_ms * 1e-3) / 1e9,
-                                     "note": "SURVEY 8(d): 128 B per hop; hops the window "
-                                             "table resolves without a gather are priced too, "
-                                             "so this is not a byte count of the kernel"},
+                                     "GBps": ref_bytes / (roof["kernel_ms"] * 1e-3) / 1e9,
+                                     "note": "SURVEY 8(d): 128 B per hop, summed over ranks; "
+                                             "hops the window table resolves without a gather "
+                                             "are priced too, so this is not a byte count of "
+                                             "the kernel"},
             "cpu_baseline": cpu,
+            "arc": arc,
+            "churn_route_ready": churn,
             "gather_roofline": gather,
             "route_variant": route_variant,
             "route_table_bytes": table_bytes,
             "route_cz_escapes": cz_escapes,
-            "mean_hops": sum_hops / Q,
+            "mean_hops": sum_hops / (world * Q),
             "bad_status": bad,
             "route_owner_equals_successor": owner_eq,
+            "counting_build_same_results": counting_same,
             "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
-            "exact_successor_eytzinger_lookups_per_s": Q / (eyt_ms * 1e-3),
-            "exact_successor_wave16_lookups_per_s": Q / (wave_ms * 1e-3),
-            "route_variant_kernel_ms": variant_ms,
             "route_random_src": {"kernel_ms": rsrc_ms, "lookups_per_s": Q / (rsrc_ms * 1e-3),
                                  "bad_status": rsrc_bad,
                                  "note": "same keys and kernel, src uniform in [0, N) "
                                          "(splitmix 0x5EED000A) instead of q mod N"},
-            "setup_s": {"ring_sort": t_ring, "fingers_build": t_fing},
-        }
+            "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring,
+                        "fingers_build": t_fing, "fingers_build_again": t_fing_warm,
+                        "note": "fingers_build = converged fingers + route table on fresh "
+                                "HBM (first touch of 72 GiB); fingers_build_again = the same "
+                                "build into the now-mapped tables"},
+            "ab_variants": "benches/bench_route.py --variants (route and search A/B kernels)",
+        })
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

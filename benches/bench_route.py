@@ -3,7 +3,12 @@
 keys, src = q mod N), default route kernel, HIP events over `reps` launches
 after warm-up, repeated `rounds` times (min and median reported); checks owner
 == successor.  Prints one JSON line.
-    python benches/bench_route.py [reps] [rounds]
+    python benches/bench_route.py [reps] [rounds] [--variants]
+--variants also times the A/B kernels on the same batch (moved out of bench.py,
+whose driver run keeps its HBM for the arc and churn legs): route variants
+0..5 (finger + ring gathers, route table, packed tables, lookahead tree,
+pattern-keyed window table; each builds its own table, up to 32 GiB) and the
+exact-successor searches (directory, Eytzinger, wave-cooperative 16-ary tree).
 CX_SRC=random draws each lookup's source peer uniformly instead (splitmix,
 seed 0x5EED000A): the first hops of a wave no longer leave adjacent peers.
 """
@@ -20,9 +25,44 @@ import torch  # noqa: E402
 import chordx  # noqa: E402
 
 
+def timed(fn, reps=3):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def variants(ring, src, keys, owner):
+    """A/B kernels on the same batch; every result must equal the default's."""
+    Q = keys.shape[0]
+    out = {"route_variant_kernel_ms": {}, "search_lookups_per_s": {}}
+    res = (torch.empty_like(owner), torch.empty(Q, dtype=torch.uint8, device="cuda"),
+           torch.empty(Q, dtype=torch.uint8, device="cuda"))
+    same = True
+    for v in (0, 1, 2, 3, 4, 5):
+        ring.set_route_variant(v)
+        out["route_variant_kernel_ms"][v] = timed(lambda: ring.route(src, keys, out=res))
+        same = same and bool((res[0] == owner).all())
+    ring.set_route_variant(-1)
+    succ = torch.empty_like(owner)
+    for v, name in ((1, "directory"), (0, "eytzinger"), (2, "wave16"), (3, "eyt16")):
+        ring.set_search_variant(v)
+        ms = timed(lambda: ring.successor(keys, out=succ))
+        out["search_lookups_per_s"][name] = Q / (ms * 1e-3)
+        same = same and bool((succ == owner).all())
+    ring.set_search_variant(1)
+    out["variants_equal_default"] = same
+    return out
+
+
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+    reps = int(argv[0]) if len(argv) > 0 else 10
+    rounds = int(argv[1]) if len(argv) > 1 else 5
     N, Q = 1 << 24, 1 << 25
     ids = torch.empty((N, 2), dtype=torch.int64, device="cuda")
     chordx.fill_splitmix(ids, 0x5EED0005)
@@ -55,11 +95,14 @@ def main():
         torch.cuda.synchronize()
         ms.append(a.elapsed_time(b) / reps)
     ok = bool((owner == ring.successor(keys)).all()) and int((status != 0).sum()) == 0
-    print(json.dumps({"lib": os.path.basename(os.environ.get("CHORDX_LIB", "default")),
-                      "src": src_kind,
-                      "ms_min": min(ms), "ms_median": statistics.median(ms),
-                      "lookups_per_s": Q / (min(ms) * 1e-3), "probe": ring.gather_probe(),
-                      "owner_ok": ok, "mean_hops": float(hops.double().mean())}), flush=True)
+    rec = {"lib": os.path.basename(os.environ.get("CHORDX_LIB", "default")),
+           "src": src_kind,
+           "ms_min": min(ms), "ms_median": statistics.median(ms),
+           "lookups_per_s": Q / (min(ms) * 1e-3), "probe": ring.gather_probe(),
+           "owner_ok": ok, "mean_hops": float(hops.double().mean())}
+    if "--variants" in sys.argv:
+        rec.update(variants(ring, src, keys, owner))
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

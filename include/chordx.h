@@ -83,6 +83,15 @@ int cx_version(void);
 const char *cx_last_error(void);
 /* Number of visible HIP devices (0 without a GPU; never fails). */
 int cx_device_count(int *count);
+/* Table pool: a destroyed ring's large tables (finger table, route tables,
+ * arc planes, build temporaries >= 16 MiB) are kept per process, up to
+ * CX_POOL_CAP_GIB GiB (environment, default 96, 0 = off), for the next ring of
+ * the same size -- a membership epoch reuses the previous epoch's HBM.  Any
+ * allocation that fails releases the device's idle blocks and retries.
+ * cx_pool_trim releases every idle block now (all devices); cx_pool_info
+ * reports the idle blocks and their bytes. */
+int cx_pool_trim(void);
+int cx_pool_info(uint64_t *blocks, uint64_t *bytes);
 
 /* ---- ring lifecycle (a13) ---------------------------------------------
  * Replaces the converged RemotePeerList/successor ring that Join/Stabilize/
@@ -147,7 +156,10 @@ int cx_peer_state_upload(cx_ring *ring, const cx_u128 *min_keys, const uint32_t 
  * RemotePeerList whose starting key is the peer's id, abstract_chord_peer.cpp:
  * 25), NULL = the converged lists (next min(ns, n-1) peers clockwise).
  * forward_rule: cx_fwd_rule.  0 <= ns <= 64.  Validated before it replaces the
- * current state; switches cx_route to the literal walk. */
+ * current state; switches cx_route to the literal walk.  alive == NULL and
+ * succ_lists == NULL together reset the ring to "every peer alive, converged
+ * lists": the literal walk is dropped again (unless cx_peer_state_upload or
+ * cx_fingers_upload state remains) and the arc calls accept the ring. */
 int cx_liveness_upload(cx_ring *ring, const uint8_t *alive, const uint32_t *succ_lists, int ns,
                        int forward_rule, int memkind);
 

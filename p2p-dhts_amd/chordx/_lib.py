@@ -35,7 +35,7 @@ CX_FWD_CHORD, CX_FWD_DHASH = 0, 1
 
 # Every symbol include/chordx.h declares (checked by tests/test_abi.py).
 EXPORTS = (
-    "cx_version", "cx_last_error", "cx_device_count",
+    "cx_version", "cx_last_error", "cx_device_count", "cx_pool_trim", "cx_pool_info",
     "cx_ring_create", "cx_ring_destroy", "cx_ring_size", "cx_ring_ids",
     "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_use_own_stream", "cx_ring_sync",
     "cx_successor", "cx_predecessor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
@@ -80,6 +80,8 @@ def lib() -> ctypes.CDLL:
         "cx_version": ([], i),
         "cx_last_error": ([], ctypes.c_char_p),
         "cx_device_count": ([ctypes.POINTER(ctypes.c_int)], i),
+        "cx_pool_trim": ([], i),
+        "cx_pool_info": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], i),
         "cx_ring_create": ([vp, sz, i, i, pp], i),
         "cx_ring_destroy": ([vp], i),
         "cx_ring_size": ([vp, ctypes.POINTER(ctypes.c_size_t)], i),
@@ -139,6 +141,18 @@ def check(rc: int) -> None:
     if rc != CX_OK:
         msg = lib().cx_last_error()
         raise ChordError(rc, msg.decode() if msg else f"chordx error {rc}")
+
+
+def pool_trim() -> None:
+    """Release the table pool's idle HBM blocks (cx_pool_trim)."""
+    check(lib().cx_pool_trim())
+
+
+def pool_info():
+    """(idle blocks, idle bytes) held by the table pool (cx_pool_info)."""
+    b, n = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().cx_pool_info(ctypes.byref(b), ctypes.byref(n)))
+    return b.value, n.value
 
 
 def device_count() -> int:

@@ -118,28 +118,33 @@ class ArcRouter:
         """Key-first routing in structure-of-arrays form (module docstring);
         returns the number of exchange rounds (1 on a single rank, else 2).
 
-        The batch is cut into `chunks` pieces (default: one per 2^22 lookups,
-        at most 4), partitioned up front; one all_gather carries every
-        piece's counts.  Piece c + 1's lookups travel while piece c is walked,
-        and piece c's answers travel back while piece c + 1 is walked (the
-        collectives run on RCCL's stream, the walks on the current stream)."""
+        The batch is cut into pieces (default: one per 2^22 lookups, at most
+        4; `chunks` / self.chunks fix the count), partitioned up front; one
+        all_gather carries every piece's counts.  Piece c + 1's lookups travel
+        while piece c is walked, and piece c's answers travel back while piece
+        c + 1 is walked (the collectives run on RCCL's stream, the walks on the
+        current stream).  Ranks may hold different batch sizes (or none): each
+        rank cuts its own batch, the gathered row is padded to a fixed number
+        of piece slots, and every rank runs max-over-ranks pieces, the missing
+        ones empty -- so all ranks issue the same collectives."""
         eng = self.engine
         if self.world == 1:
             eng.arc_deliver(eng.arc_route(src, keys), None, owner, hops, status)
             self.rounds = 1
             return 1
         q = int(keys.shape[0])
-        k = chunks if chunks is not None else self.chunks
-        if k is None:
-            k = max(1, min(4, q >> 22))
-        k = max(1, min(int(k), max(q, 1)))
+        fixed = chunks if chunks is not None else self.chunks
+        kmax = max(4, int(fixed)) if fixed is not None else 4  # piece slots per rank
+        k = int(fixed) if fixed is not None else max(1, min(4, q >> 22))
+        k = max(1, min(k, kmax, max(q, 1)))
         cut = [c * q // k for c in range(k + 1)]
         parts = [eng.arc_partition(self.world, src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]])
                  for c in range(k)]
         dev = self.comm_device if self.comm_device is not None else parts[0][0].device
         G = self.world
-        mine = torch.tensor([x for p in parts for x in p[3]], dtype=torch.int64, device=dev)
-        mat = torch.empty((G, k * G), dtype=torch.int64, device=dev)
+        row = [k] + [x for p in parts for x in p[3]] + [0] * ((kmax - k) * G)
+        mine = torch.tensor(row, dtype=torch.int64, device=dev)
+        mat = torch.empty((G, 1 + kmax * G), dtype=torch.int64, device=dev)
         tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
         if mat.is_cuda:
             if self._mat_host is None or self._mat_host.shape != mat.shape:
@@ -147,7 +152,13 @@ class ArcRouter:
             self._mat_host.copy_(mat, non_blocking=True)
             torch.cuda.current_stream(mat.device).synchronize()
             mat = self._mat_host
-        recv = [[int(mat[r, c * G + self.rank]) for r in range(G)] for c in range(k)]
+        kg = int(mat[:, 0].max())  # pieces every rank runs
+        recv = [[int(mat[r, 1 + c * G + self.rank]) for r in range(G)] for c in range(kg)]
+        if kg > k:  # this rank's extra pieces are empty
+            e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=keys.device),
+                 [0] * G)
+            parts += [e] * (kg - k)
+            cut += [q] * (kg - k)
 
         def send(c):
             sk, ss, _, cnt = parts[c]
@@ -155,15 +166,15 @@ class ArcRouter:
 
         inflight = send(0)
         backs = []
-        for c in range(k):
+        for c in range(kg):
             (rk, wk), (rs, ws) = inflight
             rk = self._land(rk, wk, parts[c][0])
             rs = self._land(rs, ws, parts[c][1])
-            if c + 1 < k:
+            if c + 1 < kg:
                 inflight = send(c + 1)
             res = eng.arc_route(rs, rk)
             backs.append(self._a2a(res, parts[c][3], recv[c], dev))
-        for c in range(k):
+        for c in range(kg):
             back = self._land(backs[c][0], backs[c][1], parts[c][2])
             sl = slice(cut[c], cut[c + 1])
             eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],

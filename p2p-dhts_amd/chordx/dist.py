@@ -39,10 +39,17 @@ def barrier(world: int):
         tdist.barrier()
 
 
+def _dev(device):
+    """Reduction tensors live on the GPU for RCCL and on the host for gloo."""
+    if device is None or tdist.get_backend() == "gloo":
+        return None
+    return device
+
+
 def max_over_ranks(x: float, world: int, device=None) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64, device=_dev(device))
     tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     return float(t.item())
 
@@ -50,6 +57,24 @@ def max_over_ranks(x: float, world: int, device=None) -> float:
 def sum_over_ranks(x: int, world: int, device=None) -> int:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.int64, device=device)
+    t = torch.tensor([x], dtype=torch.int64, device=_dev(device))
     tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
     return int(t.item())
+
+
+def all_over_ranks(ok: bool, world: int, device=None) -> bool:
+    """True iff `ok` holds on every rank."""
+    return sum_over_ranks(0 if ok else 1, world, device) == 0
+
+
+def gather_ids(share, world: int, backend: str):
+    """The replicated ring's IDs: every rank generates its 1/world share and
+    one all_gather (RCCL over xGMI; gloo on the host) replicates them
+    (the ring IDs are replicated with one AllGather)."""
+    if world == 1:
+        return share
+    cd = torch.device("cpu") if backend == "gloo" else share.device
+    ids = torch.empty((share.shape[0] * world,) + tuple(share.shape[1:]), dtype=share.dtype,
+                      device=cd)
+    tdist.all_gather_into_tensor(ids, share.to(cd))
+    return ids.to(share.device)

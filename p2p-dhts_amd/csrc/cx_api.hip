@@ -56,7 +56,15 @@ std::mutex g_pool_mu;
 std::vector<PoolEnt> g_pool;
 size_t g_pool_bytes = 0;
 constexpr size_t POOL_MIN = (size_t)16 << 20;
-constexpr size_t POOL_CAP = (size_t)96 << 30;
+// pool cap: CX_POOL_CAP_GIB (default 96; 0 disables pooling)
+size_t pool_cap() {
+    static const size_t cap = [] {
+        const char *e = getenv("CX_POOL_CAP_GIB");
+        const long v = e ? atol(e) : 96;
+        return (size_t)(v < 0 ? 0 : v) << 30;
+    }();
+    return cap;
+}
 
 void pool_trim_locked(int device) {
     for (size_t k = 0; k < g_pool.size();) {
@@ -107,7 +115,7 @@ void table_free(int device, void *p, size_t bytes) {
     if (!p) return;
     if (bytes >= POOL_MIN) {
         std::lock_guard<std::mutex> g(g_pool_mu);
-        while (g_pool_bytes + bytes > POOL_CAP && !g_pool.empty()) {  // oldest first
+        while (g_pool_bytes + bytes > pool_cap() && !g_pool.empty()) {  // oldest first
             int cur = 0;
             (void)hipGetDevice(&cur);
             (void)hipSetDevice(g_pool.front().device);
@@ -116,7 +124,7 @@ void table_free(int device, void *p, size_t bytes) {
             g_pool_bytes -= g_pool.front().bytes;
             g_pool.erase(g_pool.begin());
         }
-        if (g_pool_bytes + bytes <= POOL_CAP) {
+        if (g_pool_bytes + bytes <= pool_cap()) {
             g_pool.push_back(PoolEnt{device, bytes, p});
             g_pool_bytes += bytes;
             return;
@@ -124,15 +132,44 @@ void table_free(int device, void *p, size_t bytes) {
     }
     (void)hipFree(p);
 }
+
+// Plain hipMalloc that releases the idle pool blocks of the current device
+// and retries once when HBM runs out (the pool must never be the reason an
+// allocation outside it fails).
+hipError_t dev_malloc(void **p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        if (g_pool.empty()) return e;
+        pool_trim_locked(dev);
+    }
+    e = hipMalloc(p, bytes);
+    if (e != hipSuccess) *p = nullptr;
+    return e;
+}
+template <class T>
+hipError_t dev_malloc(T **p, size_t bytes) {
+    return dev_malloc(reinterpret_cast<void **>(p), bytes);
+}
 }  // namespace
 
 struct DBuf {
     void *p = nullptr;
     size_t pooled = 0;  // > 0: a table-pool block of this size (build temporaries >= 1 GiB)
+    hipStream_t user = nullptr;  // stream whose work uses a pooled block
     ~DBuf() { drop(); }
     void drop() {
         if (!p) return;
         if (pooled) {
+            // a pooled block goes back to the pool only after the work queued
+            // on it has finished (hipFree would wait; the pool does not), so
+            // another ring's build can never get it while kernels still use it
+            // -- on the error paths too, where the caller returns early
+            (void)hipStreamSynchronize(user);
             int dev = 0;
             (void)hipGetDevice(&dev);
             table_free(dev, p, pooled);
@@ -141,17 +178,21 @@ struct DBuf {
         }
         p = nullptr;
         pooled = 0;
+        user = nullptr;
     }
     hipError_t alloc(size_t bytes) {
         drop();
-        return hipMalloc(&p, bytes ? bytes : 16);
+        return dev_malloc(&p, bytes ? bytes : 16);
     }
     // through the table pool: build temporaries of the same size recur every
-    // membership epoch (the caller synchronises before the buffer is dropped)
-    hipError_t alloc_pooled(size_t bytes) {
+    // membership epoch; `stream` is the stream the block's users run on
+    hipError_t alloc_pooled(size_t bytes, hipStream_t stream) {
         drop();
         hipError_t e = table_alloc(&p, bytes ? bytes : 16);
-        if (e == hipSuccess) pooled = bytes ? bytes : 16;
+        if (e == hipSuccess) {
+            pooled = bytes ? bytes : 16;
+            user = stream;
+        }
         return e;
     }
     template <class T>
@@ -376,7 +417,7 @@ int alloc_ring(int device, cx_ring **out) {
     r->stream = r->own_stream;
     static std::atomic<uint64_t> next_serial{1};
     r->serial = next_serial++;
-    e = hipMalloc(&r->d_scratch, 1024);
+    e = dev_malloc(&r->d_scratch, 1024);
     if (e != hipSuccess) {
         (void)hipStreamDestroy(r->own_stream);
         delete r;
@@ -473,7 +514,7 @@ void route_geometry(cx_ring *r) {
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
                          DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     fv = cxk::FingerView::rows(r->d_fingers);
-    hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t));
+    hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t), s);
     if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
     if (e0 != hipSuccess) return e0;
     const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
@@ -482,7 +523,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         fv = cxk::FingerView::planes(ft_pre, r->n, L, nl);
     } else {
         if (r->table_build == 1 ||
-            ft.alloc_pooled((size_t)nl * r->n * sizeof(uint32_t)) != hipSuccess) {
+            ft.alloc_pooled((size_t)nl * r->n * sizeof(uint32_t), s) != hipSuccess) {
             (void)hipGetLastError();
             return hipSuccess;
         }
@@ -491,7 +532,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
     if (r->table_build == 0 &&
-        c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t)) == hipSuccess) {
+        c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t), s) == hipSuccess) {
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) fv.C2 = c2.as<uint32_t>();
     }
@@ -729,7 +770,7 @@ namespace {
 // BFS -> sorted index table of the Eytzinger copy (search variant 3), lazy.
 int eyt_rank_view(cx_ring *r, hipStream_t s) {
     if (r->d_eyt_rank) return CX_OK;
-    CX_HIP(hipMalloc(&r->d_eyt_rank, (r->n + 1) * sizeof(uint32_t)));
+    CX_HIP(dev_malloc(&r->d_eyt_rank, (r->n + 1) * sizeof(uint32_t)));
     CX_HIP(cxk::eyt_rank_build(r->n, r->d_eyt_rank, s));
     return CX_OK;
 }
@@ -737,7 +778,7 @@ int eyt_rank_view(cx_ring *r, hipStream_t s) {
 int stree_view(cx_ring *r, cxk::STreeView &st, hipStream_t s) {
     st = cxk::stree_plan(r->d_ring, r->n, r->d_stree);
     if (!r->d_stree && st.words) {
-        if (hipMalloc(&r->d_stree, st.words * sizeof(cell128)) != hipSuccess) {
+        if (dev_malloc(&r->d_stree, st.words * sizeof(cell128)) != hipSuccess) {
             r->d_stree = nullptr;
             return fail(CX_E_NOMEM, "hipMalloc of the 16-ary search levels failed");
         }
@@ -783,7 +824,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
     SearchView fv = ring->sv();
     fv.dir = ring->d_dir;
     if (!search_only && !ring->d_ring_key) {
-        if (hipMalloc(&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
+        if (dev_malloc(&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
             CX_HIP(cxk::ring_slice_build(ring->d_ring, ring->n, cxk::finger_key_shift(ring->n),
                                          ring->d_ring_key, s));
         else
@@ -791,7 +832,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
     }
     DBuf fws;
     const bool streaming = !search_only && ring->d_ring_key &&
-                           fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n)) == hipSuccess;
+                           fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n), s) == hipSuccess;
     CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
                               streaming ? fws.p : nullptr, ring->d_fingers, s, ft, ft_l, ft_done));
     ring->fingers_converged = true;
@@ -845,14 +886,14 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     bool ft_done = false;
     const int ft_l = ring->rt_l0 - 5;
     if (ring->variant() == 5 && ring->table_build == 0 && ft_l >= 64 &&
-        ft_pre.alloc_pooled((size_t)(CX_FINGERS - ft_l) * ring->n * sizeof(uint32_t)) != hipSuccess) {
+        ft_pre.alloc_pooled((size_t)(CX_FINGERS - ft_l) * ring->n * sizeof(uint32_t), s) != hipSuccess) {
         (void)hipGetLastError();
         ft_pre.p = nullptr;
     }
     if ((rc = build_fingers_table(ring, s, ft_pre.as<uint32_t>(), ft_l, &ft_done))) return rc;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
-        hipMalloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
+        dev_malloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
     if (ring->d_ring_ext) CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
     // the default route kernel's table is built now (outside any timed query)
@@ -948,6 +989,19 @@ int cx_liveness_upload(cx_ring *ring, const uint8_t *alive, const uint32_t *succ
     int rc = use_device(ring);
     if (rc) return rc;
     hipStream_t s = ring->stream;
+    if (!alive && !succ_lists) {
+        // reset: every peer alive with the converged lists = the converged
+        // walk again (the route table and the arc calls apply once more)
+        CX_HIP(hipStreamSynchronize(s));
+        (void)hipFree(ring->d_alive);
+        (void)hipFree(ring->d_succs);
+        ring->d_alive = nullptr;
+        ring->d_succs = nullptr;
+        ring->succ_ns = 0;
+        ring->fwd_rule = CX_FWD_CHORD;
+        ring->liveness = false;
+        return CX_OK;
+    }
     const hipMemcpyKind kind =
         memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     DBuf al, sl;
@@ -1210,7 +1264,7 @@ int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_
             while (((size_t)1 << kb) < Mmax) ++kb;  // >= 2^kb / 2 >= the merged size
             const size_t bytes = ((size_t)1 << kb) * 32;
             DBuf ws, lo, sw;
-            CX_HIP(ws.alloc_pooled(cxk::churn_dir_workspace_bytes(old_ring->n, new_ring->n)));
+            CX_HIP(ws.alloc_pooled(cxk::churn_dir_workspace_bytes(old_ring->n, new_ring->n), s));
             CX_HIP(lo.alloc((((size_t)1 << kb) + 1) * sizeof(uint32_t)));
             CX_HIP(sw.alloc(cxk::scan_workspace_words(Mmax + 1) * sizeof(uint32_t)));
             void *cdp = nullptr;
@@ -1546,11 +1600,14 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
     if (memkind == CX_MEM_HOST) {
         if ((rc = finish_out(out_len, dlen, blocks, memkind, s))) return rc;
         if ((rc = finish_out(out, dout, (size_t)(segs * m), memkind, s))) return rc;
-        uint32_t e = 0;
-        CX_HIP(hipMemcpy(&e, err, sizeof(e), hipMemcpyDeviceToHost));
-        CX_CHECK(e == 0, CX_E_HIP,
-                 "IDA decode: index bounds check failed (flags " + std::to_string(e) + ")");
     }
+    // the bounds / guard word, on both memory kinds (4 B and one wait on the
+    // null stream; the next call clears it, so it is read before returning)
+    uint32_t e = 0;
+    CX_HIP(hipMemcpyAsync(&e, err, sizeof(e), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    CX_CHECK(e == 0, CX_E_HIP,
+             "IDA decode: index bounds check failed (flags " + std::to_string(e) + ")");
     return CX_OK;
 }
 
@@ -1584,7 +1641,7 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     }
     route_geometry(ring);
     if (!ring->d_ring_ext) {
-        CX_HIP(hipMalloc(&ring->d_ring_ext, (n + 1) * sizeof(cell128)));
+        CX_HIP(dev_malloc(&ring->d_ring_ext, (n + 1) * sizeof(cell128)));
         CX_HIP(cxk::ring_ext_build(ring->d_ring, n, ring->d_ring_ext, s));
     }
     const int l0 = ring->rt_l0;
@@ -1656,7 +1713,7 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     }
     (void)hipFree(ring->d_arc_bounds);
     ring->d_arc_bounds = nullptr;
-    CX_HIP(hipMalloc(&ring->d_arc_bounds, b.size() * sizeof(ArcBound)));
+    CX_HIP(dev_malloc(&ring->d_arc_bounds, b.size() * sizeof(ArcBound)));
     CX_HIP(hipMemcpy(ring->d_arc_bounds, b.data(), b.size() * sizeof(ArcBound),
                      hipMemcpyHostToDevice));
     CX_HIP(hipStreamSynchronize(s));
@@ -1886,7 +1943,7 @@ int cxi_route_counters(cx_ring *ring, int enable, uint64_t *out) {
     int rc = use_device(ring);
     if (rc) return rc;
     hipStream_t s = ring->stream;
-    if (!ring->d_stats) CX_HIP(hipMalloc(&ring->d_stats, 4 * sizeof(unsigned long long)));
+    if (!ring->d_stats) CX_HIP(dev_malloc(&ring->d_stats, 4 * sizeof(unsigned long long)));
     if (enable) {
         CX_HIP(hipMemsetAsync(ring->d_stats, 0, 4 * sizeof(unsigned long long), s));
         ring->counting = true;
@@ -1962,9 +2019,18 @@ int cxi_set_table_build(cx_ring *ring, int variant) {
 }
 
 // Releases every pooled table (all devices).
-int cxi_pool_trim(void) {
+int cx_pool_trim(void) {
     std::lock_guard<std::mutex> g(g_pool_mu);
     pool_trim_locked(-1);
+    return CX_OK;
+}
+int cxi_pool_trim(void) { return cx_pool_trim(); }
+
+int cx_pool_info(uint64_t *blocks, uint64_t *bytes) {
+    CX_CHECK(blocks && bytes, CX_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    *blocks = g_pool.size();
+    *bytes = g_pool_bytes;
     return CX_OK;
 }
 

@@ -4740,7 +4740,10 @@ __global__ __launch_bounds__(256) void k_ida_decode(const uint16_t *frags, const
             if (c + D < c1) issue(sl[k], c + D);  // loads overlap this chunk's math
             const uint32_t r0 = __shfl(r, 0);  // r < runs (checked at issue)
             const bool uniform = __ballot(r != r0) == 0;
-            if (uniform && r0 != staged) {  // stage the shared inverse (wave-uniform branch)
+            // stage the shared inverse (wave-uniform branch); a run whose
+            // inverse failed ("N is not invertible") has rows k_ida_inverse
+            // never wrote and no lane that would read them: not staged
+            if (uniform && r0 != staged && okf[r0]) {
                 __builtin_amdgcn_wave_barrier();  // previous readers of As are done
                 const int32_t *A = inv + (size_t)r0 * m * m;
                 for (int t = lane; t < m * IDA_AROW; t += 64) {

@@ -59,12 +59,20 @@ def test_c4_every_lookup_reaches_the_successor(c4):
     assert 11.5 < mean < 12.3  # ~ log2(N)/2 on a uniform ring
 
 
-def test_c4_oracle_walk_and_fingers_on_samples(O, c4):
-    ring, keys, src, owner, hops, status = c4
+@pytest.fixture(scope="module")
+def c4_host(O, c4):
+    """The oracle's C4 ring and the engine's finger table on the host."""
+    ring = c4[0]
     want_ring = O.ring_build(O.splitmix_keys(0x5EED0005, N4))
+    F = ring.fingers_device().cpu().numpy().view(np.uint32)
+    return want_ring, F
+
+
+def test_c4_oracle_walk_and_fingers_on_samples(O, c4, c4_host):
+    ring, keys, src, owner, hops, status = c4
+    want_ring, F = c4_host
     ids = ring.ids()
     assert (ids == want_ring).all()
-    F = ring.fingers_device().cpu().numpy().view(np.uint32)
     for p0 in (0, N4 // 2 - 2048, N4 - 4096):
         assert (F[p0:p0 + 4096] == O.fingers(want_ring, rows=(p0, p0 + 4096))).all(), p0
     sample = 1 << 20
@@ -74,6 +82,55 @@ def test_c4_oracle_walk_and_fingers_on_samples(O, c4):
     assert (ws == 0).all()
     assert (owner[:sample].cpu().numpy().view(np.uint32) == wo).all()
     assert (hops[:sample].cpu().numpy() == wh).all()
+
+
+@pytest.mark.parametrize("d", [0, 3, 7])
+def test_c4_arc_layout_g8(O, c4, c4_host, d):
+    """C4 as BASELINE.json states it, on one GPU: the 2^24 ring's arc layout for
+    G = 8 ranks (top levels replicated, lower levels for the arc + its 2^122
+    halo), rank d's received lookups -- the pieces that cx_arc_partition of
+    each of the 8 origin ranks' 2^22 C4 keys sends to d -- walked by
+    cx_arc_route and delivered by cx_arc_deliver: owner / hops / status equal
+    the replicated cx_route's on every received lookup, and the oracle's
+    literal walk (chord_peer.cpp:185-211) on a 2^18 sample."""
+    import torch
+    ring, keys, src, owner, hops, status = c4
+    want_ring, F = c4_host
+    G, per = 8, 1 << 22
+    ring.arc_build(G, d)
+    top, rows, plane_bytes = ring.arc_info()
+    assert top == 6 and N4 // G < rows < N4 // G + N4 // 32  # the arc plus its halo
+    rk, rs, total = [], [], 0
+    for r in range(G):
+        sl = slice(r * per, (r + 1) * per)
+        sk, ss, perm, counts = ring.arc_partition(G, src[sl], keys[sl])
+        assert sum(counts) == per
+        assert torch.equal(torch.sort(perm.long()).values, torch.arange(per, device="cuda:0"))
+        off = sum(counts[:d])
+        rk.append(sk[off:off + counts[d]])
+        rs.append(ss[off:off + counts[d]])
+        total += counts[d]
+    rk, rs = torch.cat(rk), torch.cat(rs)
+    assert abs(total - per) < per // 50  # about an eighth of 2^25 lookups
+    # every received key's owner lies in arc d
+    lo, hi = d * N4 // G, (d + 1) * N4 // G
+    succ = ring.successor(rk)
+    assert bool(((succ >= lo) & (succ < hi)).all())
+    res = ring.arc_route(rs, rk)
+    ao = torch.full((total,), -7, dtype=torch.int32, device="cuda:0")
+    ah = torch.full((total,), 77, dtype=torch.uint8, device="cuda:0")
+    ast = torch.full((total,), 9, dtype=torch.uint8, device="cuda:0")
+    ring.arc_deliver(res, None, ao, ah, ast)
+    wo, wh, ws = ring.route(rs, rk)
+    torch.cuda.synchronize()
+    assert torch.equal(ao, wo) and torch.equal(ah, wh) and torch.equal(ast, ws)
+    assert int((ast != 0).sum()) == 0 and torch.equal(ao, succ)
+    sample = 1 << 18
+    oo, oh, os_ = O.route(O.Peers(want_ring, F), rs[:sample].cpu().numpy().view(np.uint32),
+                          rk[:sample].cpu().numpy().view(np.uint64))
+    assert (os_ == 0).all()
+    assert (ao[:sample].cpu().numpy().view(np.uint32) == oo).all()
+    assert (ah[:sample].cpu().numpy() == oh).all()
 
 
 def test_c5_full_size_churn_and_misplaced_scan(O):

@@ -121,3 +121,28 @@ def test_rejected_uploads_leave_state(cx, O):
         assert (a == b).all()
     wo, wh, ws = O.route(O.Peers(ids, F2), src, keys)
     assert (after[0] == wo).all() and (after[1] == wh).all()
+
+
+def test_liveness_reset_restores_converged_walk(cx, O):
+    """cx_liveness_upload(NULL, NULL) resets the ring to "all alive, converged
+    lists": route() leaves the literal walk (the route table applies again,
+    same owners/hops as before any upload) and the arc calls accept the ring
+    (the literal walk used to stay on for good)."""
+    ids = O.ring_build(O.splitmix_keys(91, 3000))
+    ring = cx.Ring(ids)
+    ring.build_fingers()
+    keys = O.splitmix_keys(92, 4000)
+    src = (np.arange(4000) % len(ids)).astype(np.uint32)
+    base = ring.route(src, keys)
+    alive = np.ones(len(ids), np.uint8)
+    alive[::7] = 0
+    ring.upload_liveness(alive=alive, rule=cx.CX_FWD_DHASH)
+    assert ring.route_info()[0] == -1          # literal walk
+    with pytest.raises(cx.ChordError):
+        ring.arc_build(2, 0)
+    ring.upload_liveness()                     # reset
+    assert ring.route_info()[0] == 5           # converged table walk again
+    again = ring.route(src, keys)
+    for a, b in zip(base, again):
+        assert (a == b).all()
+    ring.arc_build(2, 0)                       # accepted after the reset

@@ -192,7 +192,7 @@ class OracleArcEngine:
 
 
 def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="records",
-                chunks=None):
+                chunks=None, sizes=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import sys
@@ -208,7 +208,9 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="reco
     dist.init("gloo")
     ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
     P = O.Peers(ring, O.fingers(ring, threads=2))
-    keys = O.splitmix_keys(0x5EED0006, per_rank, offset=rank * per_rank)
+    if sizes is not None:  # uneven per-rank batches (one may be empty)
+        per_rank = sizes[rank]
+    keys = O.splitmix_keys(0x5EED0006, per_rank, offset=rank * 1000)
     src = torch.from_numpy(((np.arange(per_rank) * 7 + rank) % len(ring)).astype(np.int32))
     owner = torch.full((per_rank,), -9, dtype=torch.int32)
     hops = torch.zeros(per_rank, dtype=torch.uint8)
@@ -236,7 +238,7 @@ def test_arc_router_protocol_gloo(world, key_first, protocol, chunks):
     ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
     P = O.Peers(ring, O.fingers(ring))
     for r in range(world):
-        keys = O.splitmix_keys(0x5EED0006, per_rank, offset=r * per_rank)
+        keys = O.splitmix_keys(0x5EED0006, per_rank, offset=r * 1000)
         src = ((np.arange(per_rank) * 7 + r) % len(ring)).astype(np.uint32)
         ow, hp, st = O.route(P, src, keys)
         assert out[r][0] == ow.tolist() and out[r][1] == hp.tolist()
@@ -244,6 +246,30 @@ def test_arc_router_protocol_gloo(world, key_first, protocol, chunks):
         # records: walk -> result -> home, then drained; soa: there and back
         assert out[r][3] == (3 if protocol == "records" else 2)
         assert out[r][4] > 0            # records crossed ranks
+
+
+@pytest.mark.parametrize("chunks", [None, 3])
+def test_arc_router_soa_uneven_batches_gloo(chunks):
+    """Ranks with different batch sizes, one of them empty, run the same
+    collectives (the piece count is agreed in the count all_gather) and every
+    lookup still equals the oracle walk (route_soa hung when the
+    local batch size chose the piece count)."""
+    import oracle as O
+    world, sizes = 3, [700, 0, 350]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_arc_worker, args=(world, _free_port(), 0, out, True, "soa", chunks,
+                                          sizes),
+                       nprocs=world, join=True, start_method="spawn")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    P = O.Peers(ring, O.fingers(ring))
+    for r in range(world):
+        keys = O.splitmix_keys(0x5EED0006, sizes[r], offset=r * 1000)
+        src = ((np.arange(sizes[r]) * 7 + r) % len(ring)).astype(np.uint32)
+        ow, hp, st = O.route(P, src, keys) if sizes[r] else ([], [], [])
+        assert out[r][0] == list(map(int, ow)) and out[r][1] == list(map(int, hp))
+        assert out[r][2] == list(map(int, st))
+        assert out[r][3] == 2
 
 
 def test_bench_launches_n_ranks_itself():
@@ -258,13 +284,18 @@ def test_bench_launches_n_ranks_itself():
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env.update(CX_BENCH_DRYRUN="1", CX_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
-                        "--steps", "3", "--warmup", "1"], env=env, capture_output=True,
+                        "--steps", "3", "--warmup", "1", "--cpu-seconds", "1"], env=env,
+                       capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1
+    # every world size carries the CPU baseline (rank 0) and the whole-node roofline
+    assert rec["cpu_baseline"] is not None and rec["cpu_baseline"]["value"] > 0
+    assert rec["cpu_baseline"]["n_gpus_beside"] == 2
+    assert rec["roofline"]["n_gpus"] == 2 and rec["roofline"]["peak"] == 2 * 8000.0
 
 
 def test_bench_rejects_world_mismatch():
