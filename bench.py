@@ -43,8 +43,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
-import subprocess
 import sys
 import time
 
@@ -94,29 +92,12 @@ def parse():
     return ap.parse_args()
 
 
-def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def launch(args):
     """One process per GPU.  Without a torch.distributed environment and with
     --gpus N > 1, run this script under torch.distributed.run as a CHILD
     process (nothing here has touched the GPU yet) and return its exit
     status; None = run the benchmark in this process."""
-    ws = os.environ.get("WORLD_SIZE")
-    if ws is None:
-        if args.gpus <= 1:
-            return None
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
-               f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-        return subprocess.run(cmd).returncode
-    if int(ws) != args.gpus:
-        print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}", file=sys.stderr)
-        return 2
-    return None
+    return dist.launch_self(args.gpus, __file__, sys.argv[1:])
 
 
 def host_threads() -> int:

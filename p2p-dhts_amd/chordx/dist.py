@@ -34,6 +34,62 @@ def shard(rank: int, per_rank: int):
     return rank * per_rank, (rank + 1) * per_rank
 
 
+def shard_range(rank: int, world: int, total: int):
+    """[begin, end) of a fixed `total` split over `world` ranks (strong
+    scaling: C5's 2^26 keys scanned by N ranks)."""
+    return rank * total // world, (rank + 1) * total // world
+
+
+def gather_rows(t, world: int, backend: str = "gloo"):
+    """Concatenation over ranks (rank order) of every rank's rows of `t`
+    (shards may differ in length): one all_gather of the row counts, one of
+    the rows padded to the longest shard.  Returns the full tensor on every
+    rank (on t's device)."""
+    if world == 1:
+        return t
+    cd = torch.device("cpu") if backend == "gloo" else t.device
+    x = t.to(cd).contiguous()
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=cd)
+    ns = torch.empty(world, dtype=torch.int64, device=cd)
+    tdist.all_gather_into_tensor(ns, n)
+    counts = [int(c) for c in ns.cpu()]
+    m = max(counts)
+    pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=cd)
+    pad[: x.shape[0]] = x
+    allp = torch.empty((world * m,) + tuple(x.shape[1:]), dtype=x.dtype, device=cd)
+    tdist.all_gather_into_tensor(allp, pad)
+    parts = [allp[r * m: r * m + counts[r]] for r in range(world)]
+    return torch.cat(parts).to(t.device)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_self(gpus: int, script: str, argv):
+    """One process per GPU: without a torch.distributed environment and with
+    gpus > 1, run `script argv` under torch.distributed.run as a CHILD process
+    (the caller has not touched the GPU) and return its exit status; None =
+    run in this process.  2 when WORLD_SIZE disagrees with gpus."""
+    import subprocess
+    import sys
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if gpus <= 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1",
+               f"--master-port={free_port()}", os.path.abspath(script)] + list(argv)
+        return subprocess.run(cmd).returncode
+    if int(ws) != gpus:
+        print(f"{os.path.basename(script)}: WORLD_SIZE={ws} but --gpus {gpus}", file=sys.stderr)
+        return 2
+    return None
+
+
 def barrier(world: int):
     if world > 1:
         tdist.barrier()
