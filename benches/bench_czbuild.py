@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Route-table build A/B (row f2): a 2^24-peer ring (seed 0x5EED0007), the
+converged fingers + pattern-keyed table built twice (the second into mapped
+HBM), wall time and route_table_hash of the second build.  The build variant
+comes from the environment (CX_CZ_PAIR, CX_CZ_CHUNK, CX_CZ_STORE: read once
+per process), so run one process per variant under rocprofv3 --kernel-trace
+--stats for per-kernel times.  With CX_CZ_PAIR in {0, 1} the hash must equal
+the default build's.
+    python benches/bench_czbuild.py [log2 peers]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "p2p-dhts_amd"))
+
+import torch  # noqa: E402
+
+import chordx  # noqa: E402
+
+
+def main():
+    lg = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    ids = torch.empty((1 << lg, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(ids, 0x5EED0007)
+    ring = chordx.Ring(ids)
+    del ids
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ring.build_fingers()
+        ring.sync()
+        ts.append(time.perf_counter() - t0)
+    v, esc, tb = ring.route_info()
+    out = {"log2_peers": lg, "variant_env": {k: os.environ.get(k) for k in
+                                             ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE")},
+           "fingers_and_table_s": ts, "route_table_hash": ring.route_table_hash(),
+           "route_variant": v, "escapes": esc}
+    if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1"):
+        q = 1 << 22
+        keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
+        chordx.fill_splitmix(keys, 0x5EED0008)
+        src = (torch.arange(q, device="cuda", dtype=torch.int64) % ring.n).to(torch.int32)
+        o, h, s = ring.route(src, keys)
+        out["route_ok"] = bool((o == ring.successor(keys)).all()) and int((s != 0).sum()) == 0
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -3,12 +3,13 @@
 keys, src = q mod N), default route kernel, HIP events over `reps` launches
 after warm-up, repeated `rounds` times (min and median reported); checks owner
 == successor.  Prints one JSON line.
-    python benches/bench_route.py [reps] [rounds] [--variants]
+    python benches/bench_route.py [reps] [rounds] [--variants] [--footprint]
 --variants also times the A/B kernels on the same batch (moved out of bench.py,
 whose driver run keeps its HBM for the arc and churn legs): route variants
 0..5 (finger + ring gathers, route table, packed tables, lookahead tree,
 pattern-keyed window table; each builds its own table, up to 32 GiB) and the
 exact-successor searches (directory, Eytzinger, wave-cooperative 16-ary tree).
+CX_ORDER=keysorted routes the batch in key order (sort time reported apart).
 CX_SRC=random draws each lookup's source peer uniformly instead (splitmix,
 seed 0x5EED000A): the first hops of a wave no longer leave adjacent peers.
 """
@@ -79,6 +80,22 @@ def main():
         del r
     else:
         src = (torch.arange(Q, device="cuda", dtype=torch.int64) % N).to(torch.int32)
+    order = os.environ.get("CX_ORDER", "input")
+    sort_ms = None
+    if order == "keysorted":
+        # A/B: the batch in key order -- adjacent lookups'
+        # last hops share lower-plane lines -- with the sort's own time (a
+        # 64-bit sort of the keys' high words, the pairs permuted along)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        hi = keys[:, 1] ^ torch.iinfo(torch.int64).min  # unsigned order as signed
+        perm = torch.sort(hi).indices
+        keys = keys[perm].contiguous()
+        src = src[perm].contiguous()
+        b.record()
+        torch.cuda.synchronize()
+        sort_ms = a.elapsed_time(b)
+        del hi, perm
     owner = torch.empty(Q, dtype=torch.int32, device="cuda")
     hops = torch.empty(Q, dtype=torch.uint8, device="cuda")
     status = torch.empty(Q, dtype=torch.uint8, device="cuda")
@@ -96,10 +113,14 @@ def main():
         ms.append(a.elapsed_time(b) / reps)
     ok = bool((owner == ring.successor(keys)).all()) and int((status != 0).sum()) == 0
     rec = {"lib": os.path.basename(os.environ.get("CHORDX_LIB", "default")),
-           "src": src_kind,
+           "src": src_kind, "order": order, "sort_ms": sort_ms,
            "ms_min": min(ms), "ms_median": statistics.median(ms),
            "lookups_per_s": Q / (min(ms) * 1e-3), "probe": ring.gather_probe(),
            "owner_ok": ok, "mean_hops": float(hops.double().mean())}
+    if "--footprint" in sys.argv:
+        # request ceiling vs table footprint, on the real route table's memory
+        rec["probe_by_span_GiB"] = {g: ring.gather_probe(span=g << 30)
+                                    for g in (1, 4, 16, 32, 48, 64)}
     if "--variants" in sys.argv:
         rec.update(variants(ring, src, keys, owner))
     print(json.dumps(rec), flush=True)

@@ -274,9 +274,17 @@ class Ring:
         L.check(f(self._h, int(bool(enable)), _ptr(out)))
         return None if enable else tuple(int(x) for x in out)
 
-    def gather_probe(self, lanes: int = 1 << 19, hops: int = 64) -> float:
+    def gather_probe(self, lanes: int = 1 << 19, hops: int = 64, span: int = 0) -> float:
         """Internal: dependent random 64-B gathers/s on this ring's own route
-        table (the walk's access pattern without the walk)."""
+        table (the walk's access pattern without the walk); span > 0: over
+        the table's first `span` bytes only (footprint A/B)."""
+        if span:
+            f = L.lib().cxi_gather_probe_span
+            f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                          ctypes.POINTER(ctypes.c_double)]
+            r = ctypes.c_double()
+            L.check(f(self._h, lanes, hops, span, ctypes.byref(r)))
+            return r.value
         f = L.lib().cxi_gather_probe
         f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                       ctypes.POINTER(ctypes.c_double)]

@@ -1979,6 +1979,21 @@ int cxi_gather_probe(const cx_ring *ring, int lanes, int hops, double *rate) {
     return CX_OK;
 }
 
+// The same probe over the first span_bytes of the route table (footprint A/B:
+// the request ceiling of a smaller table, measured on real table memory).
+int cxi_gather_probe_span(const cx_ring *ring, int lanes, int hops, uint64_t span_bytes,
+                          double *rate) {
+    CX_CHECK(ring && rate, CX_E_INVALID, "null argument");
+    CX_CHECK(ring->cz_valid, CX_E_STATE, "no pattern-keyed table built");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    size_t bytes = ring->n * (size_t)ring->rt_R * 128;
+    if (span_bytes && span_bytes < bytes) bytes = span_bytes & ~(uint64_t)63;
+    CX_CHECK(bytes >= 64 * 1024, CX_E_INVALID, "span too small");
+    CX_HIP(cxk::gather_probe(ring->d_cz, bytes, lanes, hops, rate, ring->stream));
+    return CX_OK;
+}
+
 // Hash of the route table the ring built (the pattern-keyed window table, or
 // the arc planes when arc mode is on): A/B identity of two builds.
 int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {

@@ -2442,6 +2442,149 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
     if (bad) atomicAdd(esc, bad);
 }
 
+// Two lanes per entry (A/B, CX_CZ_PAIR=1): the sixteen slots split by their
+// level-(i-2) bit into two independent subtrees -- even slots hang off nd0
+// (the window root), odd slots off nd1 = f(nd0, i-2) -- so each lane of a
+// pair computes eight nodes (half the live registers of k_cz_build: twice
+// the waves per SIMD for the same dependent-gather chain).  Both lanes gather
+// the root (one address: one request).  Dispatch order and the whole-line
+// stores through LDS are k_cz_build's (K-row-block chunks, XCD-aware); a
+// wave holds 32 entries (2 KiB).  probe: 0 = build, 1 = stores only (the
+// dispatch pattern's write ceiling), 2 = compute only (no table stores).
+__global__ __launch_bounds__(256) void k_cz_build_pair(FingerView fv, const cell128 *ring,
+                                                       const uint64_t *rh, uint32_t n,
+                                                       int lvl_base, int nlev, uint32_t p_first,
+                                                       uint32_t M, int gs, uint4 *cz,
+                                                       uint32_t *esc, uint32_t K, int probe) {
+    __shared__ uint32_t stage[256 * 8];  // 128 entries x 16 words
+    constexpr uint32_t RB = 128;         // rows (entries) per block
+    uint32_t plane, lb;
+    {
+        const uint32_t P = (uint32_t)nlev * 2, B = blockIdx.x;
+        const uint32_t chunk = B / (K * P), rem = B - chunk * K * P;
+        plane = rem / K;
+        const uint32_t sub = rem - plane * K;
+        lb = chunk * K + (sub & 7) * (K >> 3) + (sub >> 3);
+    }
+    const int b = (int)(plane & 1);
+    const int i = lvl_base + (int)(plane >> 1);
+    const int hl = (int)(threadIdx.x & 1);    // 0: even slots, 1: odd slots
+    const uint32_t e_loc = threadIdx.x >> 1;  // entry within the block
+    const uint32_t j = lb * RB + e_loc;
+    auto fat = [&](uint32_t x, int l) -> uint32_t { return fv.F[(size_t)(l - fv.L) * fv.sl + x]; };
+    auto c2 = [&](uint32_t x, int l) -> uint32_t { return fv.C2[(size_t)(l - fv.L - 1) * fv.sl + x]; };
+    uint32_t oob = 0, bad = 0;
+    auto chk = [&](uint32_t x) -> uint32_t {
+        if (x >= n) {
+            oob = 1;
+            return 0u;
+        }
+        return x;
+    };
+    uint32_t out[8];
+    if (j < M && probe != 1) {
+        uint64_t pw = (uint64_t)p_first + j;
+        if (pw >= n) pw -= n;
+        const uint32_t p = (uint32_t)pw;
+        const uint64_t ph = rh[p];
+        uint32_t A = 0, a = p, nd0;
+        int al = i;
+        if (b) {
+            A = chk(fat(p, i));
+            a = A;
+            al = i - 1;
+            nd0 = chk(c2(p, i));
+        } else {
+            nd0 = chk(fat(p, i));
+        }
+        // this lane's eight nodes: w = slot >> 1; slot = 2w + hl
+        uint32_t nd[8];
+        if (hl == 0) {
+            nd[0] = nd0;                      // slot 0
+            nd[1] = chk(fat(nd0, i - 3));     // slot 2
+            nd[2] = chk(fat(nd0, i - 4));     // slot 4
+            nd[3] = chk(c2(nd0, i - 3));      // slot 6
+            nd[4] = chk(fat(nd0, i - 5));     // slot 8
+            nd[6] = chk(c2(nd0, i - 4));      // slot 12
+            nd[5] = chk(fat(nd[1], i - 5));   // slot 10
+            nd[7] = chk(c2(nd[1], i - 4));    // slot 14
+        } else {
+            nd[0] = chk(fat(nd0, i - 2));     // slot 1
+            nd[1] = chk(c2(nd0, i - 2));      // slot 3
+            nd[2] = chk(fat(nd[0], i - 4));   // slot 5
+            nd[3] = chk(fat(nd[1], i - 4));   // slot 7
+            nd[4] = chk(fat(nd[0], i - 5));   // slot 9
+            nd[5] = chk(fat(nd[1], i - 5));   // slot 11
+            nd[6] = chk(c2(nd[0], i - 4));    // slot 13
+            nd[7] = b ? A : chk(c2(nd[1], i - 4));  // slot 15
+        }
+        uint64_t hv[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) hv[w] = rh[nd[w]];
+        if (hl == 0) {
+            const uint64_t ah = b ? rh[A] : ph;
+            out[0] = cz_encode_hi(n, gs, a, ah, al, nd[0], hv[0], ring);
+            // slot 2w's parent: the slot without its highest bit (even, this lane)
+#pragma unroll
+            for (int w = 1; w < 8; ++w) {
+                const int v = 2 * w;
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pw2 = (v & ~(1 << hb)) >> 1;
+                out[w] = cz_encode_hi(n, gs, nd[pw2], hv[pw2], i - 2 - hb, nd[w], hv[w], ring);
+            }
+        } else {
+            // slot 1's parent is slot 0 = nd0 (the other lane's root, gathered here too)
+            const uint64_t h0 = rh[nd0];
+            out[0] = cz_encode_hi(n, gs, nd0, h0, i - 2, nd[0], hv[0], ring);
+#pragma unroll
+            for (int w = 1; w < 8; ++w) {
+                const int v = 2 * w + 1;
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pv = v & ~(1 << hb);  // odd (contains bit 0)
+                out[w] = cz_encode_hi(n, gs, nd[pv >> 1], hv[pv >> 1], i - 2 - hb, nd[w], hv[w],
+                                      ring);
+            }
+            if (b) out[7] = cz_encode_hi(n, gs, p, ph, i, A, hv[7], ring);
+        }
+#pragma unroll
+        for (int w = 0; w < 8; ++w) bad += out[w] == CZ_NONE;
+    } else {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) out[w] = j * 16 + 2 * w + hl;
+    }
+    if (probe == 2) {  // compute only: keep the results live, store nothing
+        uint32_t x = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) x ^= out[w];
+        if (x == 0x9E3779B9u) atomicAdd(esc, 0u);
+    } else {
+        // the wave's 32 entries (2 KiB, contiguous) leave through LDS as two
+        // 1-KiB stores: every store instruction writes whole lines
+        const int lane = threadIdx.x & 63;
+        uint32_t *ws = stage + (threadIdx.x >> 6) * 512;
+        const int el = lane >> 1;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) ws[el * 16 + 2 * w + hl] = out[w];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t j0 = lb * RB + ((threadIdx.x & ~63u) >> 1);  // the wave's first entry
+        const size_t t0 = (size_t)plane * M + j0;
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = k * 64 + lane;  // 16-B chunk of the wave's 2 KiB
+            if (j0 + (c >> 2) < M) {
+                const uint4 u = reinterpret_cast<const uint4 *>(ws)[c];
+                const v4u wv = {u.x, u.y, u.z, u.w};
+                __builtin_nontemporal_store(wv, reinterpret_cast<v4u *>(cz + t0 * 4) + c);
+            }
+        }
+    }
+    if (oob) atomicOr(esc + 1, 1u);
+    if (bad) atomicAdd(esc, bad);
+}
+
 hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                     int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s) {
     return cz_build_part(fv, ring, rh, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s);
@@ -2487,6 +2630,21 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const char *e = getenv("CX_CZ_STORE");
         return e ? (atoi(e) & 3) : 3;
     }();
+    // CX_CZ_PAIR: 1 = two lanes per entry (k_cz_build_pair); 2 / 3 = its
+    // stores-only / compute-only probes (A/B of the build's two halves)
+    static const int pair = [] {
+        const char *e = getenv("CX_CZ_PAIR");
+        return e ? atoi(e) : 0;
+    }();
+    if (planes && fv.C2 && pair >= 1 && pair <= 3) {
+        const uint32_t Kp = K ? K : 16;
+        const uint64_t nrb = ((uint64_t)M + 127) / 128, chunks = (nrb + Kp - 1) / Kp;
+        const uint64_t blocks = chunks * Kp * (uint64_t)nlev * 2;
+        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+        k_cz_build_pair<<<(unsigned)blocks, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
+                                                         p_first, M, gs, out, esc, Kp, pair - 1);
+        return hipGetLastError();
+    }
     if (planes && fv.C2 && store != 1) {
         if (store == 0)
             k_cz_build<2, 0><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,

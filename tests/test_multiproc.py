@@ -306,3 +306,54 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+
+
+# ---------------------------------------------------------------------------
+# C5 key-sharded over ranks (benches/bench_c5.py's layout): replicated old/new
+# rings, each rank scans its dist.shard_range of the keys; the concatenation
+# (dist.gather_rows) must equal the single-process RunGlobalMaintenance scan.
+# ---------------------------------------------------------------------------
+def _c5_worker(rank, world, port, total, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "p2p-dhts_amd"), os.path.join(root, "oracle")]
+    import torch
+    import torch.distributed as tdist
+    import oracle as O
+    from chordx import dist
+    dist.init("gloo")
+    old = O.ring_build(O.splitmix_keys(0x5EED0007, 4000))
+    joins = O.splitmix_keys(0x5EED0009, 40)
+    leaves = old[(np.arange(40) * 0x9E3779B1) % len(old)]
+    new, o2n = O.churn(old, joins, leaves)
+    k0, k1 = dist.shard_range(rank, world, total)
+    keys = O.splitmix_keys(0x5EED0008, k1 - k0, offset=k0)
+    lists, count, mask, target = O.misplaced(old, new, o2n, keys, 14, threads=2)
+    got = [dist.gather_rows(torch.from_numpy(a.astype(np.int64)), world, "gloo").numpy()
+           for a in (lists, count, mask, target)]
+    out[rank] = [g.tolist() for g in got] + [(k0, k1)]
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(2, 3001), (3, 2000)])
+def test_c5_key_sharded_scan_equals_single_process(world, total):
+    import oracle as O
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_c5_worker, args=(world, _free_port(), total, out), nprocs=world,
+                       join=True, start_method="spawn")
+    old = O.ring_build(O.splitmix_keys(0x5EED0007, 4000))
+    joins = O.splitmix_keys(0x5EED0009, 40)
+    leaves = old[(np.arange(40) * 0x9E3779B1) % len(old)]
+    new, o2n = O.churn(old, joins, leaves)
+    keys = O.splitmix_keys(0x5EED0008, total)
+    want = O.misplaced(old, new, o2n, keys, 14)
+    spans = [out[r][4] for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == total
+    assert all(spans[r][1] == spans[r + 1][0] for r in range(world - 1))
+    for r in range(world):  # every rank holds the whole concatenation
+        for g, w in zip(out[r][:4], want):
+            assert np.array_equal(np.asarray(g).reshape(w.shape), w.astype(np.int64))
+    assert 0 < int((want[2] != 0).sum()) < total
