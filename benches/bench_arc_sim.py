@@ -110,7 +110,7 @@ def run(G, N, Q, ids, reps, top, key_first):
     return best
 
 
-def run_soa(G, N, Q, ids, reps, top, want=None):
+def run_soa(G, N, Q, ids, reps, top, want=None, regions=False):
     """Key-first SoA protocol (ArcRouter.route_soa): per rank partition, walk
     of the receive buffer, delivery; xGMI = 20 B out + 8 B back per remote
     lookup.  want = replicated (owner, hops) to check against."""
@@ -132,17 +132,28 @@ def run_soa(G, N, Q, ids, reps, top, want=None):
     best = None
     for _ in range(reps):
         part_ms, route_ms, deliv_ms, remote_out, remote_in = [], [], [], [], []
-        parts = []
+        parts, caps = [], []
+        cap = q // G + q // (4 * G) + 4096
         for g in range(G):
             a, b = ev(), ev()
             a.record()
-            parts.append(rings[g].arc_partition(G, srcs[g], keys[g]))
+            p = rings[g].arc_partition_regions(G, srcs[g], keys[g], cap) if regions else None
+            if p is None:
+                p = rings[g].arc_partition(G, srcs[g], keys[g])
+            parts.append(p)
             b.record()
             torch.cuda.synchronize()
+            caps.append(cap if p[0].shape[0] == G * cap and regions else 0)
             part_ms.append(a.elapsed_time(b))
             remote_out.append(sum(parts[g][3]) - parts[g][3][g])
-        ks = [torch.split(p[0], p[3]) for p in parts]
-        ss = [torch.split(p[1], p[3]) for p in parts]
+
+        def views(t, g):
+            c, cnt = caps[g], parts[g][3]
+            if c:
+                return [t[d * c: d * c + cnt[d]] for d in range(G)]
+            return list(torch.split(t, cnt))
+        ks = [views(p[0], g) for g, p in enumerate(parts)]
+        ss = [views(p[1], g) for g, p in enumerate(parts)]
         back = [[None] * G for _ in range(G)]
         for d in range(G):
             rk = torch.cat([ks[g][d] for g in range(G)])
@@ -158,7 +169,12 @@ def run_soa(G, N, Q, ids, reps, top, want=None):
                 back[g][d] = part
             del rk, rs, res
         for g in range(G):
-            bk = torch.cat(back[g])
+            if caps[g]:  # answers in their region slots (the return all_to_all's layout)
+                bk = torch.empty(G * caps[g], dtype=torch.int64, device="cuda")
+                for d in range(G):
+                    bk[d * caps[g]: d * caps[g] + parts[g][3][d]] = back[g][d]
+            else:
+                bk = torch.cat(back[g])
             a, b = ev(), ev()
             a.record()
             rings[g].arc_deliver(bk, parts[g][2], *outs[g])
@@ -170,7 +186,8 @@ def run_soa(G, N, Q, ids, reps, top, want=None):
         # each rank sends and receives over its 7 links; bound by the larger side
         xg = (max(max(remote_out), max(remote_in)) * 20 + max(max(remote_out), max(remote_in)) * 8) \
             / (7 * XGMI_LINK) * 1e3
-        res = {"G": G, "mode": "soa", "keys_total": Q, "keys_per_rank": q,
+        res = {"G": G, "mode": "soa_regions" if regions else "soa", "keys_total": Q,
+               "keys_per_rank": q,
                "top_levels": info[0][0], "local_rows_max": max(i[1] for i in info),
                "route_plane_bytes_per_gpu_max": max(i[2] for i in info),
                "partition_ms_max": max(part_ms), "route_ms_max": max(route_ms),
@@ -224,8 +241,9 @@ def main():
     torch.cuda.empty_cache()
     for G in [int(x) for x in a.groups.split(",")]:
         for mode in a.modes.split(","):
-            if mode == "soa":
-                out["arc"].append(run_soa(G, N, Q, ids, a.reps, a.top_levels, want))
+            if mode in ("soa", "soa_regions"):
+                out["arc"].append(run_soa(G, N, Q, ids, a.reps, a.top_levels, want,
+                                          regions=mode == "soa_regions"))
             else:
                 out["arc"].append(run(G, N, Q, ids, a.reps, a.top_levels, mode == "key_first"))
             print(json.dumps(out["arc"][-1]), file=sys.stderr, flush=True)

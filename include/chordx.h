@@ -377,6 +377,14 @@ int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *
 int cx_arc_partition(const cx_ring *ring, int world, const uint32_t *src, const cx_u128 *keys,
                      size_t q, cx_u128 *send_keys, uint32_t *send_src, uint32_t *perm,
                      uint64_t *counts);
+/* Single-pass variant of cx_arc_partition: destination d's lookups go to the
+ * region [d cap, (d + 1) cap) of send_keys / send_src (world x cap entries
+ * each; counts[d] filled), perm[i] = the region slot of lookup i, so no count
+ * pass precedes the scatter.  CX_E_STATE when some destination receives more
+ * than cap lookups (nothing of it is written; use cx_arc_partition). */
+int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src,
+                             const cx_u128 *keys, size_t q, uint64_t cap, cx_u128 *send_keys,
+                             uint32_t *send_src, uint32_t *perm, uint64_t *counts);
 int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
                  uint64_t *res);
 int cx_arc_deliver(const cx_ring *ring, const uint64_t *res, const uint32_t *perm, size_t q,

@@ -70,6 +70,7 @@ class ArcRouter:
         self.key_first = world > 1
         self._mat_host = None  # pinned landing buffer of the count matrix
         self.chunks = None     # route_soa pipeline depth (None: by batch size)
+        self.regions = True    # single-pass partition into destination regions
 
     def _exchange(self, send, counts):
         """Returns (received records, global number of records in flight)."""
@@ -109,6 +110,33 @@ class ArcRouter:
                                        async_op=True)
         return out, work
 
+    def _a2a_regions(self, t, counts, cap, out_splits, dev):
+        """Asynchronous all_to_all of destination regions: rows [d cap, d cap
+        + counts[d]) of t go to rank d (no compaction on RCCL: a list
+        all_to_all over region views).  gloo has no list all_to_all: the
+        regions are packed first (test path)."""
+        views = [t[d * cap: d * cap + counts[d]] for d in range(self.world)]
+        if torch.device(dev).type == "cuda" and t.is_cuda:
+            out = torch.empty((sum(out_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+            outs = list(torch.split(out, out_splits))
+            work = tdist.all_to_all(outs, views, group=self.group, async_op=True)
+            return out, work
+        return self._a2a(torch.cat(views), out_splits, list(counts), dev)
+
+    def _a2a_into_regions(self, t, in_splits, counts, cap, like, dev):
+        """Asynchronous all_to_all whose arrivals from rank d land at rows
+        [d cap, d cap + counts[d]) of a world x cap buffer (the answers coming
+        home to the region slots perm names)."""
+        G = self.world
+        if torch.device(dev).type == "cuda" and t.is_cuda:
+            back = torch.empty((G * cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+            outs = [back[d * cap: d * cap + counts[d]] for d in range(G)]
+            work = tdist.all_to_all(outs, list(torch.split(t, in_splits)), group=self.group,
+                                    async_op=True)
+            return back, work, None
+        packed, work = self._a2a(t, list(counts), in_splits, dev)
+        return packed, work, (counts, cap)
+
     @staticmethod
     def _land(t, work, like):
         work.wait()  # the current stream waits for the collective
@@ -138,10 +166,24 @@ class ArcRouter:
         k = int(fixed) if fixed is not None else max(1, min(4, q >> 22))
         k = max(1, min(k, kmax, max(q, 1)))
         cut = [c * q // k for c in range(k + 1)]
-        parts = [eng.arc_partition(self.world, src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]])
-                 for c in range(k)]
-        dev = self.comm_device if self.comm_device is not None else parts[0][0].device
         G = self.world
+        # single-pass partition into per-destination regions when the engine
+        # has it (cap = 1/G of the piece + slack; a piece whose keys crowd one
+        # arc past it is partitioned in two passes instead)
+        regions = hasattr(eng, "arc_partition_regions") and self.regions
+        parts, caps = [], []
+        for c in range(k):
+            ps, pk = src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]]
+            part = None
+            if regions:
+                qc = cut[c + 1] - cut[c]
+                cap = max(1, qc // G + qc // (4 * G) + 4096)
+                part = eng.arc_partition_regions(G, ps, pk, cap)
+            if part is None:
+                part, cap = eng.arc_partition(G, ps, pk), 0
+            parts.append(part)
+            caps.append(cap)
+        dev = self.comm_device if self.comm_device is not None else parts[0][0].device
         row = [k] + [x for p in parts for x in p[3]] + [0] * ((kmax - k) * G)
         mine = torch.tensor(row, dtype=torch.int64, device=dev)
         mat = torch.empty((G, 1 + kmax * G), dtype=torch.int64, device=dev)
@@ -158,10 +200,14 @@ class ArcRouter:
             e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=keys.device),
                  [0] * G)
             parts += [e] * (kg - k)
+            caps += [0] * (kg - k)
             cut += [q] * (kg - k)
 
         def send(c):
             sk, ss, _, cnt = parts[c]
+            if caps[c]:
+                return (self._a2a_regions(sk, cnt, caps[c], recv[c], dev),
+                        self._a2a_regions(ss, cnt, caps[c], recv[c], dev))
             return self._a2a(sk, recv[c], cnt, dev), self._a2a(ss, recv[c], cnt, dev)
 
         inflight = send(0)
@@ -173,9 +219,20 @@ class ArcRouter:
             if c + 1 < kg:
                 inflight = send(c + 1)
             res = eng.arc_route(rs, rk)
-            backs.append(self._a2a(res, parts[c][3], recv[c], dev))
+            if caps[c]:
+                backs.append(self._a2a_into_regions(res, recv[c], parts[c][3], caps[c],
+                                                    parts[c][2], dev))
+            else:
+                backs.append(self._a2a(res, parts[c][3], recv[c], dev) + (None,))
         for c in range(kg):
             back = self._land(backs[c][0], backs[c][1], parts[c][2])
+            if backs[c][2] is not None:  # gloo: packed answers -> their regions
+                cnt, cap = backs[c][2]
+                full = torch.empty((G * cap,) + tuple(back.shape[1:]), dtype=back.dtype,
+                                   device=back.device)
+                for d, piece in enumerate(torch.split(back, list(cnt))):
+                    full[d * cap: d * cap + cnt[d]] = piece
+                back = full
             sl = slice(cut[c], cut[c + 1])
             eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
                             status[sl] if status is not None else None)

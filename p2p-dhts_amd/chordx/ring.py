@@ -486,6 +486,28 @@ class Ring:
                                          _ptr(ssrc), _ptr(perm), _ptr(counts)))
         return skeys, ssrc, perm, [int(c) for c in counts]
 
+    def arc_partition_regions(self, world: int, src, keys, cap: int):
+        """Single-pass partition (cx_arc_partition_regions): (send_keys,
+        send_src, perm, counts) with destination d's lookups at rows
+        [d cap, d cap + counts[d]) of send_keys / send_src; None when some
+        destination exceeds cap (the caller falls back to arc_partition)."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        skeys = torch.empty((world * cap, 2), dtype=torch.int64, device=keys.device)
+        ssrc = torch.empty(world * cap, dtype=torch.int32, device=keys.device)
+        perm = torch.empty(q, dtype=torch.int32, device=keys.device)
+        counts = np.zeros(world, dtype=np.uint64)
+        self._arc_stream()
+        rc = L.lib().cx_arc_partition_regions(self._h, world, _ptr(src), _ptr(keys), q, cap,
+                                              _ptr(skeys), _ptr(ssrc), _ptr(perm), _ptr(counts))
+        if rc == L.CX_E_STATE and "region" in (L.lib().cx_last_error() or b"").decode():
+            return None
+        L.check(rc)
+        return skeys, ssrc, perm, [int(c) for c in counts]
+
     def arc_route(self, src, keys, res=None):
         """Packed results (int64: owner | hops << 32 | status << 40 | 1 << 63)
         of lookups received from every rank, in input order (cx_arc_route)."""

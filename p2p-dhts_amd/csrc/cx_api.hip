@@ -1874,6 +1874,40 @@ int cx_arc_partition(const cx_ring *ring, int world, const uint32_t *src, const 
     return CX_OK;
 }
 
+int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src,
+                             const cx_u128 *keys, size_t q, uint64_t cap, cx_u128 *send_keys,
+                             uint32_t *send_src, uint32_t *perm, uint64_t *counts) {
+    CX_CHECK(ring && counts, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(q == 0 || (src && keys && send_keys && send_src && perm), CX_E_INVALID,
+             "null buffer");
+    CX_CHECK(cap >= 1 && (uint64_t)world * cap < (1ull << 32) && q < (1ull << 32), CX_E_INVALID,
+             "cap must be >= 1 with world * cap < 2^32");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    uint32_t *dcur = ring->d_scratch + CX_ARC_MAX_RANKS, *dovf = ring->d_scratch + 2 * CX_ARC_MAX_RANKS;
+    uint32_t hc[CX_ARC_MAX_RANKS + 1];
+    for (int g = 0; g < world; ++g) hc[g] = (uint32_t)(g * cap);
+    hc[world] = 0;
+    CX_HIP(hipMemcpyAsync(dcur, hc, world * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    CX_HIP(hipMemsetAsync(dovf, 0, sizeof(uint32_t), s));
+    CX_HIP(cxk::arc_partition_regions(src, reinterpret_cast<const cell128 *>(keys), q,
+                                      ring->d_arc_bounds, ring->arc_nb, world, (uint32_t)cap,
+                                      dcur, dovf, reinterpret_cast<cell128 *>(send_keys),
+                                      send_src, perm, s));
+    uint32_t ovf = 0;
+    CX_HIP(hipMemcpyAsync(hc, dcur, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipMemcpyAsync(&ovf, dovf, sizeof(ovf), hipMemcpyDeviceToHost, s));
+    CX_HIP(hipStreamSynchronize(s));
+    for (int g = 0; g < world; ++g) counts[g] = hc[g] - (uint64_t)g * cap;
+    CX_CHECK(!ovf, CX_E_STATE, "arc partition: a destination's lookups exceed its region (cap)");
+    return CX_OK;
+}
+
 int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
                  uint64_t *res) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");

@@ -3527,10 +3527,16 @@ __global__ __launch_bounds__(256) void k_arc_scatter(ArcIn<SEED> in, size_t q,
 // written in lookup order: coalesced).  Results come back in send order (the
 // arc rank answers its receive buffer in order and the return exchange swaps
 // the splits), so no record carries an origin or an index across xGMI.
+// cap > 0 (single-pass partition, cx_arc_partition_regions): destination d
+// owns the region [d cap, (d + 1) cap) of the send arrays and cursor[d]
+// starts at d cap, so no count pass is needed before the scatter; a block
+// whose reservation would cross its region's end writes nothing of it and
+// raises *ovf (the caller then partitions with the two-pass kernel).
 __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t q,
                                                          const ArcBound *bounds, int nb, int G,
                                                          uint32_t *cursor, cell128 *skeys,
-                                                         uint32_t *ssrc, uint32_t *slot_of) {
+                                                         uint32_t *ssrc, uint32_t *slot_of,
+                                                         uint32_t cap, uint32_t *ovf) {
     __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
@@ -3553,12 +3559,17 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
 #pragma unroll
         for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
         __syncthreads();
-        for (int j = threadIdx.x; j < G; j += blockDim.x)
+        for (int j = threadIdx.x; j < G; j += blockDim.x) {
             basep[j] = h[j] ? atomicAdd(&cursor[j], h[j]) : 0u;
+            if (cap && h[j] && (uint64_t)basep[j] + h[j] > (uint64_t)(j + 1) * cap) {
+                atomicOr(ovf, 1u);
+                basep[j] = 0xFFFFFFFFu;  // nothing of this destination is written
+            }
+        }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < ARC_SCAT_R; ++k)
-            if (d[k] >= 0) {
+            if (d[k] >= 0 && basep[d[k]] != 0xFFFFFFFFu) {
                 const uint32_t o = basep[d[k]] + slot[k];
                 skeys[o] = cell128{r[k].w0, r[k].w1};
                 ssrc[o] = r[k].cur;
@@ -3617,7 +3628,19 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
     hipError_t e = arc_bucket_in(in, q, bounds, nb, G, counts_dev, cursor_dev, nullptr, s, false);
     if (e != hipSuccess || q == 0) return e;
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
-        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm);
+        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, 0u, nullptr);
+    return hipGetLastError();
+}
+
+// Single pass: cursor_dev[d] = d * cap already (the caller's), ovf zeroed.
+hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_t q,
+                                 const ArcBound *bounds, int nb, int G, uint32_t cap,
+                                 uint32_t *cursor_dev, uint32_t *ovf, cell128 *skeys,
+                                 uint32_t *ssrc, uint32_t *perm, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const ArcIn<true> in{nullptr, src, keys, 0};
+    k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
+        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, cap, ovf);
     return hipGetLastError();
 }
 

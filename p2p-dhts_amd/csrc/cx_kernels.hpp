@@ -181,6 +181,10 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
                          const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
                          uint32_t *cursor_dev, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
                          hipStream_t s);
+hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_t q,
+                                 const ArcBound *bounds, int nb, int G, uint32_t cap,
+                                 uint32_t *cursor_dev, uint32_t *ovf, cell128 *skeys,
+                                 uint32_t *ssrc, uint32_t *perm, hipStream_t s);
 hipError_t arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q, uint32_t *owner,
                        uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,

@@ -78,6 +78,7 @@ class OracleArcEngine:
 
     def __init__(self, P, n):
         self.P, self.n = P, n
+        self.region_cap = None  # force a region capacity (overflow fallback test)
 
     def arc_build(self, world, rank):
         from chordx.arc import arc_bounds
@@ -145,6 +146,25 @@ class OracleArcEngine:
                 src[torch.from_numpy(order)].contiguous(),
                 torch.from_numpy(slot.astype(np.int32)), counts)
 
+    def arc_partition_regions(self, world, src, keys, cap):
+        """Region layout of cx_arc_partition_regions: destination d's lookups
+        at rows [d cap, d cap + count_d), perm = region slot; None past cap."""
+        import torch
+        sk, ss, slot, counts = self.arc_partition(world, src, keys)
+        if self.region_cap is not None:
+            cap = self.region_cap
+        if any(c > cap for c in counts):
+            return None
+        start = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        rk = torch.zeros((world * cap, 2), dtype=torch.int64)
+        rs = torch.zeros(world * cap, dtype=torch.int32)
+        dest = np.repeat(np.arange(world), counts)
+        new_slot = dest * cap + (np.arange(len(dest)) - start[dest])
+        rk[torch.from_numpy(new_slot)] = sk
+        rs[torch.from_numpy(new_slot)] = ss
+        perm = torch.from_numpy(new_slot[slot.numpy()].astype(np.int32))
+        return rk, rs, perm, counts
+
     def arc_route(self, src, keys):
         import torch
         import oracle as O
@@ -192,7 +212,7 @@ class OracleArcEngine:
 
 
 def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="records",
-                chunks=None, sizes=None):
+                chunks=None, sizes=None, regions=False, region_cap=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import sys
@@ -215,7 +235,10 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="reco
     owner = torch.full((per_rank,), -9, dtype=torch.int32)
     hops = torch.zeros(per_rank, dtype=torch.uint8)
     status = torch.full((per_rank,), 7, dtype=torch.uint8)
-    router = ArcRouter(OracleArcEngine(P, len(ring)), len(ring), rank, world)
+    eng = OracleArcEngine(P, len(ring))
+    eng.region_cap = region_cap
+    router = ArcRouter(eng, len(ring), rank, world)
+    router.regions = regions
     router.chunks = chunks
     rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status,
                           key_first=key_first, protocol=protocol)
@@ -246,6 +269,30 @@ def test_arc_router_protocol_gloo(world, key_first, protocol, chunks):
         # records: walk -> result -> home, then drained; soa: there and back
         assert out[r][3] == (3 if protocol == "records" else 2)
         assert out[r][4] > 0            # records crossed ranks
+
+
+@pytest.mark.parametrize("region_cap", [None, 5])
+@pytest.mark.parametrize("world", [2, 3])
+def test_arc_router_soa_regions_gloo(world, region_cap):
+    """Single-pass partition into destination regions (the layout of
+    cx_arc_partition_regions): answers land in their region slots and every
+    lookup equals the oracle walk; region_cap = 5 overflows every piece and
+    exercises the two-pass fallback."""
+    import oracle as O
+    per_rank = 600
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_arc_worker, args=(world, _free_port(), per_rank, out, True, "soa", 2,
+                                          None, True, region_cap),
+                       nprocs=world, join=True, start_method="spawn")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    P = O.Peers(ring, O.fingers(ring))
+    for r in range(world):
+        keys = O.splitmix_keys(0x5EED0006, per_rank, offset=r * 1000)
+        src = ((np.arange(per_rank) * 7 + r) % len(ring)).astype(np.uint32)
+        ow, hp, st = O.route(P, src, keys)
+        assert out[r][0] == ow.tolist() and out[r][1] == hp.tolist()
+        assert out[r][2] == st.tolist()
 
 
 @pytest.mark.parametrize("chunks", [None, 3])
