@@ -370,7 +370,9 @@ int cx_arc_send_ahead(const cx_ring *ring, int world, int rank, const uint32_t *
  *      own rows (a walk that needs a lower level is within 2^(128 - T) of its
  *      key: in the key's arc or its halo);
  *   3. res goes back with the splits swapped (8 B per lookup) and lands in
- *      send order; cx_arc_deliver writes owner / hops / status of lookup i
+ *      send order (or in the partition's regions, cx_arc_partition_regions:
+ *      perm then indexes world x cap slots); cx_arc_deliver writes owner /
+ *      hops / status of lookup i
  *      from res[perm[i]] (perm == NULL: identity, the single-rank case).
  * Owners, hops and statuses equal cx_route's on the replicated ring.  Device
  * buffers; perm, send_* sized q. */

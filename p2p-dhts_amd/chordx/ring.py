@@ -527,13 +527,15 @@ class Ring:
 
     def arc_deliver(self, res, perm, owner, hops, status=None):
         """owner/hops/status of lookup i from the returned results (send
-        order) at perm[i] (None: identity) (cx_arc_deliver)."""
-        q = res.shape[0]
+        order, or the region layout of arc_partition_regions) at perm[i]
+        (None: identity) (cx_arc_deliver).  perm's entries must index res
+        (they do when perm comes from the partition that laid res out)."""
         if not (_is_dev(res) and res.element_size() == 8 and res.is_contiguous()):
             raise TypeError("res must be a contiguous 8-byte device tensor")
+        q = res.shape[0] if perm is None else perm.numel()
         if perm is not None and not (_is_dev(perm) and perm.element_size() == 4
-                                     and perm.is_contiguous() and perm.numel() == q):
-            raise TypeError("perm must be a contiguous 4-byte device tensor of len(res)")
+                                     and perm.is_contiguous() and perm.numel() <= res.numel()):
+            raise TypeError("perm must be a contiguous 4-byte device tensor, no longer than res")
         for t, w, name in ((owner, 4, "owner"), (hops, 1, "hops"), (status, 1, "status")):
             if t is not None and not (_is_dev(t) and t.element_size() == w and t.numel() >= q):
                 raise TypeError(f"{name}: device tensor of {w}-byte elements, >= q")

@@ -240,7 +240,7 @@ def test_arc_refuses_hand_edited_state(cx, O):
 # Structure-of-arrays key-first protocol (ArcRouter.route_soa): partition by
 # the key's arc, walk in receive order, answers back in send order.
 # ---------------------------------------------------------------------------
-def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0):
+def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0):
     import torch
     rings = [cx.Ring(ids_dev) for _ in range(G)]
     for g, r in enumerate(rings):
@@ -255,13 +255,24 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0):
         rings[0].arc_deliver(rings[0].arc_route(srcs[0], keys[0]), None, *outs[0])
         torch.cuda.synchronize()
         return outs, 0
-    parts = [rings[g].arc_partition(G, srcs[g], keys[g]) for g in range(G)]
-    for g, (sk, ss, perm, counts) in enumerate(parts):
-        assert sum(counts) == keys[g].shape[0]
-        assert torch.equal(torch.sort(perm.long()).values,
-                           torch.arange(keys[g].shape[0], device="cuda"))
-    ks = [torch.split(p[0], p[3]) for p in parts]
-    ss = [torch.split(p[1], p[3]) for p in parts]
+    if cap:  # single-pass partition into destination regions
+        parts = [rings[g].arc_partition_regions(G, srcs[g], keys[g], cap) for g in range(G)]
+        assert all(p is not None for p in parts)
+        for g, (sk, ss, perm, counts) in enumerate(parts):
+            assert sum(counts) == keys[g].shape[0]
+            want = torch.cat([torch.arange(d * cap, d * cap + counts[d], device="cuda")
+                              for d in range(G)])
+            assert torch.equal(torch.sort(perm.long()).values, want)
+        ks = [[p[0][d * cap: d * cap + p[3][d]] for d in range(G)] for p in parts]
+        ss = [[p[1][d * cap: d * cap + p[3][d]] for d in range(G)] for p in parts]
+    else:
+        parts = [rings[g].arc_partition(G, srcs[g], keys[g]) for g in range(G)]
+        for g, (sk, ss, perm, counts) in enumerate(parts):
+            assert sum(counts) == keys[g].shape[0]
+            assert torch.equal(torch.sort(perm.long()).values,
+                               torch.arange(keys[g].shape[0], device="cuda"))
+        ks = [torch.split(p[0], p[3]) for p in parts]
+        ss = [torch.split(p[1], p[3]) for p in parts]
     back = [[None] * G for _ in range(G)]
     for d in range(G):
         rk = torch.cat([ks[g][d] for g in range(G)])
@@ -271,7 +282,13 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0):
             back[g][d] = part
     sent = 0
     for g in range(G):
-        rings[g].arc_deliver(torch.cat(back[g]), parts[g][2], *outs[g])
+        if cap:  # the answers land in their region slots
+            bk = torch.zeros(G * cap, dtype=torch.int64, device="cuda")
+            for d in range(G):
+                bk[d * cap: d * cap + parts[g][3][d]] = back[g][d]
+        else:
+            bk = torch.cat(back[g])
+        rings[g].arc_deliver(bk, parts[g][2], *outs[g])
         sent += sum(parts[g][3]) - parts[g][3][g]
     torch.cuda.synchronize()
     return outs, sent
@@ -291,6 +308,26 @@ def test_arc_soa_equals_replicated(cx, O, n, G):
         assert torch.equal(outs[g][2], st), (n, G, g)
     if G > 1 and n > 100:
         assert sent > 0
+
+
+@pytest.mark.parametrize("n,G", [(5000, 2), (5000, 8), (1 << 16, 8), (70001, 5), (9000, 33)])
+def test_arc_soa_regions_equals_replicated(cx, O, n, G):
+    """cx_arc_partition_regions (single pass, destination regions of cap
+    slots) + delivery through region slots == the replicated route; a cap
+    below some destination's count is refused (None) and writes nothing."""
+    import torch
+    q = 4096
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2E0 + n + G)
+    cap = q // G + q // (4 * G) + 64
+    outs, sent = simulate_soa(cx, ids_dev, G, srcs, keys, cap=cap)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow), (n, G, g)
+        assert torch.equal(outs[g][1], hp), (n, G, g)
+        assert torch.equal(outs[g][2], st), (n, G, g)
+    r = cx.Ring(ids_dev)
+    r.arc_build(G, 0)
+    assert r.arc_partition_regions(G, srcs[0], keys[0], 1) is None
 
 
 @pytest.mark.parametrize("top", [1, 3, 6, 12])

@@ -28,4 +28,7 @@ tail -1 "$OUT/c5_n1.json" | cut -c1-400
 CX_DIST_BACKEND=gloo timeout -k 10 400 python3 -u benches/bench_c5.py --gpus 2 --peers-log2 22 \
   --keys-log2 24 --steps 3 --warmup 1 > "$OUT/c5_n2.json" 2> "$OUT/c5_n2.err"
 tail -1 "$OUT/c5_n2.json" | cut -c1-400
+timeout -k 10 400 python3 -u benches/bench_arc_sim.py --keys-log2 28 --groups 8 --modes soa,soa_regions \
+  --reps 2 > "$OUT/arc_sim_g8.json" 2> "$OUT/arc_sim_g8.err"
+tail -1 "$OUT/arc_sim_g8.json" | cut -c1-400
 echo done
