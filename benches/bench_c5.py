@@ -42,7 +42,9 @@ from chordx import dist  # noqa: E402
 
 SEED_RING, SEED_KEYS, SEED_CHURN = 0x5EED0007, 0x5EED0008, 0x5EED0009
 HBM_PEAK = 8.0e12
-BYTES_PER_KEY = 139  # SURVEY 8(d) DHash model: 16 + 64 + 56 + 1 + 2
+BYTES_MISPLACED = 139  # SURVEY 8(d) DHash model: 16 + 64 + 56 + 1 + 2 per key
+BYTES_NSUCC = 137      # key 16 + one 64-B directory line + 14 x 4 list + 1 count per key
+BYTES_PER_KEY = BYTES_MISPLACED + BYTES_NSUCC
 
 
 def parse():
@@ -160,8 +162,13 @@ def main():
                          "achieved": Q * BYTES_PER_KEY / (dt_max / args.steps) / 1e9,
                          "peak": HBM_PEAK * world / 1e9,
                          "frac": Q * BYTES_PER_KEY / (dt_max / args.steps) / (HBM_PEAK * world),
-                         "model": "SURVEY 8(d): 139 B per key (misplaced scan) over the "
-                                  "step time (which also runs cx_nsucc)"},
+                         "model": f"{BYTES_NSUCC} B per key (cx_nsucc) + {BYTES_MISPLACED} B "
+                                  "per key (cx_misplaced, SURVEY 8(d)) over the step time, "
+                                  "whole node",
+                         "per_kernel_rank0": {
+                             "nsucc_frac": q * BYTES_NSUCC / (nsucc_ms * 1e-3) / HBM_PEAK,
+                             "misplaced_frac": q * BYTES_MISPLACED / (misplaced_ms * 1e-3)
+                             / HBM_PEAK}},
             "churn_ms": t_churn * 1e3,
             "new_lists_equal_new_window": ok_lists,
             "keys_with_misplaced_holder": misplaced_keys,
