@@ -110,7 +110,7 @@ def run(G, N, Q, ids, reps, top, key_first):
     return best
 
 
-def run_soa(G, N, Q, ids, reps, top, want=None, regions=False):
+def run_soa(G, N, Q, ids, reps, top, want=None, regions=False, hints=False):
     """Key-first SoA protocol (ArcRouter.route_soa): per rank partition, walk
     of the receive buffer, delivery; xGMI = 20 B out + 8 B back per remote
     lookup.  want = replicated (owner, hops) to check against."""
@@ -137,7 +137,8 @@ def run_soa(G, N, Q, ids, reps, top, want=None, regions=False):
         for g in range(G):
             a, b = ev(), ev()
             a.record()
-            p = rings[g].arc_partition_regions(G, srcs[g], keys[g], cap) if regions else None
+            p = rings[g].arc_partition_regions(G, srcs[g], keys[g], cap, hints=hints) \
+                if regions else None
             if p is None:
                 p = rings[g].arc_partition(G, srcs[g], keys[g])
             parts.append(p)
@@ -154,14 +155,16 @@ def run_soa(G, N, Q, ids, reps, top, want=None, regions=False):
             return list(torch.split(t, cnt))
         ks = [views(p[0], g) for g, p in enumerate(parts)]
         ss = [views(p[1], g) for g, p in enumerate(parts)]
+        hs = [views(p[4], g) for g, p in enumerate(parts)] if hints else None
         back = [[None] * G for _ in range(G)]
         for d in range(G):
             rk = torch.cat([ks[g][d] for g in range(G)])
             rs = torch.cat([ss[g][d] for g in range(G)])
+            rh = torch.cat([hs[g][d] for g in range(G)]) if hints else None
             remote_in.append(rk.shape[0] - parts[d][3][d])
             a, b = ev(), ev()
             a.record()
-            res = rings[d].arc_route(rs, rk)
+            res = rings[d].arc_route(rs, rk, hint=rh)
             b.record()
             torch.cuda.synchronize()
             route_ms.append(a.elapsed_time(b))
@@ -184,9 +187,11 @@ def run_soa(G, N, Q, ids, reps, top, want=None, regions=False):
         del parts, ks, ss, back
         comp = max(part_ms) + max(route_ms) + max(deliv_ms)
         # each rank sends and receives over its 7 links; bound by the larger side
-        xg = (max(max(remote_out), max(remote_in)) * 20 + max(max(remote_out), max(remote_in)) * 8) \
+        wire = 28 if hints else 20  # bytes out per remote lookup (+ 8 back)
+        xg = (max(max(remote_out), max(remote_in)) * wire + max(max(remote_out), max(remote_in)) * 8) \
             / (7 * XGMI_LINK) * 1e3
-        res = {"G": G, "mode": "soa_regions" if regions else "soa", "keys_total": Q,
+        res = {"G": G, "mode": ("soa_hints" if hints else "soa_regions") if regions else "soa",
+               "keys_total": Q,
                "keys_per_rank": q,
                "top_levels": info[0][0], "local_rows_max": max(i[1] for i in info),
                "route_plane_bytes_per_gpu_max": max(i[2] for i in info),
@@ -241,9 +246,9 @@ def main():
     torch.cuda.empty_cache()
     for G in [int(x) for x in a.groups.split(",")]:
         for mode in a.modes.split(","):
-            if mode in ("soa", "soa_regions"):
+            if mode in ("soa", "soa_regions", "soa_hints"):
                 out["arc"].append(run_soa(G, N, Q, ids, a.reps, a.top_levels, want,
-                                          regions=mode == "soa_regions"))
+                                          regions=mode != "soa", hints=mode == "soa_hints"))
             else:
                 out["arc"].append(run(G, N, Q, ids, a.reps, a.top_levels, mode == "key_first"))
             print(json.dumps(out["arc"][-1]), file=sys.stderr, flush=True)

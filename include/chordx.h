@@ -383,12 +383,23 @@ int cx_arc_partition(const cx_ring *ring, int world, const uint32_t *src, const 
  * region [d cap, (d + 1) cap) of send_keys / send_src (world x cap entries
  * each; counts[d] filled), perm[i] = the region slot of lookup i, so no count
  * pass precedes the scatter.  CX_E_STATE when some destination receives more
- * than cap lookups (nothing of it is written; use cx_arc_partition). */
+ * than cap lookups (nothing of it is written; use cx_arc_partition).
+ * send_hint (world x cap, may be NULL): the origin resolves each lookup's
+ * start at its source -- StoredLocally(key) at src (abstract_chord_peer.cpp:
+ * 720-725) and d = (key - id_src) >> (116 - ceil(log2 n)) -- reading the
+ * sources' (pred, self) IDs in lookup order, so the arc rank's walk
+ * (cx_arc_route_hinted) needs no source IDs: 8 B more per lookup on the wire,
+ * one random 32-B gather less per lookup at the arc. */
 int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src,
                              const cx_u128 *keys, size_t q, uint64_t cap, cx_u128 *send_keys,
-                             uint32_t *send_src, uint32_t *perm, uint64_t *counts);
+                             uint32_t *send_src, uint64_t *send_hint, uint32_t *perm,
+                             uint64_t *counts);
 int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
                  uint64_t *res);
+/* cx_arc_route with the origins' source hints (cx_arc_partition_regions
+ * send_hint, received alongside keys and sources): same results. */
+int cx_arc_route_hinted(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
+                        const uint64_t *hint, size_t q, uint64_t *res);
 int cx_arc_deliver(const cx_ring *ring, const uint64_t *res, const uint32_t *perm, size_t q,
                    uint32_t *owner, uint8_t *hops, uint8_t *status);
 

@@ -184,6 +184,7 @@ public:
     // Liveness and successors_ lists (n x ns, CX_NONE-padded; nullptr = the
     // converged lists) for ForwardRequest's dead-finger branch; rule =
     // CX_FWD_CHORD (chord_peer.cpp:201-208) or CX_FWD_DHASH (dhash_peer.cpp:516-526).
+    // Both nullptr: reset to "all alive, converged lists" (the converged walk).
     void SetLiveness(const std::vector<uint8_t> *alive, const std::vector<uint32_t> *succs, int ns,
                      int rule = CX_FWD_CHORD) {
         if (alive && alive->size() != Size()) throw Error(CX_E_INVALID, "alive size");

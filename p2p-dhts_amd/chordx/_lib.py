@@ -44,7 +44,8 @@ EXPORTS = (
     "cx_uuid5_dns", "cx_fill_splitmix",
     "cx_arc_build", "cx_arc_info", "cx_arc_seed", "cx_arc_start", "cx_arc_step",
     "cx_arc_bucket", "cx_arc_send_ahead",
-    "cx_arc_partition", "cx_arc_partition_regions", "cx_arc_route", "cx_arc_deliver",
+    "cx_arc_partition", "cx_arc_partition_regions", "cx_arc_route", "cx_arc_route_hinted",
+    "cx_arc_deliver",
     "cx_hex_parse", "cx_hex_format",
     "cx_ida_segments", "cx_ida_encode", "cx_ida_decode",
     "cx_wire_create", "cx_wire_destroy", "cx_wire_ring", "cx_wire_handle", "cx_wire_free",
@@ -126,7 +127,8 @@ def lib() -> ctypes.CDLL:
         "cx_arc_bucket": ([vp, i, vp, sz, vp, vp], i),
         "cx_arc_send_ahead": ([vp, i, i, vp, vp, sz, vp, vp], i),
         "cx_arc_partition": ([vp, i, vp, vp, sz, vp, vp, vp, vp], i),
-        "cx_arc_partition_regions": ([vp, i, vp, vp, sz, u64, vp, vp, vp, vp], i),
+        "cx_arc_partition_regions": ([vp, i, vp, vp, sz, u64, vp, vp, vp, vp, vp], i),
+        "cx_arc_route_hinted": ([vp, vp, vp, vp, sz, vp], i),
         "cx_arc_route": ([vp, vp, vp, sz, vp], i),
         "cx_arc_deliver": ([vp, vp, vp, sz, vp, vp, vp], i),
     }

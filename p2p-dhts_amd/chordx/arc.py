@@ -71,6 +71,7 @@ class ArcRouter:
         self._mat_host = None  # pinned landing buffer of the count matrix
         self.chunks = None     # route_soa pipeline depth (None: by batch size)
         self.regions = True    # single-pass partition into destination regions
+        self.hints = True      # origin-resolved source hints with the lookups
 
     def _exchange(self, send, counts):
         """Returns (received records, global number of records in flight)."""
@@ -171,6 +172,9 @@ class ArcRouter:
         # has it (cap = 1/G of the piece + slack; a piece whose keys crowd one
         # arc past it is partitioned in two passes instead)
         regions = hasattr(eng, "arc_partition_regions") and self.regions
+        # origin-resolved source hints ride along (8 B) when the engine has
+        # them: the arc rank's walk then needs no source IDs (a random gather)
+        hints = regions and self.hints and getattr(eng, "arc_hints", False)
         parts, caps = [], []
         for c in range(k):
             ps, pk = src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]]
@@ -178,13 +182,16 @@ class ArcRouter:
             if regions:
                 qc = cut[c + 1] - cut[c]
                 cap = max(1, qc // G + qc // (4 * G) + 4096)
-                part = eng.arc_partition_regions(G, ps, pk, cap)
+                part = eng.arc_partition_regions(G, ps, pk, cap, hints=hints) if hints else \
+                    eng.arc_partition_regions(G, ps, pk, cap)
             if part is None:
                 part, cap = eng.arc_partition(G, ps, pk), 0
             parts.append(part)
             caps.append(cap)
+        hinted = [len(p) > 4 for p in parts]
         dev = self.comm_device if self.comm_device is not None else parts[0][0].device
-        row = [k] + [x for p in parts for x in p[3]] + [0] * ((kmax - k) * G)
+        my_h = bool(hints) and all(hinted)
+        row = [k | (int(my_h) << 20)] + [x for p in parts for x in p[3]] + [0] * ((kmax - k) * G)
         mine = torch.tensor(row, dtype=torch.int64, device=dev)
         mat = torch.empty((G, 1 + kmax * G), dtype=torch.int64, device=dev)
         tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
@@ -194,31 +201,42 @@ class ArcRouter:
             self._mat_host.copy_(mat, non_blocking=True)
             torch.cuda.current_stream(mat.device).synchronize()
             mat = self._mat_host
-        kg = int(mat[:, 0].max())  # pieces every rank runs
+        kg = int((mat[:, 0] & 0xFFFFF).max())  # pieces every rank runs
+        use_h = bool(int((mat[:, 0] >> 20).min()))  # every rank's pieces carry hints
         recv = [[int(mat[r, 1 + c * G + self.rank]) for r in range(G)] for c in range(kg)]
         if kg > k:  # this rank's extra pieces are empty
             e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=keys.device),
-                 [0] * G)
+                 [0] * G, torch.empty(0, dtype=torch.int64, device=keys.device))
             parts += [e] * (kg - k)
             caps += [0] * (kg - k)
             cut += [q] * (kg - k)
+        # every rank exchanges the same arrays: hints travel only when every
+        # rank's every piece carries them (bit 20 of the gathered row's first
+        # word; a rank whose piece fell back to the two-pass partition has none)
 
         def send(c):
-            sk, ss, _, cnt = parts[c]
+            sk, ss, _, cnt = parts[c][:4]
             if caps[c]:
-                return (self._a2a_regions(sk, cnt, caps[c], recv[c], dev),
-                        self._a2a_regions(ss, cnt, caps[c], recv[c], dev))
-            return self._a2a(sk, recv[c], cnt, dev), self._a2a(ss, recv[c], cnt, dev)
+                out = [self._a2a_regions(sk, cnt, caps[c], recv[c], dev),
+                       self._a2a_regions(ss, cnt, caps[c], recv[c], dev)]
+                if use_h:
+                    out.append(self._a2a_regions(parts[c][4], cnt, caps[c], recv[c], dev))
+                return out
+            out = [self._a2a(sk, recv[c], cnt, dev), self._a2a(ss, recv[c], cnt, dev)]
+            if use_h:  # an empty piece (kg > k) still takes part in every exchange
+                out.append(self._a2a(parts[c][4], recv[c], cnt, dev))
+            return out
 
         inflight = send(0)
         backs = []
         for c in range(kg):
-            (rk, wk), (rs, ws) = inflight
-            rk = self._land(rk, wk, parts[c][0])
-            rs = self._land(rs, ws, parts[c][1])
+            got = inflight
+            rk = self._land(got[0][0], got[0][1], parts[c][0])
+            rs = self._land(got[1][0], got[1][1], parts[c][1])
+            rh = self._land(got[2][0], got[2][1], parts[c][0]) if use_h else None
             if c + 1 < kg:
                 inflight = send(c + 1)
-            res = eng.arc_route(rs, rk)
+            res = eng.arc_route(rs, rk, hint=rh) if use_h else eng.arc_route(rs, rk)
             if caps[c]:
                 backs.append(self._a2a_into_regions(res, recv[c], parts[c][3], caps[c],
                                                     parts[c][2], dev))

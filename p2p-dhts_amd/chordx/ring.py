@@ -73,6 +73,8 @@ def _ptr(a):
 class Ring:
     """Sorted, de-duplicated ring of 128-bit peer IDs on one GPU."""
 
+    arc_hints = True  # arc_partition_regions(..., hints=True) / arc_route(..., hint=)
+
     def __init__(self, ids, device: int = 0, _handle=None):
         self._h = None
         if _handle is not None:
@@ -486,11 +488,13 @@ class Ring:
                                          _ptr(ssrc), _ptr(perm), _ptr(counts)))
         return skeys, ssrc, perm, [int(c) for c in counts]
 
-    def arc_partition_regions(self, world: int, src, keys, cap: int):
+    def arc_partition_regions(self, world: int, src, keys, cap: int, hints: bool = False):
         """Single-pass partition (cx_arc_partition_regions): (send_keys,
         send_src, perm, counts) with destination d's lookups at rows
         [d cap, d cap + counts[d]) of send_keys / send_src; None when some
-        destination exceeds cap (the caller falls back to arc_partition)."""
+        destination exceeds cap (the caller falls back to arc_partition).
+        hints=True: (send_keys, send_src, perm, counts, send_hint), the
+        origin-resolved source hints for arc_route(..., hint=)."""
         keys = self._prep_keys(keys)
         src = self._prep_u32(src, "src", keys.shape[0])
         if not (_is_dev(keys) and _is_dev(src)):
@@ -499,23 +503,37 @@ class Ring:
         skeys = torch.empty((world * cap, 2), dtype=torch.int64, device=keys.device)
         ssrc = torch.empty(world * cap, dtype=torch.int32, device=keys.device)
         perm = torch.empty(q, dtype=torch.int32, device=keys.device)
+        shint = torch.empty(world * cap, dtype=torch.int64, device=keys.device) if hints else None
         counts = np.zeros(world, dtype=np.uint64)
         self._arc_stream()
         rc = L.lib().cx_arc_partition_regions(self._h, world, _ptr(src), _ptr(keys), q, cap,
-                                              _ptr(skeys), _ptr(ssrc), _ptr(perm), _ptr(counts))
+                                              _ptr(skeys), _ptr(ssrc), _ptr(shint), _ptr(perm),
+                                              _ptr(counts))
         if rc == L.CX_E_STATE and "region" in (L.lib().cx_last_error() or b"").decode():
             return None
         L.check(rc)
-        return skeys, ssrc, perm, [int(c) for c in counts]
+        out = (skeys, ssrc, perm, [int(c) for c in counts])
+        return out + (shint,) if hints else out
 
-    def arc_route(self, src, keys, res=None):
+    def arc_route(self, src, keys, res=None, hint=None):
         """Packed results (int64: owner | hops << 32 | status << 40 | 1 << 63)
-        of lookups received from every rank, in input order (cx_arc_route)."""
+        of lookups received from every rank, in input order (cx_arc_route;
+        with the origins' source hints: cx_arc_route_hinted)."""
         keys = self._prep_keys(keys)
         src = self._prep_u32(src, "src", keys.shape[0])
         if not (_is_dev(keys) and _is_dev(src)):
             raise TypeError("arc routing takes device tensors")
         q = keys.shape[0]
+        if hint is not None:
+            if not (_is_dev(hint) and hint.element_size() == 8 and hint.is_contiguous()
+                    and hint.numel() == q):
+                raise TypeError("hint must be a contiguous 8-byte device tensor of q elements")
+            if res is None:
+                res = torch.empty(q, dtype=torch.int64, device=keys.device)
+            self._arc_stream()
+            L.check(L.lib().cx_arc_route_hinted(self._h, _ptr(src), _ptr(keys), _ptr(hint), q,
+                                                _ptr(res)))
+            return res
         if res is None:
             res = torch.empty(q, dtype=torch.int64, device=keys.device)
         elif not (_is_dev(res) and res.element_size() == 8 and res.numel() == q

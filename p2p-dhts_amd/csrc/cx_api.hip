@@ -1876,7 +1876,8 @@ int cx_arc_partition(const cx_ring *ring, int world, const uint32_t *src, const 
 
 int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src,
                              const cx_u128 *keys, size_t q, uint64_t cap, cx_u128 *send_keys,
-                             uint32_t *send_src, uint32_t *perm, uint64_t *counts) {
+                             uint32_t *send_src, uint64_t *send_hint, uint32_t *perm,
+                             uint64_t *counts) {
     CX_CHECK(ring && counts, CX_E_INVALID, "null argument");
     CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
     CX_CHECK(q == 0 || (src && keys && send_keys && send_src && perm), CX_E_INVALID,
@@ -1886,6 +1887,7 @@ int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src
     CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
              "arc not built for this world size (cx_arc_build)");
     CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    CX_CHECK(!send_hint || ring->d_ring_ext, CX_E_STATE, "arc not built (cx_arc_build)");
     int rc = use_device(ring);
     if (rc) return rc;
     hipStream_t s = ring->stream;
@@ -1898,13 +1900,31 @@ int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src
     CX_HIP(cxk::arc_partition_regions(src, reinterpret_cast<const cell128 *>(keys), q,
                                       ring->d_arc_bounds, ring->arc_nb, world, (uint32_t)cap,
                                       dcur, dovf, reinterpret_cast<cell128 *>(send_keys),
-                                      send_src, perm, s));
+                                      send_src, perm, send_hint, ring->d_ring_ext, ring->n,
+                                      ring->pk_ib, s));
     uint32_t ovf = 0;
     CX_HIP(hipMemcpyAsync(hc, dcur, world * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     CX_HIP(hipMemcpyAsync(&ovf, dovf, sizeof(ovf), hipMemcpyDeviceToHost, s));
     CX_HIP(hipStreamSynchronize(s));
     for (int g = 0; g < world; ++g) counts[g] = hc[g] - (uint64_t)g * cap;
     CX_CHECK(!ovf, CX_E_STATE, "arc partition: a destination's lookups exceed its region (cap)");
+    return CX_OK;
+}
+
+int cx_arc_route_hinted(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
+                        const uint64_t *hint, size_t q, uint64_t *res) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    CX_CHECK(q == 0 || (src && keys && res && hint), CX_E_INVALID, "null buffer");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    SearchView v = ring->sv();
+    v.dir = ring->d_dir;
+    CX_HIP(cxk::route_arc_kf(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
+                             ring->rt_l0, ring->rt_R, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
+                             ring->arc_M, src, reinterpret_cast<const cell128 *>(keys), q, res,
+                             ring->stream, hint));
     return CX_OK;
 }
 

@@ -2835,6 +2835,7 @@ struct TreeIO {
     uint8_t *hops;
     uint8_t *status;
     uint64_t *res_out;   // key-first arc walk: packed results in input order
+    const uint64_t *dh;  // key-first arc walk: the origin's source hints (or null)
     // STATS build only: [0] 64-B table gathers, [1] exact 16-B ring gathers,
     // [2] exact hops (one F + one ring gather each), [3] lookups started
     unsigned long long *stats;
@@ -2901,6 +2902,7 @@ void k_route_tree(TreeIO io) {
     uint64_t pqid = 0;
     u128 pkey = 0, pa = 0, pb = 0;
     uint32_t psrc = 0, ph = 0;
+    uint64_t pdh = 0;          // KF with hints: the origin's source hint
     uint32_t n_g64 = 0, n_r16 = 0, n_xc = 0, n_q = 0;  // STATS counters
     uint32_t *xcp = STATS ? &n_xc : nullptr;
 
@@ -2951,6 +2953,7 @@ void k_route_tree(TreeIO io) {
                 } else {  // a new lookup (arc mode: issued on this rank)
                     pkey = ld128(io.keys + pq);
                     psrc = io.src[pq];
+                    if (KF && io.dh) pdh = io.dh[pq];
                     pqid = (ARC && !KF) ? ((uint64_t)io.self << ARC_ORIGIN_SHIFT) | pq : pq;
                     ph = 0;
                     pkind = ARC_NEW;
@@ -3006,7 +3009,9 @@ void k_route_tree(TreeIO io) {
             xb = ld128(io.ring + pn);
         }
         if (bst == B_KS) {
-            if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
+            if (KF && io.dh) {
+                // the origin resolved the start: no source pair to load
+            } else if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
                 if (pkind == ARC_NEW) pa = ld128(io.ring_ext + psrc);  // pred: local check only
                 pb = ld128(io.ring_ext + psrc + 1);
             }
@@ -3144,6 +3149,22 @@ void k_route_tree(TreeIO io) {
                 done = 0;
             } else if (cur >= n) {
                 st = CX_Q_BADPEER;
+            } else if (KF && io.dh) {
+                if (pdh == ARC_HINT_LOCAL) {
+                    own = cur;  // StoredLocally at the source (the origin checked it)
+                } else {
+                    // d = key - id_src in units of 2^gs from the origin; id_src is
+                    // fetched (A_FIXC) only if a decision needs it exactly
+                    cex = false;
+                    dmin = dmax = pdh;
+                    done = cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs, ri,
+                                   ent32, own, st, xcp);
+                    if (done == 2) {
+                        own = CX_NONE;
+                        st = CX_QI_ARC_MISS;
+                        done = 1;
+                    }
+                }
             } else if (pkind == ARC_NEW && (n == 1 || (key - pa - 1) <= (pb - pa - 1))) {
                 own = cur;  // StoredLocally at the source: 0 hops
             } else {
@@ -3341,9 +3362,10 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
 hipError_t route_arc_kf(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                         int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo,
                         uint32_t M, const uint32_t *src, const cell128 *keys, size_t q,
-                        uint64_t *res, hipStream_t s) {
+                        uint64_t *res, hipStream_t s, const uint64_t *dh) {
     if (q == 0) return hipSuccess;
     TreeIO io = {};
+    io.dh = dh;
     io.src = src;
     io.keys = keys;
     io.ring_ext = ring_ext;
@@ -3532,11 +3554,19 @@ __global__ __launch_bounds__(256) void k_arc_scatter(ArcIn<SEED> in, size_t q,
 // starts at d cap, so no count pass is needed before the scatter; a block
 // whose reservation would cross its region's end writes nothing of it and
 // raises *ovf (the caller then partitions with the two-pass kernel).
+// hint (sd != nullptr): the origin resolves the lookup's start at its source,
+// reading (pred, self) of src from ring_ext in lookup order (coalesced: src =
+// q mod N is sequential), and sends d = (key - id_src) >> gs with it, or
+// ARC_HINT_LOCAL when StoredLocally holds at the source (0 hops), so the arc
+// rank's walk starts without the source pair -- a random 32-B gather per
+// lookup there, since the lookups it receives come from every origin.
 __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t q,
                                                          const ArcBound *bounds, int nb, int G,
                                                          uint32_t *cursor, cell128 *skeys,
                                                          uint32_t *ssrc, uint32_t *slot_of,
-                                                         uint32_t cap, uint32_t *ovf) {
+                                                         uint32_t cap, uint32_t *ovf,
+                                                         uint64_t *sd, const cell128 *ring_ext,
+                                                         uint32_t n, int gs) {
     __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
@@ -3556,6 +3586,19 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
                 d[k] = arc_dest(r[k], sb, nb, G);
             }
         }
+        uint64_t dh[ARC_SCAT_R];
+        if (sd) {
+#pragma unroll
+            for (int k = 0; k < ARC_SCAT_R; ++k) {
+                dh[k] = ARC_HINT_BAD;
+                if (d[k] >= 0 && r[k].cur < n) {
+                    const u128 key = ((u128)r[k].w1 << 64) | r[k].w0;
+                    const u128 pa = ld128(ring_ext + r[k].cur), pb = ld128(ring_ext + r[k].cur + 1);
+                    dh[k] = (n == 1 || (key - pa - 1) <= (pb - pa - 1)) ? ARC_HINT_LOCAL
+                                                                         : (uint64_t)((key - pb) >> gs);
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
         __syncthreads();
@@ -3573,6 +3616,7 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
                 const uint32_t o = basep[d[k]] + slot[k];
                 skeys[o] = cell128{r[k].w0, r[k].w1};
                 ssrc[o] = r[k].cur;
+                if (sd) sd[o] = dh[k];
                 slot_of[r[k].qid & ARC_INDEX_MASK] = o;
             }
         __syncthreads();
@@ -3628,7 +3672,8 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
     hipError_t e = arc_bucket_in(in, q, bounds, nb, G, counts_dev, cursor_dev, nullptr, s, false);
     if (e != hipSuccess || q == 0) return e;
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
-        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, 0u, nullptr);
+        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, 0u, nullptr, nullptr, nullptr, 0u,
+        0);
     return hipGetLastError();
 }
 
@@ -3636,11 +3681,13 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
 hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_t q,
                                  const ArcBound *bounds, int nb, int G, uint32_t cap,
                                  uint32_t *cursor_dev, uint32_t *ovf, cell128 *skeys,
-                                 uint32_t *ssrc, uint32_t *perm, hipStream_t s) {
+                                 uint32_t *ssrc, uint32_t *perm, uint64_t *sd,
+                                 const cell128 *ring_ext, size_t n, int ib, hipStream_t s) {
     if (q == 0) return hipSuccess;
     const ArcIn<true> in{nullptr, src, keys, 0};
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
-        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, cap, ovf);
+        in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, cap, ovf, sd, ring_ext,
+        (uint32_t)n, cz_shift(ib));
     return hipGetLastError();
 }
 

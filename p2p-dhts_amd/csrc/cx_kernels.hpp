@@ -31,6 +31,9 @@ struct ArcBound {
     uint32_t rank, pad;
 };
 #define ARC_INDEX_MASK ((1ull << ARC_ORIGIN_SHIFT) - 1)
+// source hints of the key-first exchange (d >> gs < 2^36, so these are free)
+#define ARC_HINT_LOCAL 0xFFFFFFFFFFFFFFFFull  // StoredLocally at the source: 0 hops
+#define ARC_HINT_BAD 0xFFFFFFFFFFFFFFFEull    // src not a ring index (BADPEER at the arc)
 enum { ARC_NEW = 0, ARC_RESULT = 1, ARC_WALK = 2, ARC_NONE = 3 };
 
 // Peer liveness and successors_ lists for the literal walk's dead-finger
@@ -176,7 +179,7 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
 hipError_t route_arc_kf(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                         int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo,
                         uint32_t M, const uint32_t *src, const cell128 *keys, size_t q,
-                        uint64_t *res, hipStream_t s);
+                        uint64_t *res, hipStream_t s, const uint64_t *dh = nullptr);
 hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
                          const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
                          uint32_t *cursor_dev, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
@@ -184,7 +187,8 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
 hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_t q,
                                  const ArcBound *bounds, int nb, int G, uint32_t cap,
                                  uint32_t *cursor_dev, uint32_t *ovf, cell128 *skeys,
-                                 uint32_t *ssrc, uint32_t *perm, hipStream_t s);
+                                 uint32_t *ssrc, uint32_t *perm, uint64_t *sd,
+                                 const cell128 *ring_ext, size_t n, int ib, hipStream_t s);
 hipError_t arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q, uint32_t *owner,
                        uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,

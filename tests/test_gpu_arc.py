@@ -240,7 +240,7 @@ def test_arc_refuses_hand_edited_state(cx, O):
 # Structure-of-arrays key-first protocol (ArcRouter.route_soa): partition by
 # the key's arc, walk in receive order, answers back in send order.
 # ---------------------------------------------------------------------------
-def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0):
+def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0, hints=False):
     import torch
     rings = [cx.Ring(ids_dev) for _ in range(G)]
     for g, r in enumerate(rings):
@@ -256,7 +256,8 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0):
         torch.cuda.synchronize()
         return outs, 0
     if cap:  # single-pass partition into destination regions
-        parts = [rings[g].arc_partition_regions(G, srcs[g], keys[g], cap) for g in range(G)]
+        parts = [rings[g].arc_partition_regions(G, srcs[g], keys[g], cap, hints=hints)
+                 for g in range(G)]
         assert all(p is not None for p in parts)
         for g, (sk, ss, perm, counts) in enumerate(parts):
             assert sum(counts) == keys[g].shape[0]
@@ -265,6 +266,8 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0):
             assert torch.equal(torch.sort(perm.long()).values, want)
         ks = [[p[0][d * cap: d * cap + p[3][d]] for d in range(G)] for p in parts]
         ss = [[p[1][d * cap: d * cap + p[3][d]] for d in range(G)] for p in parts]
+        hs = [[p[4][d * cap: d * cap + p[3][d]] for d in range(G)] for p in parts] if hints \
+            else None
     else:
         parts = [rings[g].arc_partition(G, srcs[g], keys[g]) for g in range(G)]
         for g, (sk, ss, perm, counts) in enumerate(parts):
@@ -277,7 +280,10 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0):
     for d in range(G):
         rk = torch.cat([ks[g][d] for g in range(G)])
         rs = torch.cat([ss[g][d] for g in range(G)])
-        res = rings[d].arc_route(rs, rk)
+        if hints:
+            res = rings[d].arc_route(rs, rk, hint=torch.cat([hs[g][d] for g in range(G)]))
+        else:
+            res = rings[d].arc_route(rs, rk)
         for g, part in enumerate(torch.split(res, [parts[g][3][d] for g in range(G)])):
             back[g][d] = part
     sent = 0
@@ -310,8 +316,10 @@ def test_arc_soa_equals_replicated(cx, O, n, G):
         assert sent > 0
 
 
-@pytest.mark.parametrize("n,G", [(5000, 2), (5000, 8), (1 << 16, 8), (70001, 5), (9000, 33)])
-def test_arc_soa_regions_equals_replicated(cx, O, n, G):
+@pytest.mark.parametrize("hints", [False, True])
+@pytest.mark.parametrize("n,G", [(5000, 2), (5000, 8), (1 << 16, 8), (70001, 5), (9000, 33),
+                                 (2, 2), (3, 4)])
+def test_arc_soa_regions_equals_replicated(cx, O, n, G, hints):
     """cx_arc_partition_regions (single pass, destination regions of cap
     slots) + delivery through region slots == the replicated route; a cap
     below some destination's count is refused (None) and writes nothing."""
@@ -319,7 +327,9 @@ def test_arc_soa_regions_equals_replicated(cx, O, n, G):
     q = 4096
     ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2E0 + n + G)
     cap = q // G + q // (4 * G) + 64
-    outs, sent = simulate_soa(cx, ids_dev, G, srcs, keys, cap=cap)
+    if n < 10:
+        cap = q  # tiny rings: every key may land in one arc
+    outs, sent = simulate_soa(cx, ids_dev, G, srcs, keys, cap=cap, hints=hints)
     for g in range(G):
         ow, hp, st = ring.route(srcs[g], keys[g])
         assert torch.equal(outs[g][0], ow), (n, G, g)
@@ -328,6 +338,31 @@ def test_arc_soa_regions_equals_replicated(cx, O, n, G):
     r = cx.Ring(ids_dev)
     r.arc_build(G, 0)
     assert r.arc_partition_regions(G, srcs[0], keys[0], 1) is None
+
+
+def test_arc_hints_bad_sources_and_local_keys(cx, O):
+    """Source hints at the edges: out-of-range sources (BADPEER at the arc
+    rank), keys stored at their source (0 hops, resolved at the origin), and
+    keys equal to a peer's ID -- all equal to the replicated route."""
+    import torch
+    n, q, G = 20000, 3000, 4
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2E9)
+    ids = ring.ids_device()
+    for g in range(G):
+        srcs[g][::13] = n + 3
+        # key = the source's own ID (StoredLocally at the source) and the ID of
+        # the peer after the source
+        k = keys[g].clone()
+        s = srcs[g].clone().long().clamp(max=n - 1)
+        k[1::7] = ids[s[1::7]]
+        k[2::7] = ids[(s[2::7] + 1) % n]
+        keys[g] = k.contiguous()
+    outs, _ = simulate_soa(cx, ids_dev, G, srcs, keys, cap=q, hints=True)
+    for g in range(G):
+        ow, hp, st = ring.route(srcs[g], keys[g])
+        assert torch.equal(outs[g][0], ow) and torch.equal(outs[g][1], hp)
+        assert torch.equal(outs[g][2], st)
+        assert int((st == cx.CX_Q_BADPEER).sum()) > 0 and int((hp == 0).sum()) > 0
 
 
 @pytest.mark.parametrize("top", [1, 3, 6, 12])

@@ -146,7 +146,9 @@ class OracleArcEngine:
                 src[torch.from_numpy(order)].contiguous(),
                 torch.from_numpy(slot.astype(np.int32)), counts)
 
-    def arc_partition_regions(self, world, src, keys, cap):
+    arc_hints = True  # plumbing check: hint = 7 src + 1 must arrive next to its src
+
+    def arc_partition_regions(self, world, src, keys, cap, hints=False):
         """Region layout of cx_arc_partition_regions: destination d's lookups
         at rows [d cap, d cap + count_d), perm = region slot; None past cap."""
         import torch
@@ -163,11 +165,15 @@ class OracleArcEngine:
         rk[torch.from_numpy(new_slot)] = sk
         rs[torch.from_numpy(new_slot)] = ss
         perm = torch.from_numpy(new_slot[slot.numpy()].astype(np.int32))
+        if hints:
+            return rk, rs, perm, counts, rs.to(torch.int64) * 7 + 1
         return rk, rs, perm, counts
 
-    def arc_route(self, src, keys):
+    def arc_route(self, src, keys, hint=None):
         import torch
         import oracle as O
+        if hint is not None:  # the hints travelled with their lookups
+            assert torch.equal(hint, src.to(torch.int64) * 7 + 1)
         k = keys.numpy().view(np.uint64).reshape(-1, 2)
         ow, hp, st = O.route(self.P, src.numpy().astype(np.uint32), k)
         own = np.asarray(ow, dtype=np.uint64)
