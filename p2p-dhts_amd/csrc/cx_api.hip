@@ -462,14 +462,28 @@ void free_ring(cx_ring *r) {
 #define CX_DIR_EXTRA_DEFAULT 1
 #endif
 
-// Eytzinger copy + bucket directory of r->d_ring (r->n set).
-int build_search(cx_ring *r, hipStream_t s) {
-    const size_t m = r->n;
+// Eytzinger copy of r->d_ring: only the Eytzinger searches (variants 0 and 3)
+// read it, so it is built when one of them is selected (256 MiB and 0.2 ms at
+// 2^24 that a default ring -- and every churn epoch -- no longer pays).
+int ensure_eyt(cx_ring *r, hipStream_t s) {
+    if (r->d_eyt || !r->d_ring) return CX_OK;
     DBuf E;
-    CX_HIP(E.alloc((m + 1) * sizeof(cell128)));
-    CX_HIP(cxk::eyt_build(r->d_ring, m, E.as<cell128>(), s));
+    CX_HIP(E.alloc((r->n + 1) * sizeof(cell128)));
+    CX_HIP(cxk::eyt_build(r->d_ring, r->n, E.as<cell128>(), s));
+    CX_HIP(hipStreamSynchronize(s));
     r->d_eyt = E.as<cell128>();
     E.release();
+    return CX_OK;
+}
+
+// Bucket directory (and, for the Eytzinger searches, the Eytzinger copy) of
+// r->d_ring (r->n set).
+int build_search(cx_ring *r, hipStream_t s) {
+    const size_t m = r->n;
+    if (r->search_variant == 0 || r->search_variant == 3) {
+        int rc = ensure_eyt(r, s);
+        if (rc) return rc;
+    }
     // 2^k buckets, k = ceil(log2 n) + extra: a query's bucket entry resolves it
     // unless the bucket holds >= 2 peers and the key lies past the first; each
     // extra bit halves the load factor (fewer second gathers, 2x the bytes).
@@ -2118,6 +2132,11 @@ int cxi_set_churn_variant(cx_ring *ring, int variant) {
 int cxi_set_search_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0, 1, 2 or 3");
+    if (variant == 0 || variant == 3) {
+        int rc = use_device(ring);
+        if (rc) return rc;
+        if ((rc = ensure_eyt(ring, ring->stream))) return rc;
+    }
     ring->search_variant = variant;
     return CX_OK;
 }
