@@ -6,7 +6,7 @@ comes from the environment (CX_CZ_PAIR, CX_CZ_CHUNK, CX_CZ_STORE: read once
 per process), so run one process per variant under rocprofv3 --kernel-trace
 --stats for per-kernel times.  With CX_CZ_PAIR in {0, 1} the hash must equal
 the default build's.
-    python benches/bench_czbuild.py [log2 peers]
+    python benches/bench_czbuild.py [log2 peers] [table_build variant: 0 default, 3 roots]
 """
 import json
 import os
@@ -23,10 +23,12 @@ import chordx  # noqa: E402
 
 def main():
     lg = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    tb = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # cxi_set_table_build variant
     ids = torch.empty((1 << lg, 2), dtype=torch.int64, device="cuda")
     chordx.fill_splitmix(ids, 0x5EED0007)
     ring = chordx.Ring(ids)
     del ids
+    ring.set_table_build(tb)
     ts = []
     for _ in range(3):
         torch.cuda.synchronize()
@@ -35,7 +37,7 @@ def main():
         ring.sync()
         ts.append(time.perf_counter() - t0)
     v, esc, tb = ring.route_info()
-    out = {"log2_peers": lg, "variant_env": {k: os.environ.get(k) for k in
+    out = {"log2_peers": lg, "table_build": tb, "variant_env": {k: os.environ.get(k) for k in
                                              ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE")},
            "fingers_and_table_s": ts, "route_table_hash": ring.route_table_hash(),
            "route_variant": v, "escapes": esc}

@@ -545,10 +545,13 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         if (e != hipSuccess) return e;
         fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
-    if (r->table_build == 0 &&
+    if ((r->table_build == 0 || r->table_build == 3) &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t), s) == hipSuccess) {
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
-        if (e == hipSuccess) fv.C2 = c2.as<uint32_t>();
+        if (e == hipSuccess) {
+            fv.C2 = c2.as<uint32_t>();
+            fv.roots = r->table_build == 3 ? 1 : 0;
+        }
     }
     (void)hipGetLastError();
     return e;
@@ -899,7 +902,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     DBuf ft_pre;
     bool ft_done = false;
     const int ft_l = ring->rt_l0 - 5;
-    if (ring->variant() == 5 && ring->table_build == 0 && ft_l >= 64 &&
+    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
         ft_pre.alloc_pooled((size_t)(CX_FINGERS - ft_l) * ring->n * sizeof(uint32_t), s) != hipSuccess) {
         (void)hipGetLastError();
         ft_pre.p = nullptr;
@@ -2092,11 +2095,12 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
 }
 
 // Route-table build input: 0 = finger level planes + two-hop planes (default),
-// 1 = row-major finger table, 2 = level planes only.  Takes effect at the next
+// 1 = row-major finger table, 2 = level planes only, 3 = level + two-hop
+// planes, root-centric windows (k_cz_build_roots).  Takes effect at the next
 // finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 2, CX_E_INVALID, "variant must be 0, 1 or 2");
+    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0, 1, 2 or 3");
     ring->table_build = variant;
     return CX_OK;
 }

@@ -2585,6 +2585,181 @@ __global__ __launch_bounds__(256) void k_cz_build_pair(FingerView fv, const cell
     if (bad) atomicAdd(esc, bad);
 }
 
+// Root-centric build (table_build 0): of the two entries (p, i, 0) and
+// (p, i, 1) only one word depends on p -- enc(A rel p) with A = f(p, i),
+// slot 0 of the b = 0 entry and slot 15 of the b = 1 entry -- while the other
+// fifteen words of each are a function of (A, i): W0(A, i) = the window
+// below A over levels i-2..i-5 (slots 1..15), W1(A, i) = A' = f(A, i-1)
+// relative to A (slot 0) and the window below A' (slots 1..14).  A block
+// takes 256 consecutive rows of one level (both planes): the rows' roots are
+// non-decreasing along the ring (f(., i) is monotone up to one wrap), so the
+// block compacts them to their distinct values (~0.63 per row on a uniform
+// ring), computes both windows once per distinct root into LDS (30 words),
+// and writes the 2 x 256 entries as coalesced 16-B chunks assembled from LDS
+// (whole lines per store instruction, no staging copy).  Bit-identical to
+// k_cz_build (route_table_hash, tests/test_gpu_parity.py); dispatch order
+// is k_cz_build's K-row-block chunks over all levels.
+constexpr int CZR_W = 31;  // LDS words per root: W0[1..15], W1[0..14], CZ_NONE count
+__global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cell128 *ring,
+                                                        const uint64_t *rh, uint32_t n,
+                                                        int lvl_base, int nlev, uint32_t p_first,
+                                                        uint32_t M, int gs, uint4 *cz,
+                                                        uint32_t *esc, uint32_t K) {
+    __shared__ uint32_t win[256 * CZR_W];
+    __shared__ uint32_t e0s[256];
+    __shared__ uint32_t roots[256];
+    __shared__ uint16_t ridx[256];
+    __shared__ uint32_t wcnt[4];
+    uint32_t lvl, lb;
+    {
+        const uint32_t B = blockIdx.x;
+        const uint32_t chunk = B / (K * (uint32_t)nlev), rem = B - chunk * K * (uint32_t)nlev;
+        lvl = rem / K;
+        const uint32_t sub = rem - lvl * K;
+        lb = chunk * K + (sub & 7) * (K >> 3) + (sub >> 3);
+    }
+    const int i = lvl_base + (int)lvl;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t j0 = lb * 256u;
+    const uint32_t rows = M > j0 ? (M - j0 < 256u ? M - j0 : 256u) : 0u;
+    if (rows == 0) return;  // block-uniform
+    auto fat = [&](uint32_t x, int l) -> uint32_t { return fv.F[(size_t)(l - fv.L) * fv.sl + x]; };
+    auto c2 = [&](uint32_t x, int l) -> uint32_t { return fv.C2[(size_t)(l - fv.L - 1) * fv.sl + x]; };
+    uint32_t oob = 0;
+    auto chk = [&](uint32_t x) -> uint32_t {
+        if (x >= n) {
+            oob = 1;
+            return 0u;
+        }
+        return x;
+    };
+    // ---- rows: root and the row's own word ----
+    const bool valid = (uint32_t)t < rows;
+    uint32_t A = 0xFFFFFFFFu;
+    uint32_t bad = 0;
+    if (valid) {
+        uint64_t pw = (uint64_t)p_first + j0 + t;
+        if (pw >= n) pw -= n;
+        const uint32_t p = (uint32_t)pw;
+        A = chk(fat(p, i));
+        const uint32_t e0 = cz_encode_hi(n, gs, p, rh[p], i, A, rh[A], ring);
+        e0s[t] = e0;
+        bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
+    }
+    roots[t] = A;  // staged for the neighbour compare
+    __syncthreads();
+    const bool first = valid && (t == 0 || roots[t - 1] != A);
+    const uint64_t fm = __ballot(first);
+    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(fm);
+    __syncthreads();
+    uint32_t base = 0, nr = 0;
+    for (int w = 0; w < 4; ++w) {
+        base += w < wv ? wcnt[w] : 0u;
+        nr += wcnt[w];
+    }
+    const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+    const uint32_t incl = rank + (first ? 1u : 0u);  // distinct roots up to and including t
+    __syncthreads();  // every lane has read roots[t - 1]
+    if (first) roots[rank] = A;
+    if (valid) ridx[t] = (uint16_t)(incl - 1);
+    __syncthreads();
+    // ---- windows of the distinct roots (lanes 0 .. nr-1) ----
+    if ((uint32_t)t < nr) {
+        const uint32_t R = roots[t];
+        uint32_t *wr = win + t * CZR_W;
+        uint32_t wbad = 0;
+        // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
+        {
+            uint32_t nd[16];
+            nd[0] = R;
+            nd[1] = chk(fat(R, i - 2));
+            nd[2] = chk(fat(R, i - 3));
+            nd[3] = chk(c2(R, i - 2));
+            nd[4] = chk(fat(R, i - 4));
+            nd[6] = chk(c2(R, i - 3));
+            nd[8] = chk(fat(R, i - 5));
+            nd[12] = chk(c2(R, i - 4));
+            nd[5] = chk(fat(nd[1], i - 4));
+            nd[7] = chk(fat(nd[3], i - 4));
+            nd[9] = chk(fat(nd[1], i - 5));
+            nd[10] = chk(fat(nd[2], i - 5));
+            nd[11] = chk(fat(nd[3], i - 5));
+            nd[13] = chk(c2(nd[1], i - 4));
+            nd[14] = chk(c2(nd[2], i - 4));
+            nd[15] = chk(c2(nd[3], i - 4));
+            uint64_t hv[16];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) hv[v] = rh[nd[v]];
+#pragma unroll
+            for (int v = 1; v < 16; ++v) {
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pv = v & ~(1 << hb);
+                const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                wbad += o == CZ_NONE;
+                wr[v - 1] = o;
+            }
+        }
+        // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
+        {
+            uint32_t nd[15];
+            nd[0] = chk(fat(R, i - 1));
+            nd[1] = chk(fat(nd[0], i - 2));
+            nd[2] = chk(fat(nd[0], i - 3));
+            nd[3] = chk(c2(nd[0], i - 2));
+            nd[4] = chk(fat(nd[0], i - 4));
+            nd[6] = chk(c2(nd[0], i - 3));
+            nd[8] = chk(fat(nd[0], i - 5));
+            nd[12] = chk(c2(nd[0], i - 4));
+            nd[5] = chk(fat(nd[1], i - 4));
+            nd[7] = chk(fat(nd[3], i - 4));
+            nd[9] = chk(fat(nd[1], i - 5));
+            nd[10] = chk(fat(nd[2], i - 5));
+            nd[11] = chk(fat(nd[3], i - 5));
+            nd[13] = chk(c2(nd[1], i - 4));
+            nd[14] = chk(c2(nd[2], i - 4));
+            uint64_t hv[15];
+#pragma unroll
+            for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
+            const uint32_t o0 = cz_encode_hi(n, gs, R, rh[R], i - 1, nd[0], hv[0], ring);
+            wbad += o0 == CZ_NONE;
+            wr[15] = o0;
+#pragma unroll
+            for (int v = 1; v < 15; ++v) {
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pv = v & ~(1 << hb);
+                const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                wbad += o == CZ_NONE;
+                wr[15 + v] = o;
+            }
+        }
+        wr[30] = wbad;
+    }
+    __syncthreads();
+    if (valid) bad += win[ridx[t] * CZR_W + 30];
+    // ---- stores: 2 planes x rows entries x 4 chunks of 16 B, assembled from LDS ----
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const size_t t0 = (size_t)(2 * lvl) * M + j0;
+    for (uint32_t c = t; c < 2u * 256u * 4u; c += 256u) {
+        const uint32_t pl = c >> 10, cc = c & 1023u, e = cc >> 2, qq = cc & 3u;
+        if (e >= rows) continue;
+        const uint32_t *wr = win + ridx[e] * CZR_W;
+        uint32_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t word = qq * 4u + (uint32_t)u;
+            if (pl == 0)
+                w[u] = word == 0 ? e0s[e] : wr[word - 1];
+            else
+                w[u] = word == 15 ? e0s[e] : wr[15 + word];
+        }
+        const v4u wv4 = {w[0], w[1], w[2], w[3]};
+        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (t0 + (size_t)pl * M + e) * 4) + qq);
+    }
+    if (oob) atomicOr(esc + 1, 1u);
+    if (bad) atomicAdd(esc, bad);
+}
+
 hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                     int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s) {
     return cz_build_part(fv, ring, rh, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s);
@@ -2636,6 +2811,15 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const char *e = getenv("CX_CZ_PAIR");
         return e ? atoi(e) : 0;
     }();
+    if (planes && fv.C2 && fv.roots) {
+        const uint32_t Kr = K ? K : 16;
+        const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
+        const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
+        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+        k_cz_build_roots<<<(unsigned)blocks, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
+                                                          p_first, M, gs, out, esc, Kr);
+        return hipGetLastError();
+    }
     if (planes && fv.C2 && pair >= 1 && pair <= 3) {
         const uint32_t Kp = K ? K : 16;
         const uint64_t nrb = ((uint64_t)M + 127) / 128, chunks = (nrb + Kp - 1) / Kp;

@@ -120,14 +120,15 @@ struct FingerView {
     // planes only, optional: two-hop planes C2[(l - L - 1) * sl + x] =
     // F[F[x][l]][l - 1] for l in (L, L + nl) (fingers_pairs)
     const uint32_t *C2 = nullptr;
+    int roots = 0;  // host-side build choice: 1 = root-centric windows (needs C2)
     __host__ __device__ uint32_t at(uint32_t x, int l) const {
         return F[(size_t)x * sx + (size_t)(l - L) * sl];
     }
     static FingerView rows(const uint32_t *F) {
-        return FingerView{F, CX_FINGERS, 1, 0, CX_FINGERS, nullptr};
+        return FingerView{F, CX_FINGERS, 1, 0, CX_FINGERS, nullptr, 0};
     }
     static FingerView planes(const uint32_t *FT, size_t n, int L, int nl) {
-        return FingerView{FT, 1, n, L, nl, nullptr};
+        return FingerView{FT, 1, n, L, nl, nullptr, 0};
     }
 };
 // Order-sensitive 64-bit hash of `bytes` (multiple of 8) into *out (device).

@@ -259,7 +259,8 @@ def simulate_soa(cx, ids_dev, G, srcs, keys, status=True, top=0, cap=0, hints=Fa
         parts = [rings[g].arc_partition_regions(G, srcs[g], keys[g], cap, hints=hints)
                  for g in range(G)]
         assert all(p is not None for p in parts)
-        for g, (sk, ss, perm, counts) in enumerate(parts):
+        for g, p in enumerate(parts):
+            sk, ss, perm, counts = p[:4]
             assert sum(counts) == keys[g].shape[0]
             want = torch.cat([torch.arange(d * cap, d * cap + counts[d], device="cuda")
                               for d in range(G)])
