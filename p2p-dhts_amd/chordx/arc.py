@@ -103,12 +103,20 @@ class ArcRouter:
         return (recv.to(send.device) if recv.device != send.device else recv), inflight
 
     def _a2a(self, t, out_splits, in_splits, dev):
-        """Asynchronous all_to_all_single: (output, work)."""
+        """Asynchronous all-to-all-v of a contiguous buffer: (output, work).
+        On RCCL every SoA exchange is a list all_to_all (split views), so all
+        ranks issue the same collective kind whether their pieces were laid
+        out in regions or packed; gloo takes all_to_all_single."""
         s = t.to(dev) if t.device != torch.device(dev) else t
         out = torch.empty((sum(out_splits),) + tuple(s.shape[1:]), dtype=s.dtype, device=dev)
-        work = tdist.all_to_all_single(out, s.contiguous(), output_split_sizes=out_splits,
-                                       input_split_sizes=in_splits, group=self.group,
-                                       async_op=True)
+        if out.is_cuda:
+            work = tdist.all_to_all(list(torch.split(out, list(out_splits))),
+                                    list(torch.split(s.contiguous(), list(in_splits))),
+                                    group=self.group, async_op=True)
+        else:
+            work = tdist.all_to_all_single(out, s.contiguous(), output_split_sizes=out_splits,
+                                           input_split_sizes=in_splits, group=self.group,
+                                           async_op=True)
         return out, work
 
     def _a2a_regions(self, t, counts, cap, out_splits, dev):
