@@ -156,6 +156,9 @@ def cpu_baseline(ring_np, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s
             "sample": f"first {qa} keys of the rank-0 stream (of {len(keys_np)}) on {threads} "
                       f"threads ({dta:.1f} s), first {q1} on 1 thread ({dt1:.1f} s); "
                       "oracle/chord_oracle.c or_route, gcc -O3 -march=x86-64-v3",
+            "cores_note": "threads = this process's CPU affinity capped by OMP_NUM_THREADS, the "
+                          "job's share of the host (nproc counts the whole machine); the walk "
+                          "scales linearly in threads (value / value_1core)",
             "parity_on_sample": ok}
 
 
