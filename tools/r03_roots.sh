@@ -7,8 +7,8 @@ TAG=${1:-r03_roots}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_arc.py tests/test_gpu_parity.py \
-  -x -v --timeout 300 --timeout-method thread -k "arc or route_table" > "$OUT/pytest.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+  > "$OUT/pytest.log" 2>&1 || true   # failures are read from the log; a hang still stops here
 tail -2 "$OUT/pytest.log"
 cd /tmp && export TMPDIR=/tmp
 for tb in 0 3; do
