@@ -7,8 +7,11 @@ TAG=${1:-r03_roots}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$GRAFT_REPO_ROOT"
+rc=0
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
-  > "$OUT/pytest.log" 2>&1 || true   # failures are read from the log; a hang still stops here
+  > "$OUT/pytest.log" 2>&1 || rc=$?
+# test failures (rc 1) are read from the log; a crash, abort or time limit ends the call
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc"; tail -5 "$OUT/pytest.log"; exit $rc; fi
 tail -2 "$OUT/pytest.log"
 cd /tmp && export TMPDIR=/tmp
 for tb in 0 3; do
