@@ -256,6 +256,7 @@ struct cx_ring {
     hipStream_t stream = nullptr;
     size_t n = 0;
     cell128 *d_ring = nullptr;     // sorted unique IDs [n]
+    size_t ring_cap = 0;           // cells allocated for d_ring (>= n: before dedupe)
     cell128 *d_eyt = nullptr;      // Eytzinger copy [n+1]
     uint32_t *d_fingers = nullptr; // [n][128]
     bool fingers_converged = false;
@@ -431,10 +432,12 @@ void free_ring(cx_ring *r) {
     if (!r) return;
     (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
-    (void)hipFree(r->d_ring);
+    // the ring's per-peer arrays recur at the same sizes every membership
+    // epoch: through the pool like the tables (below 16 MiB: freed)
+    table_free(r->device, r->d_ring, r->ring_cap * sizeof(cell128));
     (void)hipFree(r->d_eyt);
-    (void)hipFree(r->d_dir);
-    (void)hipFree(r->d_ring_key);
+    table_free(r->device, r->d_dir, r->d_dir ? ((size_t)1 << r->dir_k) * sizeof(uint4) : 0);
+    table_free(r->device, r->d_ring_key, r->n * sizeof(uint32_t));
     const size_t ent = r->n * (size_t)r->rt_R;
     table_free(r->device, r->d_fingers, r->n * CX_FINGERS * sizeof(uint32_t));
     table_free(r->device, r->d_rt, ent * sizeof(RtEntry));
@@ -443,7 +446,7 @@ void free_ring(cx_ring *r) {
     table_free(r->device, r->d_cz, ent * 128);
     (void)hipFree(r->d_stree);
     (void)hipFree(r->d_eyt_rank);
-    (void)hipFree(r->d_ring_ext);
+    table_free(r->device, r->d_ring_ext, (r->n + 1) * sizeof(cell128));
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
     (void)hipFree(r->d_alive);
@@ -452,7 +455,7 @@ void free_ring(cx_ring *r) {
     table_free(r->device, r->d_arc_tree, r->arc_bytes);
     (void)hipFree(r->d_arc_bounds);
     (void)hipFree(r->d_stats);
-    (void)hipFree(r->d_o2n_canon);
+    table_free(r->device, r->d_o2n_canon, r->o2n_canon_n * sizeof(uint32_t));
     table_free(r->device, r->d_cdir, r->cdir_bytes);
     if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
     delete r;
@@ -499,8 +502,8 @@ int build_search(cx_ring *r, hipStream_t s) {
     if (k > 29) k = 29;
     r->dir_k = k;
     DBuf lo, dir;
-    CX_HIP(lo.alloc((((size_t)1 << k) + 1) * sizeof(uint32_t)));
-    CX_HIP(dir.alloc(((size_t)1 << k) * sizeof(uint4)));
+    CX_HIP(lo.alloc_pooled((((size_t)1 << k) + 1) * sizeof(uint32_t), s));
+    CX_HIP(dir.alloc_pooled(((size_t)1 << k) * sizeof(uint4), s));
     CX_HIP(cxk::dir_build(r->d_ring, m, k, lo.as<uint32_t>(), dir.as<uint4>(), s));
     CX_HIP(hipStreamSynchronize(s));
     r->d_dir = dir.as<uint4>();
@@ -617,8 +620,8 @@ int churn_merge(const cx_ring *old_ring, const cell128 *J0, size_t nj, const cel
     const size_t sw = cxk::scan_workspace_words(n_old + 2 > nj + 1 ? n_old + 2 : nj + 1);
     const size_t rw = nj ? cxk::sort_workspace_words(nj) : 0;
     CX_HIP(ws.alloc((sw > rw ? sw : rw) * sizeof(uint32_t)));
-    CX_HIP(G.alloc((n_old + 1) * sizeof(uint32_t)));
-    CX_HIP(A.alloc((n_old + 2) * sizeof(uint32_t)));
+    CX_HIP(G.alloc_pooled((n_old + 1) * sizeof(uint32_t), s));
+    CX_HIP(A.alloc_pooled((n_old + 2) * sizeof(uint32_t), s));
     CX_HIP(hipMemsetAsync(G.p, 0, (n_old + 1) * sizeof(uint32_t), s));
     CX_HIP(hipMemsetAsync(A.p, 0, (n_old + 2) * sizeof(uint32_t), s));
     CX_HIP(cxk::merge_mark(v, old_ring->d_ring, L, nl, G.as<uint32_t>(), s));
@@ -649,12 +652,13 @@ int churn_merge(const cx_ring *old_ring, const cell128 *J0, size_t nj, const cel
     CX_HIP(hipStreamSynchronize(s));
     const size_t m = n_old - gone + kept;
     CX_CHECK(m >= 1, CX_E_INVALID, "churn would leave an empty ring");
-    CX_HIP(ringbuf.alloc(m * sizeof(cell128)));
-    CX_HIP(o2n.alloc(n_old * sizeof(uint32_t)));
+    CX_HIP(ringbuf.alloc_pooled(m * sizeof(cell128), s));
+    CX_HIP(o2n.alloc_pooled(n_old * sizeof(uint32_t), s));
     CX_HIP(cxk::merge_scatter(old_ring->d_ring, n_old, G.as<uint32_t>(), A.as<uint32_t>(), J, nj,
                               pos.as<uint32_t>(), keep.as<uint32_t>(), ringbuf.as<cell128>(),
                               o2n.as<uint32_t>(), s));
     r->n = m;
+    r->ring_cap = m;
     r->d_ring = ringbuf.as<cell128>();
     ringbuf.release();
     return CX_OK;
@@ -717,7 +721,7 @@ int cx_ring_create(const cx_u128 *ids, size_t n, int memkind, int device, cx_rin
         CX_HIP(pos.alloc(n * sizeof(uint32_t)));
         CX_HIP(cxk::radix_sort(k0.as<cell128>(), t0.as<uint32_t>(), k1.as<cell128>(),
                                t1.as<uint32_t>(), n, ws.as<uint32_t>(), s));
-        CX_HIP(ring.alloc(n * sizeof(cell128)));
+        CX_HIP(ring.alloc_pooled(n * sizeof(cell128), s));
         CX_HIP(cxk::unique_sorted(k0.as<cell128>(), t0.as<uint32_t>(), n, pos.as<uint32_t>(),
                                   ws.as<uint32_t>(), ring.as<cell128>(), nullptr,
                                   r->d_scratch, s));
@@ -726,6 +730,7 @@ int cx_ring_create(const cx_u128 *ids, size_t n, int memkind, int device, cx_rin
         CX_HIP(hipStreamSynchronize(s));
         CX_CHECK(m >= 1 && m <= n, CX_E_HIP, "ring build produced an invalid size");
         r->n = m;
+        r->ring_cap = n;
         r->d_ring = ring.as<cell128>();
         ring.release();
         return build_search(r, s);
@@ -841,7 +846,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
     SearchView fv = ring->sv();
     fv.dir = ring->d_dir;
     if (!search_only && !ring->d_ring_key) {
-        if (dev_malloc(&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
+        if (table_alloc((void **)&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
             CX_HIP(cxk::ring_slice_build(ring->d_ring, ring->n, cxk::finger_key_shift(ring->n),
                                          ring->d_ring_key, s));
         else
@@ -910,7 +915,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     if ((rc = build_fingers_table(ring, s, ft_pre.as<uint32_t>(), ft_l, &ft_done))) return rc;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
-        dev_malloc(&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
+        table_alloc((void **)&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
     if (ring->d_ring_ext) CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
     // the default route kernel's table is built now (outside any timed query)
@@ -1215,6 +1220,7 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         CX_HIP(hipStreamSynchronize(s));
         CX_CHECK(m >= 1 && m <= total, CX_E_HIP, "churn produced an invalid ring size");
         r->n = m;
+        r->ring_cap = total;
         r->d_ring = ringbuf.as<cell128>();
         ringbuf.release();
         r->search_variant = old_ring->search_variant;
