@@ -6,7 +6,7 @@ comes from the environment (CX_CZ_PAIR, CX_CZ_CHUNK, CX_CZ_STORE: read once
 per process), so run one process per variant under rocprofv3 --kernel-trace
 --stats for per-kernel times.  With CX_CZ_PAIR in {0, 1} the hash must equal
 the default build's.
-    python benches/bench_czbuild.py [log2 peers] [table_build variant: 0 default, 3 roots]
+    python benches/bench_czbuild.py [log2 peers] [table_build: 0 root-centric (default), 3 one lane per entry]
 """
 import json
 import os
@@ -36,7 +36,7 @@ def main():
         ring.build_fingers()
         ring.sync()
         ts.append(time.perf_counter() - t0)
-    v, esc, tb = ring.route_info()
+    v, esc, table_bytes = ring.route_info()
     out = {"log2_peers": lg, "table_build": tb, "variant_env": {k: os.environ.get(k) for k in
                                              ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE")},
            "fingers_and_table_s": ts, "route_table_hash": ring.route_table_hash(),

@@ -304,9 +304,10 @@ class Ring:
         return h.value
 
     def set_table_build(self, v: int):
-        """Internal A/B switch for the route-table build's finger input:
-        0 = level planes + two-hop planes (default), 1 = the row-major finger
-        table, 2 = level planes only."""
+        """Internal A/B switch for the route-table build: 0 = level + two-hop
+        planes, root-centric windows (default), 1 = the row-major finger
+        table, 2 = level planes only, 3 = level + two-hop planes, one lane per
+        entry (the round-2 build).  All build the same table."""
         f = L.lib().cxi_set_table_build
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))

@@ -270,7 +270,7 @@ struct cx_ring {
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
     uint64_t *d_cz = nullptr;      // pattern-keyed window table [rt_R][2][n][8 x u64] (variant 5)
-    int table_build = 0;           // route-table build input: 0 level + two-hop planes,
+    int table_build = 0;           // route-table build input: 0 level + two-hop planes (roots),
                                    // 1 row-major fingers, 2 level planes only (A/B)
     bool cz_valid = false;
     uint64_t cz_escapes = 0;       // nodes the compressed format could not represent
@@ -553,7 +553,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) {
             fv.C2 = c2.as<uint32_t>();
-            fv.roots = r->table_build == 3 ? 1 : 0;
+            fv.roots = r->table_build == 0 ? 1 : 0;  // 3: one lane per entry (round 2)
         }
     }
     (void)hipGetLastError();
@@ -2100,9 +2100,10 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
     return CX_OK;
 }
 
-// Route-table build input: 0 = finger level planes + two-hop planes (default),
-// 1 = row-major finger table, 2 = level planes only, 3 = level + two-hop
-// planes, root-centric windows (k_cz_build_roots).  Takes effect at the next
+// Route-table build input: 0 = finger level + two-hop planes, root-centric
+// windows (k_cz_build_roots, default), 1 = row-major finger table, 2 = level
+// planes only, 3 = level + two-hop planes, one lane per entry (k_cz_build,
+// the round-2 build).  All give the same table.  Takes effect at the next
 // finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");

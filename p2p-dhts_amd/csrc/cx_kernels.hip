@@ -2585,7 +2585,7 @@ __global__ __launch_bounds__(256) void k_cz_build_pair(FingerView fv, const cell
     if (bad) atomicAdd(esc, bad);
 }
 
-// Root-centric build (table_build 0): of the two entries (p, i, 0) and
+// Root-centric build (table_build 0, the default): of the two entries (p, i, 0) and
 // (p, i, 1) only one word depends on p -- enc(A rel p) with A = f(p, i),
 // slot 0 of the b = 0 entry and slot 15 of the b = 1 entry -- while the other
 // fifteen words of each are a function of (A, i): W0(A, i) = the window

@@ -609,10 +609,10 @@ def test_route_table_from_level_planes_identical(lg):
     ring.set_table_build(2)
     ring.build_fingers()
     h_planes_only = ring.route_table_hash()
-    ring.set_table_build(3)  # root-centric windows
+    ring.set_table_build(3)  # one lane per entry (the default is root-centric)
     ring.build_fingers()
-    h_roots = ring.route_table_hash()
-    assert h_planes == h_rows == h_planes_only == h_roots and h_planes != 0
+    h_entry = ring.route_table_hash()
+    assert h_planes == h_rows == h_planes_only == h_entry and h_planes != 0
 
 
 @pytest.mark.parametrize("kind", ["small", "mixed", "clustered"])
@@ -638,7 +638,7 @@ def test_route_table_builds_edge_rings(cx, O, kind):
     ring.set_table_build(2)
     ring.build_fingers()
     h2, e2 = ring.route_table_hash(), ring.route_info()[1]
-    ring.set_table_build(3)  # root-centric windows
+    ring.set_table_build(3)  # one lane per entry (the default is root-centric)
     ring.build_fingers()
     h3, e3 = ring.route_table_hash(), ring.route_info()[1]
     assert h0 == h2 == h3 and e0 == e2 == e3 and h0 != 0
