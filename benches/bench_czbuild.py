@@ -38,7 +38,8 @@ def main():
         ts.append(time.perf_counter() - t0)
     v, esc, table_bytes = ring.route_info()
     out = {"log2_peers": lg, "table_build": tb, "variant_env": {k: os.environ.get(k) for k in
-                                             ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE")},
+                                             ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE",
+                                              "CX_CZ_ROOTS_RB")},
            "fingers_and_table_s": ts, "route_table_hash": ring.route_table_hash(),
            "route_variant": v, "escapes": esc}
     if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1"):

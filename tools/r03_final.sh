@@ -42,4 +42,11 @@ cut -c1-200 "$OUT/bench_n2.json"
 CX_DIST_BACKEND=gloo timeout -k 10 400 python3 -u benches/bench_c5.py --gpus 2 --peers-log2 22 \
   --keys-log2 24 --steps 3 --warmup 1 > "$OUT/c5_n2.json" 2> "$OUT/c5_n2.err"
 tail -1 "$OUT/c5_n2.json" | cut -c1-200
+# root-centric build rows-per-block A/B (256 / 192 / 128) at 2^24
+cd /tmp
+for rb in 256 192 128; do
+  CX_CZ_ROOTS_RB=$rb timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/rb$rb" -o run \
+    --output-format csv -- python3 "$R/benches/bench_czbuild.py" 24 0 > "$OUT/rb$rb.json" 2> "$OUT/rb$rb.err"
+  tail -1 "$OUT/rb$rb.json" | cut -c1-200
+done
 echo done
