@@ -39,10 +39,12 @@ def main():
     v, esc, table_bytes = ring.route_info()
     out = {"log2_peers": lg, "table_build": tb, "variant_env": {k: os.environ.get(k) for k in
                                              ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE",
-                                              "CX_CZ_ROOTS_RB")},
+                                              "CX_CZ_ROOTS_MODE")},
            "fingers_and_table_s": ts, "route_table_hash": ring.route_table_hash(),
            "route_variant": v, "escapes": esc}
-    if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1"):
+    # probes (stores-only / compute-only) leave an unspecified table: no route
+    if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1") and \
+            os.environ.get("CX_CZ_ROOTS_MODE", "0") == "0":
         q = 1 << 22
         keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
         chordx.fill_splitmix(keys, 0x5EED0008)

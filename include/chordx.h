@@ -203,6 +203,16 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
 int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_t *old_to_new,
                  const cx_u128 *keys, size_t q, int n, uint32_t *new_lists, uint8_t *count,
                  uint16_t *mask, uint8_t *target, int memkind);
+/* C5's step in one pass over the keys: cx_nsucc(old_ring, keys, n) into
+ * old_lists / old_count (DHashPeer::Create's placement on the pre-churn ring,
+ * dhash_peer.cpp:103-129) + cx_misplaced (RunGlobalMaintenance,
+ * dhash_peer.cpp:298-348).  Outputs equal the two calls' outputs; the scan
+ * already resolves each key's old successor, so the placement costs only its
+ * list stores.  All buffers in memkind. */
+int cx_dhash_maintenance(const cx_ring *old_ring, const cx_ring *new_ring,
+                         const uint32_t *old_to_new, const cx_u128 *keys, size_t q, int n,
+                         uint32_t *old_lists, uint8_t *old_count, uint32_t *new_lists,
+                         uint8_t *count, uint16_t *mask, uint8_t *target, int memkind);
 /* Same scan with explicit holders (q x nh ring indices, CX_NONE = empty), e.g.
  * keys inserted straight into a non-owner's db (dhash_test.cpp:123-149).
  * target is q x nh.  nh <= 16. */

@@ -40,7 +40,7 @@ EXPORTS = (
     "cx_ring_ids_device", "cx_ring_set_stream", "cx_ring_use_own_stream", "cx_ring_sync",
     "cx_successor", "cx_predecessor", "cx_fingers_build", "cx_fingers_upload", "cx_fingers_device",
     "cx_peer_state_upload", "cx_liveness_upload", "cx_route", "cx_nsucc", "cx_dhash_check",
-    "cx_churn", "cx_misplaced", "cx_misplaced_holders", "cx_in_between",
+    "cx_churn", "cx_misplaced", "cx_dhash_maintenance", "cx_misplaced_holders", "cx_in_between",
     "cx_uuid5_dns", "cx_fill_splitmix",
     "cx_arc_build", "cx_arc_info", "cx_arc_seed", "cx_arc_start", "cx_arc_step",
     "cx_arc_bucket", "cx_arc_send_ahead",
@@ -103,6 +103,7 @@ def lib() -> ctypes.CDLL:
         "cx_dhash_check": ([vp, i, i], i),
         "cx_churn": ([vp, vp, sz, vp, sz, i, pp, vp], i),
         "cx_misplaced": ([vp, vp, vp, vp, sz, i, vp, vp, vp, vp, i], i),
+        "cx_dhash_maintenance": ([vp, vp, vp, vp, sz, i, vp, vp, vp, vp, vp, vp, i], i),
         "cx_misplaced_holders": ([vp, vp, sz, vp, i, i, vp, vp, vp, vp, i], i),
         "cx_in_between": ([vp, vp, vp, sz, i, vp, i], i),
         "cx_uuid5_dns": ([vp, vp, sz, vp, i, i], i),

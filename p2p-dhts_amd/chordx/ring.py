@@ -389,6 +389,25 @@ class Ring:
                                      _ptr(lists), _ptr(count), _ptr(mask), _ptr(target), mk))
         return lists, count, mask, target
 
+    def dhash_maintenance(self, new_ring: "Ring", old_to_new, keys, n: int):
+        """nsucc(keys, n) on this (old) ring + misplaced(new_ring, ...) in one
+        pass (cx_dhash_maintenance): (old_lists, old_count, new_lists, count,
+        mask, target), each equal to the separate calls' outputs."""
+        keys = self._prep_keys(keys)
+        o2n = self._prep_u32(old_to_new, "old_to_new", self.n)
+        q = keys.shape[0]
+        old_lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
+        old_count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
+        count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        mask = self._empty(keys, (q,), np.uint16, torch and torch.int16)
+        target = self._empty(keys, (q, n), np.uint8, torch and torch.uint8)
+        mk = new_ring._mem(keys, o2n, lists)
+        L.check(L.lib().cx_dhash_maintenance(self._h, new_ring._h, _ptr(o2n), _ptr(keys), q, n,
+                                             _ptr(old_lists), _ptr(old_count), _ptr(lists),
+                                             _ptr(count), _ptr(mask), _ptr(target), mk))
+        return old_lists, old_count, lists, count, mask, target
+
     def misplaced_holders(self, keys, holders, n: int):
         keys = self._prep_keys(keys)
         holders = self._prep_u32(holders, "holders", keys.shape[0])

@@ -1250,27 +1250,34 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
     return CX_OK;
 }
 
-int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_t *old_to_new,
-                 const cx_u128 *keys, size_t q, int n, uint32_t *new_lists, uint8_t *count,
-                 uint16_t *mask, uint8_t *target, int memkind) {
+// cx_misplaced, and with old_lists / old_count the fused cx_dhash_maintenance
+static int misplaced_impl(const cx_ring *old_ring, const cx_ring *new_ring,
+                          const uint32_t *old_to_new, const cx_u128 *keys, size_t q, int n,
+                          uint32_t *old_lists, uint8_t *old_count, uint32_t *new_lists,
+                          uint8_t *count, uint16_t *mask, uint8_t *target, int memkind) {
     CX_CHECK(old_ring && new_ring, CX_E_INVALID, "null ring");
     CX_CHECK(old_ring->device == new_ring->device, CX_E_INVALID, "rings on different devices");
     CX_CHECK(n >= 1 && n <= CX_MAX_NSUCC, CX_E_INVALID, "n must be in [1, 16]");
     int rc = use_device(new_ring);
     if (rc) return rc;
     hipStream_t s = new_ring->stream;
-    DBuf to2n, tk, tl, tc, tm, tt;
+    DBuf to2n, tk, tl, tc, tm, tt, tol, toc;
     const uint32_t *d_o2n;
     const cx_u128 *dk;
-    uint32_t *dl;
-    uint8_t *dc, *dt;
+    uint32_t *dl, *dol = nullptr;
+    uint8_t *dc, *dt, *doc = nullptr;
     uint16_t *dm;
+    const bool fused = old_lists != nullptr;
     if ((rc = stage_in(old_to_new, old_ring->n, memkind, to2n, &d_o2n, s))) return rc;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
     if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl))) return rc;
     if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
     if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
     if ((rc = stage_out(target, q * (size_t)n, memkind, tt, &dt))) return rc;
+    if (fused) {
+        if ((rc = stage_out(old_lists, q * (size_t)n, memkind, tol, &dol))) return rc;
+        if ((rc = stage_out(old_count, q, memkind, toc, &doc))) return rc;
+    }
     // churn directory: the new ring came from cx_churn(old_ring) and the
     // caller's mapping equals the one it returned (checked on the device)
     cxk::ChurnDirArgs cda{};
@@ -1313,15 +1320,35 @@ int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_
     }
     CX_HIP(cxk::misplaced_churn(old_ring->sv(), new_ring->sv(), d_o2n,
                                 reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, dm, dt,
-                                cd_ok ? &cda : nullptr, s));
+                                cd_ok ? &cda : nullptr, s, dol, doc));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(new_lists, dl, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
         CX_HIP(hipMemcpyAsync(count, dc, q, hipMemcpyDeviceToHost, s));
         CX_HIP(hipMemcpyAsync(mask, dm, q * 2, hipMemcpyDeviceToHost, s));
         CX_HIP(hipMemcpyAsync(target, dt, q * (size_t)n, hipMemcpyDeviceToHost, s));
+        if (fused) {
+            CX_HIP(hipMemcpyAsync(old_lists, dol, q * (size_t)n * 4, hipMemcpyDeviceToHost, s));
+            CX_HIP(hipMemcpyAsync(old_count, doc, q, hipMemcpyDeviceToHost, s));
+        }
         CX_HIP(hipStreamSynchronize(s));
     }
     return CX_OK;
+}
+
+int cx_misplaced(const cx_ring *old_ring, const cx_ring *new_ring, const uint32_t *old_to_new,
+                 const cx_u128 *keys, size_t q, int n, uint32_t *new_lists, uint8_t *count,
+                 uint16_t *mask, uint8_t *target, int memkind) {
+    return misplaced_impl(old_ring, new_ring, old_to_new, keys, q, n, nullptr, nullptr, new_lists,
+                          count, mask, target, memkind);
+}
+
+int cx_dhash_maintenance(const cx_ring *old_ring, const cx_ring *new_ring,
+                         const uint32_t *old_to_new, const cx_u128 *keys, size_t q, int n,
+                         uint32_t *old_lists, uint8_t *old_count, uint32_t *new_lists,
+                         uint8_t *count, uint16_t *mask, uint8_t *target, int memkind) {
+    CX_CHECK(old_lists && old_count, CX_E_INVALID, "null old_lists / old_count");
+    return misplaced_impl(old_ring, new_ring, old_to_new, keys, q, n, old_lists, old_count,
+                          new_lists, count, mask, target, memkind);
 }
 
 int cx_misplaced_holders(const cx_ring *ring, const cx_u128 *keys, size_t q,

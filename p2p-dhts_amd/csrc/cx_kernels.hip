@@ -2604,7 +2604,7 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
                                                         const uint64_t *rh, uint32_t n,
                                                         int lvl_base, int nlev, uint32_t p_first,
                                                         uint32_t M, int gs, uint4 *cz,
-                                                        uint32_t *esc, uint32_t K) {
+                                                        uint32_t *esc, uint32_t K, int mode) {
     __shared__ uint32_t win[256 * CZR_W];
     __shared__ uint32_t e0s[256];
     __shared__ uint32_t roots[256];
@@ -2623,6 +2623,11 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
     const uint32_t j0 = lb * 256u;
     const uint32_t rows = M > j0 ? (M - j0 < 256u ? M - j0 : 256u) : 0u;
     if (rows == 0) return;  // block-uniform
+    // mode (A/B probes, CX_CZ_ROOTS_MODE; 0 = the build): 1 compute only, 2
+    // stores only (LDS contents unspecified), 3 = even blocks compute only, odd
+    // blocks store only (do the two halves overlap when different waves run them?)
+    const bool do_compute = mode == 0 || mode == 1 || (mode == 3 && !(lb & 1));
+    const bool do_store = mode == 0 || mode == 2 || (mode == 3 && (lb & 1));
     auto fat = [&](uint32_t x, int l) -> uint32_t { return fv.F[(size_t)(l - fv.L) * fv.sl + x]; };
     auto c2 = [&](uint32_t x, int l) -> uint32_t { return fv.C2[(size_t)(l - fv.L - 1) * fv.sl + x]; };
     uint32_t oob = 0;
@@ -2637,110 +2642,115 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
     const bool valid = (uint32_t)t < rows;
     uint32_t A = 0xFFFFFFFFu;
     uint32_t bad = 0;
-    if (valid) {
-        uint64_t pw = (uint64_t)p_first + j0 + t;
-        if (pw >= n) pw -= n;
-        const uint32_t p = (uint32_t)pw;
-        A = chk(fat(p, i));
-        const uint32_t e0 = cz_encode_hi(n, gs, p, rh[p], i, A, rh[A], ring);
-        e0s[t] = e0;
-        bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
-    }
-    roots[t] = A;  // staged for the neighbour compare
-    __syncthreads();
-    const bool first = valid && (t == 0 || roots[t - 1] != A);
-    const uint64_t fm = __ballot(first);
-    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(fm);
-    __syncthreads();
-    uint32_t base = 0, nr = 0;
-    for (int w = 0; w < 4; ++w) {
-        base += w < wv ? wcnt[w] : 0u;
-        nr += wcnt[w];
-    }
-    const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-    const uint32_t incl = rank + (first ? 1u : 0u);  // distinct roots up to and including t
-    __syncthreads();  // every lane has read roots[t - 1]
-    if (first) roots[rank] = A;
-    if (valid) ridx[t] = (uint16_t)(incl - 1);
-    __syncthreads();
-    // ---- windows of the distinct roots (lanes 0 .. nr-1) ----
-    if ((uint32_t)t < nr) {
-        const uint32_t R = roots[t];
-        uint32_t *wr = win + t * CZR_W;
-        uint32_t wbad = 0;
-        // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
-        {
-            uint32_t nd[16];
-            nd[0] = R;
-            nd[1] = chk(fat(R, i - 2));
-            nd[2] = chk(fat(R, i - 3));
-            nd[3] = chk(c2(R, i - 2));
-            nd[4] = chk(fat(R, i - 4));
-            nd[6] = chk(c2(R, i - 3));
-            nd[8] = chk(fat(R, i - 5));
-            nd[12] = chk(c2(R, i - 4));
-            nd[5] = chk(fat(nd[1], i - 4));
-            nd[7] = chk(fat(nd[3], i - 4));
-            nd[9] = chk(fat(nd[1], i - 5));
-            nd[10] = chk(fat(nd[2], i - 5));
-            nd[11] = chk(fat(nd[3], i - 5));
-            nd[13] = chk(c2(nd[1], i - 4));
-            nd[14] = chk(c2(nd[2], i - 4));
-            nd[15] = chk(c2(nd[3], i - 4));
-            uint64_t hv[16];
-#pragma unroll
-            for (int v = 0; v < 16; ++v) hv[v] = rh[nd[v]];
-#pragma unroll
-            for (int v = 1; v < 16; ++v) {
-                const int hb = 31 - __builtin_clz((unsigned)v);
-                const int pv = v & ~(1 << hb);
-                const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
-                wbad += o == CZ_NONE;
-                wr[v - 1] = o;
-            }
+    if (!do_compute) {
+        if (valid) ridx[t] = 0;
+        __syncthreads();
+    } else {
+        if (valid) {
+            uint64_t pw = (uint64_t)p_first + j0 + t;
+            if (pw >= n) pw -= n;
+            const uint32_t p = (uint32_t)pw;
+            A = chk(fat(p, i));
+            const uint32_t e0 = cz_encode_hi(n, gs, p, rh[p], i, A, rh[A], ring);
+            e0s[t] = e0;
+            bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
         }
-        // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
-        {
-            uint32_t nd[15];
-            nd[0] = chk(fat(R, i - 1));
-            nd[1] = chk(fat(nd[0], i - 2));
-            nd[2] = chk(fat(nd[0], i - 3));
-            nd[3] = chk(c2(nd[0], i - 2));
-            nd[4] = chk(fat(nd[0], i - 4));
-            nd[6] = chk(c2(nd[0], i - 3));
-            nd[8] = chk(fat(nd[0], i - 5));
-            nd[12] = chk(c2(nd[0], i - 4));
-            nd[5] = chk(fat(nd[1], i - 4));
-            nd[7] = chk(fat(nd[3], i - 4));
-            nd[9] = chk(fat(nd[1], i - 5));
-            nd[10] = chk(fat(nd[2], i - 5));
-            nd[11] = chk(fat(nd[3], i - 5));
-            nd[13] = chk(c2(nd[1], i - 4));
-            nd[14] = chk(c2(nd[2], i - 4));
-            uint64_t hv[15];
-#pragma unroll
-            for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
-            const uint32_t o0 = cz_encode_hi(n, gs, R, rh[R], i - 1, nd[0], hv[0], ring);
-            wbad += o0 == CZ_NONE;
-            wr[15] = o0;
-#pragma unroll
-            for (int v = 1; v < 15; ++v) {
-                const int hb = 31 - __builtin_clz((unsigned)v);
-                const int pv = v & ~(1 << hb);
-                const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
-                wbad += o == CZ_NONE;
-                wr[15 + v] = o;
-            }
+        roots[t] = A;  // staged for the neighbour compare
+        __syncthreads();
+        const bool first = valid && (t == 0 || roots[t - 1] != A);
+        const uint64_t fm = __ballot(first);
+        if (lane == 0) wcnt[wv] = (uint32_t)__popcll(fm);
+        __syncthreads();
+        uint32_t base = 0, nr = 0;
+        for (int w = 0; w < 4; ++w) {
+            base += w < wv ? wcnt[w] : 0u;
+            nr += wcnt[w];
         }
-        wr[30] = wbad;
-    }
-    __syncthreads();
-    if (valid) bad += win[ridx[t] * CZR_W + 30];
+        const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+        const uint32_t incl = rank + (first ? 1u : 0u);  // distinct roots up to and including t
+        __syncthreads();  // every lane has read roots[t - 1]
+        if (first) roots[rank] = A;
+        if (valid) ridx[t] = (uint16_t)(incl - 1);
+        __syncthreads();
+        // ---- windows of the distinct roots (lanes 0 .. nr-1) ----
+        if ((uint32_t)t < nr) {
+            const uint32_t R = roots[t];
+            uint32_t *wr = win + t * CZR_W;
+            uint32_t wbad = 0;
+            // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
+            {
+                uint32_t nd[16];
+                nd[0] = R;
+                nd[1] = chk(fat(R, i - 2));
+                nd[2] = chk(fat(R, i - 3));
+                nd[3] = chk(c2(R, i - 2));
+                nd[4] = chk(fat(R, i - 4));
+                nd[6] = chk(c2(R, i - 3));
+                nd[8] = chk(fat(R, i - 5));
+                nd[12] = chk(c2(R, i - 4));
+                nd[5] = chk(fat(nd[1], i - 4));
+                nd[7] = chk(fat(nd[3], i - 4));
+                nd[9] = chk(fat(nd[1], i - 5));
+                nd[10] = chk(fat(nd[2], i - 5));
+                nd[11] = chk(fat(nd[3], i - 5));
+                nd[13] = chk(c2(nd[1], i - 4));
+                nd[14] = chk(c2(nd[2], i - 4));
+                nd[15] = chk(c2(nd[3], i - 4));
+                uint64_t hv[16];
+#pragma unroll
+                for (int v = 0; v < 16; ++v) hv[v] = rh[nd[v]];
+#pragma unroll
+                for (int v = 1; v < 16; ++v) {
+                    const int hb = 31 - __builtin_clz((unsigned)v);
+                    const int pv = v & ~(1 << hb);
+                    const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                    wbad += o == CZ_NONE;
+                    wr[v - 1] = o;
+                }
+            }
+            // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
+            {
+                uint32_t nd[15];
+                nd[0] = chk(fat(R, i - 1));
+                nd[1] = chk(fat(nd[0], i - 2));
+                nd[2] = chk(fat(nd[0], i - 3));
+                nd[3] = chk(c2(nd[0], i - 2));
+                nd[4] = chk(fat(nd[0], i - 4));
+                nd[6] = chk(c2(nd[0], i - 3));
+                nd[8] = chk(fat(nd[0], i - 5));
+                nd[12] = chk(c2(nd[0], i - 4));
+                nd[5] = chk(fat(nd[1], i - 4));
+                nd[7] = chk(fat(nd[3], i - 4));
+                nd[9] = chk(fat(nd[1], i - 5));
+                nd[10] = chk(fat(nd[2], i - 5));
+                nd[11] = chk(fat(nd[3], i - 5));
+                nd[13] = chk(c2(nd[1], i - 4));
+                nd[14] = chk(c2(nd[2], i - 4));
+                uint64_t hv[15];
+#pragma unroll
+                for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
+                const uint32_t o0 = cz_encode_hi(n, gs, R, rh[R], i - 1, nd[0], hv[0], ring);
+                wbad += o0 == CZ_NONE;
+                wr[15] = o0;
+#pragma unroll
+                for (int v = 1; v < 15; ++v) {
+                    const int hb = 31 - __builtin_clz((unsigned)v);
+                    const int pv = v & ~(1 << hb);
+                    const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                    wbad += o == CZ_NONE;
+                    wr[15 + v] = o;
+                }
+            }
+            wr[30] = wbad;
+        }
+        __syncthreads();
+        if (valid) bad += win[ridx[t] * CZR_W + 30];
+    }  // do_compute
     // ---- stores: 2 planes x rows entries x 4 chunks of 16 B, assembled from LDS ----
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     const size_t t0 = (size_t)(2 * lvl) * M + j0;
-    for (uint32_t c = t; c < 2u * 256u * 4u; c += 256u) {
+    for (uint32_t c = t; do_store && c < 2u * 256u * 4u; c += 256u) {
         const uint32_t pl = c >> 10, cc = c & 1023u, e = cc >> 2, qq = cc & 3u;
         if (e >= rows) continue;
         const uint32_t *wr = win + ridx[e] * CZR_W;
@@ -2812,12 +2822,16 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         return e ? atoi(e) : 0;
     }();
     if (planes && fv.C2 && fv.roots) {
+        static const int mode = [] {
+            const char *e = getenv("CX_CZ_ROOTS_MODE");
+            return e ? (atoi(e) & 3) : 0;
+        }();
         const uint32_t Kr = K ? K : 16;
         const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
         k_cz_build_roots<<<(unsigned)blocks, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                          p_first, M, gs, out, esc, Kr);
+                                                          p_first, M, gs, out, esc, Kr, mode);
         return hipGetLastError();
     }
     if (planes && fv.C2 && pair >= 1 && pair <= 3) {
@@ -4209,6 +4223,9 @@ __device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, uint32_t n
 // (holder - s_new) mod n_new < nn.  Rows (new list, targets) are staged in LDS
 // per block of 256 consecutive keys and written coalesced.  CD: the churn
 // directory settles most keys in one gather (cd_lookup) when *cd.ok.
+// old_lists / old_count (CHURN, may be null): the keys' old n-successor lists
+// as cx_nsucc on the old ring gives them -- the scan already holds the old
+// successor, so DHash placement + maintenance share one pass over the keys.
 template <bool CHURN, bool DIR, bool CD = false>
 __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, SearchView sv_old,
                                                          const uint32_t *old_to_new,
@@ -4216,7 +4233,8 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                                                          const cell128 *keys, size_t q, int nlist,
                                                          uint32_t *new_lists, uint8_t *count,
                                                          uint16_t *mask, uint8_t *target,
-                                                         ChurnDir cd) {
+                                                         ChurnDir cd, uint32_t *old_lists = nullptr,
+                                                         uint8_t *old_count = nullptr) {
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
     __shared__ __attribute__((aligned(16))) uint32_t stage_l[ROW_BLOCK * CX_MAX_NSUCC];
@@ -4236,6 +4254,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
          base += (size_t)gridDim.x * ROW_BLOCK) {
         const size_t i = base + threadIdx.x;
         const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
+        uint32_t so_row = 0;  // the key's old successor (old_lists)
         if (i < q) {
             const u128 key = ld128(keys + i);
             uint32_t sn = 0, so = 0, has = 0, m = 0;
@@ -4304,6 +4323,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                     else if (j < nslots) m |= 1u << j;
                 }
             }
+            so_row = so;
             uint32_t *l = stage_l + threadIdx.x * nlist;
             for (int j = 0; j < nlist; ++j) {
                 uint32_t v = sn + (uint32_t)j;
@@ -4333,25 +4353,44 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
         flush_rows(stage_l, new_lists, base, cnt, nlist);
         flush_rows(stage_t, target, base, cnt, nslots);
         __syncthreads();
+        if (CHURN && old_lists) {  // grid-uniform
+            if (i < q) {
+                uint32_t *l = stage_l + threadIdx.x * nlist;
+                for (int j = 0; j < nlist; ++j) {
+                    uint32_t v = so_row + (uint32_t)j;  // j < no <= n_old: one wrap at most
+                    if (v >= n_old) v -= n_old;
+                    l[j] = j < no ? v : CX_NONE;
+                }
+                old_count[i] = (uint8_t)no;
+            }
+            __syncthreads();
+            flush_rows(stage_l, old_lists, base, cnt, nlist);
+            __syncthreads();
+        }
     }
 }
 
 hipError_t misplaced_churn(const SearchView &sv_old, const SearchView &sv_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
-                           const ChurnDirArgs *cda, hipStream_t s) {
+                           const ChurnDirArgs *cda, hipStream_t s, uint32_t *old_lists,
+                           uint8_t *old_count) {
     if (q == 0) return hipSuccess;
+    if ((old_lists == nullptr) != (old_count == nullptr)) return hipErrorInvalidValue;
     ChurnDir cd = {};
     if (cda) cd = ChurnDir{cda->cd, cda->kb, sv_old.ring, sv_new.ring, cda->ok};
     if (cda && sv_new.dir && sv_old.dir)
         k_misplaced<true, true, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd);
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
+            old_lists, old_count);
     else if (sv_new.dir && sv_old.dir)
         k_misplaced<true, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd);
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
+            old_lists, old_count);
     else
         k_misplaced<true, false><<<cx_grid(q, ROW_BLOCK, 256), ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd);
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
+            old_lists, old_count);
     return hipGetLastError();
 }
 

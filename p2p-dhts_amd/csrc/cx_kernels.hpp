@@ -225,7 +225,8 @@ struct ChurnDirArgs {
 hipError_t misplaced_churn(const SearchView &ev_old, const SearchView &ev_new,
                            const uint32_t *old_to_new, const cell128 *keys, size_t q, int n,
                            uint32_t *lists, uint8_t *count, uint16_t *mask, uint8_t *target,
-                           const ChurnDirArgs *cda, hipStream_t s);
+                           const ChurnDirArgs *cda, hipStream_t s, uint32_t *old_lists = nullptr,
+                           uint8_t *old_count = nullptr);
 size_t churn_dir_workspace_bytes(size_t n_old, size_t n_new);
 // lo: 2^kb + 1 words; scan_ws: scan_workspace_words(max(n_old, n_new) + 1).
 hipError_t churn_dir_build(const SearchView &sv_old, const SearchView &sv_new,

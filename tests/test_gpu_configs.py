@@ -165,3 +165,16 @@ def test_c5_full_size_churn_and_misplaced_scan(O):
     assert (count == wc).all() and (mask == wm).all()
     assert (lists == wl).all() and (target == wt).all()
     assert 0 < int((mask != 0).sum()) < q
+    del lists, count, mask, target
+    # the fused step (bench_c5's): old lists = the old ring's window, the rest
+    # = the scan's outputs (all 2^26 keys)
+    keys_d = torch.from_numpy(keys.view(np.int64)).cuda()
+    o2n_d = torch.from_numpy(o2n.view(np.int32)).cuda()
+    ol, oc, nl, nc, nm, nt = old.dhash_maintenance(new, o2n_d, keys_d, n)
+    succ = old.successor(keys_d).to(torch.int64)
+    want = (succ[:, None] + torch.arange(n, device="cuda:0")) % old.n
+    assert bool((ol.to(torch.int64) == want).all()) and bool((oc == n).all())
+    del want, succ
+    assert (nl.cpu().numpy().view(np.uint32) == wl).all()
+    assert (nc.cpu().numpy() == wc).all() and (nm.cpu().numpy().view(np.uint16) == wm).all()
+    assert (nt.cpu().numpy() == wt).all()

@@ -712,6 +712,28 @@ def test_misplaced_churn_directory(cx, O, case):
         for a, b, c in zip(got, two, exp):
             assert (a == c).all(), (name, n)
             assert (b == c).all(), (name, n)
+        # fused placement + scan (cx_dhash_maintenance), directory and two-search paths
+        wl_old, wc_old = nsucc_window(O, want_old, keys, n)
+        for variant in (1, 0):
+            new.set_misplaced_variant(variant)
+            fz = old.dhash_maintenance(new, o2n, keys, n)
+            assert (fz[0] == wl_old).all() and (fz[1] == wc_old).all(), (name, n, variant)
+            for a, c in zip(fz[2:], exp):
+                assert (a == c).all(), (name, n, variant)
+        new.set_misplaced_variant(1)
+        ol, oc = old.nsucc(keys, n)
+        assert (ol == wl_old).all() and (oc == wc_old).all()
+
+
+def nsucc_window(O, ring, keys, n):
+    """GetNSuccessors' converged result (abstract_chord_peer.cpp:345-373):
+    ring[(succ(key) + j) mod N] for j < min(n, N), CX_NONE after."""
+    N = len(ring)
+    s = O.successor(ring, keys).astype(np.int64)
+    j = np.arange(n, dtype=np.int64)
+    w = ((s[:, None] + j) % N).astype(np.uint32)
+    w[:, j >= min(n, N)] = 0xFFFFFFFF
+    return w, np.full(len(keys), min(n, N), dtype=np.uint8)
 
 
 def test_misplaced_churn_directory_device_and_foreign_parent(cx, O):
@@ -733,9 +755,15 @@ def test_misplaced_churn_directory_device_and_foreign_parent(cx, O):
     got = old.misplaced(new, od, kd, 14)
     for a, b in zip(got, exp):
         assert (a.cpu().numpy().view(b.dtype).reshape(b.shape) == b).all()
+    fz = old.dhash_maintenance(new, od, kd, 14)
+    for a, b in zip(fz, nsucc_window(O, want_old, keys, 14) + tuple(exp)):
+        assert (a.cpu().numpy().view(b.dtype).reshape(b.shape) == b).all()
     other = cx.Ring(ids)   # same IDs, not new's parent
     got = other.misplaced(new, o2n, keys, 14)
     for a, b in zip(got, exp):
+        assert (a == b).all()
+    fz = other.dhash_maintenance(new, o2n, keys, 14)
+    for a, b in zip(fz, nsucc_window(O, want_old, keys, 14) + tuple(exp)):
         assert (a == b).all()
     bent = o2n.copy()
     bent[17] = 0xFFFFFFFF

@@ -42,11 +42,15 @@ cut -c1-200 "$OUT/bench_n2.json"
 CX_DIST_BACKEND=gloo timeout -k 10 400 python3 -u benches/bench_c5.py --gpus 2 --peers-log2 22 \
   --keys-log2 24 --steps 3 --warmup 1 > "$OUT/c5_n2.json" 2> "$OUT/c5_n2.err"
 tail -1 "$OUT/c5_n2.json" | cut -c1-200
-# root-centric build rows-per-block A/B (256 / 192 / 128) at 2^24
+# root-centric build and its probes at 2^24: 0 = the build, 1 compute only,
+# 2 stores only, 3 half the blocks each
 cd /tmp
-for rb in 256 192 128; do
-  CX_CZ_ROOTS_RB=$rb timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/rb$rb" -o run \
-    --output-format csv -- python3 "$R/benches/bench_czbuild.py" 24 0 > "$OUT/rb$rb.json" 2> "$OUT/rb$rb.err"
-  tail -1 "$OUT/rb$rb.json" | cut -c1-200
+for mode in 0 1 2 3; do
+  CX_CZ_ROOTS_MODE=$mode timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/mode$mode" -o run \
+    --output-format csv -- python3 "$R/benches/bench_czbuild.py" 24 0 > "$OUT/mode$mode.json" 2> "$OUT/mode$mode.err"
+  python3 -c "
+import csv
+k=[float(r['AverageNs'])/1e6 for r in csv.DictReader(open('$OUT/mode$mode/run_kernel_stats.csv')) if 'cz_build' in r['Name']]
+print('mode', $mode, 'kernel_ms', k)"
 done
 echo done

@@ -23,4 +23,15 @@ k=[float(r['AverageNs'])/1e6 for r in csv.DictReader(open('$OUT/rb${rb}_$pass/ru
 print('rb', $rb, '$pass', 'kernel_ms', k, 'hash', d['route_table_hash'])"
   done
 done
+# overlap probe (192 rows a block): compute only, stores only, and half the
+# blocks each (different waves on one CU running the two halves)
+for mode in 1 2 3; do
+  CX_CZ_ROOTS_MODE=$mode timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/mode$mode" -o run \
+    --output-format csv -- python3 "$R/benches/bench_czbuild.py" 24 0 > "$OUT/mode$mode.json" 2> "$OUT/mode$mode.err"
+  python3 -c "
+import csv
+k=[float(r['AverageNs'])/1e6 for r in csv.DictReader(open('$OUT/mode$mode/run_kernel_stats.csv')) if 'cz_build' in r['Name']]
+print('mode', $mode, 'kernel_ms', k)"
+done
+bash "$R/tools/r03_c5.sh" "${TAG}_c5"
 echo done
