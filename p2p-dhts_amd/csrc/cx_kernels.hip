@@ -3950,11 +3950,51 @@ __device__ __forceinline__ void flush_rows(const T *stage, T *out, size_t base, 
     for (int t = t0 + threadIdx.x; t < total; t += blockDim.x) dst[t] = stage[t];
 }
 
+// Rows of `w` ring indices (s[k] + j) mod N for j < nvalid, CX_NONE after, for
+// keys [base, base + cnt) of the block, s[k] staged in LDS: every word of the
+// block's contiguous output range is computed where it is stored (16-B
+// streaming stores), with no staging of the rows themselves.
+__device__ __forceinline__ void flush_window(const uint32_t *s, uint32_t *out, size_t base,
+                                             int cnt, int w, int nvalid, uint32_t N) {
+    const int total = cnt * w;
+    uint32_t *dst = out + base * (size_t)w;
+    auto val = [&](int k, int j) -> uint32_t {
+        uint32_t v = s[k] + (uint32_t)j;
+        if (v >= N) v -= N;
+        return j < nvalid ? v : CX_NONE;
+    };
+    int t0 = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const int nv = total >> 2;
+        v4u *dv = reinterpret_cast<v4u *>(dst);
+        for (int t = threadIdx.x; t < nv; t += blockDim.x) {
+            int k = (4 * t) / w, j = 4 * t - k * w;
+            uint32_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                x[u] = val(k, j);
+                if (++j == w) {
+                    j = 0;
+                    ++k;
+                }
+            }
+            const v4u xv = {x[0], x[1], x[2], x[3]};
+            __builtin_nontemporal_store(xv, dv + t);
+        }
+        t0 = nv << 2;
+    }
+    for (int t = t0 + threadIdx.x; t < total; t += blockDim.x) {
+        const int k = t / w;
+        dst[t] = val(k, t - k * w);
+    }
+}
+
 template <bool DIR>
 __global__ __launch_bounds__(ROW_BLOCK) void k_nsucc(SearchView sv, const cell128 *keys, size_t q,
                                                      int nlist, uint32_t *lists, uint8_t *count) {
     __shared__ u128 lds[Searcher<DIR>::LDS];
-    __shared__ __attribute__((aligned(16))) uint32_t stage[ROW_BLOCK * CX_MAX_NSUCC];
+    __shared__ uint32_t s_succ[ROW_BLOCK];
     Searcher<DIR>::stage(sv, lds);
     const uint32_t n = sv.ev.n;
     const int nn = (uint32_t)nlist < n ? nlist : (int)n;
@@ -3963,17 +4003,11 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_nsucc(SearchView sv, const cell12
         const size_t i = base + threadIdx.x;
         const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
         if (i < q) {
-            const uint32_t s0 = Searcher<DIR>::find(sv, lds, ld128(keys + i));
-            uint32_t *l = stage + threadIdx.x * nlist;
-            for (int j = 0; j < nlist; ++j) {
-                uint32_t v = s0 + (uint32_t)j;
-                if (v >= n) v -= n;
-                l[j] = j < nn ? v : CX_NONE;
-            }
+            s_succ[threadIdx.x] = Searcher<DIR>::find(sv, lds, ld128(keys + i));
             count[i] = (uint8_t)nn;
         }
         __syncthreads();
-        flush_rows(stage, lists, base, cnt, nlist);
+        flush_window(s_succ, lists, base, cnt, nlist, nn, n);
         __syncthreads();
     }
 }
@@ -4152,12 +4186,19 @@ struct ChurnDir {
     const uint32_t *ok;       // device flag: old_to_new equals cx_churn's mapping
 };
 
-// 1 = settled (so, sn, has, mis set), 0 = take the search path.
-__device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, uint32_t n_old,
-                                         uint32_t n_new, int no, int nn, uint32_t &so,
-                                         uint32_t &sn, uint32_t &has, uint32_t &mis) {
+// The key's 32-B bucket entry.
+__device__ __forceinline__ void cd_fetch(const ChurnDir &c, u128 key, uint4 &A, uint4 &B) {
     const size_t b = (size_t)(uint64_t)(key >> (128 - c.kb));
-    const uint4 A = c.cd[2 * b], B = c.cd[2 * b + 1];
+    A = c.cd[2 * b];
+    B = c.cd[2 * b + 1];
+}
+
+// 1 = settled (so, sn, has, mis set), 0 = take the search path.  A, B = the
+// key's bucket entry (cd_fetch).
+__device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, const uint4 A,
+                                         const uint4 B, uint32_t n_old, uint32_t n_new, int no,
+                                         int nn, uint32_t &so, uint32_t &sn, uint32_t &has,
+                                         uint32_t &mis) {
     const uint64_t xf = (uint64_t)(key >> (64 - c.kb));
     const uint64_t h0 = ((uint64_t)A.y << 32) | A.x;
     uint64_t tg = ((uint64_t)B.y << 32) | B.x;
@@ -4237,7 +4278,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                                                          uint8_t *old_count = nullptr) {
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t stage_l[ROW_BLOCK * CX_MAX_NSUCC];
+    __shared__ uint32_t s_sn[ROW_BLOCK], s_so[ROW_BLOCK];  // the tile's successors
     __shared__ uint8_t stage_t[ROW_BLOCK * CX_MAX_NSUCC];
     Searcher<DIR>::stage(sv_new, lds_new);
     if (CHURN) Searcher<DIR>::stage(sv_old, lds_old);
@@ -4254,12 +4295,13 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
          base += (size_t)gridDim.x * ROW_BLOCK) {
         const size_t i = base + threadIdx.x;
         const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
-        uint32_t so_row = 0;  // the key's old successor (old_lists)
         if (i < q) {
             const u128 key = ld128(keys + i);
             uint32_t sn = 0, so = 0, has = 0, m = 0;
+            uint4 A = {0, 0, 0, 0}, B = {0, 0, 0, 0};
+            if (use_cd) cd_fetch(cd, key, A, B);
             const bool settled =
-                use_cd && cd_lookup(cd, key, n_old, n_new, no, nn, so, sn, has, m);
+                use_cd && cd_lookup(cd, key, A, B, n_old, n_new, no, nn, so, sn, has, m);
             if (!settled) {
                 // Both searches are issued together: deriving the new successor
                 // from a verified old->new mapping saves a search for ~98 % of
@@ -4323,14 +4365,10 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                     else if (j < nslots) m |= 1u << j;
                 }
             }
-            so_row = so;
-            uint32_t *l = stage_l + threadIdx.x * nlist;
-            for (int j = 0; j < nlist; ++j) {
-                uint32_t v = sn + (uint32_t)j;
-                if (v >= n_new) v -= n_new;
-                l[j] = j < nn ? v : CX_NONE;
-            }
+            s_sn[threadIdx.x] = sn;
+            s_so[threadIdx.x] = so;
             count[i] = (uint8_t)nn;
+            if (CHURN && old_lists) old_count[i] = (uint8_t)no;
             // pass 2: misplaced holders in rank order take the first lacking rank
             uint8_t *tg = stage_t + threadIdx.x * nslots;
 #pragma unroll
@@ -4350,23 +4388,12 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
             mask[i] = (uint16_t)m;
         }
         __syncthreads();
-        flush_rows(stage_l, new_lists, base, cnt, nlist);
+        // new lists (sn + j mod n_new, j < nn) and old lists (so + j mod
+        // n_old, j < no <= n_old: one wrap at most) straight from the successors
+        flush_window(s_sn, new_lists, base, cnt, nlist, nn, n_new);
+        if (CHURN && old_lists) flush_window(s_so, old_lists, base, cnt, nlist, no, n_old);
         flush_rows(stage_t, target, base, cnt, nslots);
         __syncthreads();
-        if (CHURN && old_lists) {  // grid-uniform
-            if (i < q) {
-                uint32_t *l = stage_l + threadIdx.x * nlist;
-                for (int j = 0; j < nlist; ++j) {
-                    uint32_t v = so_row + (uint32_t)j;  // j < no <= n_old: one wrap at most
-                    if (v >= n_old) v -= n_old;
-                    l[j] = j < no ? v : CX_NONE;
-                }
-                old_count[i] = (uint8_t)no;
-            }
-            __syncthreads();
-            flush_rows(stage_l, old_lists, base, cnt, nlist);
-            __syncthreads();
-        }
     }
 }
 

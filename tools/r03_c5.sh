@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -v \
-  -k "misplaced or c5" --timeout 400 --timeout-method thread > "$OUT/pytest.log" 2>&1
+  -k "misplaced or c5 or nsucc or dhash" --timeout 400 --timeout-method thread > "$OUT/pytest.log" 2>&1
 tail -1 "$OUT/pytest.log"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/c5" -o run --output-format csv \
