@@ -2604,10 +2604,13 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
                                                         const uint64_t *rh, uint32_t n,
                                                         int lvl_base, int nlev, uint32_t p_first,
                                                         uint32_t M, int gs, uint4 *cz,
-                                                        uint32_t *esc, uint32_t K, int mode) {
+                                                        uint32_t *esc, uint32_t K, int mode,
+                                                        int a1_rows) {
     __shared__ uint32_t win[256 * CZR_W];
     __shared__ uint32_t e0s[256];
     __shared__ uint32_t roots[256];
+    __shared__ uint32_t roots_a1[256];  // A' = f(R, i - 1) = C2(p, i) of the root's first row
+    __shared__ uint64_t roots_h[256];   // rh[R]
     __shared__ uint16_t ridx[256];
     __shared__ uint32_t wcnt[4];
     uint32_t lvl, lb;
@@ -2640,7 +2643,8 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
     };
     // ---- rows: root and the row's own word ----
     const bool valid = (uint32_t)t < rows;
-    uint32_t A = 0xFFFFFFFFu;
+    uint32_t A = 0xFFFFFFFFu, A1 = 0;
+    uint64_t hA = 0;
     uint32_t bad = 0;
     if (!do_compute) {
         if (valid) ridx[t] = 0;
@@ -2651,7 +2655,11 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
             if (pw >= n) pw -= n;
             const uint32_t p = (uint32_t)pw;
             A = chk(fat(p, i));
-            const uint32_t e0 = cz_encode_hi(n, gs, p, rh[p], i, A, rh[A], ring);
+            // A' of the b = 1 entry from the row's two-hop plane: one gather beside
+            // A instead of one after it (a1_rows = 0: from A, for A/B)
+            if (a1_rows) A1 = chk(c2(p, i));
+            hA = rh[A];
+            const uint32_t e0 = cz_encode_hi(n, gs, p, rh[p], i, A, hA, ring);
             e0s[t] = e0;
             bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
         }
@@ -2670,12 +2678,17 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
         const uint32_t incl = rank + (first ? 1u : 0u);  // distinct roots up to and including t
         __syncthreads();  // every lane has read roots[t - 1]
-        if (first) roots[rank] = A;
+        if (first) {
+        roots[rank] = A;
+        roots_a1[rank] = A1;
+        roots_h[rank] = hA;
+    }
         if (valid) ridx[t] = (uint16_t)(incl - 1);
         __syncthreads();
         // ---- windows of the distinct roots (lanes 0 .. nr-1) ----
         if ((uint32_t)t < nr) {
             const uint32_t R = roots[t];
+            const uint64_t hR = roots_h[t];
             uint32_t *wr = win + t * CZR_W;
             uint32_t wbad = 0;
             // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
@@ -2698,8 +2711,9 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
                 nd[14] = chk(c2(nd[2], i - 4));
                 nd[15] = chk(c2(nd[3], i - 4));
                 uint64_t hv[16];
+                hv[0] = hR;
 #pragma unroll
-                for (int v = 0; v < 16; ++v) hv[v] = rh[nd[v]];
+                for (int v = 1; v < 16; ++v) hv[v] = rh[nd[v]];
 #pragma unroll
                 for (int v = 1; v < 16; ++v) {
                     const int hb = 31 - __builtin_clz((unsigned)v);
@@ -2712,7 +2726,7 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
             // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
             {
                 uint32_t nd[15];
-                nd[0] = chk(fat(R, i - 1));
+                nd[0] = a1_rows ? roots_a1[t] : chk(fat(R, i - 1));
                 nd[1] = chk(fat(nd[0], i - 2));
                 nd[2] = chk(fat(nd[0], i - 3));
                 nd[3] = chk(c2(nd[0], i - 2));
@@ -2730,7 +2744,7 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
                 uint64_t hv[15];
 #pragma unroll
                 for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
-                const uint32_t o0 = cz_encode_hi(n, gs, R, rh[R], i - 1, nd[0], hv[0], ring);
+                const uint32_t o0 = cz_encode_hi(n, gs, R, hR, i - 1, nd[0], hv[0], ring);
                 wbad += o0 == CZ_NONE;
                 wr[15] = o0;
 #pragma unroll
@@ -2826,12 +2840,17 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             const char *e = getenv("CX_CZ_ROOTS_MODE");
             return e ? (atoi(e) & 3) : 0;
         }();
+        static const int a1_rows = [] {
+            const char *e = getenv("CX_CZ_ROOTS_A1");
+            return e ? (atoi(e) != 0) : 1;
+        }();
         const uint32_t Kr = K ? K : 16;
         const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
         k_cz_build_roots<<<(unsigned)blocks, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                          p_first, M, gs, out, esc, Kr, mode);
+                                                          p_first, M, gs, out, esc, Kr, mode,
+                                                          a1_rows);
         return hipGetLastError();
     }
     if (planes && fv.C2 && pair >= 1 && pair <= 3) {
