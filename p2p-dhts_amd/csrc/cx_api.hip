@@ -55,7 +55,9 @@ struct PoolEnt {
 std::mutex g_pool_mu;
 std::vector<PoolEnt> g_pool;
 size_t g_pool_bytes = 0;
-constexpr size_t POOL_MIN = (size_t)16 << 20;
+// blocks from 64 KiB up: a churn's temporaries (2^17 joins: 0.5-3 MiB each)
+// recur every epoch too, and each hipFree costs 0.1-0.3 ms
+constexpr size_t POOL_MIN = (size_t)64 << 10;
 // pool cap: CX_POOL_CAP_GIB (default 96; 0 disables pooling)
 size_t pool_cap() {
     static const size_t cap = [] {
@@ -260,6 +262,11 @@ struct cx_ring {
     cell128 *d_eyt = nullptr;      // Eytzinger copy [n+1]
     uint32_t *d_fingers = nullptr; // [n][128]
     bool fingers_converged = false;
+    // converged, but the row-major table d_fingers is not written yet: the
+    // default route (cz walk) needs only the level planes the finger build
+    // hands to the route-table build, so cx_fingers_build without fingers_out
+    // defers the 8 GiB of rows (2^24) to their first reader (ensure_fingers_rows)
+    bool rows_deferred = false;
     RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
@@ -407,23 +414,48 @@ int sync_if_host(int memkind, hipStream_t s) {
     return CX_OK;
 }
 
+// A ring handle's own stream and 1-KiB scratch word block are kept for the
+// next handle on the device when a ring is destroyed (a membership epoch
+// creates one ring and destroys one: hipStreamCreate + hipMalloc cost ~1 ms,
+// hipStreamDestroy another).  Returned idle (the ring synchronised it).
+struct RingRes {
+    int device;
+    hipStream_t stream;
+    void *scratch;
+};
+std::mutex g_res_mu;
+std::vector<RingRes> g_res;
+constexpr size_t RES_KEEP = 16;  // per process
+
 int alloc_ring(int device, cx_ring **out) {
     cx_ring *r = new cx_ring();
     r->device = device;
-    hipError_t e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-        delete r;
-        return fail(CX_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    {
+        std::lock_guard<std::mutex> g(g_res_mu);
+        for (size_t k = g_res.size(); k-- > 0;)
+            if (g_res[k].device == device) {
+                r->own_stream = g_res[k].stream;
+                r->d_scratch = static_cast<uint32_t *>(g_res[k].scratch);
+                g_res.erase(g_res.begin() + k);
+                break;
+            }
+    }
+    if (!r->own_stream) {
+        hipError_t e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete r;
+            return fail(CX_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        }
+        e = dev_malloc(&r->d_scratch, 1024);
+        if (e != hipSuccess) {
+            (void)hipStreamDestroy(r->own_stream);
+            delete r;
+            return fail(CX_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
     }
     r->stream = r->own_stream;
     static std::atomic<uint64_t> next_serial{1};
     r->serial = next_serial++;
-    e = dev_malloc(&r->d_scratch, 1024);
-    if (e != hipSuccess) {
-        (void)hipStreamDestroy(r->own_stream);
-        delete r;
-        return fail(CX_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
-    }
     *out = r;
     return CX_OK;
 }
@@ -451,13 +483,25 @@ void free_ring(cx_ring *r) {
     (void)hipFree(r->d_preds);
     (void)hipFree(r->d_alive);
     (void)hipFree(r->d_succs);
-    (void)hipFree(r->d_scratch);
     table_free(r->device, r->d_arc_tree, r->arc_bytes);
     (void)hipFree(r->d_arc_bounds);
     (void)hipFree(r->d_stats);
     table_free(r->device, r->d_o2n_canon, r->o2n_canon_n * sizeof(uint32_t));
     table_free(r->device, r->d_cdir, r->cdir_bytes);
-    if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
+    if (r->own_stream) {
+        // the own stream was synchronised above (r->stream may be a user stream:
+        // then the own stream has seen no work since its last synchronisation)
+        (void)hipStreamSynchronize(r->own_stream);
+        std::lock_guard<std::mutex> g(g_res_mu);
+        if (r->d_scratch && g_res.size() < RES_KEEP) {
+            g_res.push_back(RingRes{r->device, r->own_stream, r->d_scratch});
+        } else {
+            (void)hipStreamDestroy(r->own_stream);
+            (void)hipFree(r->d_scratch);
+        }
+    } else {
+        (void)hipFree(r->d_scratch);
+    }
     delete r;
 }
 
@@ -562,8 +606,11 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
 
 // Builds (once per finger build) the table the selected route variant reads.
 // Without HBM for it the route falls back to variant 0 (finger + ring gathers).
+int ensure_fingers_rows(cx_ring *ring, hipStream_t s);
+
 int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     if (!r->fingers_converged || !r->d_ring_ext) return CX_OK;
+
     const size_t ent = r->n * (size_t)r->rt_R;
     if (r->variant() == 5 && !r->cz_valid) {
         if (!r->d_cz && table_alloc((void **)&r->d_cz, ent * 128) != hipSuccess) {
@@ -574,6 +621,9 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
             DBuf ft, hi, c2;
             cxk::FingerView fv;
+            if (!ft_pre || r->table_build == 1) {  // the planes come from the rows
+                if (int rc = ensure_fingers_rows(r, s)) return rc;
+            }
             CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre));
             CX_HIP(cxk::cz_build(fv, r->d_ring, hi.as<uint64_t>(), r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_cz,
                                  r->d_scratch, s));
@@ -589,12 +639,14 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
         if (!r->d_rt && table_alloc((void **)&r->d_rt, ent * sizeof(RtEntry)) != hipSuccess)
             r->d_rt = nullptr;
         if (r->d_rt) {
+            if (int rc = ensure_fingers_rows(r, s)) return rc;
             CX_HIP(cxk::rt_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->d_rt, r->d_ring_ext, s));
             r->rt_valid = true;
         }
     } else if ((r->variant() == 2 || r->variant() == 3) && !r->pk_valid) {
         if (!r->d_pk && table_alloc((void **)&r->d_pk, ent * 16) != hipSuccess) r->d_pk = nullptr;
         if (r->d_pk) {
+            if (int rc = ensure_fingers_rows(r, s)) return rc;
             CX_HIP(cxk::pk_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_pk, s));
             r->pk_valid = true;
         }
@@ -602,6 +654,7 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
         if (!r->d_tree && table_alloc((void **)&r->d_tree, ent * 64) != hipSuccess)
             r->d_tree = nullptr;
         if (r->d_tree) {
+            if (int rc = ensure_fingers_rows(r, s)) return rc;
             CX_HIP(cxk::tree_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_tree, s));
             r->tree_valid = true;
         }
@@ -616,40 +669,62 @@ int churn_merge(const cx_ring *old_ring, const cell128 *J0, size_t nj, const cel
     const size_t n_old = old_ring->n;
     SearchView v = old_ring->sv();
     v.dir = old_ring->d_dir;
+    // every temporary recurs at the same size each membership epoch: through
+    // the pool (plain hipMalloc / hipFree cost ~0.7 ms per churn at 2^24)
     DBuf G, A, ws, jk0, jk1, jt0, jt1, pos, keep, ringbuf;
-    const size_t sw = cxk::scan_workspace_words(n_old + 2 > nj + 1 ? n_old + 2 : nj + 1);
-    const size_t rw = nj ? cxk::sort_workspace_words(nj) : 0;
-    CX_HIP(ws.alloc((sw > rw ? sw : rw) * sizeof(uint32_t)));
-    CX_HIP(G.alloc_pooled((n_old + 1) * sizeof(uint32_t), s));
-    CX_HIP(A.alloc_pooled((n_old + 2) * sizeof(uint32_t), s));
-    CX_HIP(hipMemsetAsync(G.p, 0, (n_old + 1) * sizeof(uint32_t), s));
-    CX_HIP(hipMemsetAsync(A.p, 0, (n_old + 2) * sizeof(uint32_t), s));
-    CX_HIP(cxk::merge_mark(v, old_ring->d_ring, L, nl, G.as<uint32_t>(), s));
+    // joins: bucket sort (CX_JOIN_SORT=radix for the radix sort, A/B), and the
+    // radix sort when a bucket overflowed (clustered joins)
+    static const bool radix_only = [] {
+        const char *e = getenv("CX_JOIN_SORT");
+        return e && strcmp(e, "radix") == 0;
+    }();
+    uint32_t *d_ovf = static_cast<uint32_t *>(r->d_scratch) + 64;
+    uint32_t gone = 0, kept = 0, ovf = 0;
     const cell128 *J = J0;
-    if (nj) {
-        CX_HIP(jk0.alloc(nj * sizeof(cell128)));
-        CX_HIP(jk1.alloc(nj * sizeof(cell128)));
-        CX_HIP(jt0.alloc(nj * sizeof(uint32_t)));
-        CX_HIP(jt1.alloc(nj * sizeof(uint32_t)));
-        CX_HIP(cxk::copy_tagged(J0, nj, 0, jk0.as<cell128>(), jt0.as<uint32_t>(), s));
-        CX_HIP(cxk::radix_sort(jk0.as<cell128>(), jt0.as<uint32_t>(), jk1.as<cell128>(),
-                               jt1.as<uint32_t>(), nj, ws.as<uint32_t>(), s));
-        J = jk0.as<cell128>();
-        CX_HIP(pos.alloc(nj * sizeof(uint32_t)));
-        CX_HIP(keep.alloc((nj + 1) * sizeof(uint32_t)));
-        CX_HIP(hipMemsetAsync(keep.p, 0, (nj + 1) * sizeof(uint32_t), s));
-        CX_HIP(cxk::merge_join_pos(v, old_ring->d_ring, n_old, G.as<uint32_t>(), J, nj,
-                                   pos.as<uint32_t>(), keep.as<uint32_t>(), A.as<uint32_t>(), s));
-        CX_HIP(cxk::exclusive_scan(keep.as<uint32_t>(), nj + 1, ws.as<uint32_t>(), s));
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const bool radix = radix_only || attempt == 1;
+        size_t sw = cxk::scan_workspace_words(n_old + 2 > nj + 1 ? n_old + 2 : nj + 1);
+        const size_t rw = nj ? (radix ? cxk::sort_workspace_words(nj)
+                                      : cxk::bucket_sort_workspace_words(nj)) : 0;
+        if (rw > sw) sw = rw;
+        CX_HIP(ws.alloc_pooled(sw * sizeof(uint32_t), s));
+        CX_HIP(G.alloc_pooled((n_old + 1) * sizeof(uint32_t), s));
+        CX_HIP(A.alloc_pooled((n_old + 2) * sizeof(uint32_t), s));
+        CX_HIP(hipMemsetAsync(G.p, 0, (n_old + 1) * sizeof(uint32_t), s));
+        CX_HIP(hipMemsetAsync(A.p, 0, (n_old + 2) * sizeof(uint32_t), s));
+        CX_HIP(hipMemsetAsync(d_ovf, 0, sizeof(uint32_t), s));
+        CX_HIP(cxk::merge_mark(v, old_ring->d_ring, L, nl, G.as<uint32_t>(), s));
+        if (nj) {
+            CX_HIP(jk0.alloc_pooled(nj * sizeof(cell128), s));
+            if (radix) {
+                CX_HIP(jk1.alloc_pooled(nj * sizeof(cell128), s));
+                CX_HIP(jt0.alloc_pooled(nj * sizeof(uint32_t), s));
+                CX_HIP(jt1.alloc_pooled(nj * sizeof(uint32_t), s));
+                CX_HIP(cxk::copy_tagged(J0, nj, 0, jk0.as<cell128>(), jt0.as<uint32_t>(), s));
+                CX_HIP(cxk::radix_sort(jk0.as<cell128>(), jt0.as<uint32_t>(), jk1.as<cell128>(),
+                                       jt1.as<uint32_t>(), nj, ws.as<uint32_t>(), s));
+            } else {
+                CX_HIP(cxk::bucket_sort(J0, nj, jk0.as<cell128>(), ws.as<uint32_t>(), d_ovf, s));
+            }
+            J = jk0.as<cell128>();
+            CX_HIP(pos.alloc_pooled(nj * sizeof(uint32_t), s));
+            CX_HIP(keep.alloc_pooled((nj + 1) * sizeof(uint32_t), s));
+            CX_HIP(hipMemsetAsync(keep.p, 0, (nj + 1) * sizeof(uint32_t), s));
+            CX_HIP(cxk::merge_join_pos(v, old_ring->d_ring, n_old, G.as<uint32_t>(), J, nj,
+                                       pos.as<uint32_t>(), keep.as<uint32_t>(), A.as<uint32_t>(),
+                                       s));
+            CX_HIP(cxk::exclusive_scan(keep.as<uint32_t>(), nj + 1, ws.as<uint32_t>(), s));
+        }
+        CX_HIP(cxk::exclusive_scan(G.as<uint32_t>(), n_old + 1, ws.as<uint32_t>(), s));
+        CX_HIP(cxk::exclusive_scan(A.as<uint32_t>(), n_old + 2, ws.as<uint32_t>(), s));
+        CX_HIP(hipMemcpyAsync(&gone, G.as<uint32_t>() + n_old, sizeof(gone),
+                              hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(&kept, A.as<uint32_t>() + n_old + 1, sizeof(kept),
+                              hipMemcpyDeviceToHost, s));
+        CX_HIP(hipMemcpyAsync(&ovf, d_ovf, sizeof(ovf), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        if (!ovf) break;  // else: clustered joins, sort again with the radix sort
     }
-    CX_HIP(cxk::exclusive_scan(G.as<uint32_t>(), n_old + 1, ws.as<uint32_t>(), s));
-    CX_HIP(cxk::exclusive_scan(A.as<uint32_t>(), n_old + 2, ws.as<uint32_t>(), s));
-    uint32_t gone = 0, kept = 0;
-    CX_HIP(hipMemcpyAsync(&gone, G.as<uint32_t>() + n_old, sizeof(gone), hipMemcpyDeviceToHost,
-                          s));
-    CX_HIP(hipMemcpyAsync(&kept, A.as<uint32_t>() + n_old + 1, sizeof(kept),
-                          hipMemcpyDeviceToHost, s));
-    CX_HIP(hipStreamSynchronize(s));
     const size_t m = n_old - gone + kept;
     CX_CHECK(m >= 1, CX_E_INVALID, "churn would leave an empty ring");
     CX_HIP(ringbuf.alloc_pooled(m * sizeof(cell128), s));
@@ -839,7 +914,7 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
 namespace {
 // The converged n x 128 finger table into ring->d_fingers (allocated).
 int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, int ft_l = 0,
-                        bool *ft_done = nullptr) {
+                        bool *ft_done = nullptr, bool rows = true) {
     // streaming per-block window build (needs the directory and the ID
     // slices); CX_FINGERS_SEARCH=1 keeps one search per entry (A/B)
     static const bool search_only = getenv("CX_FINGERS_SEARCH") != nullptr;
@@ -855,10 +930,42 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
     DBuf fws;
     const bool streaming = !search_only && ring->d_ring_key &&
                            fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n), s) == hipSuccess;
+    // planes only (rows deferred) needs the streaming build with every plane a tile level
+    if (!streaming || !ft || ft_l < cxk::FINGERS_TILE_L0 || ring->n < ((size_t)1 << 18)) rows = true;
+    if (rows && !ring->d_fingers &&
+        table_alloc((void **)&ring->d_fingers, ring->n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
+        ring->d_fingers = nullptr;
+        return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
+    }
     CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
-                              streaming ? fws.p : nullptr, ring->d_fingers, s, ft, ft_l, ft_done));
+                              streaming ? fws.p : nullptr, rows ? ring->d_fingers : nullptr, s, ft,
+                              ft_l, ft_done));
     ring->fingers_converged = true;
+    ring->rows_deferred = !rows;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
+    return CX_OK;
+}
+}  // namespace
+
+namespace {
+// Writes the deferred row-major finger table (same kernels, rows instead of
+// planes) before anything that reads d_fingers.
+int ensure_fingers_rows(cx_ring *ring, hipStream_t s) {
+    if (!ring->rows_deferred) return CX_OK;
+    if (!ring->d_fingers &&
+        table_alloc((void **)&ring->d_fingers, ring->n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
+        ring->d_fingers = nullptr;
+        return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
+    }
+    SearchView fv = ring->sv();
+    fv.dir = ring->d_dir;
+    DBuf fws;
+    const bool streaming = ring->d_ring_key &&
+                           fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n), s) == hipSuccess;
+    CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
+                              streaming ? fws.p : nullptr, ring->d_fingers, s, nullptr, 0,
+                              nullptr));
+    ring->rows_deferred = false;
     return CX_OK;
 }
 }  // namespace
@@ -894,25 +1001,27 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     if (rc) return rc;
     hipStream_t s = ring->stream;
     const size_t cnt = ring->n * CX_FINGERS;
-    if (!ring->d_fingers) {
-        hipError_t e = table_alloc((void **)&ring->d_fingers, cnt * sizeof(uint32_t));
-        if (e != hipSuccess) {
-            ring->d_fingers = nullptr;
-            return fail(CX_E_NOMEM, "hipMalloc of the finger table failed");
-        }
-    }
     route_geometry(ring);
+    // rows deferred (planes only) when nobody asked for them and the default
+    // route reads planes from the streaming build; CX_FINGERS_ROWS=1 writes
+    // them now (A/B)
+    static const bool eager_rows = getenv("CX_FINGERS_ROWS") != nullptr;
+    const int ft_l = ring->rt_l0 - 5;
+    const bool defer = !eager_rows && !fingers_out && ring->variant() == 5 &&
+                       (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
+                       ring->n >= ((size_t)1 << 18) && ft_l >= cxk::FINGERS_TILE_L0;
     // the default route table reads the fingers as level planes: the streaming
     // finger build writes them alongside the rows (no transpose pass)
     DBuf ft_pre;
     bool ft_done = false;
-    const int ft_l = ring->rt_l0 - 5;
     if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
         ft_pre.alloc_pooled((size_t)(CX_FINGERS - ft_l) * ring->n * sizeof(uint32_t), s) != hipSuccess) {
         (void)hipGetLastError();
         ft_pre.p = nullptr;
     }
-    if ((rc = build_fingers_table(ring, s, ft_pre.as<uint32_t>(), ft_l, &ft_done))) return rc;
+    if ((rc = build_fingers_table(ring, s, ft_pre.as<uint32_t>(), ft_l, &ft_done,
+                                  !defer || !ft_pre.p)))
+        return rc;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         table_alloc((void **)&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
@@ -955,12 +1064,19 @@ int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
     ring->d_fingers = staged.as<uint32_t>();
     staged.release();
     ring->fingers_converged = false;
+    ring->rows_deferred = false;
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
     return CX_OK;
 }
 
 int cx_fingers_device(const cx_ring *ring, const uint32_t **fingers) {
     CX_CHECK(ring && fingers, CX_E_INVALID, "null argument");
+    if (ring->rows_deferred) {  // materialised now, complete when this returns
+        int rc = use_device(ring);
+        if (rc) return rc;
+        if ((rc = ensure_fingers_rows(const_cast<cx_ring *>(ring), ring->stream))) return rc;
+        CX_HIP(hipStreamSynchronize(ring->stream));
+    }
     *fingers = ring->d_fingers;
     return CX_OK;
 }
@@ -1059,7 +1175,7 @@ int cx_liveness_upload(cx_ring *ring, const uint8_t *alive, const uint32_t *succ
 int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
              uint32_t *owner, uint8_t *hops, uint8_t *status, int memkind) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(ring->d_fingers != nullptr, CX_E_STATE,
+    CX_CHECK(ring->d_fingers != nullptr || ring->rows_deferred, CX_E_STATE,
              "finger table not built (cx_fingers_build / cx_fingers_upload)");
     int rc = use_device(ring);
     if (rc) return rc;
@@ -1079,9 +1195,16 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
         if (e2) return e2;
     }
     const int v = ring->literal() ? -1 : ring->variant();
+    if (v != 5 || !ring->cz_valid) {
+        // every other walk reads the row-major finger table
+        int e2 = ensure_fingers_rows(const_cast<cx_ring *>(ring), s);
+        if (e2) return e2;
+    }
+    SearchView dsv = ring->sv();
+    dsv.dir = ring->d_dir;
     if (v == 5 && ring->cz_valid)
         CX_HIP(cxk::route_cz(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
-                             ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
+                             ring->rt_R, ring->pk_ib, ring->d_fingers, dsv, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst,
                              ring->counting ? ring->d_stats : nullptr, s));
     else if (v == 4 && ring->tree_valid)
@@ -1680,6 +1803,7 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
              "arc routing walks the converged ring; peer-state / liveness uploads need cx_route");
     CX_CHECK(!ring->d_fingers || ring->fingers_converged, CX_E_STATE,
              "arc routing walks the converged ring; uploaded fingers need cx_route");
+    if ((rc = ensure_fingers_rows(ring, s))) return rc;  // deferred rows: written now
     const bool own_fingers = !ring->d_fingers;
     if (own_fingers) {
         if (!ring->d_fingers &&

@@ -220,6 +220,81 @@ hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size
     return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// Bucket sort of a small batch of uniformly distributed keys (a churn's joins:
+// 2^17 keys at 1 % of 2^24 peers).  The radix sort's 16 passes x 4 launches
+// cost ~1 ms of launch-bound time there; this takes 2^kb buckets by the top kb
+// bits (about one key per bucket), counts, scans, scatters, and sorts each
+// bucket in place (one lane per bucket, insertion sort).  A bucket above
+// BS_MAX keys (clustered input) sets *overflow and is left unsorted: the
+// caller then sorts with radix_sort.  Not stable (equal keys are equal values).
+// ---------------------------------------------------------------------------
+constexpr uint32_t BS_MAX = 32;
+
+__global__ void k_bs_count(const cell128 *keys, size_t n, int kb, uint32_t *cnt) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        atomicAdd(cnt + (kb ? keys[i].hi >> (64 - kb) : 0), 1u);
+}
+
+// cnt holds the buckets' exclusive offsets; afterwards cnt[b] = end of bucket b
+__global__ void k_bs_scatter(const cell128 *keys, size_t n, int kb, uint32_t *cnt, cell128 *out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const cell128 k = keys[i];
+        const uint32_t pos = atomicAdd(cnt + (kb ? k.hi >> (64 - kb) : 0), 1u);
+        out[pos] = k;
+    }
+}
+
+__global__ void k_bs_sort(cell128 *v, const uint32_t *end, uint32_t nb, uint32_t *overflow) {
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x) {
+        const uint32_t lo = b ? end[b - 1] : 0u, hi = end[b];
+        if (hi - lo > BS_MAX) {
+            atomicOr(overflow, 1u);
+            continue;
+        }
+        for (uint32_t x = lo + 1; x < hi; ++x) {
+            const cell128 k = v[x];
+            const u128 kk = ((u128)k.hi << 64) | k.lo;
+            uint32_t y = x;
+            while (y > lo) {
+                const cell128 w = v[y - 1];
+                if ((((u128)w.hi << 64) | w.lo) <= kk) break;
+                v[y] = w;
+                --y;
+            }
+            v[y] = k;
+        }
+    }
+}
+
+size_t bucket_sort_workspace_words(size_t n) {
+    int kb = 0;
+    while (((size_t)1 << kb) < n) ++kb;
+    const size_t nb = (size_t)1 << kb;
+    return nb + 1 + scan_workspace_words(nb + 1);
+}
+
+// keys (n) -> out (n) in ascending order unless *overflow (device word, zeroed
+// here) comes back nonzero.
+hipError_t bucket_sort(const cell128 *keys, size_t n, cell128 *out, uint32_t *ws,
+                       uint32_t *overflow, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    int kb = 0;
+    while (((size_t)1 << kb) < n) ++kb;
+    if (kb > 30) return hipErrorInvalidValue;
+    const size_t nb = (size_t)1 << kb;
+    uint32_t *cnt = ws, *scan_ws = ws + nb + 1;
+    if ((e = hipMemsetAsync(cnt, 0, (nb + 1) * sizeof(uint32_t), s)) != hipSuccess) return e;
+    k_bs_count<<<cx_grid(n, 256), 256, 0, s>>>(keys, n, kb, cnt);
+    if ((e = exclusive_scan(cnt, nb + 1, scan_ws, s)) != hipSuccess) return e;
+    k_bs_scatter<<<cx_grid(n, 256), 256, 0, s>>>(keys, n, kb, cnt, out);
+    k_bs_sort<<<cx_grid(nb, 256), 256, 0, s>>>(out, cnt, (uint32_t)nb, overflow);
+    return hipGetLastError();
+}
+
 // ===========================================================================
 // Dedupe / compaction (equal IDs rejected, remote_peer_list.cpp:56-58).
 // ===========================================================================
@@ -720,6 +795,7 @@ constexpr int FT_W = 192;   // window elements per level (block span + ~4 sigma)
 constexpr int FT_CH = 8;    // levels whose windows are in LDS at once
 constexpr int FT_COLS = 40; // tile columns: levels FT_L0..127
 constexpr int FT_L0 = CX_FINGERS - FT_COLS;
+static_assert(FT_L0 == FINGERS_TILE_L0, "header constant");
 static_assert(FT_L0 >= 64, "tile levels need 2^i >= 2^64 (window keys from the top halves)");
 constexpr int FT_ROW = FT_COLS + 1;  // padded row: conflict-free column writes
 
@@ -884,9 +960,10 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
         __builtin_amdgcn_wave_barrier();  // searches done before the next chunk's keys
     }
     __syncthreads();
-    // write-back: 8 rows per pass, 16 B per thread, full 512-B rows
+    // write-back: 8 rows per pass, 16 B per thread, full 512-B rows (F null:
+    // planes only -- the row-major table is materialised later, on demand)
     const int chunk = threadIdx.x & 31;
-    for (int r = threadIdx.x >> 5; r < (int)rows; r += 8) {
+    for (int r = threadIdx.x >> 5; F && r < (int)rows; r += 8) {
         const uint32_t p = a + r;
         const uint32_t nx = p + 1 == n ? 0u : p + 1;
         const int g = glog[r];
@@ -960,7 +1037,10 @@ hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32
                          bool *planes_done) {
     const size_t n = sv.ev.n;
     if (planes_done) *planes_done = false;
-    if (ring_key && ws && sv.dir && n >= ((size_t)1 << 18)) {
+    const bool stream_ok = ring_key && ws && sv.dir && n >= ((size_t)1 << 18);
+    // F null = planes only: needs the streaming build and every plane a tile level
+    if (!F && (!stream_ok || !FT || Lft < FT_L0 || Lft >= CX_FINGERS)) return hipErrorInvalidValue;
+    if (stream_ok) {
         const uint32_t nblk = (uint32_t)((n + FT_P - 1) / FT_P);
         uint32_t *S0 = static_cast<uint32_t *>(ws);
         uint8_t *glog = reinterpret_cast<uint8_t *>(S0 + (size_t)nblk * FT_COLS);
@@ -2600,13 +2680,20 @@ __global__ __launch_bounds__(256) void k_cz_build_pair(FingerView fv, const cell
 // k_cz_build (route_table_hash, tests/test_gpu_parity.py); dispatch order
 // is k_cz_build's K-row-block chunks over all levels.
 constexpr int CZR_W = 31;  // LDS words per root: W0[1..15], W1[0..14], CZ_NONE count
-__global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cell128 *ring,
-                                                        const uint64_t *rh, uint32_t n,
-                                                        int lvl_base, int nlev, uint32_t p_first,
-                                                        uint32_t M, int gs, uint4 *cz,
-                                                        uint32_t *esc, uint32_t K, int mode,
-                                                        int a1_rows) {
-    __shared__ uint32_t win[256 * CZR_W];
+// SPLIT: the two planes leave one after the other through one 16-word window
+// buffer (W0 first, W1 held in registers meanwhile): 21 instead of 37 KB of
+// LDS per block, so more blocks fit per CU when the VGPR budget (WPE waves
+// per SIMD) allows them.  The build is bound by the rows in flight per CU:
+// 4 -> 3 -> 2 resident blocks take 27.4 -> 31.0 -> 41.4 ms at 2^24
+// (profiles/r03/build_lat/).
+template <int SPLIT, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, uint32_t n,
+                      int lvl_base, int nlev, uint32_t p_first, uint32_t M, int gs, uint4 *cz,
+                      uint32_t *esc, uint32_t K, int mode, int a1_rows, int late_e0) {
+    constexpr int WS = SPLIT ? 16 : CZR_W;  // LDS words per root
+    constexpr int WC = SPLIT ? 15 : 30;     // the root's CZ_NONE count
+    __shared__ uint32_t win[256 * WS];
     __shared__ uint32_t e0s[256];
     __shared__ uint32_t roots[256];
     __shared__ uint32_t roots_a1[256];  // A' = f(R, i - 1) = C2(p, i) of the root's first row
@@ -2643,9 +2730,10 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
     };
     // ---- rows: root and the row's own word ----
     const bool valid = (uint32_t)t < rows;
-    uint32_t A = 0xFFFFFFFFu, A1 = 0;
-    uint64_t hA = 0;
-    uint32_t bad = 0;
+    uint32_t A = 0xFFFFFFFFu, A1 = 0, p = 0;
+    uint64_t hA = 0, hp = 0;
+    uint32_t bad = 0, nroots = 0;
+    uint32_t o1[SPLIT ? 15 : 1];  // SPLIT: the W1 words until plane 0 has left
     if (!do_compute) {
         if (valid) ridx[t] = 0;
         __syncthreads();
@@ -2653,15 +2741,21 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
         if (valid) {
             uint64_t pw = (uint64_t)p_first + j0 + t;
             if (pw >= n) pw -= n;
-            const uint32_t p = (uint32_t)pw;
+            p = (uint32_t)pw;
             A = chk(fat(p, i));
             // A' of the b = 1 entry from the row's two-hop plane: one gather beside
             // A instead of one after it (a1_rows = 0: from A, for A/B)
             if (a1_rows) A1 = chk(c2(p, i));
-            hA = rh[A];
-            const uint32_t e0 = cz_encode_hi(n, gs, p, rh[p], i, A, hA, ring);
-            e0s[t] = e0;
-            bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
+            hp = rh[p];
+            if (!late_e0) {
+                // late_e0: rh[A] is gathered once per distinct root in the window
+                // phase, beside its first window gathers, and the row's own word is
+                // encoded after it (one dependent gather less per block)
+                hA = rh[A];
+                const uint32_t e0 = cz_encode_hi(n, gs, p, hp, i, A, hA, ring);
+                e0s[t] = e0;
+                bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
+            }
         }
         roots[t] = A;  // staged for the neighbour compare
         __syncthreads();
@@ -2686,10 +2780,12 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
         if (valid) ridx[t] = (uint16_t)(incl - 1);
         __syncthreads();
         // ---- windows of the distinct roots (lanes 0 .. nr-1) ----
+        nroots = nr;
         if ((uint32_t)t < nr) {
             const uint32_t R = roots[t];
-            const uint64_t hR = roots_h[t];
-            uint32_t *wr = win + t * CZR_W;
+            const uint64_t hR = late_e0 ? rh[R] : roots_h[t];
+            if (late_e0) roots_h[t] = hR;
+            uint32_t *wr = win + t * WS;
             uint32_t wbad = 0;
             // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
             {
@@ -2746,28 +2842,44 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
                 for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
                 const uint32_t o0 = cz_encode_hi(n, gs, R, hR, i - 1, nd[0], hv[0], ring);
                 wbad += o0 == CZ_NONE;
-                wr[15] = o0;
+                if (SPLIT)
+                    o1[0] = o0;
+                else
+                    wr[15] = o0;
 #pragma unroll
                 for (int v = 1; v < 15; ++v) {
                     const int hb = 31 - __builtin_clz((unsigned)v);
                     const int pv = v & ~(1 << hb);
                     const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
                     wbad += o == CZ_NONE;
-                    wr[15 + v] = o;
+                    if (SPLIT)
+                        o1[v] = o;
+                    else
+                        wr[15 + v] = o;
                 }
             }
-            wr[30] = wbad;
+            wr[WC] = wbad;
         }
         __syncthreads();
-        if (valid) bad += win[ridx[t] * CZR_W + 30];
+        if (valid) {
+            const uint32_t rx = ridx[t];
+            bad += win[rx * WS + WC];
+            if (late_e0) {
+                const uint32_t e0 = cz_encode_hi(n, gs, p, hp, i, A, roots_h[rx], ring);
+                e0s[t] = e0;
+                bad += 2 * (e0 == CZ_NONE);
+            }
+        }
+        if (late_e0) __syncthreads();
     }  // do_compute
     // ---- stores: 2 planes x rows entries x 4 chunks of 16 B, assembled from LDS ----
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     const size_t t0 = (size_t)(2 * lvl) * M + j0;
-    for (uint32_t c = t; do_store && c < 2u * 256u * 4u; c += 256u) {
+    // chunk c: plane c >> 10, entry (c >> 2) & 255, 16-B quarter c & 3
+    auto store_chunk = [&](uint32_t c) {
         const uint32_t pl = c >> 10, cc = c & 1023u, e = cc >> 2, qq = cc & 3u;
-        if (e >= rows) continue;
-        const uint32_t *wr = win + ridx[e] * CZR_W;
+        if (e >= rows) return;
+        const uint32_t *wr = win + ridx[e] * WS;
         uint32_t w[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -2775,10 +2887,24 @@ __global__ __launch_bounds__(256) void k_cz_build_roots(FingerView fv, const cel
             if (pl == 0)
                 w[u] = word == 0 ? e0s[e] : wr[word - 1];
             else
-                w[u] = word == 15 ? e0s[e] : wr[15 + word];
+                w[u] = word == 15 ? e0s[e] : wr[(SPLIT ? 0 : 15) + word];
         }
         const v4u wv4 = {w[0], w[1], w[2], w[3]};
         __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (t0 + (size_t)pl * M + e) * 4) + qq);
+    };
+    if (!SPLIT) {
+        for (uint32_t c = t; do_store && c < 2u * 256u * 4u; c += 256u) store_chunk(c);
+    } else {
+        for (uint32_t c = t; do_store && c < 1024u; c += 256u) store_chunk(c);
+        if (do_compute) {
+            __syncthreads();  // plane 0 has read every W0 word
+            if ((uint32_t)t < nroots) {
+#pragma unroll
+                for (int v = 0; v < (SPLIT ? 15 : 1); ++v) win[t * WS + v] = o1[v];
+            }
+            __syncthreads();
+        }
+        for (uint32_t c = 1024u + t; do_store && c < 2048u; c += 256u) store_chunk(c);
     }
     if (oob) atomicOr(esc + 1, 1u);
     if (bad) atomicAdd(esc, bad);
@@ -2844,13 +2970,45 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             const char *e = getenv("CX_CZ_ROOTS_A1");
             return e ? (atoi(e) != 0) : 1;
         }();
+        static const int late_e0 = [] {
+            const char *e = getenv("CX_CZ_ROOTS_LATE");
+            return e ? (atoi(e) != 0) : 0;
+        }();
+        // probe: extra dynamic LDS per block (fewer resident blocks per CU), to
+        // measure how the build scales with the rows in flight
+        static const unsigned lds_pad = [] {
+            const char *e = getenv("CX_CZ_LDS_PAD");
+            const int v = e ? atoi(e) : 0;
+            return (unsigned)(v > 0 && v <= 65536 ? v : 0);
+        }();
         const uint32_t Kr = K ? K : 16;
         const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
-        k_cz_build_roots<<<(unsigned)blocks, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                          p_first, M, gs, out, esc, Kr, mode,
-                                                          a1_rows);
+        // CX_CZ_ROOTS_SPLIT / CX_CZ_ROOTS_WPE: LDS split and waves per SIMD (A/B)
+        static const int split = [] {
+            const char *e = getenv("CX_CZ_ROOTS_SPLIT");
+            return e ? (atoi(e) != 0) : 0;
+        }();
+        static const int wpe = [] {
+            const char *e = getenv("CX_CZ_ROOTS_WPE");
+            return e ? atoi(e) : 4;
+        }();
+#define CX_ROOTS_LAUNCH(SP, W)                                                                   \
+    k_cz_build_roots<SP, W><<<(unsigned)blocks, 256, lds_pad, s>>>(                              \
+        fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode, a1_rows, \
+        late_e0)
+        if (!split)
+            CX_ROOTS_LAUNCH(0, 4);
+        else if (wpe >= 8)
+            CX_ROOTS_LAUNCH(1, 8);
+        else if (wpe >= 6)
+            CX_ROOTS_LAUNCH(1, 6);
+        else if (wpe == 5)
+            CX_ROOTS_LAUNCH(1, 5);
+        else
+            CX_ROOTS_LAUNCH(1, 4);
+#undef CX_ROOTS_LAUNCH
         return hipGetLastError();
     }
     if (planes && fv.C2 && pair >= 1 && pair <= 3) {
@@ -2928,8 +3086,11 @@ __device__ __forceinline__ int cz_exact(const PkCtx &c, u128 key, u128 &clo, uin
                                         uint64_t &dmax, uint32_t &cur, uint32_t &h, int i,
                                         uint32_t &own, uint8_t &st, uint32_t *xc = nullptr) {
     if (xc) ++*xc;  // counter build only: one F gather + one ring gather
-    const uint32_t nxt =
-        c.arc ? finger_of(c.sv, c.ring, c.n, cur, i, clo) : c.F[(size_t)cur * CX_FINGERS + i];
+    // arc mode, or a ring whose row-major finger table is not materialised
+    // (cx_fingers_build defers it: the cz walk reads it only here): the finger
+    // from the ring (next peer) or the directory
+    const uint32_t nxt = (c.arc || !c.F) ? finger_of(c.sv, c.ring, c.n, cur, i, clo)
+                                         : c.F[(size_t)cur * CX_FINGERS + i];
     const u128 idn = ld128(c.ring + nxt);
     ++h;
     if (key - clo <= idn - clo) {
@@ -3489,15 +3650,16 @@ template <class K>
 static unsigned resident_grid(K kernel, int block);
 
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
-                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
-                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                    uint8_t *status, unsigned long long *stats, hipStream_t s) {
+                    int l0, int R, int ib, const uint32_t *F, const SearchView &sv,
+                    const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
+                    uint8_t *hops, uint8_t *status, unsigned long long *stats, hipStream_t s) {
     if (q == 0) return hipSuccess;
     TreeIO io = {};
     io.ring_ext = ring_ext;
     io.ring = ring;
     io.n = (uint32_t)n;
     io.stats = stats;
+    io.sv = sv;  // exact hops when F is null (rows not materialised)
     io.tree = reinterpret_cast<const uint4 *>(cz);
     io.l0 = l0;
     io.R = R;

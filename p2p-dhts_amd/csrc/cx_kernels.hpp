@@ -54,7 +54,17 @@ namespace cxk {
 size_t scan_workspace_words(size_t n);
 hipError_t exclusive_scan(uint32_t *data, size_t n, uint32_t *ws, hipStream_t s);
 
+// First level the streaming finger build's tile holds (planes-only builds need
+// every plane level at or above it).
+constexpr int FINGERS_TILE_L0 = 88;
+
 size_t sort_workspace_words(size_t n);
+// Small batches of uniformly distributed keys (a churn's joins): top-bit
+// buckets + per-bucket insertion sort; *overflow (device) != 0 = a bucket was
+// too full (clustered input) and out is not sorted: use radix_sort.
+size_t bucket_sort_workspace_words(size_t n);
+hipError_t bucket_sort(const cell128 *keys, size_t n, cell128 *out, uint32_t *ws,
+                       uint32_t *overflow, hipStream_t s);
 hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
                       uint32_t *ws, hipStream_t s);
 hipError_t unique_sorted(const cell128 *keys, const uint32_t *tags, size_t n, uint32_t *pos,
@@ -162,9 +172,9 @@ hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s);
 hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                     int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s);
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
-                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
-                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                    uint8_t *status, unsigned long long *stats, hipStream_t s);
+                    int l0, int R, int ib, const uint32_t *F, const SearchView &sv,
+                    const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
+                    uint8_t *hops, uint8_t *status, unsigned long long *stats, hipStream_t s);
 // Dependent random gathers of 64-B entries (four lanes, one 16-B load each),
 // the walk's access pattern, over `bytes` of `table` (read only): entries/s.
 hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, double *rate,

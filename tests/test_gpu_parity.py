@@ -383,6 +383,10 @@ def test_churn_edge_cases(cx, O, churn):
         (O.splitmix_keys(77, 50), want_old[1:]),                   # all but one leave
         (O.keys_from_ints([]), want_old[:0]),                      # no-op
         (O.keys_from_ints([v[3], v[4]]), want_old[:0]),            # joins = survivors only
+        # 300 joins sharing their top bits, shuffled: the join bucket sort
+        # overflows (one bucket) and the merge sorts them with the radix sort
+        (O.keys_from_ints([v[5] + 1 + (k * 7919) % 300 for k in range(300)]),
+         O.keys_from_ints([v[6]])),
     ]
     for joins, leaves in cases:
         old = cx.Ring(want_old)
