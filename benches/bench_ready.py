@@ -27,6 +27,9 @@ def main():
     ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
     chordx.fill_splitmix(ids, 0x5EED0005)
     ring = chordx.Ring(ids)
+    # CX_READY_REPAIR=1: the churned rings remap the parent's finger planes
+    # (the f2 repair A/B) instead of searching them from scratch
+    ring.set_fingers_repair(os.environ.get("CX_READY_REPAIR", "0") == "1")
     ring.build_fingers()
     ring.sync()
     nj = N // 100
@@ -46,13 +49,16 @@ def main():
         new.sync()
         t2 = time.perf_counter()
         hashes.add(new.route_table_hash())
+        repaired, searched = new.fingers_repair_info()
         new.close()
         del new
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         rows.append({"churn_ms": (t1 - t0) * 1e3, "fingers_and_table_ms": (t2 - t1) * 1e3,
-                     "route_ready_ms": (t2 - t0) * 1e3, "close_ms": (t3 - t2) * 1e3})
-    print(json.dumps({"log2_peers": lg, "reps": rows, "hashes_equal": len(hashes) == 1}), flush=True)
+                     "route_ready_ms": (t2 - t0) * 1e3, "close_ms": (t3 - t2) * 1e3,
+                     "fingers_repaired": repaired, "repair_searched": searched})
+    print(json.dumps({"log2_peers": lg, "reps": rows, "hashes_equal": len(hashes) == 1,
+                      "hash": hashes.pop()}), flush=True)
 
 
 if __name__ == "__main__":

@@ -312,6 +312,26 @@ class Ring:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))
 
+    def set_fingers_repair(self, on: bool):
+        """Internal A/B switch (row f2): a ring churned from this one remaps its
+        parent's finger level planes (True; the ring then keeps its planes for
+        its children) or searches them from scratch (False, default: the
+        streaming build is faster).  Inherited by churned rings."""
+        f = L.lib().cxi_set_fingers_repair
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.check(f(self._h, int(bool(on))))
+
+    def fingers_repair_info(self):
+        """(repaired, searched) of the last finger build: whether its planes
+        were remapped from the parent ring, and how many fingers the repair
+        searched exactly (churn events at the finger, joined peers)."""
+        f = L.lib().cxi_fingers_repair_info
+        f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                      ctypes.POINTER(ctypes.c_uint64)]
+        r, n = ctypes.c_int(), ctypes.c_uint64()
+        L.check(f(self._h, ctypes.byref(r), ctypes.byref(n)))
+        return bool(r.value), n.value
+
     def set_churn_variant(self, v: int):
         """Internal A/B switch: 0 = full re-sort, 1 = merge of sorted joins (default)."""
         f = L.lib().cxi_set_churn_variant

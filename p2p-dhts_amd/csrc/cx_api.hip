@@ -8,6 +8,7 @@
 #include <cstring>
 #include <initializer_list>
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -252,6 +253,17 @@ hipError_t arena_carve(IdaArena &a, int slot, std::initializer_list<size_t> size
 
 }  // namespace
 
+// The finger level planes a ring's route-table build read (kept with the
+// ring: the next churn's finger repair remaps them).  Shared between a ring
+// and the rings churned from it until their first finger build.
+struct PlaneSet {
+    int device = 0;
+    uint32_t *p = nullptr;
+    size_t bytes = 0, n = 0;
+    int L = 0, nl = 0;
+    ~PlaneSet() { table_free(device, p, bytes); }  // holders synchronise first
+};
+
 struct cx_ring {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -267,6 +279,15 @@ struct cx_ring {
     // hands to the route-table build, so cx_fingers_build without fingers_out
     // defers the 8 GiB of rows (2^24) to their first reader (ensure_fingers_rows)
     bool rows_deferred = false;
+    std::shared_ptr<PlaneSet> planes;         // level planes of the last finger build
+    std::shared_ptr<PlaneSet> parent_planes;  // cx_churn: the parent's, until the first build
+    // cxi_set_fingers_repair (A/B, default off): the repair is bit-identical
+    // but slower than the streaming build (2^24, 1 %/1 % churn: 5.2 vs 1.7 ms
+    // for the planes, profiles/r03/repair/); on, a ring keeps its planes
+    // (2.3 GiB at 2^24) for the rings churned from it
+    int fingers_repair = 0;
+    int planes_repaired = 0;                  // last build: planes remapped from the parent
+    uint64_t repair_searched = 0;             //   fingers searched exactly in that repair
     RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
@@ -464,6 +485,9 @@ void free_ring(cx_ring *r) {
     if (!r) return;
     (void)hipSetDevice(r->device);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
+    if (r->own_stream) (void)hipStreamSynchronize(r->own_stream);
+    r->planes.reset();
+    r->parent_planes.reset();
     // the ring's per-peer arrays recur at the same sizes every membership
     // epoch: through the pool like the tables (below 16 MiB: freed)
     table_free(r->device, r->d_ring, r->ring_cap * sizeof(cell128));
@@ -959,6 +983,13 @@ int ensure_fingers_rows(cx_ring *ring, hipStream_t s) {
     }
     SearchView fv = ring->sv();
     fv.dir = ring->d_dir;
+    if (!ring->d_ring_key && ring->n >= ((size_t)1 << 18)) {  // a repaired ring has none yet
+        if (table_alloc((void **)&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
+            CX_HIP(cxk::ring_slice_build(ring->d_ring, ring->n, cxk::finger_key_shift(ring->n),
+                                         ring->d_ring_key, s));
+        else
+            ring->d_ring_key = nullptr;
+    }
     DBuf fws;
     const bool streaming = ring->d_ring_key &&
                            fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n), s) == hipSuccess;
@@ -1011,30 +1042,76 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
                        (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
                        ring->n >= ((size_t)1 << 18) && ft_l >= cxk::FINGERS_TILE_L0;
     // the default route table reads the fingers as level planes: the streaming
-    // finger build writes them alongside the rows (no transpose pass)
-    DBuf ft_pre;
+    // finger build writes them alongside the rows (no transpose pass), and the
+    // ring keeps them for the finger repair of the next churn
+    std::shared_ptr<PlaneSet> ps;
     bool ft_done = false;
-    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
-        ft_pre.alloc_pooled((size_t)(CX_FINGERS - ft_l) * ring->n * sizeof(uint32_t), s) != hipSuccess) {
-        (void)hipGetLastError();
-        ft_pre.p = nullptr;
+    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64) {
+        const int nl = (int)CX_FINGERS - ft_l;
+        const size_t bytes = (size_t)nl * ring->n * sizeof(uint32_t);
+        void *pp = nullptr;
+        if (table_alloc(&pp, bytes) == hipSuccess) {
+            ps = std::make_shared<PlaneSet>();
+            ps->device = ring->device;
+            ps->p = static_cast<uint32_t *>(pp);
+            ps->bytes = bytes;
+            ps->n = ring->n;
+            ps->L = ft_l;
+            ps->nl = nl;
+        } else {
+            (void)hipGetLastError();
+        }
     }
-    if ((rc = build_fingers_table(ring, s, ft_pre.as<uint32_t>(), ft_l, &ft_done,
-                                  !defer || !ft_pre.p)))
+    // f2 finger repair: a churned ring remaps its parent's planes (cx_churn
+    // handed them over with the old_to_new map) instead of searching every
+    // finger; the rows stay deferred either way
+    std::shared_ptr<PlaneSet> par = std::move(ring->parent_planes);
+    ring->planes_repaired = 0;
+    ring->repair_searched = 0;
+    uint32_t searched = 0;
+    const bool repair = ps && par && defer && ring->fingers_repair && par->device == ring->device &&
+                        par->L == ps->L && par->nl == ps->nl && ring->d_o2n_canon &&
+                        ring->o2n_canon_n == par->n && ring->d_dir;
+    if (repair) {
+        DBuf n2o;
+        CX_HIP(n2o.alloc_pooled(ring->n * sizeof(uint32_t), s));
+        uint32_t *d_cnt = ring->d_scratch + 96;
+        CX_HIP(hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), s));
+        SearchView sv = ring->sv();
+        sv.dir = ring->d_dir;
+        CX_HIP(cxk::planes_repair(sv, ring->d_ring, ring->n, par->p, par->n, ring->d_o2n_canon,
+                                  n2o.as<uint32_t>(), ps->L, ps->nl, ps->p, d_cnt, s));
+        CX_HIP(hipMemcpyAsync(&searched, d_cnt, sizeof(searched), hipMemcpyDeviceToHost, s));
+        ring->fingers_converged = true;
+        ring->rows_deferred = true;
+        ring->planes_repaired = 1;
+        ft_done = true;
+    } else if ((rc = build_fingers_table(ring, s, ps ? ps->p : nullptr, ft_l, &ft_done,
+                                         !defer || !ps))) {
         return rc;
+    }
     ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         table_alloc((void **)&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
     if (ring->d_ring_ext) CX_HIP(cxk::ring_ext_build(ring->d_ring, ring->n, ring->d_ring_ext, s));
     // the default route kernel's table is built now (outside any timed query)
-    if (int rc2 = ensure_route_table(ring, s, ft_done ? ft_pre.as<uint32_t>() : nullptr))
+    if (int rc2 = ensure_route_table(ring, s, ft_done ? ps->p : nullptr)) {
+        (void)hipStreamSynchronize(s);  // before the planes go back to the pool
         return rc2;
+    }
     if (fingers_out) {
         const hipMemcpyKind kind =
             memkind == CX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
         CX_HIP(hipMemcpyAsync(fingers_out, ring->d_fingers, cnt * sizeof(uint32_t), kind, s));
     }
+    if (repair || !ft_done) {
+        // the repair read the parent's planes (and its count); unused planes
+        // are dropped: both wait for the stream
+        CX_HIP(hipStreamSynchronize(s));
+        ring->repair_searched = searched;
+    }
+    ring->planes = (ft_done && ring->fingers_repair) ? ps : nullptr;
     return sync_if_host(memkind, s);
 }
 
@@ -1305,6 +1382,8 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
             r->churn_parent = old_ring->serial;
             r->o2n_canon_n = n_old;
             r->d_o2n_canon = o2n.as<uint32_t>();
+            r->parent_planes = old_ring->planes;  // the finger repair's input
+            r->fingers_repair = old_ring->fingers_repair;
             o2n.release();
             return CX_OK;
         }
@@ -1362,6 +1441,8 @@ int cx_churn(const cx_ring *old_ring, const cx_u128 *joins, size_t nj, const cx_
         r->churn_parent = old_ring->serial;
         r->o2n_canon_n = n_old;
         r->d_o2n_canon = o2n.as<uint32_t>();
+        r->parent_planes = old_ring->planes;  // the finger repair's input
+        r->fingers_repair = old_ring->fingers_repair;
         o2n.release();
         return CX_OK;
     }();
@@ -2260,6 +2341,25 @@ int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0, 1, 2 or 3");
     ring->table_build = variant;
+    return CX_OK;
+}
+
+// f2 finger repair (A/B): 1 = a churned ring's finger planes are remapped from
+// its parent's, 0 = searched from scratch by the streaming build (default:
+// faster).  Inherited by churned rings; a ring keeps its planes for its
+// children only while it is on.  Takes effect at the next finger build.
+int cxi_set_fingers_repair(cx_ring *ring, int on) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    ring->fingers_repair = on ? 1 : 0;
+    return CX_OK;
+}
+
+// Last finger build: *repaired = 1 when its planes were remapped from the
+// parent ring, *searched = fingers that needed an exact search in that repair.
+int cxi_fingers_repair_info(const cx_ring *ring, int *repaired, uint64_t *searched) {
+    CX_CHECK(ring && repaired && searched, CX_E_INVALID, "null argument");
+    *repaired = ring->planes_repaired;
+    *searched = ring->repair_searched;
     return CX_OK;
 }
 

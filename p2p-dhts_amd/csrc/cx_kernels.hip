@@ -1008,6 +1008,86 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
     }
 }
 
+// ---------------------------------------------------------------------------
+// f2 finger repair (finger_table.h:148-168 AdjustFingers / ReplaceDeadPeer,
+// abstract_chord_peer.cpp:615-645 FixOtherFingers, batched over a churn):
+// the finger level planes of the new ring from the parent ring's planes.  A
+// survivor p (old index o) keeps finger level l's target t = id_p + 2^l, and
+// its old finger x = succ_old(t) satisfies t in (id_{x-1}, id_x].  If x
+// survived (y = o2n[x]) and so did x - 1, with nothing inserted between them
+// (o2n[x - 1] = y - 1, cyclic), the new ring holds no peer in
+// (id_{x-1}, id_x) either, so succ_new(t) = y: the finger is remapped.
+// Otherwise -- x left (ReplaceDeadPeer), a join landed in x's gap
+// (AdjustFingers), x - 1 left, or p itself joined -- the finger is searched
+// exactly on the new ring's directory.  Bit-identical to the streaming build.
+// ---------------------------------------------------------------------------
+__global__ void k_invert_o2n(const uint32_t *o2n, uint32_t n_old, uint32_t n_new, uint32_t *n2o) {
+    for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < n_old; o += gridDim.x * blockDim.x) {
+        const uint32_t y = o2n[o];
+        if (y < n_new) n2o[y] = o;
+    }
+}
+
+constexpr int PR_MAX = CX_FINGERS - FINGERS_TILE_L0;  // plane levels at most (tile levels)
+__global__ __launch_bounds__(256) void k_planes_repair(SearchView sv, const cell128 *ring,
+                                                       uint32_t n, const uint32_t *Pold,
+                                                       uint32_t n_old, const uint32_t *o2n,
+                                                       const uint32_t *n2o, int L, int nl,
+                                                       uint32_t *Pnew, uint32_t *nsearch) {
+    // one lane per new peer; the remapped fingers go to LDS, the lane then
+    // searches its own failed levels one per round (rounds = the wave's
+    // largest count, not the number of levels any lane failed), and every
+    // level leaves as one coalesced store per wave
+    __shared__ uint32_t val[PR_MAX][256];
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = p < n;
+    const uint32_t o = valid ? n2o[p] : CX_NONE;
+    uint64_t miss = 0;
+#pragma unroll
+    for (int c = 0; c < PR_MAX; ++c) {
+        if (c >= nl || !valid) break;
+        uint32_t f = CX_NONE;
+        if (o < n_old) {
+            const uint32_t x = Pold[(size_t)c * n_old + o];
+            if (x < n_old) {
+                const uint32_t y = o2n[x];
+                const uint32_t ym = o2n[x ? x - 1 : n_old - 1];
+                if (y < n && ym == (y ? y - 1 : n - 1)) f = y;
+            }
+        }
+        if (f == CX_NONE) miss |= 1ull << c;  // joined peer, or a churn event at the finger
+        val[c][threadIdx.x] = f;
+    }
+    uint32_t searched = 0;
+    if (miss) {
+        const u128 idp = ld128(ring + p);
+        while (miss) {
+            const int c = __builtin_ctzll(miss);
+            miss &= miss - 1;
+            val[c][threadIdx.x] = dir_successor(sv, idp + ((u128)1 << (L + c)));
+            ++searched;
+        }
+    }
+    if (valid)
+        for (int c = 0; c < nl; ++c)
+            __builtin_nontemporal_store(val[c][threadIdx.x], Pnew + (size_t)c * n + p);
+    if (nsearch && searched) atomicAdd(nsearch, searched);
+}
+
+hipError_t planes_repair(const SearchView &sv, const cell128 *ring, size_t n, const uint32_t *Pold,
+                         size_t n_old, const uint32_t *o2n, uint32_t *n2o, int L, int nl,
+                         uint32_t *Pnew, uint32_t *nsearch, hipStream_t s) {
+    if (n == 0 || n_old == 0 || nl <= 0 || nl > PR_MAX || L < 0 || L + nl > CX_FINGERS || !sv.dir)
+        return hipErrorInvalidValue;
+    hipError_t e = fill_u32(n2o, n, CX_NONE, s);
+    if (e != hipSuccess) return e;
+    k_invert_o2n<<<cx_grid(n_old, 256), 256, 0, s>>>(o2n, (uint32_t)n_old, (uint32_t)n, n2o);
+    k_planes_repair<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(sv, ring, (uint32_t)n, Pold,
+                                                               (uint32_t)n_old, o2n, n2o, L, nl,
+                                                               Pnew, nsearch);
+    return hipGetLastError();
+}
+
 // Slice position of the streaming finger build: the expected span of a
 // window (FT_W gaps, 2^(135.6 - log2 n)) stays far below 2^(kb + 32), and
 // kb <= FT_L0 so every tile level is >= kb.
@@ -2728,6 +2808,51 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
         }
         return x;
     };
+    // W1 of root slot tt: A' = f(R, i - 1) relative to R (slot 0), the window
+    // below A' (1..14), into o (SPLIT) or wr[15..29]; returns its CZ_NONE count
+    auto w1_window = [&](uint32_t tt, uint32_t R, uint64_t hR, uint32_t *o,
+                         uint32_t *wr) -> uint32_t {
+            uint32_t wbad = 0;
+            {
+                uint32_t nd[15];
+                nd[0] = a1_rows ? roots_a1[tt] : chk(fat(R, i - 1));
+                nd[1] = chk(fat(nd[0], i - 2));
+                nd[2] = chk(fat(nd[0], i - 3));
+                nd[3] = chk(c2(nd[0], i - 2));
+                nd[4] = chk(fat(nd[0], i - 4));
+                nd[6] = chk(c2(nd[0], i - 3));
+                nd[8] = chk(fat(nd[0], i - 5));
+                nd[12] = chk(c2(nd[0], i - 4));
+                nd[5] = chk(fat(nd[1], i - 4));
+                nd[7] = chk(fat(nd[3], i - 4));
+                nd[9] = chk(fat(nd[1], i - 5));
+                nd[10] = chk(fat(nd[2], i - 5));
+                nd[11] = chk(fat(nd[3], i - 5));
+                nd[13] = chk(c2(nd[1], i - 4));
+                nd[14] = chk(c2(nd[2], i - 4));
+                uint64_t hv[15];
+#pragma unroll
+                for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
+                const uint32_t o0 = cz_encode_hi(n, gs, R, hR, i - 1, nd[0], hv[0], ring);
+                wbad += o0 == CZ_NONE;
+                if (SPLIT)
+                    o[0] = o0;
+                else
+                    wr[15] = o0;
+#pragma unroll
+                for (int v = 1; v < 15; ++v) {
+                    const int hb = 31 - __builtin_clz((unsigned)v);
+                    const int pv = v & ~(1 << hb);
+                    const uint32_t ow = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                    wbad += ow == CZ_NONE;
+                    if (SPLIT)
+                        o[v] = ow;
+                    else
+                        wr[15 + v] = ow;
+                }
+            }
+            return wbad;
+    };
     // ---- rows: root and the row's own word ----
     const bool valid = (uint32_t)t < rows;
     uint32_t A = 0xFFFFFFFFu, A1 = 0, p = 0;
@@ -2820,44 +2945,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
                 }
             }
             // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
-            {
-                uint32_t nd[15];
-                nd[0] = a1_rows ? roots_a1[t] : chk(fat(R, i - 1));
-                nd[1] = chk(fat(nd[0], i - 2));
-                nd[2] = chk(fat(nd[0], i - 3));
-                nd[3] = chk(c2(nd[0], i - 2));
-                nd[4] = chk(fat(nd[0], i - 4));
-                nd[6] = chk(c2(nd[0], i - 3));
-                nd[8] = chk(fat(nd[0], i - 5));
-                nd[12] = chk(c2(nd[0], i - 4));
-                nd[5] = chk(fat(nd[1], i - 4));
-                nd[7] = chk(fat(nd[3], i - 4));
-                nd[9] = chk(fat(nd[1], i - 5));
-                nd[10] = chk(fat(nd[2], i - 5));
-                nd[11] = chk(fat(nd[3], i - 5));
-                nd[13] = chk(c2(nd[1], i - 4));
-                nd[14] = chk(c2(nd[2], i - 4));
-                uint64_t hv[15];
-#pragma unroll
-                for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
-                const uint32_t o0 = cz_encode_hi(n, gs, R, hR, i - 1, nd[0], hv[0], ring);
-                wbad += o0 == CZ_NONE;
-                if (SPLIT)
-                    o1[0] = o0;
-                else
-                    wr[15] = o0;
-#pragma unroll
-                for (int v = 1; v < 15; ++v) {
-                    const int hb = 31 - __builtin_clz((unsigned)v);
-                    const int pv = v & ~(1 << hb);
-                    const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
-                    wbad += o == CZ_NONE;
-                    if (SPLIT)
-                        o1[v] = o;
-                    else
-                        wr[15 + v] = o;
-                }
-            }
+            if (SPLIT != 2) wbad += w1_window(t, R, hR, o1, wr);
             wr[WC] = wbad;
         }
         __syncthreads();
@@ -2898,7 +2986,14 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
         for (uint32_t c = t; do_store && c < 1024u; c += 256u) store_chunk(c);
         if (do_compute) {
             __syncthreads();  // plane 0 has read every W0 word
-            if ((uint32_t)t < nroots) {
+            if (SPLIT == 2) {
+                // W1 only now: the window phase held one window per lane (fewer
+                // live registers), at the price of a second dependent chain
+                if ((uint32_t)t < nroots)
+                    win[t * WS + WC] = w1_window(t, roots[t], roots_h[t], win + t * WS, nullptr);
+                __syncthreads();
+                if (valid) bad += win[ridx[t] * WS + WC];
+            } else if ((uint32_t)t < nroots) {
 #pragma unroll
                 for (int v = 0; v < (SPLIT ? 15 : 1); ++v) win[t * WS + v] = o1[v];
             }
@@ -2988,7 +3083,7 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         // CX_CZ_ROOTS_SPLIT / CX_CZ_ROOTS_WPE: LDS split and waves per SIMD (A/B)
         static const int split = [] {
             const char *e = getenv("CX_CZ_ROOTS_SPLIT");
-            return e ? (atoi(e) != 0) : 0;
+            return e ? atoi(e) : 0;
         }();
         static const int wpe = [] {
             const char *e = getenv("CX_CZ_ROOTS_WPE");
@@ -3000,6 +3095,12 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         late_e0)
         if (!split)
             CX_ROOTS_LAUNCH(0, 4);
+        else if (split == 2 && wpe >= 8)
+            CX_ROOTS_LAUNCH(2, 8);
+        else if (split == 2 && wpe >= 6)
+            CX_ROOTS_LAUNCH(2, 6);
+        else if (split == 2)
+            CX_ROOTS_LAUNCH(2, 5);
         else if (wpe >= 8)
             CX_ROOTS_LAUNCH(1, 8);
         else if (wpe >= 6)

@@ -58,6 +58,14 @@ hipError_t exclusive_scan(uint32_t *data, size_t n, uint32_t *ws, hipStream_t s)
 // every plane level at or above it).
 constexpr int FINGERS_TILE_L0 = 88;
 
+// f2 finger repair: the level planes [L, L + nl) (nl <= 128 - FINGERS_TILE_L0)
+// of a churned ring from its parent's (Pold, n_old peers) and the churn's
+// old_to_new map; n2o: n words of workspace; *nsearch (device, optional) +=
+// the fingers searched exactly instead of remapped.
+hipError_t planes_repair(const SearchView &sv, const cell128 *ring, size_t n, const uint32_t *Pold,
+                         size_t n_old, const uint32_t *o2n, uint32_t *n2o, int L, int nl,
+                         uint32_t *Pnew, uint32_t *nsearch, hipStream_t s);
+
 size_t sort_workspace_words(size_t n);
 // Small batches of uniformly distributed keys (a churn's joins): top-bit
 // buckets + per-bucket insertion sort; *overflow (device) != 0 = a bucket was
