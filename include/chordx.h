@@ -131,7 +131,12 @@ int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t 
  * Converged PopulateFingerTable (abstract_chord_peer.cpp:564-613): row p,
  * entry i = succ(GetNthRange(i).first) = succ(id_p + 2^i mod 2^128)
  * (finger_table.h:177-188).  The table stays on the device for cx_route;
- * fingers_out (n x 128 uint32, may be NULL) receives a copy. */
+ * fingers_out (n x 128 uint32, may be NULL) receives a copy.  With
+ * fingers_out NULL on a ring of 2^18 peers or more, the build hands the
+ * default route table only the finger levels it reads and writes the
+ * row-major table when it is first read (cx_fingers_device, fingers_out of a
+ * later build, a literal or non-default walk, cx_arc_build): the same table,
+ * 8 GiB fewer bytes on the churn -> route-ready path at 2^24. */
 int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind);
 /* Hand-edited / churned finger table (EditNthFinger, AdjustFingers,
  * ReplaceDeadPeer: finger_table.h:137-168), n x 128 peer indices; CX_NONE =
@@ -140,7 +145,8 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind);
  * the current table (a rejected upload changes nothing).  Switches cx_route
  * to the literal ForwardRequest walk. */
 int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind);
-/* Device pointer to the n x 128 finger table (NULL until built/uploaded). */
+/* Device pointer to the n x 128 finger table (NULL until built/uploaded);
+ * a deferred table is written first (the call returns when it is complete). */
 int cx_fingers_device(const cx_ring *ring, const uint32_t **fingers);
 /* Per-peer min_key_ and predecessor_ (CX_NONE = predecessor not set, never
  * alive), as white-box tests set them (chord_test.cpp:18-123).  Either may be
