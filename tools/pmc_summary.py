@@ -22,4 +22,8 @@ for k, ctrs in acc.items():
         for d, v in vals:
             per[d] += v  # sum over XCD/SE instances of one dispatch
         res[k][c] = sum(per.values()) / len(per)
+        # per dispatch in launch order: a kernel launched on different inputs in
+        # one run (bench.py's C4 steps, then its random-source A/B) has one
+        # value per input, which the mean above mixes
+        res[k][c + "_by_dispatch"] = [per[d] for d in sorted(per, key=lambda x: int(x or 0))]
 print(json.dumps(res, indent=1))
