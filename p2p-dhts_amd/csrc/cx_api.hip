@@ -278,7 +278,8 @@ struct cx_ring {
     // default route (cz walk) needs only the level planes the finger build
     // hands to the route-table build, so cx_fingers_build without fingers_out
     // defers the 8 GiB of rows (2^24) to their first reader (ensure_fingers_rows)
-    bool rows_deferred = false;
+    std::atomic<bool> rows_deferred{false};
+    std::mutex rows_mu;  // first readers of deferred rows (ensure_fingers_rows)
     std::shared_ptr<PlaneSet> planes;         // level planes of the last finger build
     std::shared_ptr<PlaneSet> parent_planes;  // cx_churn: the parent's, until the first build
     // cxi_set_fingers_repair (A/B, default off): the repair is bit-identical
@@ -976,6 +977,10 @@ namespace {
 // planes) before anything that reads d_fingers.
 int ensure_fingers_rows(cx_ring *ring, hipStream_t s) {
     if (!ring->rows_deferred) return CX_OK;
+    // readers on other threads / streams see rows_deferred cleared only once
+    // the rows are complete (and pass no table to the cz walk until then)
+    std::lock_guard<std::mutex> g(ring->rows_mu);
+    if (!ring->rows_deferred) return CX_OK;
     if (!ring->d_fingers &&
         table_alloc((void **)&ring->d_fingers, ring->n * CX_FINGERS * sizeof(uint32_t)) != hipSuccess) {
         ring->d_fingers = nullptr;
@@ -996,6 +1001,7 @@ int ensure_fingers_rows(cx_ring *ring, hipStream_t s) {
     CX_HIP(cxk::fingers_build(fv, ring->d_ring, streaming ? ring->d_ring_key : nullptr,
                               streaming ? fws.p : nullptr, ring->d_fingers, s, nullptr, 0,
                               nullptr));
+    CX_HIP(hipStreamSynchronize(s));
     ring->rows_deferred = false;
     return CX_OK;
 }
@@ -1152,7 +1158,6 @@ int cx_fingers_device(const cx_ring *ring, const uint32_t **fingers) {
         int rc = use_device(ring);
         if (rc) return rc;
         if ((rc = ensure_fingers_rows(const_cast<cx_ring *>(ring), ring->stream))) return rc;
-        CX_HIP(hipStreamSynchronize(ring->stream));
     }
     *fingers = ring->d_fingers;
     return CX_OK;
@@ -1281,7 +1286,8 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     dsv.dir = ring->d_dir;
     if (v == 5 && ring->cz_valid)
         CX_HIP(cxk::route_cz(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
-                             ring->rt_R, ring->pk_ib, ring->d_fingers, dsv, dsrc,
+                             ring->rt_R, ring->pk_ib, ring->rows_deferred ? nullptr : ring->d_fingers,
+                             dsv, dsrc,
                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst,
                              ring->counting ? ring->d_stats : nullptr, s));
     else if (v == 4 && ring->tree_valid)
