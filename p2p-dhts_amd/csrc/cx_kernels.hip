@@ -3080,33 +3080,22 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
-        // CX_CZ_ROOTS_SPLIT / CX_CZ_ROOTS_WPE: LDS split and waves per SIMD (A/B)
+        // CX_CZ_ROOTS_SPLIT (A/B): 1 = LDS split, 2 = LDS split + W1 after plane 0
         static const int split = [] {
             const char *e = getenv("CX_CZ_ROOTS_SPLIT");
             return e ? atoi(e) : 0;
-        }();
-        static const int wpe = [] {
-            const char *e = getenv("CX_CZ_ROOTS_WPE");
-            return e ? atoi(e) : 4;
         }();
 #define CX_ROOTS_LAUNCH(SP, W)                                                                   \
     k_cz_build_roots<SP, W><<<(unsigned)blocks, 256, lds_pad, s>>>(                              \
         fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode, a1_rows, \
         late_e0)
+        // kept A/Bs (profiles/r03/build_lat/): the split at 4 waves per SIMD and
+        // the sequential W1 at 5; the forced 5 / 6 / 8-wave variants of either
+        // spilled (44-55 ms) and were removed
         if (!split)
             CX_ROOTS_LAUNCH(0, 4);
-        else if (split == 2 && wpe >= 8)
-            CX_ROOTS_LAUNCH(2, 8);
-        else if (split == 2 && wpe >= 6)
-            CX_ROOTS_LAUNCH(2, 6);
         else if (split == 2)
             CX_ROOTS_LAUNCH(2, 5);
-        else if (wpe >= 8)
-            CX_ROOTS_LAUNCH(1, 8);
-        else if (wpe >= 6)
-            CX_ROOTS_LAUNCH(1, 6);
-        else if (wpe == 5)
-            CX_ROOTS_LAUNCH(1, 5);
         else
             CX_ROOTS_LAUNCH(1, 4);
 #undef CX_ROOTS_LAUNCH
