@@ -112,11 +112,19 @@ def main():
         torch.cuda.synchronize()
         ms.append(a.elapsed_time(b) / reps)
     ok = bool((owner == ring.successor(keys)).all()) and int((status != 0).sum()) == 0
+    hops_sum = int(hops.to(torch.int64).sum())
+    ring.route_counters(True)  # the counting build: random requests the walk issues
+    ring.route(src, keys, out=(owner, hops, status))
+    g64, r16, xc, nq = ring.route_counters(False)
+    same_counting = hops_sum == int(hops.to(torch.int64).sum())
     rec = {"lib": os.path.basename(os.environ.get("CHORDX_LIB", "default")),
            "src": src_kind, "order": order, "sort_ms": sort_ms,
            "ms_min": min(ms), "ms_median": statistics.median(ms),
            "lookups_per_s": Q / (min(ms) * 1e-3), "probe": ring.gather_probe(),
-           "owner_ok": ok, "mean_hops": float(hops.double().mean())}
+           "owner_ok": ok, "mean_hops": float(hops.double().mean()), "hops_sum": hops_sum,
+           "route_R": ring.route_info()[2] // (ring.n * 128),
+           "per_lookup": {"table_gathers": g64 / Q, "exact_id_gathers": r16 / Q,
+                          "exact_hops": xc / Q}, "counting_same_hops": same_counting}
     if "--footprint" in sys.argv:
         # request ceiling vs table footprint, on the real route table's memory
         rec["probe_by_span_GiB"] = {g: ring.gather_probe(span=g << 30)

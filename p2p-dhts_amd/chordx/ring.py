@@ -312,6 +312,13 @@ class Ring:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))
 
+    def set_route_depth(self, R: int):
+        """Internal A/B switch: the route table covers levels [128 - R, 128)
+        (0 = the default).  Before the first build_fingers only."""
+        f = L.lib().cxi_set_route_depth
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.check(f(self._h, int(R)))
+
     def set_fingers_repair(self, on: bool):
         """Internal A/B switch (row f2): a ring churned from this one remaps its
         parent's finger level planes (True; the ring then keeps its planes for

@@ -292,6 +292,7 @@ struct cx_ring {
     RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
+    int depth_override = 0;        // cxi_set_route_depth (A/B): R levels instead of the default
     bool rt_valid = false;         // d_rt matches the current converged fingers
     uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variants 2, 3)
     bool pk_valid = false;
@@ -587,6 +588,13 @@ void route_geometry(cx_ring *r) {
     int lg = 0;
     while (((size_t)1 << lg) < r->n) ++lg;
     int R = ((lg + 8 + 7) / 8) * 8;
+    // CX_ROUTE_R: table depth override (A/B of table size against exact hops)
+    static const int r_env = [] {
+        const char *e = getenv("CX_ROUTE_R");
+        return e ? atoi(e) : 0;
+    }();
+    if (r_env > 0) R = r_env;
+    if (r->depth_override > 0) R = r->depth_override;
     if (R < 16) R = 16;
     if (R > 128) R = 128;
     r->rt_R = R;
@@ -2228,6 +2236,17 @@ int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     CX_CHECK(variant >= -1 && variant <= 5, CX_E_INVALID, "variant must be -1 (auto) or 0..5");
     ring->route_variant = variant;
+    return CX_OK;
+}
+
+// Route-table depth A/B: the table covers levels [128 - R, 128) (0 = the
+// default).  Only before the ring's first finger build (the table sizes follow R).
+int cxi_set_route_depth(cx_ring *ring, int R) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(R == 0 || (R >= 16 && R <= 64), CX_E_INVALID, "R must be 0 or in [16, 64]");
+    CX_CHECK(!ring->d_cz && !ring->d_tree && !ring->d_pk && !ring->d_rt && !ring->d_arc_tree,
+             CX_E_STATE, "route depth is fixed once a route table exists");
+    ring->depth_override = R;
     return CX_OK;
 }
 

@@ -1816,7 +1816,9 @@ hipError_t route_pk(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
 //    walking in the iteration its predecessor finishes (no init round).
 // ---------------------------------------------------------------------------
 constexpr int RES_WIN = 512;
-enum { A_NONE = 0, A_HOP = 1, A_FIXC = 2, A_FIXT = 3 };
+// A_EXACT (cz walk): fetch id(cur) and id(cur + 1) for an exact hop below the
+// table in the memory round, so the hop needs no load of its own
+enum { A_NONE = 0, A_HOP = 1, A_FIXC = 2, A_FIXT = 3, A_EXACT = 4 };
 enum { B_EMPTY = 0, B_KS = 1, B_PAIR = 2 };
 
 struct PkCtx {
@@ -3174,14 +3176,35 @@ __device__ __forceinline__ void cz_exact_d(const PkCtx &c, u128 key, u128 idc, u
 // 1 = finished (own/st set), 0 = moved (cur, clo exact, dmin/dmax).
 __device__ __forceinline__ int cz_exact(const PkCtx &c, u128 key, u128 &clo, uint64_t &dmin,
                                         uint64_t &dmax, uint32_t &cur, uint32_t &h, int i,
-                                        uint32_t &own, uint8_t &st, uint32_t *xc = nullptr) {
+                                        uint32_t &own, uint8_t &st, uint32_t *xc = nullptr,
+                                        bool nh_ok = false, u128 nh = 0) {
     if (xc) ++*xc;  // counter build only: one F gather + one ring gather
-    // arc mode, or a ring whose row-major finger table is not materialised
-    // (cx_fingers_build defers it: the cz walk reads it only here): the finger
-    // from the ring (next peer) or the directory
-    const uint32_t nxt = (c.arc || !c.F) ? finger_of(c.sv, c.ring, c.n, cur, i, clo)
-                                         : c.F[(size_t)cur * CX_FINGERS + i];
-    const u128 idn = ld128(c.ring + nxt);
+    uint32_t nxt;
+    u128 idn;
+    if (nh_ok) {
+        // nh = id(cur + 1) from the memory round (A_EXACT): the finger is the
+        // next peer unless the gap to it is below 2^i (then the directory)
+        const uint32_t nx = cur + 1 == c.n ? 0u : cur + 1;
+        const u128 step = (u128)1 << i;
+        if (c.n == 1) {
+            nxt = 0;
+            idn = clo;
+        } else if (step <= nh - clo) {
+            nxt = nx;
+            idn = nh;
+        } else {
+            nxt = (c.arc || !c.F) ? dir_successor(c.sv, clo + step)
+                                  : c.F[(size_t)cur * CX_FINGERS + i];
+            idn = ld128(c.ring + nxt);
+        }
+    } else {
+        // arc mode, or a ring whose row-major finger table is not materialised
+        // (cx_fingers_build defers it: the cz walk reads it only here): the
+        // finger from the ring (next peer) or the directory
+        nxt = (c.arc || !c.F) ? finger_of(c.sv, c.ring, c.n, cur, i, clo)
+                              : c.F[(size_t)cur * CX_FINGERS + i];
+        idn = ld128(c.ring + nxt);
+    }
     ++h;
     if (key - clo <= idn - clo) {
         own = nxt;
@@ -3232,7 +3255,8 @@ __device__ __forceinline__ int cz_plan(const PkCtx &c, u128 key, u128 &clo, bool
                                        uint64_t &dmin, uint64_t &dmax, uint32_t &cur,
                                        uint32_t &h, uint32_t &pn, int &mode, int &lvl, int &rb,
                                        int &cs, int ri, const uint32_t *ent, uint32_t &own,
-                                       uint8_t &st, uint32_t *xc = nullptr) {
+                                       uint8_t &st, uint32_t *xc = nullptr,
+                                       bool nh_ok = false, u128 nh = 0) {
     for (;;) {
         int i;
         const int ma = 63 - __builtin_clzll(dmin | 1), mb = 63 - __builtin_clzll(dmax | 1);
@@ -3274,11 +3298,14 @@ __device__ __forceinline__ int cz_plan(const PkCtx &c, u128 key, u128 &clo, bool
             rb = (int)((dmax >> (i - 1 - c.gs)) & 1);  // bit i-1 of d - 2^i
             return 0;
         }
-        if (!cex) {
-            mode = A_FIXC;
+        // below the table: the exact hop takes id(cur) and id(cur + 1) from one
+        // memory round (A_EXACT; nh = id(cur + 1) once they are in)
+        if (!cex || !nh_ok) {
+            mode = A_EXACT;
             return 0;
         }
-        if (cz_exact(c, key, clo, dmin, dmax, cur, h, i, own, st, xc)) return 1;
+        if (cz_exact(c, key, clo, dmin, dmax, cur, h, i, own, st, xc, true, nh)) return 1;
+        nh_ok = false;  // cur moved: the hint is stale
     }
 }
 
@@ -3456,7 +3483,7 @@ void k_route_tree(TreeIO io) {
             addr_all[threadIdx.x] = mode == A_HOP ? e + 1 : 0;
             if (STATS) {
                 n_g64 += mode == A_HOP;
-                n_r16 += mode == A_FIXC ? 1u : (mode == A_FIXT ? 2u : 0u);
+                n_r16 += mode == A_FIXC ? 1u : ((mode == A_FIXT || mode == A_EXACT) ? 2u : 0u);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3475,6 +3502,9 @@ void k_route_tree(TreeIO io) {
         } else if (mode == A_FIXT) {
             xa = ld128(io.ring + cur);
             xb = ld128(io.ring + pn);
+        } else if (mode == A_EXACT) {  // (cur, cur + 1): adjacent cells
+            xa = ld128(io.ring + cur);
+            xb = ld128(io.ring + (cur + 1 == n ? 0u : cur + 1));
         }
         if (bst == B_KS) {
             if (KF && io.dh) {
@@ -3547,7 +3577,7 @@ void k_route_tree(TreeIO io) {
                 cex = false;
                 plan = true;
             }
-        } else if (mode == A_FIXC) {
+        } else if (mode == A_FIXC || mode == A_EXACT) {
             clo = xa;
             cex = true;
             if (CZ) cz_exact_d(c, key, xa, dmin, dmax);
@@ -3570,7 +3600,7 @@ void k_route_tree(TreeIO io) {
         if (plan) {
             const int r =
                 CZ ? cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs, ri, ent32,
-                             own, st, xcp)
+                             own, st, xcp, mode == A_EXACT, xb)
                    : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
             if (r == 1) fin = true;
             if (KF && r == 2) {
