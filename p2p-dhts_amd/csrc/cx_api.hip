@@ -608,9 +608,30 @@ void route_geometry(cx_ring *r) {
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
                          DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     fv = cxk::FingerView::rows(r->d_fingers);
-    hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t), s);
-    if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
-    if (e0 != hipSuccess) return e0;
+    // gap codes of the root-centric build: 32-bit ID slices when every ring gap
+    // is below 2^(gs + 17) (uniform rings by far), else the 64-bit high words
+    // (CX_CZ_CODES=hi forces them, A/B)
+    static const bool hi_only = [] {
+        const char *e = getenv("CX_CZ_CODES");
+        return e && strcmp(e, "hi") == 0;
+    }();
+    bool slices = false;
+    if (r->table_build == 0 && !hi_only) {
+        hipError_t e1 = hi.alloc_pooled(r->n * sizeof(uint32_t), s);
+        uint32_t *d_gap = r->d_scratch + 100;
+        if (e1 == hipSuccess)
+            e1 = cxk::ring_codes(r->d_ring, r->n, r->pk_ib, hi.as<uint32_t>(), d_gap, s);
+        uint32_t gmax = 128;
+        if (e1 == hipSuccess) e1 = hipMemcpyAsync(&gmax, d_gap, sizeof(gmax), hipMemcpyDeviceToHost, s);
+        if (e1 == hipSuccess) e1 = hipStreamSynchronize(s);
+        if (e1 != hipSuccess) return e1;
+        slices = (int)gmax < cxk::cz_shift(r->pk_ib) + 17;
+    }
+    if (!slices) {
+        hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t), s);
+        if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
+        if (e0 != hipSuccess) return e0;
+    }
     const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
     hipError_t e = hipSuccess;
     if (ft_pre && r->table_build != 1) {  // written by the finger build itself
@@ -634,6 +655,15 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         }
     }
     (void)hipGetLastError();
+    if (slices) {
+        if (fv.roots) {
+            fv.rs = hi.as<uint32_t>();
+        } else {  // no root-centric build after all: the others read high words
+            hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t), s);
+            if (e0 == hipSuccess) e0 = cxk::ring_hi(r->d_ring, r->n, hi.as<uint64_t>(), s);
+            if (e0 != hipSuccess) return e0;
+        }
+    }
     return e;
 }
 

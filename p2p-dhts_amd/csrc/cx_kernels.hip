@@ -3,6 +3,8 @@
 // Every kernel is HBM/latency bound integer work: no MFMA.  Layout
 // in HBM: ring IDs as 16-B cells (AoS, one dwordx4 per ID), finger table as
 // row-major uint32 [peer][128], Eytzinger copy of the ring for searches.
+#include <type_traits>
+
 #include "cx_kernels.hpp"
 
 namespace cxk {
@@ -2268,7 +2270,6 @@ constexpr uint8_t CX_QI_ARC_MISS = 0xFE;  // key-first arc walk left the rank's 
 constexpr int CZ_RES_WIN = 256;  // 26 KB of LDS per 256-lane block: 6 blocks per CU
 constexpr int CZ_WAVES = 5;      // waves per SIMD the VGPR budget allows (88 VGPRs; 6 spills)
 
-__host__ __device__ __forceinline__ int cz_shift(int ib) { return 116 - ib; }
 
 __device__ __forceinline__ uint32_t cz_expect(uint32_t n, int l) {
     const int sh = 128 - l;
@@ -2391,6 +2392,69 @@ __device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t pa
     }
     if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
     return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
+}
+
+// cz_encode from 32-bit ID slices s(id) = bits [gs - 15, gs + 17) of id (the
+// root-centric build's default input: half the bytes and registers of the high
+// words).  D = s(x) - s(par) - s(2^l) (mod 2^32) is bits [gs - 15, gs + 17) of
+// V = x - par - 2^l less a borrow c in {0, 1} from the bits below; when D has
+// a set bit among its low 15 the borrow cannot reach bit 15 and D >> 15 is
+// bits [gs, gs + 17) of V exactly (else, about 2^-15 of encodes, the full IDs
+// are read).  V < 2^(gs + 17) holds because V is at most the gap ending at x,
+// and the caller takes this path only when every ring gap is below 2^(gs + 17).
+__device__ __forceinline__ uint32_t cz_encode_s(uint32_t n, int gs, uint32_t par, uint32_t sp,
+                                                int l, uint32_t x, uint32_t sx,
+                                                const cell128 *ring) {
+    int d = (int)x - (int)par - (int)cz_expect(n, l);
+    const int h = (int)(n / 2);
+    const int lo = h + 1 - (int)n > -32768 ? h + 1 - (int)n : -32768;  // uniform
+    const int hi = h < 32766 ? h : 32766;
+    if ((uint32_t)(d - lo) > (uint32_t)(hi - lo)) {
+        if (d < 0) d += (int)n;
+        if (d < 0) d += (int)n;
+        if (d > h) d -= (int)n;  // [h + 1 - n, h]
+    }
+    const int sb = l - (gs - 15);  // l >= gs - 15 on every table level
+    const uint32_t D = sx - sp - (sb < 32 ? 1u << sb : 0u);
+    uint64_t code;
+    if (D & 0x7FFFu) {
+        code = D >> 15;
+    } else {
+        const u128 full = ld128(ring + x) - ld128(ring + par) - ((u128)1 << l);
+        code = (uint64_t)(full >> gs);
+        if ((full >> gs) >> 64) code = ~0ull;
+    }
+    if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
+    return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
+}
+
+// s(id) = bits [gs - 15, gs + 17) of every ID, and *maxgap = the largest
+// msb(ring[p+1] - ring[p]) over the ring (cyclic): the slice codes are exact
+// when it is below gs + 17.
+__global__ void k_ring_codes(const cell128 *ring, uint32_t n, int gs, uint32_t *rs,
+                             uint32_t *maxgap) {
+    int g = 0;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const u128 id = ld128(ring + p);
+        rs[p] = (uint32_t)(id >> (gs - 15));
+        const u128 nx = ld128(ring + (p + 1 == n ? 0u : p + 1));
+        const int m = n == 1 ? 127 : msb128(nx - id);
+        g = m > g ? m : g;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int o = __shfl_xor(g, off, 64);
+        g = o > g ? o : g;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(maxgap, (uint32_t)g);
+}
+
+hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *maxgap,
+                      hipStream_t s) {
+    hipError_t e = hipMemsetAsync(maxgap, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    k_ring_codes<<<cx_grid(n, 256), 256, 0, s>>>(ring, (uint32_t)n, cz_shift(ib), rs, maxgap);
+    return hipGetLastError();
 }
 
 // Planes [lvl_base, lvl_base + nlev) of the table for the M peers p_first,
@@ -2768,18 +2832,29 @@ constexpr int CZR_W = 31;  // LDS words per root: W0[1..15], W1[0..14], CZ_NONE 
 // per SIMD) allows them.  The build is bound by the rows in flight per CU:
 // 4 -> 3 -> 2 resident blocks take 27.4 -> 31.0 -> 41.4 ms at 2^24
 // (profiles/r03/build_lat/).
-template <int SPLIT, int WPE>
+template <int SPLIT, int WPE, bool SLICE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, uint32_t n,
                       int lvl_base, int nlev, uint32_t p_first, uint32_t M, int gs, uint4 *cz,
                       uint32_t *esc, uint32_t K, int mode, int a1_rows, int late_e0) {
+    // SLICE: gap codes from 32-bit ID slices (fv.rs, cz_encode_s) instead of
+    // the 64-bit high words (rh, cz_encode_hi)
+    using HT = typename std::conditional<SLICE, uint32_t, uint64_t>::type;
+    auto hiw = [&](uint32_t x) -> HT {
+        if constexpr (SLICE) return fv.rs[x];
+        else return rh[x];
+    };
+    auto enc = [&](uint32_t par, HT hpar, int l, uint32_t x, HT hx) -> uint32_t {
+        if constexpr (SLICE) return cz_encode_s(n, gs, par, hpar, l, x, hx, ring);
+        else return cz_encode_hi(n, gs, par, hpar, l, x, hx, ring);
+    };
     constexpr int WS = SPLIT ? 16 : CZR_W;  // LDS words per root
     constexpr int WC = SPLIT ? 15 : 30;     // the root's CZ_NONE count
     __shared__ uint32_t win[256 * WS];
     __shared__ uint32_t e0s[256];
     __shared__ uint32_t roots[256];
     __shared__ uint32_t roots_a1[256];  // A' = f(R, i - 1) = C2(p, i) of the root's first row
-    __shared__ uint64_t roots_h[256];   // rh[R]
+    __shared__ HT roots_h[256];   // rh[R]
     __shared__ uint16_t ridx[256];
     __shared__ uint32_t wcnt[4];
     uint32_t lvl, lb;
@@ -2812,7 +2887,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
     };
     // W1 of root slot tt: A' = f(R, i - 1) relative to R (slot 0), the window
     // below A' (1..14), into o (SPLIT) or wr[15..29]; returns its CZ_NONE count
-    auto w1_window = [&](uint32_t tt, uint32_t R, uint64_t hR, uint32_t *o,
+    auto w1_window = [&](uint32_t tt, uint32_t R, HT hR, uint32_t *o,
                          uint32_t *wr) -> uint32_t {
             uint32_t wbad = 0;
             {
@@ -2832,10 +2907,10 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
                 nd[11] = chk(fat(nd[3], i - 5));
                 nd[13] = chk(c2(nd[1], i - 4));
                 nd[14] = chk(c2(nd[2], i - 4));
-                uint64_t hv[15];
+                HT hv[15];
 #pragma unroll
-                for (int v = 0; v < 15; ++v) hv[v] = rh[nd[v]];
-                const uint32_t o0 = cz_encode_hi(n, gs, R, hR, i - 1, nd[0], hv[0], ring);
+                for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
+                const uint32_t o0 = enc(R, hR, i - 1, nd[0], hv[0]);
                 wbad += o0 == CZ_NONE;
                 if (SPLIT)
                     o[0] = o0;
@@ -2845,7 +2920,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
                 for (int v = 1; v < 15; ++v) {
                     const int hb = 31 - __builtin_clz((unsigned)v);
                     const int pv = v & ~(1 << hb);
-                    const uint32_t ow = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                    const uint32_t ow = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
                     wbad += ow == CZ_NONE;
                     if (SPLIT)
                         o[v] = ow;
@@ -2858,7 +2933,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
     // ---- rows: root and the row's own word ----
     const bool valid = (uint32_t)t < rows;
     uint32_t A = 0xFFFFFFFFu, A1 = 0, p = 0;
-    uint64_t hA = 0, hp = 0;
+    HT hA = 0, hp = 0;
     uint32_t bad = 0, nroots = 0;
     uint32_t o1[SPLIT ? 15 : 1];  // SPLIT: the W1 words until plane 0 has left
     if (!do_compute) {
@@ -2873,13 +2948,13 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
             // A' of the b = 1 entry from the row's two-hop plane: one gather beside
             // A instead of one after it (a1_rows = 0: from A, for A/B)
             if (a1_rows) A1 = chk(c2(p, i));
-            hp = rh[p];
+            hp = hiw(p);
             if (!late_e0) {
                 // late_e0: rh[A] is gathered once per distinct root in the window
                 // phase, beside its first window gathers, and the row's own word is
                 // encoded after it (one dependent gather less per block)
-                hA = rh[A];
-                const uint32_t e0 = cz_encode_hi(n, gs, p, hp, i, A, hA, ring);
+                hA = hiw(A);
+                const uint32_t e0 = enc(p, hp, i, A, hA);
                 e0s[t] = e0;
                 bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
             }
@@ -2910,7 +2985,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
         nroots = nr;
         if ((uint32_t)t < nr) {
             const uint32_t R = roots[t];
-            const uint64_t hR = late_e0 ? rh[R] : roots_h[t];
+            const HT hR = late_e0 ? hiw(R) : roots_h[t];
             if (late_e0) roots_h[t] = hR;
             uint32_t *wr = win + t * WS;
             uint32_t wbad = 0;
@@ -2933,15 +3008,15 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
                 nd[13] = chk(c2(nd[1], i - 4));
                 nd[14] = chk(c2(nd[2], i - 4));
                 nd[15] = chk(c2(nd[3], i - 4));
-                uint64_t hv[16];
+                HT hv[16];
                 hv[0] = hR;
 #pragma unroll
-                for (int v = 1; v < 16; ++v) hv[v] = rh[nd[v]];
+                for (int v = 1; v < 16; ++v) hv[v] = hiw(nd[v]);
 #pragma unroll
                 for (int v = 1; v < 16; ++v) {
                     const int hb = 31 - __builtin_clz((unsigned)v);
                     const int pv = v & ~(1 << hb);
-                    const uint32_t o = cz_encode_hi(n, gs, nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v], ring);
+                    const uint32_t o = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
                     wbad += o == CZ_NONE;
                     wr[v - 1] = o;
                 }
@@ -2955,7 +3030,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
             const uint32_t rx = ridx[t];
             bad += win[rx * WS + WC];
             if (late_e0) {
-                const uint32_t e0 = cz_encode_hi(n, gs, p, hp, i, A, roots_h[rx], ring);
+                const uint32_t e0 = enc(p, hp, i, A, roots_h[rx]);
                 e0s[t] = e0;
                 bad += 2 * (e0 == CZ_NONE);
             }
@@ -3083,21 +3158,39 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
         // CX_CZ_ROOTS_SPLIT (A/B): 1 = LDS split, 2 = LDS split + W1 after plane 0
-        static const int split = [] {
+        // default: W1 after plane 0 through the split LDS at 5 waves per SIMD
+        // with the 32-bit slice codes (88 VGPRs, 21 KB: 5 blocks per CU; 24.4-25.0
+        // vs 26.7-26.9 ms at 2^24), the one-pass kernel at 4 with the high words
+        static const int split_env = [] {
             const char *e = getenv("CX_CZ_ROOTS_SPLIT");
-            return e ? atoi(e) : 0;
+            return e ? atoi(e) : -1;
         }();
+        const int split = split_env >= 0 ? split_env : (fv.rs ? 2 : 0);
 #define CX_ROOTS_LAUNCH(SP, W)                                                                   \
-    k_cz_build_roots<SP, W><<<(unsigned)blocks, 256, lds_pad, s>>>(                              \
-        fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode, a1_rows, \
-        late_e0)
+    do {                                                                                         \
+        if (fv.rs)                                                                               \
+            k_cz_build_roots<SP, W, true><<<(unsigned)blocks, 256, lds_pad, s>>>(                \
+                fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode,   \
+                a1_rows, late_e0);                                                                \
+        else                                                                                     \
+            k_cz_build_roots<SP, W, false><<<(unsigned)blocks, 256, lds_pad, s>>>(               \
+                fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode,   \
+                a1_rows, late_e0);                                                                \
+    } while (0)
         // kept A/Bs (profiles/r03/build_lat/): the split at 4 waves per SIMD and
         // the sequential W1 at 5; the forced 5 / 6 / 8-wave variants of either
-        // spilled (44-55 ms) and were removed
+        // spilled (44-55 ms) with 64-bit high words and were removed; with the
+        // 32-bit slice codes the split is tried at 5 / 6 waves (3 / 4)
         if (!split)
             CX_ROOTS_LAUNCH(0, 4);
         else if (split == 2)
             CX_ROOTS_LAUNCH(2, 5);
+        else if (split == 3)
+            CX_ROOTS_LAUNCH(1, 5);
+        else if (split == 4)
+            CX_ROOTS_LAUNCH(1, 6);
+        else if (split == 5)
+            CX_ROOTS_LAUNCH(2, 6);
         else
             CX_ROOTS_LAUNCH(1, 4);
 #undef CX_ROOTS_LAUNCH

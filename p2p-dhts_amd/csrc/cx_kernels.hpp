@@ -54,6 +54,10 @@ namespace cxk {
 size_t scan_workspace_words(size_t n);
 hipError_t exclusive_scan(uint32_t *data, size_t n, uint32_t *ws, hipStream_t s);
 
+// Gap-code shift of the pattern-keyed route table: codes are successor gaps in
+// units of 2^(116 - ib), ib = ceil(log2 n).
+__host__ __device__ __forceinline__ int cz_shift(int ib) { return 116 - ib; }
+
 // First level the streaming finger build's tile holds (planes-only builds need
 // every plane level at or above it).
 constexpr int FINGERS_TILE_L0 = 88;
@@ -139,6 +143,10 @@ struct FingerView {
     // F[F[x][l]][l - 1] for l in (L, L + nl) (fingers_pairs)
     const uint32_t *C2 = nullptr;
     int roots = 0;  // host-side build choice: 1 = root-centric windows (needs C2)
+    // root-centric build, optional: 32-bit ID slices (ring_codes) for the gap
+    // codes instead of the 64-bit high words; only when every ring gap is
+    // below 2^(gs + 17)
+    const uint32_t *rs = nullptr;
     __host__ __device__ uint32_t at(uint32_t x, int l) const {
         return F[(size_t)x * sx + (size_t)(l - L) * sl];
     }
@@ -177,6 +185,11 @@ hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hip
 // rh = the IDs' high words (ring_hi); the build needs l0 >= 69 and ib <= 51.
 // esc[0] += slots not representable; esc[1] |= 1 if a finger was out of range.
 hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s);
+// rs[p] = bits [gs - 15, gs + 17) of ring[p] (gs = 116 - ib), *maxgap (device)
+// = the largest msb of a cyclic ring gap: rs serves the root-centric build
+// when *maxgap < gs + 17.
+hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *maxgap,
+                      hipStream_t s);
 hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                     int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s);
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
