@@ -618,14 +618,14 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
     bool slices = false;
     if (r->table_build == 0 && !hi_only) {
         hipError_t e1 = hi.alloc_pooled(r->n * sizeof(uint32_t), s);
-        uint32_t *d_gap = r->d_scratch + 100;
+        uint32_t *d_wide = r->d_scratch + 100;
         if (e1 == hipSuccess)
-            e1 = cxk::ring_codes(r->d_ring, r->n, r->pk_ib, hi.as<uint32_t>(), d_gap, s);
-        uint32_t gmax = 128;
-        if (e1 == hipSuccess) e1 = hipMemcpyAsync(&gmax, d_gap, sizeof(gmax), hipMemcpyDeviceToHost, s);
+            e1 = cxk::ring_codes(r->d_ring, r->n, r->pk_ib, hi.as<uint32_t>(), d_wide, s);
+        uint32_t wide = 1;
+        if (e1 == hipSuccess) e1 = hipMemcpyAsync(&wide, d_wide, sizeof(wide), hipMemcpyDeviceToHost, s);
         if (e1 == hipSuccess) e1 = hipStreamSynchronize(s);
         if (e1 != hipSuccess) return e1;
-        slices = (int)gmax < cxk::cz_shift(r->pk_ib) + 17;
+        slices = wide == 0;
     }
     if (!slices) {
         hipError_t e0 = hi.alloc_pooled(r->n * sizeof(uint64_t), s);

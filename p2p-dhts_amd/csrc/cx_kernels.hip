@@ -2318,21 +2318,52 @@ __global__ void k_fingers_levels(const uint32_t *F, uint32_t n, int L, int nl, u
 
 // Two-hop planes: C2[(l - L - 1) n + x] = F[F[x][l]][l - 1].  One gather per
 // entry into the plane below (adjacent x -> adjacent fingers: coalesced-ish).
+// Rings whose size is not a multiple of four: one lane per peer, a plane per
+// grid row.
+__global__ void k_fingers_pairs_1(const uint32_t *FT, uint32_t n, int nl, uint32_t *C2) {
+    const size_t k = blockIdx.y;
+    const uint32_t *up = FT + (k + 1) * (size_t)n, *lo = FT + k * (size_t)n;
+    uint32_t *out = C2 + k * (size_t)n;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const uint32_t y = up[x];
+        __builtin_nontemporal_store(y < n ? lo[y] : CX_NONE, out + x);
+    }
+}
+
+// One plane per grid row (no 64-bit division per element), four consecutive
+// peers per lane: 16-B loads of the level-(l) plane, four gathers into the
+// level-(l - 1) plane (near-consecutive: the fingers of consecutive peers),
+// one 16-B streaming store.
 __global__ void k_fingers_pairs(const uint32_t *FT, uint32_t n, int nl, uint32_t *C2) {
-    const size_t total = (size_t)(nl - 1) * n;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-         t += (size_t)gridDim.x * blockDim.x) {
-        const size_t k = t / n;  // plane of level L + 1 + k
-        const size_t x = t - k * n;
-        const uint32_t y = FT[(k + 1) * n + x];
-        __builtin_nontemporal_store(y < n ? FT[k * n + y] : CX_NONE, C2 + t);
+    const size_t k = blockIdx.y;  // C2 plane k = level L + 1 + k
+    const uint32_t *up = FT + (k + 1) * (size_t)n, *lo = FT + k * (size_t)n;
+    uint32_t *out = C2 + k * (size_t)n;
+    const uint32_t n4 = n / 4;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
+        const uint4 y = reinterpret_cast<const uint4 *>(up)[q];
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u r = {y.x < n ? lo[y.x] : CX_NONE, y.y < n ? lo[y.y] : CX_NONE,
+                       y.z < n ? lo[y.z] : CX_NONE, y.w < n ? lo[y.w] : CX_NONE};
+        __builtin_nontemporal_store(r, reinterpret_cast<v4u *>(out) + q);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3u)) {  // tail
+        const uint32_t x = n4 * 4 + threadIdx.x;
+        const uint32_t y = up[x];
+        out[x] = y < n ? lo[y] : CX_NONE;
     }
 }
 
 hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hipStream_t s) {
     if (n == 0 || nl < 2) return hipSuccess;
-    k_fingers_pairs<<<cx_grid((size_t)(nl - 1) * n, 256, 16384), 256, 0, s>>>(FT, (uint32_t)n, nl,
-                                                                               C2);
+    // planes start at multiples of n words: 16-B aligned rows need n % 4 == 0;
+    // otherwise one lane per peer
+    if (n % 4 != 0 || (uintptr_t)FT % 16 != 0 || (uintptr_t)C2 % 16 != 0) {
+        k_fingers_pairs_1<<<dim3(cx_grid(n, 256, 4096), (unsigned)(nl - 1)), 256, 0, s>>>(
+            FT, (uint32_t)n, nl, C2);
+        return hipGetLastError();
+    }
+    k_fingers_pairs<<<dim3(cx_grid(n / 4, 256, 4096), (unsigned)(nl - 1)), 256, 0, s>>>(
+        FT, (uint32_t)n, nl, C2);
     return hipGetLastError();
 }
 
@@ -2428,32 +2459,24 @@ __device__ __forceinline__ uint32_t cz_encode_s(uint32_t n, int gs, uint32_t par
     return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
 }
 
-// s(id) = bits [gs - 15, gs + 17) of every ID, and *maxgap = the largest
-// msb(ring[p+1] - ring[p]) over the ring (cyclic): the slice codes are exact
-// when it is below gs + 17.
+// s(id) = bits [gs - 15, gs + 17) of every ID; *wide (device, zeroed here) =
+// 1 if some cyclic ring gap reaches 2^(gs + 17) (then the slice codes are not
+// exact and the build keeps the high words).  Only such gaps write the flag.
 __global__ void k_ring_codes(const cell128 *ring, uint32_t n, int gs, uint32_t *rs,
-                             uint32_t *maxgap) {
-    int g = 0;
+                             uint32_t *wide) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u128 id = ld128(ring + p);
         rs[p] = (uint32_t)(id >> (gs - 15));
         const u128 nx = ld128(ring + (p + 1 == n ? 0u : p + 1));
-        const int m = n == 1 ? 127 : msb128(nx - id);
-        g = m > g ? m : g;
+        if (n == 1 || msb128(nx - id) >= gs + 17) atomicOr(wide, 1u);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const int o = __shfl_xor(g, off, 64);
-        g = o > g ? o : g;
-    }
-    if ((threadIdx.x & 63) == 0) atomicMax(maxgap, (uint32_t)g);
 }
 
-hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *maxgap,
+hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *wide,
                       hipStream_t s) {
-    hipError_t e = hipMemsetAsync(maxgap, 0, sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(wide, 0, sizeof(uint32_t), s);
     if (e != hipSuccess || n == 0) return e;
-    k_ring_codes<<<cx_grid(n, 256), 256, 0, s>>>(ring, (uint32_t)n, cz_shift(ib), rs, maxgap);
+    k_ring_codes<<<cx_grid(n, 256), 256, 0, s>>>(ring, (uint32_t)n, cz_shift(ib), rs, wide);
     return hipGetLastError();
 }
 

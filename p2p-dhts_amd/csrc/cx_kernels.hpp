@@ -185,10 +185,10 @@ hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hip
 // rh = the IDs' high words (ring_hi); the build needs l0 >= 69 and ib <= 51.
 // esc[0] += slots not representable; esc[1] |= 1 if a finger was out of range.
 hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s);
-// rs[p] = bits [gs - 15, gs + 17) of ring[p] (gs = 116 - ib), *maxgap (device)
-// = the largest msb of a cyclic ring gap: rs serves the root-centric build
-// when *maxgap < gs + 17.
-hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *maxgap,
+// rs[p] = bits [gs - 15, gs + 17) of ring[p] (gs = 116 - ib); *wide (device)
+// = 1 if a cyclic ring gap reaches 2^(gs + 17): rs serves the root-centric
+// build when *wide == 0.
+hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *wide,
                       hipStream_t s);
 hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                     int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s);
