@@ -2862,9 +2862,15 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
                       uint32_t *esc, uint32_t K, int mode, int a1_rows, int late_e0) {
     // SLICE: gap codes from 32-bit ID slices (fv.rs, cz_encode_s) instead of
     // the 64-bit high words (rh, cz_encode_hi)
+    // gathers as a wave-uniform plane base plus a 32-bit byte offset (x < n <
+    // 2^30): the scalar-base form of the load, one VGPR of address per gather
+    // instead of a 64-bit pointer
+    auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
+    };
     using HT = typename std::conditional<SLICE, uint32_t, uint64_t>::type;
     auto hiw = [&](uint32_t x) -> HT {
-        if constexpr (SLICE) return fv.rs[x];
+        if constexpr (SLICE) return ld32(fv.rs, x);
         else return rh[x];
     };
     auto enc = [&](uint32_t par, HT hpar, int l, uint32_t x, HT hx) -> uint32_t {
@@ -2877,7 +2883,10 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
     __shared__ uint32_t e0s[256];
     __shared__ uint32_t roots[256];
     __shared__ uint32_t roots_a1[256];  // A' = f(R, i - 1) = C2(p, i) of the root's first row
-    __shared__ HT roots_h[256];   // rh[R]
+    // rh[R] per root (high words); the slice build gathers rs[R] again instead
+    // (one more independent load beside a window's first ones), which keeps its
+    // LDS at 20 KB: 8 blocks per CU
+    __shared__ HT roots_h[SLICE ? 1 : 256];
     __shared__ uint16_t ridx[256];
     __shared__ uint32_t wcnt[4];
     uint32_t lvl, lb;
@@ -2898,8 +2907,12 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
     // blocks store only (do the two halves overlap when different waves run them?)
     const bool do_compute = mode == 0 || mode == 1 || (mode == 3 && !(lb & 1));
     const bool do_store = mode == 0 || mode == 2 || (mode == 3 && (lb & 1));
-    auto fat = [&](uint32_t x, int l) -> uint32_t { return fv.F[(size_t)(l - fv.L) * fv.sl + x]; };
-    auto c2 = [&](uint32_t x, int l) -> uint32_t { return fv.C2[(size_t)(l - fv.L - 1) * fv.sl + x]; };
+    auto fat = [&](uint32_t x, int l) -> uint32_t {
+        return ld32(fv.F + (size_t)(l - fv.L) * fv.sl, x);
+    };
+    auto c2 = [&](uint32_t x, int l) -> uint32_t {
+        return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
+    };
     uint32_t oob = 0;
     auto chk = [&](uint32_t x) -> uint32_t {
         if (x >= n) {
@@ -3000,7 +3013,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
         if (first) {
         roots[rank] = A;
         roots_a1[rank] = A1;
-        roots_h[rank] = hA;
+        if (!SLICE) roots_h[rank] = hA;
     }
         if (valid) ridx[t] = (uint16_t)(incl - 1);
         __syncthreads();
@@ -3008,8 +3021,8 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
         nroots = nr;
         if ((uint32_t)t < nr) {
             const uint32_t R = roots[t];
-            const HT hR = late_e0 ? hiw(R) : roots_h[t];
-            if (late_e0) roots_h[t] = hR;
+            const HT hR = (SLICE || late_e0) ? hiw(R) : roots_h[t];
+            if (!SLICE && late_e0) roots_h[t] = hR;
             uint32_t *wr = win + t * WS;
             uint32_t wbad = 0;
             // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
@@ -3053,7 +3066,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
             const uint32_t rx = ridx[t];
             bad += win[rx * WS + WC];
             if (late_e0) {
-                const uint32_t e0 = enc(p, hp, i, A, roots_h[rx]);
+                const uint32_t e0 = enc(p, hp, i, A, SLICE ? hiw(A) : roots_h[rx]);
                 e0s[t] = e0;
                 bad += 2 * (e0 == CZ_NONE);
             }
@@ -3090,7 +3103,8 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
                 // W1 only now: the window phase held one window per lane (fewer
                 // live registers), at the price of a second dependent chain
                 if ((uint32_t)t < nroots)
-                    win[t * WS + WC] = w1_window(t, roots[t], roots_h[t], win + t * WS, nullptr);
+                    win[t * WS + WC] = w1_window(t, roots[t], SLICE ? hiw(roots[t]) : roots_h[t],
+                                                 win + t * WS, nullptr);
                 __syncthreads();
                 if (valid) bad += win[ridx[t] * WS + WC];
             } else if ((uint32_t)t < nroots) {
@@ -3214,6 +3228,8 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             CX_ROOTS_LAUNCH(1, 6);
         else if (split == 5)
             CX_ROOTS_LAUNCH(2, 6);
+        else if (split == 6)
+            CX_ROOTS_LAUNCH(2, 8);
         else
             CX_ROOTS_LAUNCH(1, 4);
 #undef CX_ROOTS_LAUNCH
