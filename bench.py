@@ -283,10 +283,13 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
                     "(checked on every rank)"}
 
 
-def churn_leg(ring, dev):
+def churn_leg(ring, keys, src, dev, depth_ab=28):
     """1 % joins + 1 % leaves of the bench ring -> route-ready, twice: cold (the
-    new ring's 72 GiB of tables are fresh HBM) and warm (the table pool hands
-    back the first new ring's blocks, as every later membership epoch gets)."""
+    new ring's tables are fresh HBM) and warm (the table pool hands back the
+    first new ring's blocks, as every later membership epoch gets).  Then the
+    same at a shallower route table (`depth_ab` levels instead of the default
+    32, cxi_set_route_depth) and the per-launch cost of that trade: the bench's
+    own keys routed on both warm rings in interleaved rounds (results equal)."""
     N = ring.n
     nj = N // 100
     joins = torch.empty((nj, 2), dtype=torch.int64, device=dev)
@@ -296,36 +299,86 @@ def churn_leg(ring, dev):
     leaves = ring.ids_device()[pick].contiguous()
     out = {}
     hashes = []
-    for phase in ("cold", "warm"):
+    warm = {}
+
+    def epoch(depth):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         new, _ = ring.churn(joins, leaves)
         new.sync()
         t1 = time.perf_counter()
+        if depth:
+            new.set_route_depth(depth)
         new.build_fingers()
         new.sync()
         t2 = time.perf_counter()
+        return new, {"route_ready_ms": (t2 - t0) * 1e3, "churn_ms": (t1 - t0) * 1e3,
+                     "fingers_and_table_ms": (t2 - t1) * 1e3}
+
+    for phase in ("cold", "warm"):
+        new, out[phase] = epoch(0)
         hashes.append(new.route_table_hash())
-        out[phase] = {"route_ready_ms": (t2 - t0) * 1e3, "churn_ms": (t1 - t0) * 1e3,
-                      "fingers_and_table_ms": (t2 - t1) * 1e3}
         if phase == "warm":
             q = 1 << 22
-            keys = torch.empty((q, 2), dtype=torch.int64, device=dev)
-            chordx.fill_splitmix(keys, SEED_KEYS + 0x100)
-            src = (torch.arange(q, device=dev, dtype=torch.int64) % new.n).to(torch.int32)
-            o, h, s = new.route(src, keys)
-            out["new_ring_route_equals_successor"] = bool((o == new.successor(keys)).all().item()) \
-                and int((s != 0).sum().item()) == 0
+            k2 = torch.empty((q, 2), dtype=torch.int64, device=dev)
+            chordx.fill_splitmix(k2, SEED_KEYS + 0x100)
+            s2 = (torch.arange(q, device=dev, dtype=torch.int64) % new.n).to(torch.int32)
+            o, h, st = new.route(s2, k2)
+            out["new_ring_route_equals_successor"] = bool((o == new.successor(k2)).all().item()) \
+                and int((st != 0).sum().item()) == 0
             out["new_ring_peers"] = new.n
-        new.close()
-        del new
+            warm[0] = new
+        else:
+            new.close()
+            del new
     out["table_hash_equal"] = hashes[0] == hashes[1]
     out["route_ready_ms"] = {"cold": out["cold"]["route_ready_ms"],
                              "warm": out["warm"]["route_ready_ms"]}
+    # shallower table: route-ready and the per-launch cost on the bench's keys
+    sub = {}
+    if depth_ab:
+        new, sub["cold"] = epoch(depth_ab)
+        new.close()
+        del new
+        warm[depth_ab], sub["warm"] = epoch(depth_ab)
+        Q = keys.shape[0]
+        res = {d: (torch.empty(Q, dtype=torch.int32, device=dev),
+                   torch.empty(Q, dtype=torch.uint8, device=dev),
+                   torch.empty(Q, dtype=torch.uint8, device=dev)) for d in warm}
+        srcw = (src.to(torch.int64) % warm[0].n).to(torch.int32)
+        for d in warm:
+            warm[d].route(srcw, keys, out=res[d])
+        ms = {d: [] for d in warm}
+        stream = torch.cuda.current_stream(dev)
+        for k in range(6):
+            for d in (list(warm) if k % 2 == 0 else list(warm)[::-1]):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(3):
+                    warm[d].route(srcw, keys, out=res[d])
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                ms[d].append(e0.elapsed_time(e1) / 3)
+        same = all(bool((res[d][0] == res[0][0]).all().item()) and
+                   bool((res[d][1] == res[0][1]).all().item()) and
+                   int((res[d][2] != 0).sum().item()) == 0 for d in warm)
+        med = {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
+        sub.update({"route_levels": depth_ab,
+                    "route_ms_median": {"default": med[0], f"R{depth_ab}": med[depth_ab]},
+                    "per_launch_cost": med[depth_ab] / med[0] - 1.0,
+                    "results_equal_default": same,
+                    "note": f"the new ring built with a {depth_ab}-level route table instead of 32 "
+                            "(cxi_set_route_depth): fewer table bytes to build, more exact hops "
+                            "below the table; route_ms = the bench's keys on the two warm new "
+                            "rings in interleaved rounds (median)"})
+        out["shallower_table"] = sub
+    for d in list(warm):
+        warm[d].close()
+    warm.clear()
     out["workload"] = (f"cx_churn of the bench ring: {nj} joins (splitmix 0x5EED0009) + {nj} "
                        "leaves (distinct peers), then cx_fingers_build (fingers + route table)")
-    out["note"] = ("cold = fresh hipMalloc'd HBM for the new ring's fingers (8 GiB) and route "
-                   "table (64 GiB at 2^24): first-touch page mapping dominates, as in "
+    out["note"] = ("cold = fresh hipMalloc'd HBM for the new ring's tables (64 GiB of route "
+                   "table at 2^24): first-touch page mapping dominates, as in "
                    "setup_s.fingers_build; warm = the table pool returns the previous epoch's "
                    "blocks (the steady state of a membership epoch)")
     return out
@@ -490,11 +543,16 @@ def main():
     # ---- churn -> route-ready (f2), cold then warm ----
     churn = None
     if not args.no_churn:
-        churn = churn_leg(ring, dev)
+        churn = churn_leg(ring, keys, src, dev)
         chordx.pool_trim()  # the new rings' blocks are not needed by the arc leg
         churn["route_ready_ms_max_over_ranks"] = {
             k: dist.max_over_ranks(v, world, dev) for k, v in churn["route_ready_ms"].items()}
         churn["table_hash_equal"] = dist.all_over_ranks(churn["table_hash_equal"], world, dev)
+        if "shallower_table" in churn:
+            st = churn["shallower_table"]
+            st["results_equal_default"] = dist.all_over_ranks(st["results_equal_default"], world, dev)
+            st["route_ready_ms_warm_max_over_ranks"] = dist.max_over_ranks(
+                st["warm"]["route_ready_ms"], world, dev)
 
     # ---- arc-sharded C4 (all_to_all-v) on the same keys and steps ----
     arc = None
