@@ -855,7 +855,8 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
     const uint32_t b = blockIdx.x, a = b * FT_P;
     const uint32_t rows = n - a < (uint32_t)FT_P ? n - a : (uint32_t)FT_P;
     const int l0 = lvl0_g[b];
-    const int lt = l0 > FT_L0 ? l0 : FT_L0;  // first tile level
+    int lt = l0 > FT_L0 ? l0 : FT_L0;  // first tile level
+    if (!F && Lft > lt) lt = Lft;  // planes only: nothing below the first plane level
     if (threadIdx.x < FT_COLS)
         s0[threadIdx.x] = threadIdx.x + FT_L0 >= (unsigned)l0 ? S0[(size_t)b * FT_COLS + threadIdx.x]
                                                              : 0u;
@@ -3190,7 +3191,11 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             const int v = e ? atoi(e) : 0;
             return (unsigned)(v > 0 && v <= 65536 ? v : 0);
         }();
-        const uint32_t Kr = K ? K : 16;
+        // chunk of 32 row-blocks x all levels (CX_CZ_CHUNK overrides): 22.6 ms
+        // against 22.8-24.6 / 24.7-24.9 / 23.8-24.5 ms for 16 / 8 / 64 at 2^24
+        // (profiles/r03/codes/chunk_summary.txt)
+        static const bool k_env = getenv("CX_CZ_CHUNK") != nullptr;
+        const uint32_t Kr = k_env ? (K ? K : 16) : 32;
         const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
