@@ -2914,13 +2914,12 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
     auto c2 = [&](uint32_t x, int l) -> uint32_t {
         return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
     };
-    uint32_t oob = 0;
+    // a finger outside the ring (never from a converged build; reported, never
+    // followed): a wave-uniform flag (scalar), not a per-lane register
+    bool oob = false;
     auto chk = [&](uint32_t x) -> uint32_t {
-        if (x >= n) {
-            oob = 1;
-            return 0u;
-        }
-        return x;
+        if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
+        return x < n ? x : 0u;
     };
     // W1 of root slot tt: A' = f(R, i - 1) relative to R (slot 0), the window
     // below A' (1..14), into o (SPLIT) or wr[15..29]; returns its CZ_NONE count
@@ -3191,11 +3190,11 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             const int v = e ? atoi(e) : 0;
             return (unsigned)(v > 0 && v <= 65536 ? v : 0);
         }();
-        // chunk of 32 row-blocks x all levels (CX_CZ_CHUNK overrides): 22.6 ms
-        // against 22.8-24.6 / 24.7-24.9 / 23.8-24.5 ms for 16 / 8 / 64 at 2^24
-        // (profiles/r03/codes/chunk_summary.txt)
-        static const bool k_env = getenv("CX_CZ_CHUNK") != nullptr;
-        const uint32_t Kr = k_env ? (K ? K : 16) : 32;
+        // chunk of 16 row-blocks x all levels (CX_CZ_CHUNK overrides).  At 7
+        // blocks per CU 32 measured best (22.6 vs 22.8-24.6 ms,
+        // profiles/r03/codes/chunk_summary.txt); at 8 blocks per CU (64 VGPRs)
+        // 16 is: 22.9 vs 24.1-24.5 ms (occ8_summary.txt)
+        const uint32_t Kr = K ? K : 16;
         const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
         const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
         if (blocks >= (1ull << 31)) return hipErrorInvalidValue;

@@ -22,10 +22,9 @@ k={r['Name'][:20]: round(float(r['AverageNs'])/1e6,3) for r in csv.DictReader(op
 print('$name', k, 'hash', d['route_table_hash'], 'route_ok', d.get('route_ok'), 'wall', [round(x*1e3,1) for x in d['fingers_and_table_s']])"
 }
 for pass in a b; do
-  run k16_$pass X=0
-  run k8_$pass CX_CZ_CHUNK=8
-  run k32_$pass CX_CZ_CHUNK=32
-  run k64_$pass CX_CZ_CHUNK=64
+  run default_$pass X=0
+  run k16_$pass CX_CZ_CHUNK=16
+  run hi_$pass CX_CZ_CODES=hi
 done
 cd "$R"
 timeout -k 10 200 python3 benches/bench_ready.py 24 6 > "$OUT/ready.json" 2> "$OUT/ready.err"
