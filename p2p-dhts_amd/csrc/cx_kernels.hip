@@ -838,6 +838,10 @@ __global__ __launch_bounds__(256) void k_fingers_plan(SearchView sv, const cell1
         S0[(size_t)b * FT_COLS + lane] = dir_successor(sv, ld128(ring + a) + ((u128)1 << i));
 }
 
+// ROWS = false (F null, planes only): every search result goes straight to its
+// level plane (coalesced across the wave's rows) instead of through the 21-KB
+// row tile, so the block's LDS is the window keys alone (more blocks per CU).
+template <bool ROWS>
 __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell128 *ring,
                                                       const uint32_t *ring_key, int kb,
                                                       const uint8_t *glog_g, const uint8_t *lvl0_g,
@@ -846,7 +850,7 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
     constexpr int LPW = FT_CH / 4;    // levels per wave per chunk
     constexpr int EPL = FT_W / 64;    // window elements per lane per level
     static_assert(EPL * 64 == FT_W && LPW * 4 == FT_CH, "window geometry");
-    __shared__ uint32_t tile[FT_P * FT_ROW];
+    __shared__ uint32_t tile[ROWS ? FT_P * FT_ROW : 1];
     __shared__ uint32_t win[4][LPW][256];  // per wave: 32-bit window keys, padded with ~0
     __shared__ uint32_t s0[FT_COLS];
     __shared__ uint8_t glog[FT_P];
@@ -948,7 +952,13 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const uint32_t r = lane + 64 * k;
-                if (r >= rows || i <= glog[r]) continue;  // next peer: filled at write-back
+                if (r >= rows) continue;
+                if (i <= glog[r]) {  // next peer: filled at write-back (rows) / now (planes)
+                    if (!ROWS && i >= Lft)
+                        __builtin_nontemporal_store(a + r + 1 == n ? 0u : a + r + 1,
+                                                    FT + (size_t)(i - Lft) * n + a + r);
+                    continue;
+                }
                 uint32_t f = CX_NONE;
                 const uint32_t jj = j[q][k];
                 if (aok && jj < FT_W && w[jj] != cp[k]) {
@@ -957,16 +967,29 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
                 }
                 if (f == CX_NONE)  // tie on the key / past the window / no arc
                     f = dir_successor(sv, idp[k] + ((u128)1 << i));
-                tile[r * FT_ROW + (i - FT_L0)] = f;
+                if (ROWS)
+                    tile[r * FT_ROW + (i - FT_L0)] = f;
+                else if (i >= Lft)
+                    __builtin_nontemporal_store(f, FT + (size_t)(i - Lft) * n + a + r);
             }
         }
         __builtin_amdgcn_wave_barrier();  // searches done before the next chunk's keys
     }
+    if (!ROWS) {
+        // planes only: the levels below the block's first tile level are the
+        // next peer for every row (each gap is at least 2^(l0 - 1))
+        for (int k = threadIdx.x; k < (lt - Lft) * (int)FT_P; k += blockDim.x) {
+            const int c = k / FT_P, r = k - c * FT_P;
+            if (r >= (int)rows) continue;
+            const uint32_t p = a + r;
+            __builtin_nontemporal_store(p + 1 == n ? 0u : p + 1, FT + (size_t)c * n + p);
+        }
+        return;
+    }
     __syncthreads();
-    // write-back: 8 rows per pass, 16 B per thread, full 512-B rows (F null:
-    // planes only -- the row-major table is materialised later, on demand)
+    // write-back: 8 rows per pass, 16 B per thread, full 512-B rows
     const int chunk = threadIdx.x & 31;
-    for (int r = threadIdx.x >> 5; F && r < (int)rows; r += 8) {
+    for (int r = threadIdx.x >> 5; r < (int)rows; r += 8) {
         const uint32_t p = a + r;
         const uint32_t nx = p + 1 == n ? 0u : p + 1;
         const int g = glog[r];
@@ -1133,8 +1156,12 @@ hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32
         if (e != hipSuccess) return e;
         // planes straight from the tile when every plane level is a tile level
         const bool planes = FT && Lft >= FT_L0 && Lft < CX_FINGERS;
-        k_fingers_tile<<<nblk, 256, 0, s>>>(sv, ring, ring_key, finger_key_shift(n), glog, lvl0,
-                                            S0, F, planes ? FT : nullptr, Lft);
+        if (F)
+            k_fingers_tile<true><<<nblk, 256, 0, s>>>(sv, ring, ring_key, finger_key_shift(n), glog,
+                                                      lvl0, S0, F, planes ? FT : nullptr, Lft);
+        else
+            k_fingers_tile<false><<<nblk, 256, 0, s>>>(sv, ring, ring_key, finger_key_shift(n), glog,
+                                                       lvl0, S0, F, FT, Lft);
         if (planes_done) *planes_done = planes;
         return hipGetLastError();
     }
