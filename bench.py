@@ -283,13 +283,14 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
                     "(checked on every rank)"}
 
 
-def churn_leg(ring, keys, src, dev, depth_ab=28):
+def churn_leg(ring, keys, src, dev, depth_ab=32):
     """1 % joins + 1 % leaves of the bench ring -> route-ready, twice: cold (the
     new ring's tables are fresh HBM) and warm (the table pool hands back the
     first new ring's blocks, as every later membership epoch gets).  Then the
-    same at a shallower route table (`depth_ab` levels instead of the default
-    32, cxi_set_route_depth) and the per-launch cost of that trade: the bench's
-    own keys routed on both warm rings in interleaved rounds (results equal)."""
+    same at another route-table depth (`depth_ab` levels: 32, the default
+    before round 3 session 3, against 28 now at 2^24; cxi_set_route_depth) and
+    the per-launch time of that depth relative to the default: the bench's own
+    keys routed on both warm rings in interleaved rounds (results equal)."""
     N = ring.n
     nj = N // 100
     joins = torch.empty((nj, 2), dtype=torch.int64, device=dev)
@@ -334,7 +335,7 @@ def churn_leg(ring, keys, src, dev, depth_ab=28):
     out["table_hash_equal"] = hashes[0] == hashes[1]
     out["route_ready_ms"] = {"cold": out["cold"]["route_ready_ms"],
                              "warm": out["warm"]["route_ready_ms"]}
-    # shallower table: route-ready and the per-launch cost on the bench's keys
+    # the A/B depth: route-ready and the per-launch time on the bench's keys
     sub = {}
     if depth_ab:
         new, sub["cold"] = epoch(depth_ab)
@@ -363,21 +364,23 @@ def churn_leg(ring, keys, src, dev, depth_ab=28):
                    bool((res[d][1] == res[0][1]).all().item()) and
                    int((res[d][2] != 0).sum().item()) == 0 for d in warm)
         med = {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
-        sub.update({"route_levels": depth_ab,
-                    "route_ms_median": {"default": med[0], f"R{depth_ab}": med[depth_ab]},
-                    "per_launch_cost": med[depth_ab] / med[0] - 1.0,
+        r_def = warm[0].route_info()[2] // (warm[0].n * 128)
+        sub.update({"route_levels": depth_ab, "route_levels_default": r_def,
+                    "route_ms_median": {f"default_R{r_def}": med[0], f"R{depth_ab}": med[depth_ab]},
+                    "per_launch_vs_default": med[depth_ab] / med[0] - 1.0,
                     "results_equal_default": same,
-                    "note": f"the new ring built with a {depth_ab}-level route table instead of 32 "
-                            "(cxi_set_route_depth): fewer table bytes to build, more exact hops "
-                            "below the table; route_ms = the bench's keys on the two warm new "
-                            "rings in interleaved rounds (median)"})
-        out["shallower_table"] = sub
+                    "note": f"the new ring built with a {depth_ab}-level route table instead of "
+                            f"the default {r_def} (cxi_set_route_depth): a deeper table is more "
+                            "bytes to build and fewer exact hops below it; route_ms = the "
+                            "bench's keys on the two warm new rings in interleaved rounds "
+                            "(median; the ring built first tends to route ~2 % slower)"})
+        out["table_depth_ab"] = sub
     for d in list(warm):
         warm[d].close()
     warm.clear()
     out["workload"] = (f"cx_churn of the bench ring: {nj} joins (splitmix 0x5EED0009) + {nj} "
                        "leaves (distinct peers), then cx_fingers_build (fingers + route table)")
-    out["note"] = ("cold = fresh hipMalloc'd HBM for the new ring's tables (64 GiB of route "
+    out["note"] = ("cold = fresh hipMalloc'd HBM for the new ring's tables (56 GiB of route "
                    "table at 2^24): first-touch page mapping dominates, as in "
                    "setup_s.fingers_build; warm = the table pool returns the previous epoch's "
                    "blocks (the steady state of a membership epoch)")
@@ -548,8 +551,8 @@ def main():
         churn["route_ready_ms_max_over_ranks"] = {
             k: dist.max_over_ranks(v, world, dev) for k, v in churn["route_ready_ms"].items()}
         churn["table_hash_equal"] = dist.all_over_ranks(churn["table_hash_equal"], world, dev)
-        if "shallower_table" in churn:
-            st = churn["shallower_table"]
+        if "table_depth_ab" in churn:
+            st = churn["table_depth_ab"]
             st["results_equal_default"] = dist.all_over_ranks(st["results_equal_default"], world, dev)
             st["route_ready_ms_warm_max_over_ranks"] = dist.max_over_ranks(
                 st["warm"]["route_ready_ms"], world, dev)
@@ -632,7 +635,7 @@ def main():
             "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring,
                         "fingers_build": t_fing, "fingers_build_again": t_fing_warm,
                         "note": "fingers_build = converged fingers + route table on fresh "
-                                "HBM (first touch of 72 GiB); fingers_build_again = the same "
+                                "HBM (first touch of 64 GiB); fingers_build_again = the same "
                                 "build into the now-mapped tables"},
             "ab_variants": "benches/bench_route.py --variants (route and search A/B kernels)",
         })
