@@ -373,7 +373,7 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
                             f"the default {r_def} (cxi_set_route_depth): a deeper table is more "
                             "bytes to build and fewer exact hops below it; route_ms = the "
                             "bench's keys on the two warm new rings in interleaved rounds "
-                            "(median; the ring built first tends to route ~2 % slower)"})
+                            "(median; two rings of one depth differ by up to ~2 % with where their tables land, DESIGN.md 4.3)"})
         out["table_depth_ab"] = sub
     for d in list(warm):
         warm[d].close()

@@ -684,6 +684,12 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
             if (r->route_variant < 0) r->cz_failed = true;  // automatic: use variant 4
         }
         if (r->d_cz) {
+            // CX_DEBUG_TABLE_VA: the table's address on stderr (placement probes)
+            static const bool dbg_va = getenv("CX_DEBUG_TABLE_VA") != nullptr;
+            if (dbg_va)
+                fprintf(stderr, "cx: route table %p (%zu B, offset in 1 GiB %zu, in 2 MiB %zu)\n",
+                        (void *)r->d_cz, ent * 128, (size_t)(uintptr_t)r->d_cz & ((1ull << 30) - 1),
+                        (size_t)(uintptr_t)r->d_cz & ((1ull << 21) - 1));
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
             DBuf ft, hi, c2;
             cxk::FingerView fv;
