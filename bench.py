@@ -349,14 +349,20 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
         srcw = (src.to(torch.int64) % warm[0].n).to(torch.int32)
         for d in warm:
             warm[d].route(srcw, keys, out=res[d])
-        ms = {d: [] for d in warm}
+        # the bench ring itself routes the same keys in the same rounds ("bench"):
+        # separates where a ring's tables landed from the headline loop's conditions
+        res_b = tuple(torch.empty_like(x) for x in res[0])
+        ms = {d: [] for d in list(warm) + ["bench"]}
         stream = torch.cuda.current_stream(dev)
         for k in range(6):
-            for d in (list(warm) if k % 2 == 0 else list(warm)[::-1]):
+            for d in (list(ms) if k % 2 == 0 else list(ms)[::-1]):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(3):
-                    warm[d].route(srcw, keys, out=res[d])
+                    if d == "bench":
+                        ring.route(src, keys, out=res_b)
+                    else:
+                        warm[d].route(srcw, keys, out=res[d])
                 e1.record(stream)
                 torch.cuda.synchronize(dev)
                 ms[d].append(e0.elapsed_time(e1) / 3)
@@ -366,7 +372,8 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
         med = {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
         r_def = warm[0].route_info()[2] // (warm[0].n * 128)
         sub.update({"route_levels": depth_ab, "route_levels_default": r_def,
-                    "route_ms_median": {f"default_R{r_def}": med[0], f"R{depth_ab}": med[depth_ab]},
+                    "route_ms_median": {f"default_R{r_def}": med[0], f"R{depth_ab}": med[depth_ab],
+                                        "bench_ring": med["bench"]},
                     "per_launch_vs_default": med[depth_ab] / med[0] - 1.0,
                     "results_equal_default": same,
                     "note": f"the new ring built with a {depth_ab}-level route table instead of "
