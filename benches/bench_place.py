@@ -70,6 +70,19 @@ def main():
     rec["after_replacing_r1"] = timed(rings, outs, src, keys, rounds, reps)
     same = same and bool((outs["r3"][0] == outs["r2"][0]).all()) and bool((outs["r3"][1] == outs["r2"][1]).all())
     rec["identical_results"] = same
+    # a ring made by the churn path (one join, one leave: same size, near-identical
+    # IDs) beside the fresh ones: is it the construction path, not the build order?
+    j = torch.empty((1, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(j, 0x5EED0777)
+    lv = rings["r2"].ids_device()[12345:12346].contiguous()
+    ch, _ = rings["r2"].churn(j, lv)
+    ch.build_fingers()
+    rings["churned"] = ch
+    outs["churned"] = tuple(torch.empty_like(x) for x in outs["r2"])
+    for _ in range(3):
+        ch.route(src, keys, out=outs["churned"])
+    torch.cuda.synchronize()
+    rec["with_churned"] = timed(rings, outs, src, keys, rounds, reps)
     rec["pool"] = chordx.pool_info() if hasattr(chordx, "pool_info") else None
     print(json.dumps(rec), flush=True)
 
