@@ -57,6 +57,15 @@ def main():
             r.route(src, keys, out=o)
         return r, o
 
+    # PLACE_DUMMY=1: a 1000-peer ring made first and kept alive takes the
+    # process's first ring stream (and first small blocks); r1 then gets the
+    # second stream, as r2 does without it
+    dummy = None
+    if os.environ.get("PLACE_DUMMY"):
+        dids = torch.empty((1000, 2), dtype=torch.int64, device="cuda")
+        chordx.fill_splitmix(dids, 0x5EED0999)
+        dummy = chordx.Ring(dids)
+        dummy.build_fingers()
     rings, outs = {}, {}
     rings["r1"], outs["r1"] = make()
     rings["r2"], outs["r2"] = make()
@@ -84,6 +93,7 @@ def main():
     torch.cuda.synchronize()
     rec["with_churned"] = timed(rings, outs, src, keys, rounds, reps)
     rec["pool"] = chordx.pool_info() if hasattr(chordx, "pool_info") else None
+    rec["dummy_first"] = dummy is not None
     print(json.dumps(rec), flush=True)
 
 
