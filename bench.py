@@ -350,7 +350,7 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
         for d in warm:
             warm[d].route(srcw, keys, out=res[d])
         # the bench ring itself routes the same keys in the same rounds ("bench"):
-        # separates where a ring's tables landed from the headline loop's conditions
+        # separates that ring's speed from the headline loop's conditions
         res_b = tuple(torch.empty_like(x) for x in res[0])
         ms = {d: [] for d in list(warm) + ["bench"]}
         stream = torch.cuda.current_stream(dev)
@@ -380,7 +380,7 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
                             f"the default {r_def} (cxi_set_route_depth): a deeper table is more "
                             "bytes to build and fewer exact hops below it; route_ms = the "
                             "bench's keys on the two warm new rings in interleaved rounds "
-                            "(median; two rings of one depth differ by up to ~2 % with where their tables land, DESIGN.md 4.3)"})
+                            "(median; rings of one depth in one process differ by up to ~3 %, which ring varies, DESIGN.md 4.3)"})
         out["table_depth_ab"] = sub
     for d in list(warm):
         warm[d].close()
