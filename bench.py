@@ -18,8 +18,15 @@ traffic.  After the timed region the same run measures, on every rank:
            with the replicated route;
   churn    1 % joins + 1 % leaves of the bench ring (seed 0x5EED0009) ->
            route-ready (merge churn + fingers + route table), cold (fresh HBM)
-           then warm (table pool), with the two tables' hashes compared;
-  cpu      the reference-faithful CPU walk (oracle/, rank 0, every world size).
+           then warm (table pool), with the two tables' hashes compared and
+           each epoch's allocation path (fresh / pooled bytes, trims,
+           retries); then the 28- against the 32-level table in ABBA order;
+  cpu      the reference-faithful CPU walk (oracle/, rank 0, every world size),
+           with the hop histogram of its sample;
+  c5       BASELINE config C5 (DHash n = 14 lists + misplaced scan of 2^26 keys
+           after a 1 %/1 % churn of a second 2^24 ring), after the bench ring
+           is closed: one cx_dhash_maintenance pass per step, keys sharded
+           over ranks (strong scaling), parity against the oracle on a sample.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -70,6 +77,14 @@ GRANULE = 64  # one dependent random gather
 # SURVEY 8(d) reference-work model: 25 B streamed + 64 B source-peer record +
 # 128 B per hop (finger granule + ring granule).
 REF_STREAM, REF_SRC, REF_HOP = 25, 64, 128
+# C5 (configs[4]): a second ring and key stream (SURVEY 8d seeds)
+SEED_C5_RING, SEED_C5_KEYS = 0x5EED0007, 0x5EED0008
+C5_N = 14
+# cx_dhash_maintenance per key: key 16 + one 64-B search line + old 14-list 56
+# + count 1 + new 14-list 56 + count 1 + mask 2 + targets 14
+C5_BYTES_STREAM = 210
+# SURVEY 8(d)'s DHash model: 16 + 64 + 56 + 1 + 2 per key
+C5_BYTES_SURVEY = 139
 
 
 def parse():
@@ -84,6 +99,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-arc", action="store_true", help="skip the arc-sharded sub-record")
     ap.add_argument("--no-churn", action="store_true", help="skip the churn -> route-ready leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 DHash maintenance leg")
+    ap.add_argument("--c5-keys-log2", type=int, default=26, help="C5 keys (all ranks)")
+    ap.add_argument("--c5-oracle-keys", type=int, default=1 << 20,
+                    help="C5 keys checked against the oracle (rank 0)")
     ap.add_argument("--mode", choices=("replicated", "arc"), default="replicated",
                     help="replicated: every rank holds the whole route table and routes its "
                          "own keys (default; the arc layout is still measured as the `arc` "
@@ -146,10 +165,13 @@ def cpu_baseline(ring_np, F_host, keys_np, src_np, gpu_owner, gpu_hops, budget_s
     _, dt1 = timed(q1, 1)
     qa = int(min(len(keys_np), max(q1, budget_s * 2 / 3 * threads / max(per1, 1e-9))))
     (wo, wh, ws), dta = timed(qa, threads)
-    ok = None
+    ok = hist_ok = None
+    hist = np.bincount(wh, minlength=1).tolist()
     if gpu_owner is not None:
         ok = bool((wo == gpu_owner[:qa]).all() and (wh == gpu_hops[:qa]).all() and (ws == 0).all())
+        hist_ok = hist == np.bincount(gpu_hops[:qa], minlength=1).tolist()
     return {"value": qa / dta, "unit": "lookups/s", "cores": threads, "kind": "port",
+            "hops_hist": hist, "hist_equal": hist_ok,
             "value_1core": q1 / dt1,
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "n_gpus_beside": world,
@@ -250,8 +272,12 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
     from chordx.arc import ArcRouter
     Q = keys.shape[0]
     t0 = time.perf_counter()
+    # N = 1: a one-rank group (RCCL) and exchange_always, so the leg runs and
+    # times the general path -- partition, exchange, walk, exchange back,
+    # delivery -- that N ranks run, not the in-place walk
+    single = world == 1 and dist.init_single(backend, dev if backend == "nccl" else None)
     router = ArcRouter(ring, ring.n, rank, world,
-                       comm_device="cpu" if backend == "gloo" else None)
+                       comm_device="cpu" if backend == "gloo" else None, exchange_always=True)
     torch.cuda.synchronize(dev)
     t_build = time.perf_counter() - t0
     top, rows, plane_bytes = ring.arc_info()
@@ -269,7 +295,12 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
         and int((status != 0).sum().item()) == 0
     same = dist.all_over_ranks(same, world, dev)
     total = world * Q * args.steps
+    group = torch.distributed.get_backend() if torch.distributed.is_initialized() else None
+    if single:
+        torch.distributed.destroy_process_group()
     return {"value": total / dt_max, "unit": "lookups/s", "ms_per_step": dt_max * 1e3 / args.steps,
+            "process_group": {"backend": group, "world": world,
+                              "one_rank_group": bool(single)},
             "per_gpu_lookups_per_s": total / dt_max / world,
             "records_exchanged_per_lookup": sent / total,
             "rounds_per_step": router.rounds,
@@ -278,19 +309,48 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
             "route_plane_bytes_per_gpu": plane_bytes, "build_s": t_build,
             "layout": f"ring IDs all-gathered; arc-sharded route planes x{world} (top {top} "
                       "levels replicated, lower levels for the arc + halo); key-first SoA "
-                      "all_to_all-v (20 B out, 8 B back per remote lookup), pipelined pieces",
+                      "all_to_all-v with origin-resolved source hints (28 B out, 8 B back per "
+                      "lookup), single-pass region partition, pipelined pieces; at N = 1 the "
+                      "rank exchanges with itself through a one-rank RCCL group",
             "note": "owner, hops and status of every lookup equal the replicated route's "
                     "(checked on every rank)"}
 
 
+def _route_rounds(rings, keys, srcs, dev, rounds=6, per=3):
+    """Median per-launch ms of each ring routing the same keys, in interleaved
+    rounds (order reversed every other round); rings: {name: (ring, out)}."""
+    ms = {d: [] for d in rings}
+    stream = torch.cuda.current_stream(dev)
+    for k in range(rounds):
+        for d in (list(ms) if k % 2 == 0 else list(ms)[::-1]):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            r, out = rings[d]
+            e0.record(stream)
+            for _ in range(per):
+                r.route(srcs[d], keys, out=out)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms[d].append(e0.elapsed_time(e1) / per)
+    return {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
+
+
 def churn_leg(ring, keys, src, dev, depth_ab=32):
-    """1 % joins + 1 % leaves of the bench ring -> route-ready, twice: cold (the
-    new ring's tables are fresh HBM) and warm (the table pool hands back the
-    first new ring's blocks, as every later membership epoch gets).  Then the
-    same at another route-table depth (`depth_ab` levels: 32, the default
-    before round 3 session 3, against 28 now at 2^24; cxi_set_route_depth) and
-    the per-launch time of that depth relative to the default: the bench's own
-    keys routed on both warm rings in interleaved rounds (results equal)."""
+    """1 % joins + 1 % leaves of the bench ring -> route-ready.  Every epoch
+    states its allocation path: the table pool's counters around it
+    (chordx.pool_stats: bytes fresh from hipMalloc -- first-touch page
+    mapping --, bytes handed back by the pool, idle blocks trimmed to retry a
+    failed allocation, retries).  The pool is trimmed first, so the first
+    epoch of each depth is cold (fresh HBM) and the second warm (the pool
+    returns the first one's blocks, as every later membership epoch gets).
+
+    Default depth: cold, warm; the two tables' hashes must be equal and the
+    warm ring routes 2^22 keys to their exact successors.  Then the depth A/B
+    (default R against `depth_ab` levels, cxi_set_route_depth) in ABBA order,
+    so neither depth is always the one built first: order AB keeps the warm
+    default ring and builds a `depth_ab` ring (cold, then warm) beside it;
+    order BA closes both, builds `depth_ab` first and the default second.  In
+    each order the two rings (and the bench ring) route the bench's keys in
+    interleaved rounds; `per_launch_vs_default` is the mean over both orders."""
     N = ring.n
     nj = N // 100
     joins = torch.empty((nj, 2), dtype=torch.int64, device=dev)
@@ -299,11 +359,11 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
     pick = (torch.arange(nj, device=dev, dtype=torch.int64) * 0x9E3779B1) % N
     leaves = ring.ids_device()[pick].contiguous()
     out = {}
-    hashes = []
-    warm = {}
+    epochs = []
 
-    def epoch(depth):
+    def epoch(depth, label):
         torch.cuda.synchronize(dev)
+        st0 = chordx.pool_stats()
         t0 = time.perf_counter()
         new, _ = ring.churn(joins, leaves)
         new.sync()
@@ -313,84 +373,229 @@ def churn_leg(ring, keys, src, dev, depth_ab=32):
         new.build_fingers()
         new.sync()
         t2 = time.perf_counter()
-        return new, {"route_ready_ms": (t2 - t0) * 1e3, "churn_ms": (t1 - t0) * 1e3,
-                     "fingers_and_table_ms": (t2 - t1) * 1e3}
+        alloc = chordx.pool_stats_delta(st0, chordx.pool_stats())
+        rec = {"epoch": label, "route_ready_ms": (t2 - t0) * 1e3, "churn_ms": (t1 - t0) * 1e3,
+               "fingers_and_table_ms": (t2 - t1) * 1e3,
+               "route_levels": new.route_info()[2] // (new.n * 128),
+               "alloc": {"fresh_GiB": alloc["fresh_bytes"] / 2**30,
+                         "fresh_allocs": alloc["fresh_allocs"],
+                         "pooled_GiB": alloc["reused_bytes"] / 2**30,
+                         "pooled_allocs": alloc["reused_allocs"],
+                         "trimmed_blocks": alloc["trims"],
+                         "trimmed_GiB": alloc["trimmed_bytes"] / 2**30,
+                         "retries": alloc["retries"], "failures": alloc["failures"]}}
+        rec["alloc"]["path"] = ("trim-and-retry" if alloc["retries"] else
+                                "fresh hipMalloc" if alloc["fresh_bytes"] > alloc["reused_bytes"]
+                                else "pool reuse")
+        epochs.append(rec)
+        return new, rec
 
-    for phase in ("cold", "warm"):
-        new, out[phase] = epoch(0)
-        hashes.append(new.route_table_hash())
-        if phase == "warm":
-            q = 1 << 22
-            k2 = torch.empty((q, 2), dtype=torch.int64, device=dev)
-            chordx.fill_splitmix(k2, SEED_KEYS + 0x100)
-            s2 = (torch.arange(q, device=dev, dtype=torch.int64) % new.n).to(torch.int32)
-            o, h, st = new.route(s2, k2)
-            out["new_ring_route_equals_successor"] = bool((o == new.successor(k2)).all().item()) \
-                and int((st != 0).sum().item()) == 0
-            out["new_ring_peers"] = new.n
-            warm[0] = new
-        else:
-            new.close()
-            del new
-    out["table_hash_equal"] = hashes[0] == hashes[1]
+    chordx.pool_trim()
+    new, out["cold"] = epoch(0, "default cold")
+    h_cold = new.route_table_hash()
+    new.close()
+    del new
+    a1, out["warm"] = epoch(0, "default warm")
+    out["table_hash_equal"] = h_cold == a1.route_table_hash()
+    q = 1 << 22
+    k2 = torch.empty((q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(k2, SEED_KEYS + 0x100)
+    s2 = (torch.arange(q, device=dev, dtype=torch.int64) % a1.n).to(torch.int32)
+    o, h, st = a1.route(s2, k2)
+    out["new_ring_route_equals_successor"] = bool((o == a1.successor(k2)).all().item()) \
+        and int((st != 0).sum().item()) == 0
+    out["new_ring_peers"] = a1.n
+    del k2, s2, o, h, st
     out["route_ready_ms"] = {"cold": out["cold"]["route_ready_ms"],
                              "warm": out["warm"]["route_ready_ms"]}
-    # the A/B depth: route-ready and the per-launch time on the bench's keys
-    sub = {}
+    r_def = out["warm"]["route_levels"]
+
     if depth_ab:
-        new, sub["cold"] = epoch(depth_ab)
+        sub = {"route_levels": depth_ab, "route_levels_default": r_def}
+        Q = keys.shape[0]
+        srcw = (src.to(torch.int64) % a1.n).to(torch.int32)
+
+        def outs():
+            return (torch.empty(Q, dtype=torch.int32, device=dev),
+                    torch.empty(Q, dtype=torch.uint8, device=dev),
+                    torch.empty(Q, dtype=torch.uint8, device=dev))
+
+        # order AB: the warm default ring (built first) beside a depth_ab ring
+        new, sub["cold"] = epoch(depth_ab, f"R{depth_ab} cold")
         new.close()
         del new
-        warm[depth_ab], sub["warm"] = epoch(depth_ab)
-        Q = keys.shape[0]
-        res = {d: (torch.empty(Q, dtype=torch.int32, device=dev),
-                   torch.empty(Q, dtype=torch.uint8, device=dev),
-                   torch.empty(Q, dtype=torch.uint8, device=dev)) for d in warm}
-        srcw = (src.to(torch.int64) % warm[0].n).to(torch.int32)
-        for d in warm:
-            warm[d].route(srcw, keys, out=res[d])
-        # the bench ring itself routes the same keys in the same rounds ("bench"):
-        # separates that ring's speed from the headline loop's conditions
-        res_b = tuple(torch.empty_like(x) for x in res[0])
-        ms = {d: [] for d in list(warm) + ["bench"]}
-        stream = torch.cuda.current_stream(dev)
-        for k in range(6):
-            for d in (list(ms) if k % 2 == 0 else list(ms)[::-1]):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for _ in range(3):
-                    if d == "bench":
-                        ring.route(src, keys, out=res_b)
-                    else:
-                        warm[d].route(srcw, keys, out=res[d])
-                e1.record(stream)
-                torch.cuda.synchronize(dev)
-                ms[d].append(e0.elapsed_time(e1) / 3)
-        same = all(bool((res[d][0] == res[0][0]).all().item()) and
-                   bool((res[d][1] == res[0][1]).all().item()) and
-                   int((res[d][2] != 0).sum().item()) == 0 for d in warm)
-        med = {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
-        r_def = warm[0].route_info()[2] // (warm[0].n * 128)
-        sub.update({"route_levels": depth_ab, "route_levels_default": r_def,
-                    "route_ms_median": {f"default_R{r_def}": med[0], f"R{depth_ab}": med[depth_ab],
-                                        "bench_ring": med["bench"]},
-                    "per_launch_vs_default": med[depth_ab] / med[0] - 1.0,
-                    "results_equal_default": same,
-                    "note": f"the new ring built with a {depth_ab}-level route table instead of "
-                            f"the default {r_def} (cxi_set_route_depth): a deeper table is more "
-                            "bytes to build and fewer exact hops below it; route_ms = the "
-                            "bench's keys on the two warm new rings in interleaved rounds "
-                            "(median; rings of one depth in one process differ by up to ~3 %, which ring varies, DESIGN.md 4.3)"})
+        b1, sub["warm"] = epoch(depth_ab, f"R{depth_ab} warm")
+        ra, rb, rbench = outs(), outs(), outs()
+        med_ab = _route_rounds({"A": (a1, ra), "B": (b1, rb), "bench": (ring, rbench)}, keys,
+                               {"A": srcw, "B": srcw, "bench": src}, dev)
+        same = bool((ra[0] == rb[0]).all().item()) and bool((ra[1] == rb[1]).all().item()) \
+            and int((ra[2] != 0).sum().item()) == 0 and int((rb[2] != 0).sum().item()) == 0
+        a1.close()
+        b1.close()
+        del a1, b1
+        # order BA: depth_ab first, then the default
+        b2, _ = epoch(depth_ab, f"R{depth_ab} (order BA, first)")
+        a2, _ = epoch(0, "default (order BA, second)")
+        med_ba = _route_rounds({"B": (b2, rb), "A": (a2, ra), "bench": (ring, rbench)}, keys,
+                               {"A": srcw, "B": srcw, "bench": src}, dev)
+        same = same and bool((ra[0] == rb[0]).all().item()) and \
+            bool((ra[1] == rb[1]).all().item()) and int((ra[2] != 0).sum().item()) == 0
+        b2.close()
+        a2.close()
+        del b2, a2, ra, rb, rbench
+        d_ab = med_ab["B"] / med_ab["A"] - 1.0
+        d_ba = med_ba["B"] / med_ba["A"] - 1.0
+        sub.update({
+            "route_ms_median": {
+                "order_AB": {f"default_R{r_def}": med_ab["A"], f"R{depth_ab}": med_ab["B"],
+                             "bench_ring": med_ab["bench"]},
+                "order_BA": {f"R{depth_ab}": med_ba["B"], f"default_R{r_def}": med_ba["A"],
+                             "bench_ring": med_ba["bench"]}},
+            "per_launch_vs_default_by_order": {"AB": d_ab, "BA": d_ba},
+            "per_launch_vs_default": (d_ab + d_ba) / 2,
+            "results_equal_default": same,
+            "note": f"R{depth_ab} against the default R{r_def}: a deeper table is more bytes to "
+                    "build and fewer exact hops below it.  ABBA: in order AB the default ring "
+                    f"is built first, in order BA the R{depth_ab} ring; per_launch_vs_default "
+                    "(< 0: the deeper table routes faster) is the mean of the two orders, which "
+                    "cancels a build-order effect"})
         out["table_depth_ab"] = sub
-    for d in list(warm):
-        warm[d].close()
-    warm.clear()
+    else:
+        a1.close()
+        del a1
+    out["epochs"] = epochs
     out["workload"] = (f"cx_churn of the bench ring: {nj} joins (splitmix 0x5EED0009) + {nj} "
                        "leaves (distinct peers), then cx_fingers_build (fingers + route table)")
-    out["note"] = ("cold = fresh hipMalloc'd HBM for the new ring's tables (56 GiB of route "
-                   "table at 2^24): first-touch page mapping dominates, as in "
-                   "setup_s.fingers_build; warm = the table pool returns the previous epoch's "
-                   "blocks (the steady state of a membership epoch)")
+    out["note"] = ("cold = the first epoch of a depth after cx_pool_trim (its tables are fresh "
+                   "hipMalloc'd HBM: first-touch page mapping); warm = the table pool returns "
+                   "the previous epoch's blocks (the steady state of a membership epoch); each "
+                   "epoch's `alloc` states the path its allocations took")
+    return out
+
+
+def c5_leg(args, world, rank, dev, backend):
+    """BASELINE config C5 (configs[4]): a 2^24-peer ring (splitmix 0x5EED0007),
+    1 % joins (0x5EED0009) + 1 % leaves (distinct peers), and 2^26 keys
+    (0x5EED0008) sharded over ranks (strong scaling: rank r scans
+    [r Q / N, (r + 1) Q / N)).  One step = cx_dhash_maintenance: each key's
+    n = 14 successor list on the old ring (DHashPeer placement,
+    dhash_peer.cpp:103-129) and the global-maintenance misplaced scan against
+    the new ring (RunGlobalMaintenance, dhash_peer.cpp:298-348) in one pass.
+    Old ring IDs are all-gathered and every rank applies the same churn, so
+    both rings are whole on every rank and the step needs no collective.
+    Checks: old and new lists equal the rings' 14-windows on every key
+    (reduced over ranks); on rank 0 the churned ring and map equal the
+    oracle's, and lists / counts / masks / targets equal the oracle's
+    restatement on the first `c5_oracle_keys` keys."""
+    N, Q, n = 1 << args.peers_log2, 1 << args.c5_keys_log2, C5_N
+    share = torch.empty((N // world, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(share, SEED_C5_RING, offset=rank * (N // world))
+    ids = dist.gather_ids(share, world, backend)
+    old = chordx.Ring(ids, device=dev.index or 0)
+    del ids, share
+    nj = N // 100
+    joins = torch.empty((nj, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(joins, SEED_CHURN)
+    pick = (torch.arange(nj, device=dev, dtype=torch.int64) * 0x9E3779B1) % old.n
+    leaves = old.ids_device()[pick].contiguous()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    new, o2n = old.churn(joins, leaves)
+    new.sync()
+    t_churn = time.perf_counter() - t0
+    k0, k1 = dist.shard_range(rank, world, Q)
+    q = k1 - k0
+    keys = torch.empty((q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(keys, SEED_C5_KEYS, offset=k0)
+
+    def step():
+        return old.dhash_maintenance(new, o2n, keys, n)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dist.barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        res = step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier(world)
+    dt = time.perf_counter() - t0
+    dt_max = dist.max_over_ranks(dt, world, dev)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    kern_ms_max = dist.max_over_ranks(kern_ms, world, dev)
+    old_lists, old_count, lists, count, mask, target = res
+    del res
+
+    # every key: both lists are the rings' 14-windows
+    succ = new.successor(keys).to(torch.int64)
+    ok_new = bool((lists.to(torch.int64) == (succ[:, None] + torch.arange(n, device=dev))
+                   % new.n).all().item()) and bool((count == n).all().item())
+    succ = old.successor(keys).to(torch.int64)
+    ok_old = bool((old_lists.to(torch.int64) == (succ[:, None] + torch.arange(n, device=dev))
+                   % old.n).all().item()) and bool((old_count == n).all().item())
+    del succ
+    ok_new = dist.all_over_ranks(ok_new, world, dev)
+    ok_old = dist.all_over_ranks(ok_old, world, dev)
+    n_mis = dist.sum_over_ranks(int((mask != 0).sum().item()), world, dev)
+    parity = churn_ok = None
+    m = 0
+    t_or = 0.0
+    if rank == 0 and args.c5_oracle_keys:
+        import oracle as O
+        t0 = time.perf_counter()
+        old_ids, new_ids = old.ids(), new.ids()
+        want_new, want_o2n = O.churn(old_ids, joins.cpu().numpy().view(np.uint64),
+                                     leaves.cpu().numpy().view(np.uint64))
+        o2n_h = o2n.cpu().numpy().view(np.uint32)
+        churn_ok = bool((want_new == new_ids).all() and (want_o2n == o2n_h).all())
+        m = min(args.c5_oracle_keys, q)
+        km = keys[:m].cpu().numpy().view(np.uint64)
+        wl, wc, wm, wt = O.misplaced(old_ids, want_new, want_o2n, km, n, threads=host_threads())
+        parity = bool((lists[:m].cpu().numpy().view(np.uint32) == wl).all()
+                      and (count[:m].cpu().numpy() == wc).all()
+                      and (mask[:m].cpu().numpy().view(np.uint16) == wm).all()
+                      and (target[:m].cpu().numpy() == wt).all())
+        t_or = time.perf_counter() - t0
+    dist.barrier(world)
+    per_step = dt_max / args.steps
+    out = {
+        "metric": "C5 keys/s (whole node): n = 14 replica lists + misplaced scan after a "
+                  "1 %/1 % churn", "unit": "keys/s", "value": Q / per_step,
+        "ms_per_step": per_step * 1e3, "steps": args.steps, "scaling": "strong",
+        "config": {"workload": f"C5: 2^{args.peers_log2}-peer ring (splitmix 0x5EED0007), "
+                               f"2^{args.c5_keys_log2} keys (0x5EED0008) over {world} rank(s), "
+                               f"n = {n}, {nj} joins (0x5EED0009) + {nj} leaves",
+                   "peers_old": old.n, "peers_new": new.n, "keys_total": Q, "keys_per_gpu": q,
+                   "kernel": "k_misplaced<true, true, true> (churn directory, fused old lists)"},
+        "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK * world / 1e9,
+                     "kernel_ms": kern_ms_max,
+                     "achieved": Q * C5_BYTES_STREAM / (kern_ms_max * 1e-3) / 1e9,
+                     "frac": Q * C5_BYTES_STREAM / (kern_ms_max * 1e-3) / (HBM_PEAK * world),
+                     "model": f"{C5_BYTES_STREAM} B per key (key, one 64-B search line, old "
+                              "and new 14-lists with counts, mask, targets), whole node, over "
+                              "the slowest rank's kernel time",
+                     "survey_model": {
+                         "bytes_per_key": C5_BYTES_SURVEY,
+                         "achieved": Q * C5_BYTES_SURVEY / (kern_ms_max * 1e-3) / 1e9,
+                         "frac": Q * C5_BYTES_SURVEY / (kern_ms_max * 1e-3) / (HBM_PEAK * world),
+                         "note": "SURVEY 8(d): 16 key + 64 search + 56 list + 1 + 2 per key "
+                                 "(no old list)"}},
+        "churn_ms": t_churn * 1e3,
+        "new_lists_equal_new_window": ok_new, "old_lists_equal_old_window": ok_old,
+        "keys_with_misplaced_holder": n_mis,
+        "churn_equals_oracle": churn_ok,
+        "parity_on_sample": parity, "oracle_sample_keys": m, "oracle_s": t_or,
+        "note": "both rings whole on every rank (IDs all-gathered, the same churn everywhere); "
+                "no collective in the step; oracle: oracle/chord_oracle.c or_churn + "
+                "or_misplaced (dhash_peer.cpp:298-348)"}
+    old.close()
+    new.close()
     return out
 
 
@@ -466,14 +671,21 @@ def main():
 
     # ---- setup (untimed): replicated ring, converged finger + route tables ----
     ring, t_gather, t_ring = setup_ring(args, world, rank, dev, backend)
+    st0 = chordx.pool_stats()
     t0 = time.perf_counter()
     ring.build_fingers()
     ring.sync()
     t_fing = time.perf_counter() - t0
+    st1 = chordx.pool_stats()
     t0 = time.perf_counter()
     ring.build_fingers()  # same tables again: their HBM is now mapped
     ring.sync()
     t_fing_warm = time.perf_counter() - t0
+    setup_alloc = {k: {"fresh_GiB": d["fresh_bytes"] / 2**30, "pooled_GiB": d["reused_bytes"] / 2**30,
+                       "retries": d["retries"]}
+                   for k, d in (("fingers_build", chordx.pool_stats_delta(st0, st1)),
+                                ("fingers_build_again",
+                                 chordx.pool_stats_delta(st1, chordx.pool_stats())))}
     keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
     q0, q1 = dist.shard(rank, Q)
     chordx.fill_splitmix(keys, SEED_KEYS, offset=q0)
@@ -511,6 +723,11 @@ def main():
     # ---- results (all reduced over ranks) ----
     bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
     sum_hops = dist.sum_over_ranks(int(hops.to(torch.int64).sum().item()), world, dev)
+    # hop histogram (SURVEY 5 metrics), summed over ranks; hops <= 255 (hop cap)
+    hist = dist.sum_vec_over_ranks(torch.bincount(hops.to(torch.int64), minlength=256).cpu(),
+                                   world, dev)
+    max_hops = max(h for h, c in enumerate(hist) if c) if any(hist) else 0
+    hist = hist[:max_hops + 1]
     succ = torch.empty(Q, dtype=torch.int32, device=dev)
     ring.successor(keys, out=succ)  # exact successor (directory search) of every key
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -557,6 +774,8 @@ def main():
         chordx.pool_trim()  # the new rings' blocks are not needed by the arc leg
         churn["route_ready_ms_max_over_ranks"] = {
             k: dist.max_over_ranks(v, world, dev) for k, v in churn["route_ready_ms"].items()}
+        churn["alloc_retries_all_ranks"] = dist.sum_over_ranks(
+            sum(e["alloc"]["retries"] for e in churn["epochs"]), world, dev)
         churn["table_hash_equal"] = dist.all_over_ranks(churn["table_hash_equal"], world, dev)
         if "table_depth_ab" in churn:
             st = churn["table_depth_ab"]
@@ -580,6 +799,14 @@ def main():
                            args.cpu_seconds, world)
         del F_host
     dist.barrier(world)
+
+    # ---- C5 (configs[4]) after the bench ring's tables are released ----
+    c5 = None
+    if not args.no_c5:
+        ring.close()
+        chordx.pool_trim()
+        c5 = c5_leg(args, world, rank, dev, backend)
+        chordx.pool_trim()
 
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -626,11 +853,17 @@ def main():
             "cpu_baseline": cpu,
             "arc": arc,
             "churn_route_ready": churn,
+            "c5": c5,
             "gather_roofline": gather,
             "route_variant": route_variant,
             "route_table_bytes": table_bytes,
             "route_cz_escapes": cz_escapes,
             "mean_hops": sum_hops / (world * Q),
+            "hops_hist": hist,
+            "max_hops": max_hops,
+            "hops_hist_note": "hops_hist[h] = lookups of the timed batch (all ranks) that took "
+                              "h hops; the CPU baseline's sample carries the oracle's histogram "
+                              "(cpu_baseline.hist_equal)",
             "bad_status": bad,
             "route_owner_equals_successor": owner_eq,
             "counting_build_same_results": counting_same,
@@ -641,9 +874,11 @@ def main():
                                          "(splitmix 0x5EED000A) instead of q mod N"},
             "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring,
                         "fingers_build": t_fing, "fingers_build_again": t_fing_warm,
+                        "alloc": setup_alloc,
                         "note": "fingers_build = converged fingers + route table on fresh "
-                                "HBM (first touch of 64 GiB); fingers_build_again = the same "
-                                "build into the now-mapped tables"},
+                                f"HBM (first touch of the {table_bytes / 2**30:.0f} GiB route "
+                                "table); fingers_build_again = the same build into the "
+                                "now-mapped tables"},
             "ab_variants": "benches/bench_route.py --variants (route and search A/B kernels)",
         })
         print(json.dumps(line), flush=True)

@@ -84,7 +84,7 @@ const char *cx_last_error(void);
 /* Number of visible HIP devices (0 without a GPU; never fails). */
 int cx_device_count(int *count);
 /* Table pool: a destroyed ring's large tables (finger table, route tables,
- * arc planes, build temporaries >= 16 MiB) are kept per process, up to
+ * arc planes, build and churn temporaries >= 64 KiB) are kept per process, up to
  * CX_POOL_CAP_GIB GiB (environment, default 96, 0 = off), for the next ring of
  * the same size -- a membership epoch reuses the previous epoch's HBM.  Any
  * allocation that fails releases the device's idle blocks and retries.

@@ -159,6 +159,35 @@ def pool_info():
     return b.value, n.value
 
 
+POOL_STAT_KEYS = ("fresh_bytes", "fresh_allocs", "reused_bytes", "reused_allocs", "trims",
+                  "trimmed_bytes", "retries", "failures")
+
+
+def pool_stats() -> dict:
+    """Internal: allocation-path counters since the process started
+    (cxi_pool_stats): bytes / allocations fresh from hipMalloc, handed back by
+    the table pool, idle blocks trimmed to retry a failed allocation, retries
+    and failures.  Differences of two snapshots give one epoch's path."""
+    import numpy as np
+    out = np.zeros(8, dtype=np.uint64)
+    f = lib().cxi_pool_stats
+    f.argtypes = [ctypes.c_void_p]
+    check(f(out.ctypes.data_as(ctypes.c_void_p)))
+    return {k: int(v) for k, v in zip(POOL_STAT_KEYS, out)}
+
+
+def pool_stats_delta(before: dict, after: dict) -> dict:
+    return {k: after[k] - before[k] for k in POOL_STAT_KEYS}
+
+
+def set_fault(mask: int) -> None:
+    """Internal, tests only: fault injection (cxi_set_fault; bit 0 = the
+    route-table build's finger-plane allocation fails)."""
+    f = lib().cxi_set_fault
+    f.argtypes = [ctypes.c_int]
+    check(f(int(mask)))
+
+
 def device_count() -> int:
     c = ctypes.c_int(0)
     check(lib().cx_device_count(ctypes.byref(c)))

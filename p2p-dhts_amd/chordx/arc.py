@@ -55,7 +55,8 @@ def arc_of(peer: int, n: int, world: int) -> int:
 
 
 class ArcRouter:
-    def __init__(self, engine, n: int, rank: int, world: int, group=None, comm_device=None):
+    def __init__(self, engine, n: int, rank: int, world: int, group=None, comm_device=None,
+                 exchange_always: bool = False):
         if not 1 <= world <= 64:
             raise ValueError("arc routing supports 1..64 ranks")
         self.engine, self.n, self.rank, self.world = engine, n, rank, world
@@ -72,6 +73,10 @@ class ArcRouter:
         self.chunks = None     # route_soa pipeline depth (None: by batch size)
         self.regions = True    # single-pass partition into destination regions
         self.hints = True      # origin-resolved source hints with the lookups
+        # exchange_always: a single rank still partitions, exchanges (with
+        # itself, through the process group's collectives) and delivers -- the
+        # general path, so a one-GPU run executes and times what N ranks run
+        self.exchange_always = exchange_always
 
     def _exchange(self, send, counts):
         """Returns (received records, global number of records in flight)."""
@@ -165,7 +170,7 @@ class ArcRouter:
         of piece slots, and every rank runs max-over-ranks pieces, the missing
         ones empty -- so all ranks issue the same collectives."""
         eng = self.engine
-        if self.world == 1:
+        if self.world == 1 and not self.exchange_always:
             eng.arc_deliver(eng.arc_route(src, keys), None, owner, hops, status)
             self.rounds = 1
             return 1

@@ -29,6 +29,30 @@ def init(backend: str, device=None):
     return world, rank, local
 
 
+def init_single(backend: str, device=None) -> bool:
+    """A one-rank process group (no rendezvous: an in-process HashStore).  On
+    a one-GPU run this lets the collective path itself run -- the arc
+    exchange's all_gather / all_to_all execute on RCCL with the rank as its
+    own peer -- instead of being skipped.  Returns True if it created the
+    group (the caller destroys it)."""
+    if tdist.is_initialized():
+        return False
+    kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
+    tdist.init_process_group(backend, store=tdist.HashStore(), rank=0, world_size=1, **kw)
+    return True
+
+
+def sum_vec_over_ranks(v, world: int, device=None):
+    """Element-wise sum over ranks of an int64 vector (a list or 1-D tensor);
+    returns a list of ints."""
+    t = torch.as_tensor(v, dtype=torch.int64)
+    if world > 1:
+        d = _dev(device)
+        t = t.to(d) if d is not None else t.cpu()
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+    return [int(x) for x in t.cpu().tolist()]
+
+
 def shard(rank: int, per_rank: int):
     """Global key-stream range [begin, end) routed by `rank` (weak scaling)."""
     return rank * per_rank, (rank + 1) * per_rank

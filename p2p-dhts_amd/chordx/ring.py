@@ -226,7 +226,9 @@ class Ring:
         ((n, ns) indices in list order, CX_NONE-padded; None = the converged
         next-ns window) for ForwardRequest's dead-finger branch; rule =
         CX_FWD_CHORD (chord_peer.cpp:201-208) or CX_FWD_DHASH
-        (dhash_peer.cpp:516-526).  Switches route() to the literal walk."""
+        (dhash_peer.cpp:516-526).  Switches route() to the literal walk.
+        With alive=None and succs=None the ring is reset to the converged
+        walk (no liveness state); ns and rule are then ignored."""
         al = None
         if alive is not None:
             al = alive.contiguous() if _is_dev(alive) else np.ascontiguousarray(alive, np.uint8)
@@ -571,21 +573,19 @@ class Ring:
         if not (_is_dev(keys) and _is_dev(src)):
             raise TypeError("arc routing takes device tensors")
         q = keys.shape[0]
-        if hint is not None:
-            if not (_is_dev(hint) and hint.element_size() == 8 and hint.is_contiguous()
-                    and hint.numel() == q):
-                raise TypeError("hint must be a contiguous 8-byte device tensor of q elements")
-            if res is None:
-                res = torch.empty(q, dtype=torch.int64, device=keys.device)
-            self._arc_stream()
-            L.check(L.lib().cx_arc_route_hinted(self._h, _ptr(src), _ptr(keys), _ptr(hint), q,
-                                                _ptr(res)))
-            return res
         if res is None:
             res = torch.empty(q, dtype=torch.int64, device=keys.device)
         elif not (_is_dev(res) and res.element_size() == 8 and res.numel() == q
                   and res.is_contiguous()):
             raise TypeError("res must be a contiguous 8-byte device tensor of q elements")
+        if hint is not None:
+            if not (_is_dev(hint) and hint.element_size() == 8 and hint.is_contiguous()
+                    and hint.numel() == q):
+                raise TypeError("hint must be a contiguous 8-byte device tensor of q elements")
+            self._arc_stream()
+            L.check(L.lib().cx_arc_route_hinted(self._h, _ptr(src), _ptr(keys), _ptr(hint), q,
+                                                _ptr(res)))
+            return res
         self._arc_stream()
         L.check(L.lib().cx_arc_route(self._h, _ptr(src), _ptr(keys), q, _ptr(res)))
         return res

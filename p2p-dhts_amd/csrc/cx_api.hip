@@ -39,7 +39,7 @@ int fail(int code, const std::string &msg) {
 // RAII device allocation.
 // ---------------------------------------------------------------------------
 // Table pool.  A ring's large tables (finger table, route tables, arc planes:
-// 72 GiB per 2^24-peer replica) and the builds' large temporaries (>= 16 MiB)
+// 72 GiB per 2^24-peer replica) and the builds' large temporaries (>= 64 KiB)
 // are not returned to the driver
 // when the ring is destroyed but kept, up to CX_POOL_CAP bytes per process,
 // for the next ring that asks for the same size on the same device: after a
@@ -56,6 +56,19 @@ struct PoolEnt {
 std::mutex g_pool_mu;
 std::vector<PoolEnt> g_pool;
 size_t g_pool_bytes = 0;
+// Allocation-path counters (cumulative per process, under g_pool_mu; read by
+// cxi_pool_stats): where each table / temporary came from -- fresh hipMalloc
+// or a pooled block -- and how often an allocation had to trim the pool and
+// retry (near the HBM limit).
+struct PoolStats {
+    uint64_t fresh_bytes = 0, fresh_allocs = 0;     // hipMalloc'd (new HBM pages)
+    uint64_t reused_bytes = 0, reused_allocs = 0;   // handed back by the pool
+    uint64_t trims = 0, trimmed_bytes = 0;          // idle blocks released to retry
+    uint64_t retries = 0, failures = 0;             // first hipMalloc failed / both failed
+} g_stats;
+// Fault injection for tests (cxi_set_fault): bit 0 = the route-table build's
+// finger-plane allocation fails (exercises the row-major fallback).
+std::atomic<int> g_fault{0};
 // blocks from 64 KiB up: a churn's temporaries (2^17 joins: 0.5-3 MiB each)
 // recur every epoch too, and each hipFree costs 0.1-0.3 ms
 constexpr size_t POOL_MIN = (size_t)64 << 10;
@@ -72,6 +85,8 @@ size_t pool_cap() {
 void pool_trim_locked(int device) {
     for (size_t k = 0; k < g_pool.size();) {
         if (device < 0 || g_pool[k].device == device) {
+            ++g_stats.trims;
+            g_stats.trimmed_bytes += g_pool[k].bytes;
             int cur = 0;
             (void)hipGetDevice(&cur);
             (void)hipSetDevice(g_pool[k].device);
@@ -96,6 +111,8 @@ hipError_t table_alloc(void **p, size_t bytes) {
                 *p = g_pool[k].p;
                 g_pool_bytes -= bytes;
                 g_pool.erase(g_pool.begin() + k);
+                ++g_stats.reused_allocs;
+                g_stats.reused_bytes += bytes;
                 return hipSuccess;
             }
     }
@@ -104,11 +121,19 @@ hipError_t table_alloc(void **p, size_t bytes) {
         (void)hipGetLastError();
         {
             std::lock_guard<std::mutex> g(g_pool_mu);
+            ++g_stats.retries;
             pool_trim_locked(dev);
         }
         e = hipMalloc(p, bytes);
     }
-    if (e != hipSuccess) *p = nullptr;
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        ++g_stats.failures;
+    } else {
+        ++g_stats.fresh_allocs;
+        g_stats.fresh_bytes += bytes;
+    }
     return e;
 }
 
@@ -141,19 +166,32 @@ void table_free(int device, void *p, size_t bytes) {
 // allocation outside it fails).
 hipError_t dev_malloc(void **p, size_t bytes) {
     hipError_t e = hipMalloc(p, bytes);
-    if (e == hipSuccess) return e;
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (e == hipSuccess) {
+        ++g_stats.fresh_allocs;
+        g_stats.fresh_bytes += bytes;
+        return e;
+    }
     (void)hipGetLastError();
     int dev = 0;
     (void)hipGetDevice(&dev);
-    {
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        if (g_pool.empty()) return e;
-        pool_trim_locked(dev);
+    if (g_pool.empty()) {
+        ++g_stats.failures;
+        return e;
     }
+    ++g_stats.retries;
+    pool_trim_locked(dev);
     e = hipMalloc(p, bytes);
-    if (e != hipSuccess) *p = nullptr;
+    if (e != hipSuccess) {
+        *p = nullptr;
+        ++g_stats.failures;
+    } else {
+        ++g_stats.fresh_allocs;
+        g_stats.fresh_bytes += bytes;
+    }
     return e;
 }
+bool cx_fault_planes() { return g_fault.load() & 1; }
 template <class T>
 hipError_t dev_malloc(T **p, size_t bytes) {
     return dev_malloc(reinterpret_cast<void **>(p), bytes);
@@ -491,7 +529,7 @@ void free_ring(cx_ring *r) {
     r->planes.reset();
     r->parent_planes.reset();
     // the ring's per-peer arrays recur at the same sizes every membership
-    // epoch: through the pool like the tables (below 16 MiB: freed)
+    // epoch: through the pool like the tables (below 64 KiB: freed)
     table_free(r->device, r->d_ring, r->ring_cap * sizeof(cell128));
     (void)hipFree(r->d_eyt);
     table_free(r->device, r->d_dir, r->d_dir ? ((size_t)1 << r->dir_k) * sizeof(uint4) : 0);
@@ -594,12 +632,17 @@ void route_geometry(cx_ring *r) {
     // CX_ROUTE_R: table depth override (A/B of table size against exact hops)
     static const int r_env = [] {
         const char *e = getenv("CX_ROUTE_R");
-        return e ? atoi(e) : 0;
+        const int v = e ? atoi(e) : 0;
+        if (e && (v < 16 || v > 59)) {
+            fprintf(stderr, "cx: CX_ROUTE_R=%s ignored (must be in [16, 59])\n", e);
+            return 0;
+        }
+        return v;
     }();
     if (r_env > 0) R = r_env;
     if (r->depth_override > 0) R = r->depth_override;
     if (R < 16) R = 16;
-    if (R > 128) R = 128;
+    if (R > 59) R = 59;
     r->rt_R = R;
     r->rt_l0 = 128 - R;
     r->pk_ib = lg < 1 ? 1 : lg;
@@ -637,19 +680,22 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
     }
     const int L = lo - 5 < 0 ? 0 : lo - 5, nl = (int)CX_FINGERS - L;
     hipError_t e = hipSuccess;
+    bool have_planes = true;
     if (ft_pre && r->table_build != 1) {  // written by the finger build itself
         fv = cxk::FingerView::planes(ft_pre, r->n, L, nl);
+    } else if (r->table_build == 1 || cx_fault_planes() ||
+               ft.alloc_pooled((size_t)nl * r->n * sizeof(uint32_t), s) != hipSuccess) {
+        // the row-major table (forced, or no HBM for the planes): no two-hop
+        // planes and no root-centric build; the slice codes are replaced by
+        // high words below
+        (void)hipGetLastError();
+        have_planes = false;
     } else {
-        if (r->table_build == 1 ||
-            ft.alloc_pooled((size_t)nl * r->n * sizeof(uint32_t), s) != hipSuccess) {
-            (void)hipGetLastError();
-            return hipSuccess;
-        }
         e = cxk::fingers_levels(r->d_fingers, r->n, L, nl, ft.as<uint32_t>(), s);
         if (e != hipSuccess) return e;
         fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
-    if ((r->table_build == 0 || r->table_build == 3) &&
+    if (have_planes && (r->table_build == 0 || r->table_build == 3) &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t), s) == hipSuccess) {
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) {
@@ -684,12 +730,6 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
             if (r->route_variant < 0) r->cz_failed = true;  // automatic: use variant 4
         }
         if (r->d_cz) {
-            // CX_DEBUG_TABLE_VA: the table's address on stderr (placement probes)
-            static const bool dbg_va = getenv("CX_DEBUG_TABLE_VA") != nullptr;
-            if (dbg_va)
-                fprintf(stderr, "cx: route table %p (%zu B, offset in 1 GiB %zu, in 2 MiB %zu)\n",
-                        (void *)r->d_cz, ent * 128, (size_t)(uintptr_t)r->d_cz & ((1ull << 30) - 1),
-                        (size_t)(uintptr_t)r->d_cz & ((1ull << 21) - 1));
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
             DBuf ft, hi, c2;
             cxk::FingerView fv;
@@ -1518,6 +1558,12 @@ static int misplaced_impl(const cx_ring *old_ring, const cx_ring *new_ring,
     int rc = use_device(new_ring);
     if (rc) return rc;
     hipStream_t s = new_ring->stream;
+    // misplaced_churn searches both rings with the Eytzinger copy when either
+    // ring's directory is off (search variant 0): make sure both have one
+    if (!old_ring->sv().dir || !new_ring->sv().dir) {
+        if ((rc = ensure_eyt(const_cast<cx_ring *>(old_ring), s))) return rc;
+        if ((rc = ensure_eyt(const_cast<cx_ring *>(new_ring), s))) return rc;
+    }
     DBuf to2n, tk, tl, tc, tm, tt, tol, toc;
     const uint32_t *d_o2n;
     const cx_u128 *dk;
@@ -2263,6 +2309,28 @@ int cx_arc_deliver(const cx_ring *ring, const uint64_t *res, const uint32_t *per
     return CX_OK;
 }
 
+// ---- internal (not part of chordx.h): allocation-path counters since the
+// process started (bench.py reports their change per membership epoch):
+// out[8] = {fresh hipMalloc bytes, fresh allocations, bytes reused from the
+// pool, pooled allocations, pool blocks trimmed, bytes trimmed, allocations
+// retried after a trim, allocations that failed}.
+int cxi_pool_stats(uint64_t *out) {
+    CX_CHECK(out != nullptr, CX_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    const uint64_t v[8] = {g_stats.fresh_bytes, g_stats.fresh_allocs, g_stats.reused_bytes,
+                           g_stats.reused_allocs, g_stats.trims, g_stats.trimmed_bytes,
+                           g_stats.retries, g_stats.failures};
+    for (int k = 0; k < 8; ++k) out[k] = v[k];
+    return CX_OK;
+}
+
+// ---- internal: fault injection for tests (bit 0: the route-table build's
+// finger-plane allocation fails).
+int cxi_set_fault(int mask) {
+    g_fault.store(mask);
+    return CX_OK;
+}
+
 // ---- internal (not part of chordx.h): error reporting for cx_wire.cpp
 int cxi_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
 
@@ -2282,7 +2350,8 @@ int cxi_set_route_variant(cx_ring *ring, int variant) {
 // default).  Only before the ring's first finger build (the table sizes follow R).
 int cxi_set_route_depth(cx_ring *ring, int R) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(R == 0 || (R >= 16 && R <= 64), CX_E_INVALID, "R must be 0 or in [16, 64]");
+    // the pattern-keyed build needs its lowest plane level (128 - R - 5) >= 64
+    CX_CHECK(R == 0 || (R >= 16 && R <= 59), CX_E_INVALID, "R must be 0 or in [16, 59]");
     CX_CHECK(!ring->d_cz && !ring->d_tree && !ring->d_pk && !ring->d_rt && !ring->d_arc_tree,
              CX_E_STATE, "route depth is fixed once a route table exists");
     ring->depth_override = R;

@@ -464,3 +464,64 @@ def test_arc_router_two_ranks_on_one_gpu(cx, chunks):
     for r in range(2):
         assert out[r][:3] == (True, True, True), (r, out[r])
         assert out[r][3] == 2 and out[r][4] > 0
+
+
+# ---------------------------------------------------------------------------
+# ArcRouter's RCCL branches on the GPU: a one-rank "nccl" process group (RCCL)
+# with exchange_always, so route_soa runs its general path -- region partition
+# with source hints, the count all_gather and its pinned host copy, the list
+# all_to_alls over CUDA region views on RCCL's stream, work.wait() against the
+# walk's stream, and delivery through the region slots -- exactly as N ranks
+# run it (bench.py's N = 1 arc leg).  Results must equal cx_route.
+# ---------------------------------------------------------------------------
+def _rccl_worker(_i, n, q, chunks, out):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "p2p-dhts_amd")]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    import torch
+    import torch.distributed as tdist
+    import chordx
+    from chordx import dist
+    from chordx.arc import ArcRouter
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    assert dist.init_single("nccl", dev)
+    ids = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(ids, 0xA7D0)
+    ring = chordx.Ring(ids)
+    ring.build_fingers()
+    router = ArcRouter(ring, ring.n, 0, 1, exchange_always=True)
+    router.chunks = chunks
+    keys = torch.empty((q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(keys, 0xA7D1)
+    src = ((torch.arange(q, device=dev) * 7) % ring.n).to(torch.int32)
+    src[::97] = ring.n + 3  # bad sources travel and come back as CX_Q_BADPEER
+    ow, hp, st = ring.route(src, keys)
+    res = []
+    for _ in range(2):  # the second call reuses the pinned count buffer
+        owner = torch.full((q,), -5, dtype=torch.int32, device=dev)
+        hops = torch.zeros(q, dtype=torch.uint8, device=dev)
+        status = torch.full((q,), 9, dtype=torch.uint8, device=dev)
+        router.records_sent = 0
+        rounds = router.route(src, keys, owner, hops, status)
+        torch.cuda.synchronize()
+        res.append((bool(torch.equal(ow, owner)), bool(torch.equal(hp, hops)),
+                    bool(torch.equal(st, status)), rounds, router.records_sent))
+    out[0] = (tdist.get_backend(), res, int((st == chordx.CX_Q_BADPEER).sum().item()))
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("q,chunks", [(1 << 21, 1), (1 << 21, 3), (1 << 23, None)])
+def test_arc_router_rccl_world1_general_path(cx, q, chunks):
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_rccl_worker, args=(1 << 20, q, chunks, out), nprocs=1, join=True,
+                       start_method="spawn")
+    backend, res, bad = out[0]
+    assert backend == "nccl" and bad == len(range(0, q, 97))
+    for r in res:
+        assert r == (True, True, True, 2, q), r

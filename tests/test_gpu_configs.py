@@ -92,7 +92,9 @@ def test_c4_arc_layout_g8(O, c4, c4_host, d):
     each of the 8 origin ranks' 2^22 C4 keys sends to d -- walked by
     cx_arc_route and delivered by cx_arc_deliver: owner / hops / status equal
     the replicated cx_route's on every received lookup, and the oracle's
-    literal walk (chord_peer.cpp:185-211) on a 2^18 sample."""
+    literal walk (chord_peer.cpp:185-211) on a 2^18 sample.  Then the same for
+    the default path: cx_arc_partition_regions with source hints, the hinted
+    walk (cx_arc_route_hinted) and delivery through each origin's region slots."""
     import torch
     ring, keys, src, owner, hops, status = c4
     want_ring, F = c4_host
@@ -131,6 +133,57 @@ def test_c4_arc_layout_g8(O, c4, c4_host, d):
     assert (os_ == 0).all()
     assert (ao[:sample].cpu().numpy().view(np.uint32) == oo).all()
     assert (ah[:sample].cpu().numpy() == oh).all()
+
+    # ---- the default path (ArcRouter.route_soa, what bench.py and SCALE run):
+    # single-pass region partition with origin-resolved source hints
+    # (gs = 116 - ceil(log2 N) depends on the ring size), the hinted arc walk,
+    # and delivery through the region slots back at each origin
+    hk, hs, hh, slots = [], [], [], []
+    for r in range(G):
+        sl = slice(r * per, (r + 1) * per)
+        cap = per // G + per // (4 * G) + 4096  # route_soa's region capacity
+        part = ring.arc_partition_regions(G, src[sl], keys[sl], cap, hints=True)
+        assert part is not None  # uniform keys never crowd one arc past cap
+        sk, ss, perm, counts, sh = part
+        assert sum(counts) == per and max(counts) <= cap
+        r0 = d * cap
+        hk.append(sk[r0:r0 + counts[d]])
+        hs.append(ss[r0:r0 + counts[d]])
+        hh.append(sh[r0:r0 + counts[d]])
+        slots.append((perm, counts[d], cap))
+    assert sum(x.shape[0] for x in hk) == total  # the same lookups reach rank d
+    hk, hs, hh = torch.cat(hk), torch.cat(hs), torch.cat(hh)
+    hres = ring.arc_route(hs, hk, hint=hh)
+    wo, wh, ws = ring.route(hs, hk)
+    ho = torch.full((total,), -7, dtype=torch.int32, device="cuda:0")
+    hh8 = torch.full((total,), 77, dtype=torch.uint8, device="cuda:0")
+    hst = torch.full((total,), 9, dtype=torch.uint8, device="cuda:0")
+    ring.arc_deliver(hres, None, ho, hh8, hst)
+    torch.cuda.synchronize()
+    assert torch.equal(ho, wo) and torch.equal(hh8, wh) and torch.equal(hst, ws)
+    assert int((hst != 0).sum()) == 0
+    oo, oh, os_ = O.route(O.Peers(want_ring, F), hs[:sample].cpu().numpy().view(np.uint32),
+                          hk[:sample].cpu().numpy().view(np.uint64))
+    assert (os_ == 0).all()
+    assert (ho[:sample].cpu().numpy().view(np.uint32) == oo).all()
+    assert (hh8[:sample].cpu().numpy() == oh).all()
+    # delivery at each origin r: the answers of region d land at the slots perm
+    # names, and every lookup of origin r that went to d gets its own answer
+    # (lookups sent elsewhere read other regions, filled with a sentinel here)
+    off = 0
+    for r, (perm, cnt, cap) in enumerate(slots):
+        back = torch.zeros(G * cap, dtype=torch.int64, device="cuda:0")
+        back[d * cap: d * cap + cnt] = hres[off:off + cnt]
+        off += cnt
+        o = torch.empty(per, dtype=torch.int32, device="cuda:0")
+        h = torch.empty(per, dtype=torch.uint8, device="cuda:0")
+        st = torch.empty(per, dtype=torch.uint8, device="cuda:0")
+        ring.arc_deliver(back, perm, o, h, st)
+        mine = (perm.long() >= d * cap) & (perm.long() < d * cap + cnt)
+        assert int(mine.sum()) == cnt
+        sl = slice(r * per, (r + 1) * per)
+        assert torch.equal(o[mine], owner[sl][mine]) and torch.equal(h[mine], hops[sl][mine])
+        assert int((st[mine] != 0).sum()) == 0
 
 
 def test_c5_full_size_churn_and_misplaced_scan(O):

@@ -619,6 +619,37 @@ def test_route_table_from_level_planes_identical(lg):
     assert h_planes == h_rows == h_planes_only == h_entry and h_planes != 0
 
 
+@pytest.mark.parametrize("lg", [12, 16])
+def test_route_table_without_planes_memory(cx, O, lg):
+    """The default build when HBM for the finger level planes runs out
+    (fault-injected allocation failure): it falls back to the row-major finger
+    table, whose build reads 64-bit ID high words -- the 32-bit slices it had
+    prepared must be replaced, or the build reads past them.  The table must
+    equal the forced row-major build's, and routes must equal the oracle's."""
+    import torch
+    ids = torch.empty((1 << lg, 2), dtype=torch.int64, device="cuda:0")
+    cx.fill_splitmix(ids, 0x5EED0303 + lg)
+    ring = cx.Ring(ids)
+    ring.set_table_build(1)
+    ring.build_fingers()
+    h_rows = ring.route_table_hash()
+    ring.set_table_build(0)
+    from chordx import _lib
+    _lib.set_fault(1)
+    try:
+        ring.build_fingers()
+    finally:
+        _lib.set_fault(0)
+    assert ring.route_info()[0] == 5
+    assert ring.route_table_hash() == h_rows != 0
+    want = O.ring_build(ids.cpu().numpy().view(np.uint64))
+    keys = O.splitmix_keys(0x5EED0304, 4096)
+    src = (np.arange(4096) * 131 % len(want)).astype(np.uint32)
+    o, h, s = ring.route(src, keys)
+    wo, wh, ws = O.route(O.Peers(want, O.fingers(want)), src, keys)
+    assert (o == wo).all() and (h == wh).all() and (s == ws).all()
+
+
 @pytest.mark.parametrize("kind", ["small", "mixed", "clustered"])
 def test_route_table_builds_edge_rings(cx, O, kind):
     """The default route-table build (level + two-hop planes) equals the

@@ -57,8 +57,9 @@ def depth_setup(cx, O):
 
 # 16: the shallowest table (many exact hops); 20 / 32: either side of the
 # default 24 at this size; 40: planes below the streaming tile's first level
-# (the build reads them from the finger rows)
-@pytest.mark.parametrize("R", [16, 20, 32, 40])
+# (the build reads them from the finger rows); 59: the deepest the pattern-keyed
+# build takes (its lowest plane level 128 - R - 5 must be >= 64)
+@pytest.mark.parametrize("R", [16, 20, 32, 40, 59])
 def test_depth_override_same_routes(cx, depth_setup, R):
     ids, keys, src, ob, hb = depth_setup
     ring = cx.Ring(ids)
@@ -72,7 +73,7 @@ def test_depth_override_same_routes(cx, depth_setup, R):
 
 def test_depth_override_errors(cx, O):
     ring = cx.Ring(O.splitmix_keys(0x5EED0420, 5000))
-    for bad in (15, 65, -1):
+    for bad in (15, 60, 64, 65, -1):
         with pytest.raises(cx.ChordError):
             ring.set_route_depth(bad)
     ring.set_route_depth(0)  # back to the default

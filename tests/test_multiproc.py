@@ -218,7 +218,7 @@ class OracleArcEngine:
 
 
 def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="records",
-                chunks=None, sizes=None, regions=False, region_cap=None):
+                chunks=None, sizes=None, regions=False, region_cap=None, exchange_always=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))
     import sys
@@ -232,6 +232,8 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="reco
     from chordx.arc import ArcRouter
     from test_multiproc import OracleArcEngine
     dist.init("gloo")
+    if world == 1:
+        assert dist.init_single("gloo")
     ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
     P = O.Peers(ring, O.fingers(ring, threads=2))
     if sizes is not None:  # uneven per-rank batches (one may be empty)
@@ -243,7 +245,7 @@ def _arc_worker(rank, world, port, per_rank, out, key_first=True, protocol="reco
     status = torch.full((per_rank,), 7, dtype=torch.uint8)
     eng = OracleArcEngine(P, len(ring))
     eng.region_cap = region_cap
-    router = ArcRouter(eng, len(ring), rank, world)
+    router = ArcRouter(eng, len(ring), rank, world, exchange_always=exchange_always)
     router.regions = regions
     router.chunks = chunks
     rounds = router.route(src, torch.from_numpy(keys.view(np.int64).copy()), owner, hops, status,
@@ -323,6 +325,29 @@ def test_arc_router_soa_uneven_batches_gloo(chunks):
         assert out[r][0] == list(map(int, ow)) and out[r][1] == list(map(int, hp))
         assert out[r][2] == list(map(int, st))
         assert out[r][3] == 2
+
+
+@pytest.mark.parametrize("regions", [False, True])
+def test_arc_router_soa_world1_exchanges_with_itself_gloo(regions):
+    """A one-rank group with exchange_always (bench.py's N = 1 arc leg):
+    route_soa takes the general path -- partition, count all_gather, the
+    all_to_alls to and from itself, delivery through the permutation or the
+    region slots -- instead of the in-place walk, and every lookup equals the
+    oracle walk."""
+    import oracle as O
+    per_rank = 500
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_arc_worker, args=(1, _free_port(), per_rank, out, True, "soa", 2,
+                                          None, regions, None, True),
+                       nprocs=1, join=True, start_method="spawn")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    P = O.Peers(ring, O.fingers(ring))
+    keys = O.splitmix_keys(0x5EED0006, per_rank)
+    src = ((np.arange(per_rank) * 7) % len(ring)).astype(np.uint32)
+    ow, hp, st = O.route(P, src, keys)
+    assert out[0][0] == ow.tolist() and out[0][1] == hp.tolist() and out[0][2] == st.tolist()
+    assert out[0][3] == 2 and out[0][4] == per_rank  # two rounds, every lookup exchanged
 
 
 def test_bench_launches_n_ranks_itself():
