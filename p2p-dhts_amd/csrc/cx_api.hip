@@ -67,7 +67,8 @@ struct PoolStats {
     uint64_t retries = 0, failures = 0;             // first hipMalloc failed / both failed
 } g_stats;
 // Fault injection for tests (cxi_set_fault): bit 0 = the route-table build's
-// finger-plane allocation fails (exercises the row-major fallback).
+// finger-plane allocation fails (exercises the row-major fallback); bit 1 =
+// the default build's overflow launches (cxk::cz2_set_cap).
 std::atomic<int> g_fault{0};
 // blocks from 64 KiB up: a churn's temporaries (2^17 joins: 0.5-3 MiB each)
 // recur every epoch too, and each hipFree costs 0.1-0.3 ms
@@ -338,7 +339,7 @@ struct cx_ring {
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
     uint64_t *d_cz = nullptr;      // pattern-keyed window table [rt_R][2][n][8 x u64] (variant 5)
-    int table_build = 0;           // route-table build input: 0 level + two-hop planes (roots),
+    int table_build = 0;           // route-table build input (cxi_set_table_build): 0 level + two-hop planes (roots),
                                    // 1 row-major fingers, 2 level planes only (A/B)
     bool cz_valid = false;
     uint64_t cz_escapes = 0;       // nodes the compressed format could not represent
@@ -662,7 +663,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         return e && strcmp(e, "hi") == 0;
     }();
     bool slices = false;
-    if (r->table_build == 0 && !hi_only) {
+    if ((r->table_build == 0 || r->table_build == 4) && !hi_only) {
         hipError_t e1 = hi.alloc_pooled(r->n * sizeof(uint32_t), s);
         uint32_t *d_wide = r->d_scratch + 100;
         if (e1 == hipSuccess)
@@ -695,12 +696,14 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         if (e != hipSuccess) return e;
         fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
-    if (have_planes && (r->table_build == 0 || r->table_build == 3) &&
+    if (have_planes && (r->table_build == 0 || r->table_build == 3 || r->table_build == 4) &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t), s) == hipSuccess) {
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) {
             fv.C2 = c2.as<uint32_t>();
-            fv.roots = r->table_build == 0 ? 1 : 0;  // 3: one lane per entry (round 2)
+            // 0: blocks sized by distinct roots, 4: 256-row root blocks (round 3),
+            // 3: one lane per entry (round 2)
+            fv.roots = r->table_build == 0 ? 2 : (r->table_build == 4 ? 1 : 0);
         }
     }
     (void)hipGetLastError();
@@ -737,8 +740,12 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
                 if (int rc = ensure_fingers_rows(r, s)) return rc;
             }
             CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre));
+            DBuf ws;  // the default build's overflow list
+            if (fv.roots == 2)
+                CX_HIP(ws.alloc_pooled(cxk::cz_build_ws_words(r->n, r->rt_l0, r->rt_R, (uint32_t)r->n) *
+                                           sizeof(uint32_t), s));
             CX_HIP(cxk::cz_build(fv, r->d_ring, hi.as<uint64_t>(), r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_cz,
-                                 r->d_scratch, s));
+                                 r->d_scratch, s, ws.as<uint32_t>()));
             uint32_t esc[2] = {0, 0};
             CX_HIP(hipMemcpyAsync(esc, r->d_scratch, sizeof(esc), hipMemcpyDeviceToHost, s));
             CX_HIP(hipStreamSynchronize(s));
@@ -1132,14 +1139,16 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     static const bool eager_rows = getenv("CX_FINGERS_ROWS") != nullptr;
     const int ft_l = ring->rt_l0 - 5;
     const bool defer = !eager_rows && !fingers_out && ring->variant() == 5 &&
-                       (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
+                       (ring->table_build == 0 || ring->table_build == 3 ||
+                        ring->table_build == 4) && ft_l >= 64 &&
                        ring->n >= ((size_t)1 << 18) && ft_l >= cxk::FINGERS_TILE_L0;
     // the default route table reads the fingers as level planes: the streaming
     // finger build writes them alongside the rows (no transpose pass), and the
     // ring keeps them for the finger repair of the next churn
     std::shared_ptr<PlaneSet> ps;
     bool ft_done = false;
-    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64) {
+    if (ring->variant() == 5 &&
+        (ring->table_build == 0 || ring->table_build == 3 || ring->table_build == 4) && ft_l >= 64) {
         const int nl = (int)CX_FINGERS - ft_l;
         const size_t bytes = (size_t)nl * ring->n * sizeof(uint32_t);
         void *pp = nullptr;
@@ -2047,10 +2056,16 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
         DBuf ft, hi, c2;
         cxk::FingerView fv;
         CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s));
+        DBuf ws;  // the default build's overflow list (sized for the larger part)
+        if (fv.roots == 2) {
+            const size_t w0 = cxk::cz_build_ws_words(n, Lh, (int)CX_FINGERS - Lh, (uint32_t)n);
+            const size_t w1 = cxk::cz_build_ws_words(n, l0, Lh - l0, M);
+            CX_HIP(ws.alloc_pooled((w0 > w1 ? w0 : w1) * sizeof(uint32_t), s));
+        }
         CX_HIP(cxk::cz_build_part(fv, ring->d_ring, hi.as<uint64_t>(), n, Lh, (int)CX_FINGERS - Lh, 0, (uint32_t)n,
-                                  ring->pk_ib, ring->d_arc_tree, ring->d_scratch, s));
+                                  ring->pk_ib, ring->d_arc_tree, ring->d_scratch, s, ws.as<uint32_t>()));
         CX_HIP(cxk::cz_build_part(fv, ring->d_ring, hi.as<uint64_t>(), n, l0, Lh - l0, plo, M, ring->pk_ib,
-                                  ring->d_arc_tree + top_ent * 8, ring->d_scratch, s));
+                                  ring->d_arc_tree + top_ent * 8, ring->d_scratch, s, ws.as<uint32_t>()));
         uint32_t esc[2] = {0, 0};
         CX_HIP(hipMemcpyAsync(esc, ring->d_scratch, sizeof(esc), hipMemcpyDeviceToHost, s));
         CX_HIP(hipStreamSynchronize(s));  // ft and hi are freed at scope end
@@ -2325,9 +2340,11 @@ int cxi_pool_stats(uint64_t *out) {
 }
 
 // ---- internal: fault injection for tests (bit 0: the route-table build's
-// finger-plane allocation fails).
+// finger-plane allocation fails; bit 1: the default route-table build defers
+// the rows past 48 distinct roots per block to overflow launches).
 int cxi_set_fault(int mask) {
     g_fault.store(mask);
+    cxk::cz2_set_cap(mask & 2 ? 48u : 256u);
     return CX_OK;
 }
 
@@ -2466,13 +2483,14 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
 }
 
 // Route-table build input: 0 = finger level + two-hop planes, root-centric
-// windows (k_cz_build_roots, default), 1 = row-major finger table, 2 = level
-// planes only, 3 = level + two-hop planes, one lane per entry (k_cz_build,
-// the round-2 build).  All give the same table.  Takes effect at the next
-// finger build.
+// windows in blocks sized by distinct roots (k_cz_build_roots2, default),
+// 1 = row-major finger table, 2 = level planes only, 3 = level + two-hop
+// planes, one lane per entry (k_cz_build, the round-2 build), 4 = root-centric
+// windows in 256-row blocks (k_cz_build_roots, round 3).  All give the same
+// table.  Takes effect at the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0, 1, 2 or 3");
+    CX_CHECK(variant >= 0 && variant <= 4, CX_E_INVALID, "variant must be 0 .. 4");
     ring->table_build = variant;
     return CX_OK;
 }

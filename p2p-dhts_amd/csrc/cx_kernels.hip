@@ -3,6 +3,8 @@
 // Every kernel is HBM/latency bound integer work: no MFMA.  Layout
 // in HBM: ring IDs as 16-B cells (AoS, one dwordx4 per ID), finger table as
 // row-major uint32 [peer][128], Eytzinger copy of the ring for searches.
+#include <atomic>
+#include <cmath>
 #include <type_traits>
 
 #include "cx_kernels.hpp"
@@ -3146,14 +3148,376 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
     if (bad) atomicAdd(esc, bad);
 }
 
-hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
-                    int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s) {
-    return cz_build_part(fv, ring, rh, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s);
+// Root-centric build with blocks sized by distinct roots (table_build 0,
+// default since round 4; k_cz_build_roots above is table_build 4).  A block of
+// k_cz_build_roots takes 256 rows and computes one window per distinct root,
+// one lane each: on a uniform ring about half the rows of a level above the
+// mean gap share their root with the row before (the fingers of 256 adjacent
+// peers land on ~128 distinct peers), so half the lanes idle through the
+// window phase -- the dependent-gather chain that bounds the build.  Here a
+// block takes up to CZ2_RMAX rows, sized per level (host: cz2_plan) so that
+// its distinct roots come to ~90 % of the 256 lanes; the row phase runs two
+// rows per lane.  A block whose rows have more than 256 distinct roots (rare
+// on a uniform ring, frequent on a clustered one) writes the rows of its
+// first 256 roots and appends the rest (< 256 rows, so < 256 roots) to an
+// overflow list that a second launch of the same kernel finishes.  LDS stays
+// under 20 KB (8 blocks per CU): the windows' buffer also stages the rows'
+// roots before the window phase, and each window's 16th word carries its root
+// into the W1 phase (with the window's CZ_NONE count in the spare top bits).
+// Same table, bit for bit (route_table_hash against every other build).
+constexpr int CZ2_RMAX = 464;
+constexpr uint32_t CZ2_CHUNK = 4096;  // rows of a dispatch chunk (all levels)
+
+// Blocks per level per chunk: level l's bucket is clamp(floor(l - gl) + 6, 0,
+// 7) with gl = log2 of the ring's mean gap (gl256 = 256 gl, rounded); byte k
+// of the 64-bit table nbt is the block count of bucket k.
+__device__ __forceinline__ uint32_t cz2_nb(int l, int gl256, uint64_t nbt) {
+    int k = ((l * 256 - gl256) >> 8) + 6;  // arithmetic shift: floor
+    k = k < 0 ? 0 : (k > 7 ? 7 : k);
+    return (uint32_t)(nbt >> (8 * k)) & 0xFFu;
 }
+
+// items == nullptr: the main launch (blocks from the plan); else block b
+// takes overflow item b = {first row j, level | rows << 8}.  Either appends
+// its own overflow to ovf.
+template <int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
+                       uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
+                       int gl256, uint64_t nbt, const uint2 *items, uint32_t *ovf_cnt,
+                       uint2 *ovf, uint32_t cap) {
+    auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
+    };
+    auto hiw = [&](uint32_t x) -> uint32_t { return ld32(fv.rs, x); };
+    auto enc = [&](uint32_t par, uint32_t hpar, int l, uint32_t x, uint32_t hx) -> uint32_t {
+        return cz_encode_s(n, gs, par, hpar, l, x, hx, ring);
+    };
+    // win: 256 windows x 16 words (15 W0 or W1 words + the root for W1 / the
+    // W1 CZ_NONE count); before the window phase its first 2 x CZ2_RMAX words
+    // stage the rows' roots A and two-hop roots A1 (compacted in place to the
+    // distinct roots)
+    __shared__ uint32_t win[256 * 16];
+    __shared__ uint32_t ra1[256];  // A1 of each window's root, kept for W1
+    __shared__ uint32_t e0s[CZ2_RMAX];
+    __shared__ uint16_t ridx[CZ2_RMAX];
+    __shared__ uint32_t wcnt[8];
+    __shared__ uint32_t sbad;  // CZ_NONE words written by the block (rare)
+    uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
+    uint32_t j0, rows;
+    int lvl;
+    if (items) {
+        const uint2 it = items[blockIdx.x];
+        j0 = it.x;
+        lvl = (int)(it.y & 0xFFu);
+        rows = it.y >> 8;
+    } else {
+        // block -> (chunk, level, block of the level in the chunk); the level's
+        // blocks are spread over the XCDs with adjacent rows on one XCD
+        uint32_t TB = 0;
+        for (int l = 0; l < nlev; ++l) TB += cz2_nb(lvl_base + l, gl256, nbt);
+        const uint32_t chunk = blockIdx.x / TB;
+        uint32_t rem = blockIdx.x - chunk * TB;
+        lvl = 0;
+        uint32_t nbl = cz2_nb(lvl_base, gl256, nbt);
+        while (rem >= nbl) {
+            rem -= nbl;
+            ++lvl;
+            nbl = cz2_nb(lvl_base + lvl, gl256, nbt);
+        }
+        const uint32_t xm = nbl >> 3, xr = nbl & 7, xx = rem & 7;
+        const uint32_t lbl = xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
+        const uint32_t RB = (CZ2_CHUNK + nbl - 1) / nbl;
+        const uint32_t c0 = lbl * RB;
+        if (c0 >= CZ2_CHUNK) return;  // block-uniform
+        j0 = chunk * CZ2_CHUNK + c0;
+        if (j0 >= M) return;
+        rows = CZ2_CHUNK - c0 < RB ? CZ2_CHUNK - c0 : RB;
+        if (M - j0 < rows) rows = M - j0;
+    }
+    const int i = lvl_base + lvl;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    auto fat = [&](uint32_t x, int l) -> uint32_t {
+        return ld32(fv.F + (size_t)(l - fv.L) * fv.sl, x);
+    };
+    auto c2 = [&](uint32_t x, int l) -> uint32_t {
+        return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
+    };
+    bool oob = false;
+    auto chk = [&](uint32_t x) -> uint32_t {
+        if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
+        return x < n ? x : 0u;
+    };
+    if (t == 0) sbad = 0;
+    // ---- rows (two per lane): roots, two-hop roots, the row's own word ----
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t r = (uint32_t)t + 256u * k;
+        if (r < rows) {
+            uint64_t pw = (uint64_t)p_first + j0 + r;
+            if (pw >= n) pw -= n;
+            const uint32_t p = (uint32_t)pw;
+            const uint32_t A = chk(fat(p, i));
+            const uint32_t A1 = chk(c2(p, i));
+            const uint32_t e0 = enc(p, hiw(p), i, A, hiw(A));
+            e0s[r] = e0;
+            // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
+            if (e0 == CZ_NONE) atomicAdd(&sbad, 2u);
+            stA[r] = A;
+            stA1[r] = A1;
+        }
+    }
+    __syncthreads();
+    // distinct roots in row order: ballot per (row half, wave), eight counts
+    uint32_t A[2], A1[2];
+    bool first[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t r = (uint32_t)t + 256u * k;
+        const bool v = r < rows;
+        A[k] = v ? stA[r] : 0u;
+        A1[k] = v ? stA1[r] : 0u;
+        first[k] = v && (r == 0 || stA[r - 1] != A[k]);
+    }
+    const uint64_t fm0 = __ballot(first[0]), fm1 = __ballot(first[1]);
+    if (lane == 0) {
+        wcnt[wv] = (uint32_t)__popcll(fm0);
+        wcnt[4 + wv] = (uint32_t)__popcll(fm1);
+    }
+    __syncthreads();
+    uint32_t nr = 0, b0 = 0, b1 = 0;
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t c = wcnt[w];
+        b0 += w < wv ? c : 0u;
+        b1 += w < 4 + wv ? c : 0u;
+        nr += c;
+    }
+    const uint32_t rk0 = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm0 >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)fm0, 0u));
+    const uint32_t rk1 = b1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm1 >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)fm1, 0u));
+    __syncthreads();  // every lane has read its neighbour's root
+    if (first[0]) {
+        stA[rk0] = A[0];
+        stA1[rk0] = A1[0];
+    }
+    if (first[1]) {
+        stA[rk1] = A[1];
+        stA1[rk1] = A1[1];
+    }
+    if ((uint32_t)t < rows) ridx[t] = (uint16_t)(rk0 + first[0] - 1);
+    if ((uint32_t)t + 256u < rows) ridx[t + 256] = (uint16_t)(rk1 + first[1] - 1);
+    __syncthreads();
+    // more than cap (256; smaller only to test this path) roots: this block
+    // writes the rows of its first cap roots (rows [0, rhi)), an overflow
+    // launch the rest; rhi = the first row of root cap
+    uint32_t rhi = rows;
+    if (nr > cap) {  // block-uniform
+        uint32_t lo = 0, hi = rows;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ridx[mid] < cap) lo = mid + 1;
+            else hi = mid;
+        }
+        rhi = lo;
+        nr = cap;
+        if (t == 0) ovf[atomicAdd(ovf_cnt, 1u)] = make_uint2(j0 + rhi, (uint32_t)lvl | (rows - rhi) << 8);
+    }
+    const bool wl = (uint32_t)t < nr;
+    uint32_t R = 0, RA1 = 0;
+    if (wl) {
+        R = stA[t];
+        RA1 = stA1[t];
+    }
+    __syncthreads();  // the staged roots are read before win is written
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const size_t tp0 = (size_t)(2 * lvl) * M + j0;
+    uint32_t *wr = win + t * 16;
+    // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
+    if (wl) {
+        ra1[t] = RA1;
+        wr[15] = R;  // the root rides in word 15 into the W1 phase (R < n < 2^30)
+        uint32_t wbad = 0;
+        uint32_t nd[16];
+        nd[0] = R;
+        nd[1] = chk(fat(R, i - 2));
+        nd[2] = chk(fat(R, i - 3));
+        nd[3] = chk(c2(R, i - 2));
+        nd[4] = chk(fat(R, i - 4));
+        nd[6] = chk(c2(R, i - 3));
+        nd[8] = chk(fat(R, i - 5));
+        nd[12] = chk(c2(R, i - 4));
+        nd[5] = chk(fat(nd[1], i - 4));
+        nd[7] = chk(fat(nd[3], i - 4));
+        nd[9] = chk(fat(nd[1], i - 5));
+        nd[10] = chk(fat(nd[2], i - 5));
+        nd[11] = chk(fat(nd[3], i - 5));
+        nd[13] = chk(c2(nd[1], i - 4));
+        nd[14] = chk(c2(nd[2], i - 4));
+        nd[15] = chk(c2(nd[3], i - 4));
+        uint32_t hv[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) hv[v] = hiw(nd[v]);
+#pragma unroll
+        for (int v = 1; v < 16; ++v) {
+            const int hb = 31 - __builtin_clz((unsigned)v);
+            const int pv = v & ~(1 << hb);
+            const uint32_t o = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
+            wbad += o == CZ_NONE;
+            wr[v - 1] = o;
+        }
+        // the window's CZ_NONE count (rare) in the spare top bits: the low two
+        // beside the root, the high two beside A1
+        if (wbad) {
+            wr[15] |= (wbad & 3u) << 30;
+            ra1[t] |= (wbad >> 2) << 30;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // every row carries its root's W0 words
+        const uint32_t r = (uint32_t)t + 256u * k;
+        if (r < rhi) {
+            const uint32_t x = ridx[r];
+            const uint32_t wb = (win[x * 16 + 15] >> 30) | (ra1[x] >> 30) << 2;
+            if (wb) atomicAdd(&sbad, wb);
+        }
+    }
+    // plane 0: rows [0, rhi) x 4 chunks of 16 B, whole lines per store
+    for (uint32_t c = t; c < 4u * rhi; c += 256u) {
+        const uint32_t e = c >> 2, qq = c & 3u;
+        const uint32_t *w = win + ridx[e] * 16;
+        uint32_t u[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const uint32_t word = qq * 4u + (uint32_t)x;
+            u[x] = word == 0 ? e0s[e] : w[word - 1];
+        }
+        const v4u wv4 = {u[0], u[1], u[2], u[3]};
+        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + e) * 4) + qq);
+    }
+    __syncthreads();  // plane 0 has read every W0 word
+    // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
+    if (wl) {
+        uint32_t wbad = 0;
+        uint32_t nd[15];
+        const uint32_t hR = hiw(wr[15] & 0x3FFFFFFFu);  // the root itself is re-read below
+        nd[0] = ra1[t] & 0x3FFFFFFFu;
+        nd[1] = chk(fat(nd[0], i - 2));
+        nd[2] = chk(fat(nd[0], i - 3));
+        nd[3] = chk(c2(nd[0], i - 2));
+        nd[4] = chk(fat(nd[0], i - 4));
+        nd[6] = chk(c2(nd[0], i - 3));
+        nd[8] = chk(fat(nd[0], i - 5));
+        nd[12] = chk(c2(nd[0], i - 4));
+        nd[5] = chk(fat(nd[1], i - 4));
+        nd[7] = chk(fat(nd[3], i - 4));
+        nd[9] = chk(fat(nd[1], i - 5));
+        nd[10] = chk(fat(nd[2], i - 5));
+        nd[11] = chk(fat(nd[3], i - 5));
+        nd[13] = chk(c2(nd[1], i - 4));
+        nd[14] = chk(c2(nd[2], i - 4));
+        uint32_t hv[15];
+#pragma unroll
+        for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
+        const uint32_t o0 = enc(wr[15] & 0x3FFFFFFFu, hR, i - 1, nd[0], hv[0]);
+        wbad += o0 == CZ_NONE;
+        wr[0] = o0;
+#pragma unroll
+        for (int v = 1; v < 15; ++v) {
+            const int hb = 31 - __builtin_clz((unsigned)v);
+            const int pv = v & ~(1 << hb);
+            const uint32_t o = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
+            wbad += o == CZ_NONE;
+            wr[v] = o;
+        }
+        wr[15] = wbad;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // ... and its W1 words
+        const uint32_t r = (uint32_t)t + 256u * k;
+        if (r < rhi) {
+            const uint32_t wb = win[ridx[r] * 16 + 15];
+            if (wb) atomicAdd(&sbad, wb);
+        }
+    }
+    // plane 1: word 15 = the row's own word
+    for (uint32_t c = t; c < 4u * rhi; c += 256u) {
+        const uint32_t e = c >> 2, qq = c & 3u;
+        const uint32_t *w = win + ridx[e] * 16;
+        uint32_t u[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+            const uint32_t word = qq * 4u + (uint32_t)x;
+            u[x] = word == 15 ? e0s[e] : w[word];
+        }
+        const v4u wv4 = {u[0], u[1], u[2], u[3]};
+        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + M + e) * 4) + qq);
+    }
+    if (oob) atomicOr(esc + 1, 1u);
+    __syncthreads();
+    if (t == 0 && sbad) atomicAdd(esc, sbad);
+}
+
+// Block counts of k_cz_build_roots2 (cz2_nb): rows per block ~ 230 /
+// (expected distinct-root fraction of the level), from the level's finger
+// distance 2^i against the ring's mean gap 2^128 / n (uniform ring, by
+// simulation: 0.94 at 2^-4 of the mean gap, 0.89 at 2^-3, 0.80 at 2^-2, 0.685
+// at 2^-1, 0.57 at 1x, 0.51 at 2x, 0.50 from 4x up); a block with more than
+// 256 roots computes them in batches, so the estimate only sizes the blocks.
+static void cz2_plan(size_t n, int &gl256, uint64_t &nbt) {
+    const double gl = 128.0 - log2((double)n);
+    gl256 = (int)lround(gl * 256.0);
+    // bucket k covers floor(l - gl) = k - 6 (k = 0: <= -6, k = 7: >= 1)
+    static const double frac[8] = {0.97, 0.94, 0.89, 0.80, 0.685, 0.57, 0.51, 0.50};
+    nbt = 0;
+    for (int k = 0; k < 8; ++k) {
+        uint32_t rb = (uint32_t)(230.0 / frac[k]);
+        if (rb < 256) rb = 256;
+        if (rb > (uint32_t)CZ2_RMAX) rb = CZ2_RMAX;
+        uint32_t nb = (CZ2_CHUNK + rb - 1) / rb;
+        while ((CZ2_CHUNK + nb - 1) / nb > (uint32_t)CZ2_RMAX) ++nb;
+        nbt |= (uint64_t)nb << (8 * k);
+    }
+}
+
+hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
+                    int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s,
+                    uint32_t *ws) {
+    return cz_build_part(fv, ring, rh, n, l0, R, 0, (uint32_t)n, ib, cz, esc, s, ws);
+}
+
+// Blocks of the main k_cz_build_roots2 launch.
+static uint64_t cz2_blocks(size_t n, int lvl_base, int nlev, uint32_t M) {
+    int gl256;
+    uint64_t nbt;
+    cz2_plan(n, gl256, nbt);
+    uint64_t TB = 0;
+    for (int l = 0; l < nlev; ++l) {
+        int k = (((lvl_base + l) * 256 - gl256) >> 8) + 6;
+        k = k < 0 ? 0 : (k > 7 ? 7 : k);
+        TB += (nbt >> (8 * k)) & 0xFF;
+    }
+    return ((uint64_t)M + CZ2_CHUNK - 1) / CZ2_CHUNK * TB;
+}
+
+// Overflow lists of the default build: two counters (+ padding), then two
+// lists of one uint2 per block.
+size_t cz_build_ws_words(size_t n, int lvl_base, int nlev, uint32_t M) {
+    if (n == 0 || M == 0 || nlev <= 0) return 4;
+    return 4 + 4 * (size_t)cz2_blocks(n, lvl_base, nlev, M);
+}
+
+// Roots per block of k_cz_build_roots2 before it defers rows to an overflow
+// launch: 256 (one window per lane); tests lower it to exercise that path.
+static std::atomic<uint32_t> g_cz2_cap{256};
+uint32_t cz2_cap() { return g_cz2_cap.load(); }
+void cz2_set_cap(uint32_t cap) { g_cz2_cap.store(cap >= 1 && cap <= 256 ? cap : 256); }
 
 hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                          int lvl_base, int nlev, uint32_t p_first, uint32_t M, int ib,
-                         uint64_t *cz, uint32_t *esc, hipStream_t s) {
+                         uint64_t *cz, uint32_t *esc, hipStream_t s, uint32_t *ws) {
     if (M == 0 || nlev <= 0) return hipSuccess;
     if (lvl_base - 5 < fv.L || lvl_base + nlev > fv.L + fv.nl) return hipErrorInvalidValue;
     // the high-word gap codes need every level >= 64 and gs >= 64
@@ -3197,6 +3561,54 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const char *e = getenv("CX_CZ_PAIR");
         return e ? atoi(e) : 0;
     }();
+    if (planes && fv.C2 && fv.roots == 2 && fv.rs && ws) {
+        int gl256;
+        uint64_t nbt;
+        cz2_plan(n, gl256, nbt);
+        const uint64_t blocks = cz2_blocks(n, lvl_base, nlev, M);
+        if (blocks >= (1ull << 31) || nlev > 255) return hipErrorInvalidValue;
+        // two overflow lists (ping-pong), counters in ws[0], ws[1]
+        uint2 *list[2] = {reinterpret_cast<uint2 *>(ws + 4),  // 16-B aligned
+                          reinterpret_cast<uint2 *>(ws + 4) + blocks};
+        hipError_t e = hipMemsetAsync(ws, 0, 2 * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+        const uint32_t cap = cz2_cap();
+        // 66 VGPRs unconstrained: 7 waves per SIMD; CX_CZ2_WPE=8 forces 8 with
+        // 5 spilled VGPRs (A/B)
+        static const int wpe8 = [] {
+            const char *ev = getenv("CX_CZ2_WPE");
+            return ev && atoi(ev) == 8;
+        }();
+        auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
+            if (wpe8)
+                k_cz_build_roots2<8><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                          p_first, M, gs, out, esc, gl256, nbt, it,
+                                                          oc, ov, cap);
+            else
+                k_cz_build_roots2<7><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                          p_first, M, gs, out, esc, gl256, nbt, it,
+                                                          oc, ov, cap);
+        };
+        launch((unsigned)blocks, nullptr, ws, list[0]);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        // blocks with more than cap distinct roots left their last rows on a
+        // list: one block per item takes them (with cap = 256 an item has
+        // < 256 rows and finishes; every round shrinks each item by >= cap rows)
+        for (int round = 0;; ++round) {
+            uint32_t cnt = 0;
+            if ((e = hipMemcpyAsync(&cnt, ws + (round & 1), sizeof(cnt), hipMemcpyDeviceToHost,
+                                    s)) != hipSuccess ||
+                (e = hipStreamSynchronize(s)) != hipSuccess)
+                return e;
+            if (cnt == 0) break;
+            if (cnt > blocks || round >= CZ2_RMAX) return hipErrorInvalidValue;
+            uint32_t *next = ws + ((round + 1) & 1);
+            if ((e = hipMemsetAsync(next, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+            launch(cnt, list[round & 1], next, list[(round + 1) & 1]);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     if (planes && fv.C2 && fv.roots) {
         static const int mode = [] {
             const char *e = getenv("CX_CZ_ROOTS_MODE");

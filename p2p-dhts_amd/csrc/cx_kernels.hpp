@@ -142,7 +142,10 @@ struct FingerView {
     // planes only, optional: two-hop planes C2[(l - L - 1) * sl + x] =
     // F[F[x][l]][l - 1] for l in (L, L + nl) (fingers_pairs)
     const uint32_t *C2 = nullptr;
-    int roots = 0;  // host-side build choice: 1 = root-centric windows (needs C2)
+    // host-side build choice: 1 = root-centric windows, 256 rows per block
+    // (k_cz_build_roots); 2 = blocks sized by distinct roots (k_cz_build_roots2,
+    // needs rs; without it the build falls back to 1); both need C2
+    int roots = 0;
     // root-centric build, optional: 32-bit ID slices (ring_codes) for the gap
     // codes instead of the 64-bit high words; only when every ring gap is
     // below 2^(gs + 17)
@@ -190,8 +193,16 @@ hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s);
 // build when *wide == 0.
 hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint32_t *wide,
                       hipStream_t s);
+// ws (optional, cz_build_ws_words words): the overflow list of the default
+// root-centric build (fv.roots == 2); without it the build takes 256-row blocks
 hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
-                    int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s);
+                    int l0, int R, int ib, uint64_t *cz, uint32_t *esc, hipStream_t s,
+                    uint32_t *ws = nullptr);
+size_t cz_build_ws_words(size_t n, int lvl_base, int nlev, uint32_t M);
+// Distinct roots per block before the default build defers rows to an
+// overflow launch (256; tests only: lower, to exercise that path).
+uint32_t cz2_cap();
+void cz2_set_cap(uint32_t cap);
 hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                     int l0, int R, int ib, const uint32_t *F, const SearchView &sv,
                     const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
@@ -202,7 +213,7 @@ hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, do
                         hipStream_t s);
 hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64_t *rh, size_t n,
                          int lvl_base, int nlev, uint32_t p_first, uint32_t M, int ib,
-                         uint64_t *cz, uint32_t *esc, hipStream_t s);
+                         uint64_t *cz, uint32_t *esc, hipStream_t s, uint32_t *ws = nullptr);
 hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
                      int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo, uint32_t M,
                      int self, const ArcRec *in, const uint32_t *src, const cell128 *keys, size_t q,
