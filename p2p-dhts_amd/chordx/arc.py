@@ -271,6 +271,56 @@ class ArcRouter:
         self.rounds = 2
         return 2
 
+    def successor(self, keys, owner) -> int:
+        """Exact-successor mode of the arc layout: this rank's
+        keys are bucketed by the arc that holds their owner (the arc
+        splitters of cx_arc_build, as the walk's partition), sent there with
+        one all_to_all-v, searched on that rank against its own arc of the
+        ring only (StoredLocally's converged answer, abstract_chord_peer.cpp:
+        720-725, over the arc's IDs), and the owners come back with the
+        splits swapped; owner[i] = the global peer index.  Collective over the
+        group; returns the number of exchange rounds (2; 0 on a single rank
+        without exchange_always, which searches in place)."""
+        eng = self.engine
+        if self.world == 1 and not self.exchange_always:
+            owner.copy_(self._arc_ring().successor(keys).to(owner.dtype))
+            return 0
+        G = self.world
+        zero = self._zeros_src(keys)
+        sk, _, perm, counts = eng.arc_partition(G, zero, keys)[:4]
+        dev = self.comm_device if self.comm_device is not None else sk.device
+        mine = torch.tensor(list(counts), dtype=torch.int64, device=dev)
+        mat = torch.empty((G, G), dtype=torch.int64, device=dev)
+        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
+        m = mat.cpu() if mat.is_cuda else mat
+        recv = [int(m[r, self.rank]) for r in range(G)]
+        rk, work = self._a2a(sk, recv, list(counts), dev)
+        rk = self._land(rk, work, sk)
+        if rk.shape[0]:
+            got = self._arc_ring().successor(rk)  # index in this rank's arc
+            got = (got.to(torch.int64) + self.lo).to(torch.int32)
+        else:  # nothing for this arc (or an empty arc: n < world)
+            got = torch.empty(0, dtype=torch.int32, device=rk.device)
+        back, work = self._a2a(got, list(counts), recv, dev)
+        back = self._land(back, work, perm)
+        owner.copy_(back.to(owner.device)[perm.long()].to(owner.dtype))
+        self.records_sent += int(sum(counts))
+        return 2
+
+    def _zeros_src(self, keys):
+        z = getattr(self, "_zsrc", None)
+        if z is None or z.shape[0] < keys.shape[0] or z.device != keys.device:
+            z = torch.zeros(keys.shape[0], dtype=torch.int32, device=keys.device)
+            self._zsrc = z
+        return z[:keys.shape[0]]
+
+    def _arc_ring(self):
+        """This rank's arc of the ring as its own searchable ring (built once):
+        the exact-successor mode holds only these IDs."""
+        if getattr(self, "_arc", None) is None:
+            self._arc = self.engine.arc_local_ring(self.lo, self.hi)
+        return self._arc
+
     def route(self, src, keys, owner, hops, status=None, key_first=None, protocol=None) -> int:
         """Routes this rank's lookups (issued at peers src[i]); collective over
         the group.  Writes owner/hops/status at the lookups' indices and

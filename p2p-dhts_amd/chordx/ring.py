@@ -608,6 +608,14 @@ class Ring:
         L.check(L.lib().cx_arc_deliver(self._h, _ptr(res), _ptr(perm) if perm is not None
                                        else None, q, _ptr(owner), _ptr(hops), _ptr(status)))
 
+    def arc_local_ring(self, lo: int, hi: int) -> "Ring":
+        """Peers [lo, hi) of this ring as a ring of their own (the arc a rank
+        holds in the arc layout's exact-successor mode); its successor()
+        answers indices relative to lo."""
+        if not 0 <= lo < hi <= self.n:
+            raise ValueError("arc must be a non-empty range of peers")
+        return Ring(self.ids_device()[lo:hi].contiguous(), device=self.device)
+
     def arc_bucket(self, world: int, recs):
         """(send, counts): records grouped by destination rank, NONE dropped."""
         q = recs.shape[0]

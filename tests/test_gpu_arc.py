@@ -510,7 +510,14 @@ def _rccl_worker(_i, n, q, chunks, out):
         torch.cuda.synchronize()
         res.append((bool(torch.equal(ow, owner)), bool(torch.equal(hp, hops)),
                     bool(torch.equal(st, status)), rounds, router.records_sent))
-    out[0] = (tdist.get_backend(), res, int((st == chordx.CX_Q_BADPEER).sum().item()))
+    # the exact-successor mode over the same group (keys to their owner's arc,
+    # searched on the arc's own ring, owners back)
+    own = torch.full((q,), -3, dtype=torch.int32, device=dev)
+    router.records_sent = 0
+    rs = router.successor(keys, own)
+    torch.cuda.synchronize()
+    succ_ok = (bool(torch.equal(own, ring.successor(keys))), rs, router.records_sent)
+    out[0] = (tdist.get_backend(), res, int((st == chordx.CX_Q_BADPEER).sum().item()), succ_ok)
     tdist.destroy_process_group()
 
 
@@ -521,7 +528,48 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
     out = mgr.dict()
     mp.start_processes(_rccl_worker, args=(1 << 20, q, chunks, out), nprocs=1, join=True,
                        start_method="spawn")
-    backend, res, bad = out[0]
+    backend, res, bad, succ_ok = out[0]
     assert backend == "nccl" and bad == len(range(0, q, 97))
     for r in res:
         assert r == (True, True, True, 2, q), r
+    assert succ_ok == (True, 2, q)
+
+
+@pytest.mark.parametrize("G", [2, 8])
+def test_arc_exact_successor_simulated_ranks(cx, O, G):
+    """Exact-successor mode, G ranks simulated on one GPU: every rank's region
+    of every origin's partition is searched against that rank's arc of the
+    ring only (arc_local_ring); owners equal the full ring's successors and
+    the oracle's."""
+    import torch
+    n, per = 70001, 1 << 16
+    ids = O.splitmix_keys(0xA7E0, n)
+    ring = cx.Ring(ids)
+    want_ring = O.ring_build(ids)
+    keys = torch.from_numpy(edge_keys_arc(O, want_ring, 0xA7E1, G * per).view(np.int64)).cuda()
+    src = torch.zeros(keys.shape[0], dtype=torch.int32, device="cuda")
+    for d in range(G):
+        ring.arc_build(G, d)
+        lo, hi = d * ring.n // G, (d + 1) * ring.n // G
+        sub = ring.arc_local_ring(lo, hi)
+        got, want = [], []
+        for r in range(G):
+            sl = slice(r * per, (r + 1) * per)
+            sk, _, perm, counts = ring.arc_partition(G, src[sl], keys[sl])
+            off = sum(counts[:d])
+            kd = sk[off:off + counts[d]]
+            got.append(sub.successor(kd).to(torch.int64) + lo)
+            want.append(ring.successor(kd).to(torch.int64))
+        got, want = torch.cat(got), torch.cat(want)
+        assert torch.equal(got, want) and bool(((want >= lo) & (want < hi)).all())
+    assert (ring.successor(keys.cpu().numpy().view(np.uint64)) ==
+            O.successor(want_ring, keys.cpu().numpy().view(np.uint64))).all()
+
+
+def edge_keys_arc(O, ring, seed, q):
+    """Uniform keys with peer IDs, their neighbours and the ring's wrap mixed in."""
+    k = O.splitmix_keys(seed, q)
+    m = min(len(ring), q // 8)
+    k[:m] = ring[(np.arange(m) * 7919) % len(ring)]
+    k[m] = np.array([2**64 - 1, 2**64 - 1], dtype=np.uint64)
+    return k

@@ -193,6 +193,18 @@ class OracleArcEngine:
             if status is not None:
                 status[i] = (w >> 40) & 0xFF
 
+    def arc_local_ring(self, lo, hi):
+        """The arc's IDs as their own ring: successor() -> int32 indices in it."""
+        import torch
+        import oracle as O
+        sub = np.ascontiguousarray(self.P.ring[lo:hi])
+
+        class _Arc:
+            def successor(self, keys):
+                k = keys.numpy().view(np.uint64).reshape(-1, 2)
+                return torch.from_numpy(O.successor(sub, k).astype(np.int32))
+        return _Arc()
+
     def arc_bucket(self, world, recs):
         import torch
         import oracle as O
@@ -350,6 +362,57 @@ def test_arc_router_soa_world1_exchanges_with_itself_gloo(regions):
     assert out[0][3] == 2 and out[0][4] == per_rank  # two rounds, every lookup exchanged
 
 
+def _succ_worker(rank, world, port, per_rank, out, exchange_always):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "p2p-dhts_amd"), os.path.join(root, "oracle"),
+                    os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as tdist
+    import oracle as O
+    from chordx import dist
+    from chordx.arc import ArcRouter
+    from test_multiproc import OracleArcEngine
+    dist.init("gloo")
+    if world == 1:
+        assert dist.init_single("gloo")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    P = O.Peers(ring, O.fingers(ring, threads=2))
+    keys = O.splitmix_keys(0x5EED0016, per_rank, offset=rank * per_rank)
+    # keys at and around peer IDs, and past the last peer (owner: peer 0)
+    keys[:40] = ring[(np.arange(40) * 71) % len(ring)]
+    keys[40] = np.array([2**64 - 1, 2**64 - 1], dtype=np.uint64)
+    owner = torch.full((per_rank,), -9, dtype=torch.int32)
+    router = ArcRouter(OracleArcEngine(P, len(ring)), len(ring), rank, world,
+                       exchange_always=exchange_always)
+    rounds = router.successor(torch.from_numpy(keys.view(np.int64).copy()), owner)
+    out[rank] = (owner.numpy().view(np.uint32).tolist(), rounds, router.records_sent)
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,exchange_always", [(1, True), (2, False), (3, False)])
+def test_arc_exact_successor_gloo(world, exchange_always):
+    """Exact-successor mode of the arc layout: keys bucketed by
+    their owner's arc, all_to_all-v, searched against that rank's arc of the
+    ring only, owners back -- equal to the oracle's StoredLocally answer."""
+    import oracle as O
+    per_rank = 400
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_succ_worker, args=(world, _free_port(), per_rank, out, exchange_always),
+                       nprocs=world, join=True, start_method="spawn")
+    ring = O.ring_build(O.splitmix_keys(0x5EED0005, 3000))
+    for r in range(world):
+        keys = O.splitmix_keys(0x5EED0016, per_rank, offset=r * per_rank)
+        keys[:40] = ring[(np.arange(40) * 71) % len(ring)]
+        keys[40] = np.array([2**64 - 1, 2**64 - 1], dtype=np.uint64)
+        assert out[r][0] == O.successor(ring, keys).tolist()
+        assert out[r][0][40] == 0
+        assert out[r][1] == 2 and out[r][2] == per_rank
+
+
 def test_bench_launches_n_ranks_itself():
     """`bench.py --gpus 2` without torchrun starts torch.distributed.run as a
     child and rank 0 of that job reports n_gpus = 2 (CX_BENCH_DRYRUN: the
@@ -373,6 +436,9 @@ def test_bench_launches_n_ranks_itself():
     # every world size carries the CPU baseline (rank 0) and the whole-node roofline
     assert rec["cpu_baseline"] is not None and rec["cpu_baseline"]["value"] > 0
     assert rec["cpu_baseline"]["n_gpus_beside"] == 2
+    # the oracle sample's hop histogram: one bin per hop count
+    hist = rec["cpu_baseline"]["hops_hist"]
+    assert hist[0] >= 0 and sum(hist) > 0 and hist[-1] > 0
     assert rec["roofline"]["n_gpus"] == 2 and rec["roofline"]["peak"] == 2 * 8000.0
 
 
