@@ -334,7 +334,7 @@ def _route_rounds(rings, keys, srcs, dev, rounds=6, per=3):
     return {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
 
 
-def churn_leg(ring, keys, src, dev, depth_ab=32):
+def churn_leg(ring, keys, src, dev, depth_ab=28):
     """1 % joins + 1 % leaves of the bench ring -> route-ready.  Every epoch
     states its allocation path: the table pool's counters around it
     (chordx.pool_stats: bytes fresh from hipMalloc -- first-touch page

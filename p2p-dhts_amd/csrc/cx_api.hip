@@ -620,16 +620,16 @@ int build_search(cx_ring *r, hipStream_t s) {
     return CX_OK;
 }
 
-// Route-table levels [l0, 128): l0 = 128 - R, R = ceil(log2 n) + 4 rounded up
-// to 4 (28 at 2^24; ib = index bits of a packed finger).  Below the table the
-// walk takes exact hops: ~0.05 per lookup at R = log2 n + 4, 0.004 at + 8.
-// Measured at 2^24 in one process, both build orders: R = 28
-// routes within noise of R = 32 (-0.8 %) and builds 8 GiB less table, churn ->
-// route-ready 24.4-24.8 vs 26.3-27.1 ms.
+// Route-table levels [l0, 128): l0 = 128 - R, R = ceil(log2 n) + 8 rounded up
+// to 4 (32 at 2^24; ib = index bits of a packed finger).  Below the table the
+// walk takes exact hops: 0.004 per lookup at R = log2 n + 8, ~0.05 at + 4.
+// Measured at 2^24 in the bench's ABBA leg: R = 32 routes
+// 2.1 / 3.2 % faster per launch than R = 28 with either ring built first, for
+// 8 GiB more table and ~2.8 ms more churn -> route-ready.
 void route_geometry(cx_ring *r) {
     int lg = 0;
     while (((size_t)1 << lg) < r->n) ++lg;
-    int R = ((lg + 4 + 3) / 4) * 4;
+    int R = ((lg + 8 + 3) / 4) * 4;
     // CX_ROUTE_R: table depth override (A/B of table size against exact hops)
     static const int r_env = [] {
         const char *e = getenv("CX_ROUTE_R");

@@ -230,7 +230,7 @@ def test_route_default_variant_and_escapes(cx, O):
     ring = cx.Ring(O.splitmix_keys(77, 20000))
     ring.build_fingers()
     v, esc, nbytes = ring.route_info()
-    assert v == 5 and esc == 0 and nbytes == 20000 * 20 * 128  # R = 15 + 4 -> 20
+    assert v == 5 and esc == 0 and nbytes == 20000 * 24 * 128  # R = 15 + 8 -> 24
     ids = clustered_ring(O, 3000, 5, 8)
     ring = cx.Ring(ids)
     F = ring.build_fingers(copy_out=True)

@@ -2,8 +2,8 @@
 finger levels [128 - R, 128) and the walk takes exact hops below it
 (ClosestPrecedingFinger over the finger table, chord_peer.cpp:157-176, one
 level at a time).  The depth changes only where a hop's finger comes from, so
-owners, hop counts and statuses must not depend on R.  Default R = log2 n + 4
-rounded up to 4 (28 at 2^24); cxi_set_route_depth overrides it per ring before
+owners, hop counts and statuses must not depend on R.  Default R = log2 n + 8
+rounded up to 4 (32 at 2^24); cxi_set_route_depth overrides it per ring before
 its first finger build."""
 import numpy as np
 import pytest
@@ -23,7 +23,7 @@ def default_depth(n):
     lg = 0
     while (1 << lg) < n:
         lg += 1
-    return max(16, (lg + 4 + 3) // 4 * 4)
+    return max(16, (lg + 8 + 3) // 4 * 4)
 
 
 @pytest.mark.parametrize("n", [20000, (1 << 18) + 3, 1 << 20])
@@ -56,7 +56,7 @@ def depth_setup(cx, O):
 
 
 # 16: the shallowest table (many exact hops); 20 / 32: either side of the
-# default 24 at this size; 40: planes below the streaming tile's first level
+# default 28 at this size; 40: planes below the streaming tile's first level
 # (the build reads them from the finger rows); 59: the deepest the pattern-keyed
 # build takes (its lowest plane level 128 - R - 5 must be >= 64)
 @pytest.mark.parametrize("R", [16, 20, 32, 40, 59])
@@ -66,7 +66,10 @@ def test_depth_override_same_routes(cx, depth_setup, R):
     ring.set_route_depth(R)
     ring.build_fingers()
     v, esc, nbytes = ring.route_info()
-    assert v == 5 and esc < ring.n * R * 32 // 1000 and nbytes == ring.n * R * 128
+    assert v == 5 and nbytes == ring.n * R * 128
+    # escapes (nodes the walk takes exactly) stay rare down to ~2^-16 of the
+    # mean gap; levels far below it (R = 59 here: 2^-41) hold mostly escapes
+    assert R > 40 or esc < ring.n * R * 32 // 1000
     o, h, s = ring.route(src, keys)
     assert (o == ob).all() and (h == hb).all() and (s == 0).all()
 
