@@ -653,7 +653,8 @@ void route_geometry(cx_ring *r) {
 // planes in `ft` when HBM allows (cxi_set_table_build(ring, 1) forces the
 // row-major table, for A/B), else the row-major table itself.
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
-                         DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr) {
+                         DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr,
+                         DBuf *pp = nullptr) {
     fv = cxk::FingerView::rows(r->d_fingers);
     // gap codes of the root-centric build: 32-bit ID slices when every ring gap
     // is below 2^(gs + 17) (uniform rings by far), else the 64-bit high words
@@ -663,7 +664,8 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         return e && strcmp(e, "hi") == 0;
     }();
     bool slices = false;
-    if ((r->table_build == 0 || r->table_build == 4) && !hi_only) {
+    const bool roots_build = r->table_build == 0 || r->table_build == 4 || r->table_build == 5;
+    if (roots_build && !hi_only) {
         hipError_t e1 = hi.alloc_pooled(r->n * sizeof(uint32_t), s);
         uint32_t *d_wide = r->d_scratch + 100;
         if (e1 == hipSuccess)
@@ -696,14 +698,29 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         if (e != hipSuccess) return e;
         fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
-    if (have_planes && (r->table_build == 0 || r->table_build == 3 || r->table_build == 4) &&
+    // default build: pair planes {finger, ID slice} and two-hop pairs (one 8-B
+    // gather per window node instead of two 4-B ones); table_build 5 keeps the
+    // 4-B planes for A/B
+    if (have_planes && slices && r->table_build == 0 && pp &&
+        pp->alloc_pooled((size_t)nl * r->n * sizeof(uint2), s) == hipSuccess &&
+        c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint2), s) == hipSuccess) {
+        e = cxk::fingers_pairs2(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint2>(), c2.as<uint2>(), s);
+        if (e != hipSuccess) return e;
+        fv.P = pp->as<uint2>();
+        fv.P2 = c2.as<uint2>();
+        fv.roots = 2;
+        fv.rs = hi.as<uint32_t>();
+        return hipSuccess;
+    }
+    (void)hipGetLastError();
+    if (have_planes && (roots_build || r->table_build == 3) &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t), s) == hipSuccess) {
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) {
             fv.C2 = c2.as<uint32_t>();
             // 0: blocks sized by distinct roots, 4: 256-row root blocks (round 3),
             // 3: one lane per entry (round 2)
-            fv.roots = r->table_build == 0 ? 2 : (r->table_build == 4 ? 1 : 0);
+            fv.roots = (r->table_build == 0 || r->table_build == 5) ? 2 : (r->table_build == 4 ? 1 : 0);
         }
     }
     (void)hipGetLastError();
@@ -734,12 +751,12 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
         }
         if (r->d_cz) {
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
-            DBuf ft, hi, c2;
+            DBuf ft, hi, c2, pp;
             cxk::FingerView fv;
             if (!ft_pre || r->table_build == 1) {  // the planes come from the rows
                 if (int rc = ensure_fingers_rows(r, s)) return rc;
             }
-            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre));
+            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre, &pp));
             DBuf ws;  // the default build's overflow list
             if (fv.roots == 2)
                 CX_HIP(ws.alloc_pooled(cxk::cz_build_ws_words(r->n, r->rt_l0, r->rt_R, (uint32_t)r->n) *
@@ -1139,16 +1156,14 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     static const bool eager_rows = getenv("CX_FINGERS_ROWS") != nullptr;
     const int ft_l = ring->rt_l0 - 5;
     const bool defer = !eager_rows && !fingers_out && ring->variant() == 5 &&
-                       (ring->table_build == 0 || ring->table_build == 3 ||
-                        ring->table_build == 4) && ft_l >= 64 &&
+                       (ring->table_build == 0 || ring->table_build >= 3) && ft_l >= 64 &&
                        ring->n >= ((size_t)1 << 18) && ft_l >= cxk::FINGERS_TILE_L0;
     // the default route table reads the fingers as level planes: the streaming
     // finger build writes them alongside the rows (no transpose pass), and the
     // ring keeps them for the finger repair of the next churn
     std::shared_ptr<PlaneSet> ps;
     bool ft_done = false;
-    if (ring->variant() == 5 &&
-        (ring->table_build == 0 || ring->table_build == 3 || ring->table_build == 4) && ft_l >= 64) {
+    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build >= 3) && ft_l >= 64) {
         const int nl = (int)CX_FINGERS - ft_l;
         const size_t bytes = (size_t)nl * ring->n * sizeof(uint32_t);
         void *pp = nullptr;
@@ -2053,9 +2068,9 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     ring->arc_bytes = (top_ent + low_ent) * 64 + 64;
     CX_HIP(hipMemsetAsync(ring->d_scratch, 0, 2 * sizeof(uint32_t), s));
     {
-        DBuf ft, hi, c2;
+        DBuf ft, hi, c2, pp;
         cxk::FingerView fv;
-        CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s));
+        CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s, nullptr, &pp));
         DBuf ws;  // the default build's overflow list (sized for the larger part)
         if (fv.roots == 2) {
             const size_t w0 = cxk::cz_build_ws_words(n, Lh, (int)CX_FINGERS - Lh, (uint32_t)n);
@@ -2482,15 +2497,16 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
     return CX_OK;
 }
 
-// Route-table build input: 0 = finger level + two-hop planes, root-centric
-// windows in blocks sized by distinct roots (k_cz_build_roots2, default),
-// 1 = row-major finger table, 2 = level planes only, 3 = level + two-hop
-// planes, one lane per entry (k_cz_build, the round-2 build), 4 = root-centric
-// windows in 256-row blocks (k_cz_build_roots, round 3).  All give the same
-// table.  Takes effect at the next finger build.
+// Route-table build input: 0 = pair planes {finger, ID slice} + two-hop
+// pairs, root-centric windows in blocks sized by distinct roots
+// (k_cz_build_roots2<PAIR>, default), 1 = row-major finger table, 2 = level
+// planes only, 3 = level + two-hop planes, one lane per entry (k_cz_build, the
+// round-2 build), 4 = root-centric windows in 256-row blocks
+// (k_cz_build_roots, round 3), 5 = as 0 on 4-B planes (no pairs).  All give
+// the same table.  Takes effect at the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 4, CX_E_INVALID, "variant must be 0 .. 4");
+    CX_CHECK(variant >= 0 && variant <= 5, CX_E_INVALID, "variant must be 0 .. 5");
     ring->table_build = variant;
     return CX_OK;
 }

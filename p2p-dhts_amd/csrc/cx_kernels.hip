@@ -2397,6 +2397,41 @@ hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hip
     return hipGetLastError();
 }
 
+// Pair planes for the default route-table build: each finger with its 32-bit
+// ID slice beside it, P[k][x] = {F[x][L + k], rs[F[x][L + k]]} (k < nl), and
+// the two-hop planes likewise, P2[k - 1][x] = {z, rs[z]} with z =
+// F[F[x][L + k]][L + k - 1] (k >= 1).  The build's cost is the number of
+// vector-memory instructions its window gathers issue (the texture addresser
+// is busy for the whole build, profiles/r04/build_pmc/): a window node and its
+// slice then come in one 8-B gather instead of two 4-B ones.  One lane per
+// (peer, level): the plane read is coalesced, the gathers land near each
+// other (the fingers of adjacent peers), the pairs leave as coalesced 8-B
+// streaming stores.
+__global__ void k_fingers_pairs2(const uint32_t *FT, const uint32_t *rs, uint32_t n, int nl,
+                                 uint2 *P, uint2 *P2) {
+    const size_t k = blockIdx.y;
+    const uint32_t *up = FT + k * (size_t)n;
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const uint32_t y = up[x];
+        const v2u py = {y, y < n ? rs[y] : 0u};
+        __builtin_nontemporal_store(py, reinterpret_cast<v2u *>(P + k * (size_t)n + x));
+        if (k) {
+            const uint32_t z = y < n ? FT[(k - 1) * (size_t)n + y] : CX_NONE;
+            const v2u pz = {z, z < n ? rs[z] : 0u};
+            __builtin_nontemporal_store(pz, reinterpret_cast<v2u *>(P2 + (k - 1) * (size_t)n + x));
+        }
+    }
+}
+
+hipError_t fingers_pairs2(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint2 *P,
+                          uint2 *P2, hipStream_t s) {
+    if (n == 0 || nl < 2) return hipSuccess;
+    k_fingers_pairs2<<<dim3(cx_grid(n, 256, 4096), (unsigned)nl), 256, 0, s>>>(
+        FT, rs, (uint32_t)n, nl, P, P2);
+    return hipGetLastError();
+}
+
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s) {
     if (n == 0 || nl <= 0) return hipSuccess;
@@ -3180,7 +3215,7 @@ __device__ __forceinline__ uint32_t cz2_nb(int l, int gl256, uint64_t nbt) {
 // items == nullptr: the main launch (blocks from the plan); else block b
 // takes overflow item b = {first row j, level | rows << 8}.  Either appends
 // its own overflow to ovf.
-template <int WPE>
+template <int WPE, bool PAIR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
                        uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
@@ -3203,7 +3238,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     __shared__ uint16_t ridx[CZ2_RMAX];
     __shared__ uint32_t wcnt[8];
     __shared__ uint32_t sbad;  // CZ_NONE words written by the block (rare)
+    // PAIR: the slices of each window's root and of its A1, kept for W1
+    __shared__ uint32_t rsR[PAIR ? 256 : 1], ra1s[PAIR ? 256 : 1];
     uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
+    uint32_t *stS = win + 2 * CZ2_RMAX, *stS1 = win + 3 * CZ2_RMAX;  // PAIR: their slices
     uint32_t j0, rows;
     int lvl;
     if (items) {
@@ -3243,6 +3281,13 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     auto c2 = [&](uint32_t x, int l) -> uint32_t {
         return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
     };
+    // PAIR: {finger, its ID slice} in one 8-B gather (uniform plane base plus a
+    // 32-bit byte offset, x < n < 2^29)
+    auto ld64 = [](const uint2 *base, uint32_t x) -> uint2 {
+        return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + x * 8u);
+    };
+    auto fatp = [&](uint32_t x, int l) -> uint2 { return ld64(fv.P + (size_t)(l - fv.L) * n, x); };
+    auto c2p = [&](uint32_t x, int l) -> uint2 { return ld64(fv.P2 + (size_t)(l - fv.L - 1) * n, x); };
     bool oob = false;
     auto chk = [&](uint32_t x) -> uint32_t {
         if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
@@ -3257,9 +3302,20 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             uint64_t pw = (uint64_t)p_first + j0 + r;
             if (pw >= n) pw -= n;
             const uint32_t p = (uint32_t)pw;
-            const uint32_t A = chk(fat(p, i));
-            const uint32_t A1 = chk(c2(p, i));
-            const uint32_t e0 = enc(p, hiw(p), i, A, hiw(A));
+            uint32_t A, A1, sA;
+            if constexpr (PAIR) {
+                const uint2 a = fatp(p, i), a1 = c2p(p, i);
+                A = chk(a.x);
+                A1 = chk(a1.x);
+                sA = a.y;
+                stS[r] = a.y;
+                stS1[r] = a1.y;
+            } else {
+                A = chk(fat(p, i));
+                A1 = chk(c2(p, i));
+                sA = hiw(A);
+            }
+            const uint32_t e0 = enc(p, hiw(p), i, A, sA);
             e0s[r] = e0;
             // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
             if (e0 == CZ_NONE) atomicAdd(&sbad, 2u);
@@ -3269,7 +3325,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     }
     __syncthreads();
     // distinct roots in row order: ballot per (row half, wave), eight counts
-    uint32_t A[2], A1[2];
+    uint32_t A[2], A1[2], S[2], S1[2];
     bool first[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -3277,6 +3333,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         const bool v = r < rows;
         A[k] = v ? stA[r] : 0u;
         A1[k] = v ? stA1[r] : 0u;
+        if constexpr (PAIR) {
+            S[k] = v ? stS[r] : 0u;
+            S1[k] = v ? stS1[r] : 0u;
+        }
         first[k] = v && (r == 0 || stA[r - 1] != A[k]);
     }
     const uint64_t fm0 = __ballot(first[0]), fm1 = __ballot(first[1]);
@@ -3300,10 +3360,18 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (first[0]) {
         stA[rk0] = A[0];
         stA1[rk0] = A1[0];
+        if constexpr (PAIR) {
+            stS[rk0] = S[0];
+            stS1[rk0] = S1[0];
+        }
     }
     if (first[1]) {
         stA[rk1] = A[1];
         stA1[rk1] = A1[1];
+        if constexpr (PAIR) {
+            stS[rk1] = S[1];
+            stS1[rk1] = S1[1];
+        }
     }
     if ((uint32_t)t < rows) ridx[t] = (uint16_t)(rk0 + first[0] - 1);
     if ((uint32_t)t + 256u < rows) ridx[t + 256] = (uint16_t)(rk1 + first[1] - 1);
@@ -3324,10 +3392,14 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         if (t == 0) ovf[atomicAdd(ovf_cnt, 1u)] = make_uint2(j0 + rhi, (uint32_t)lvl | (rows - rhi) << 8);
     }
     const bool wl = (uint32_t)t < nr;
-    uint32_t R = 0, RA1 = 0;
+    uint32_t R = 0, RA1 = 0, SR = 0, SRA1 = 0;
     if (wl) {
         R = stA[t];
         RA1 = stA1[t];
+        if constexpr (PAIR) {
+            SR = stS[t];
+            SRA1 = stS1[t];
+        }
     }
     __syncthreads();  // the staged roots are read before win is written
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -3338,26 +3410,55 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         ra1[t] = RA1;
         wr[15] = R;  // the root rides in word 15 into the W1 phase (R < n < 2^30)
         uint32_t wbad = 0;
-        uint32_t nd[16];
+        uint32_t nd[16], hv[16];
         nd[0] = R;
-        nd[1] = chk(fat(R, i - 2));
-        nd[2] = chk(fat(R, i - 3));
-        nd[3] = chk(c2(R, i - 2));
-        nd[4] = chk(fat(R, i - 4));
-        nd[6] = chk(c2(R, i - 3));
-        nd[8] = chk(fat(R, i - 5));
-        nd[12] = chk(c2(R, i - 4));
-        nd[5] = chk(fat(nd[1], i - 4));
-        nd[7] = chk(fat(nd[3], i - 4));
-        nd[9] = chk(fat(nd[1], i - 5));
-        nd[10] = chk(fat(nd[2], i - 5));
-        nd[11] = chk(fat(nd[3], i - 5));
-        nd[13] = chk(c2(nd[1], i - 4));
-        nd[14] = chk(c2(nd[2], i - 4));
-        nd[15] = chk(c2(nd[3], i - 4));
-        uint32_t hv[16];
+        if constexpr (PAIR) {
+            rsR[t] = SR;
+            ra1s[t] = SRA1;
+            hv[0] = SR;
+            uint2 q[16];
+            q[1] = fatp(R, i - 2);
+            q[2] = fatp(R, i - 3);
+            q[3] = c2p(R, i - 2);
+            q[4] = fatp(R, i - 4);
+            q[6] = c2p(R, i - 3);
+            q[8] = fatp(R, i - 5);
+            q[12] = c2p(R, i - 4);
+            nd[1] = chk(q[1].x);
+            nd[2] = chk(q[2].x);
+            nd[3] = chk(q[3].x);
+            q[5] = fatp(nd[1], i - 4);
+            q[7] = fatp(nd[3], i - 4);
+            q[9] = fatp(nd[1], i - 5);
+            q[10] = fatp(nd[2], i - 5);
+            q[11] = fatp(nd[3], i - 5);
+            q[13] = c2p(nd[1], i - 4);
+            q[14] = c2p(nd[2], i - 4);
+            q[15] = c2p(nd[3], i - 4);
 #pragma unroll
-        for (int v = 0; v < 16; ++v) hv[v] = hiw(nd[v]);
+            for (int v = 1; v < 16; ++v) {
+                nd[v] = chk(q[v].x);
+                hv[v] = q[v].y;
+            }
+        } else {
+            nd[1] = chk(fat(R, i - 2));
+            nd[2] = chk(fat(R, i - 3));
+            nd[3] = chk(c2(R, i - 2));
+            nd[4] = chk(fat(R, i - 4));
+            nd[6] = chk(c2(R, i - 3));
+            nd[8] = chk(fat(R, i - 5));
+            nd[12] = chk(c2(R, i - 4));
+            nd[5] = chk(fat(nd[1], i - 4));
+            nd[7] = chk(fat(nd[3], i - 4));
+            nd[9] = chk(fat(nd[1], i - 5));
+            nd[10] = chk(fat(nd[2], i - 5));
+            nd[11] = chk(fat(nd[3], i - 5));
+            nd[13] = chk(c2(nd[1], i - 4));
+            nd[14] = chk(c2(nd[2], i - 4));
+            nd[15] = chk(c2(nd[3], i - 4));
+#pragma unroll
+            for (int v = 0; v < 16; ++v) hv[v] = hiw(nd[v]);
+        }
 #pragma unroll
         for (int v = 1; v < 16; ++v) {
             const int hb = 31 - __builtin_clz((unsigned)v);
@@ -3400,26 +3501,54 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
     if (wl) {
         uint32_t wbad = 0;
-        uint32_t nd[15];
-        const uint32_t hR = hiw(wr[15] & 0x3FFFFFFFu);  // the root itself is re-read below
+        uint32_t nd[15], hv[15];
+        uint32_t hR;
         nd[0] = ra1[t] & 0x3FFFFFFFu;
-        nd[1] = chk(fat(nd[0], i - 2));
-        nd[2] = chk(fat(nd[0], i - 3));
-        nd[3] = chk(c2(nd[0], i - 2));
-        nd[4] = chk(fat(nd[0], i - 4));
-        nd[6] = chk(c2(nd[0], i - 3));
-        nd[8] = chk(fat(nd[0], i - 5));
-        nd[12] = chk(c2(nd[0], i - 4));
-        nd[5] = chk(fat(nd[1], i - 4));
-        nd[7] = chk(fat(nd[3], i - 4));
-        nd[9] = chk(fat(nd[1], i - 5));
-        nd[10] = chk(fat(nd[2], i - 5));
-        nd[11] = chk(fat(nd[3], i - 5));
-        nd[13] = chk(c2(nd[1], i - 4));
-        nd[14] = chk(c2(nd[2], i - 4));
-        uint32_t hv[15];
+        if constexpr (PAIR) {
+            hR = rsR[t];
+            hv[0] = ra1s[t];
+            uint2 q[15];
+            q[1] = fatp(nd[0], i - 2);
+            q[2] = fatp(nd[0], i - 3);
+            q[3] = c2p(nd[0], i - 2);
+            q[4] = fatp(nd[0], i - 4);
+            q[6] = c2p(nd[0], i - 3);
+            q[8] = fatp(nd[0], i - 5);
+            q[12] = c2p(nd[0], i - 4);
+            nd[1] = chk(q[1].x);
+            nd[2] = chk(q[2].x);
+            nd[3] = chk(q[3].x);
+            q[5] = fatp(nd[1], i - 4);
+            q[7] = fatp(nd[3], i - 4);
+            q[9] = fatp(nd[1], i - 5);
+            q[10] = fatp(nd[2], i - 5);
+            q[11] = fatp(nd[3], i - 5);
+            q[13] = c2p(nd[1], i - 4);
+            q[14] = c2p(nd[2], i - 4);
 #pragma unroll
-        for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
+            for (int v = 1; v < 15; ++v) {
+                nd[v] = chk(q[v].x);
+                hv[v] = q[v].y;
+            }
+        } else {
+            hR = hiw(wr[15] & 0x3FFFFFFFu);  // the root itself is re-read below
+            nd[1] = chk(fat(nd[0], i - 2));
+            nd[2] = chk(fat(nd[0], i - 3));
+            nd[3] = chk(c2(nd[0], i - 2));
+            nd[4] = chk(fat(nd[0], i - 4));
+            nd[6] = chk(c2(nd[0], i - 3));
+            nd[8] = chk(fat(nd[0], i - 5));
+            nd[12] = chk(c2(nd[0], i - 4));
+            nd[5] = chk(fat(nd[1], i - 4));
+            nd[7] = chk(fat(nd[3], i - 4));
+            nd[9] = chk(fat(nd[1], i - 5));
+            nd[10] = chk(fat(nd[2], i - 5));
+            nd[11] = chk(fat(nd[3], i - 5));
+            nd[13] = chk(c2(nd[1], i - 4));
+            nd[14] = chk(c2(nd[2], i - 4));
+#pragma unroll
+            for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
+        }
         const uint32_t o0 = enc(wr[15] & 0x3FFFFFFFu, hR, i - 1, nd[0], hv[0]);
         wbad += o0 == CZ_NONE;
         wr[0] = o0;
@@ -3561,7 +3690,8 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const char *e = getenv("CX_CZ_PAIR");
         return e ? atoi(e) : 0;
     }();
-    if (planes && fv.C2 && fv.roots == 2 && fv.rs && ws) {
+    if (fv.P && !(ws && fv.rs && fv.P2)) return hipErrorInvalidValue;  // pairs: roots2 only
+    if (planes && (fv.C2 || fv.P2) && fv.roots == 2 && fv.rs && ws) {
         int gl256;
         uint64_t nbt;
         cz2_plan(n, gl256, nbt);
@@ -3580,14 +3710,18 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             return ev && atoi(ev) == 8;
         }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
-            if (wpe8)
-                k_cz_build_roots2<8><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                          p_first, M, gs, out, esc, gl256, nbt, it,
-                                                          oc, ov, cap);
+            if (fv.P && fv.P2)  // pair planes (the default when they fit)
+                k_cz_build_roots2<7, true><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
+                                                                nlev, p_first, M, gs, out, esc,
+                                                                gl256, nbt, it, oc, ov, cap);
+            else if (wpe8)
+                k_cz_build_roots2<8, false><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
+                                                                 nlev, p_first, M, gs, out, esc,
+                                                                 gl256, nbt, it, oc, ov, cap);
             else
-                k_cz_build_roots2<7><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                          p_first, M, gs, out, esc, gl256, nbt, it,
-                                                          oc, ov, cap);
+                k_cz_build_roots2<7, false><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
+                                                                 nlev, p_first, M, gs, out, esc,
+                                                                 gl256, nbt, it, oc, ov, cap);
         };
         launch((unsigned)blocks, nullptr, ws, list[0]);
         if ((e = hipGetLastError()) != hipSuccess) return e;
