@@ -664,7 +664,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         return e && strcmp(e, "hi") == 0;
     }();
     bool slices = false;
-    const bool roots_build = r->table_build == 0 || r->table_build == 4 || r->table_build == 5;
+    const bool roots_build = r->table_build == 0 || r->table_build >= 4;
     if (roots_build && !hi_only) {
         hipError_t e1 = hi.alloc_pooled(r->n * sizeof(uint32_t), s);
         uint32_t *d_wide = r->d_scratch + 100;
@@ -701,7 +701,21 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
     // default build: pair planes {finger, ID slice} and two-hop pairs (one 8-B
     // gather per window node instead of two 4-B ones); table_build 5 keeps the
     // 4-B planes for A/B
-    if (have_planes && slices && r->table_build == 0 && pp &&
+    // default build: quad planes {finger, ID slice, two-hop finger, ID slice}
+    // of one (level, peer) in 16 B (table_build 0), or pair planes (6): a
+    // window node and its slice in one gather instead of two, both children
+    // of a node at one level in one; table_build 5 keeps the 4-B planes (A/B)
+    if (have_planes && slices && r->table_build == 0 && pp && r->n < ((size_t)1 << 28) &&
+        pp->alloc_pooled((size_t)nl * r->n * sizeof(uint4), s) == hipSuccess) {
+        e = cxk::fingers_quads(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint4>(), s);
+        if (e != hipSuccess) return e;
+        fv.Q = pp->as<uint4>();
+        fv.roots = 2;
+        fv.rs = hi.as<uint32_t>();
+        return hipSuccess;
+    }
+    (void)hipGetLastError();
+    if (have_planes && slices && (r->table_build == 0 || r->table_build == 6) && pp &&
         pp->alloc_pooled((size_t)nl * r->n * sizeof(uint2), s) == hipSuccess &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint2), s) == hipSuccess) {
         e = cxk::fingers_pairs2(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint2>(), c2.as<uint2>(), s);
@@ -720,7 +734,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
             fv.C2 = c2.as<uint32_t>();
             // 0: blocks sized by distinct roots, 4: 256-row root blocks (round 3),
             // 3: one lane per entry (round 2)
-            fv.roots = (r->table_build == 0 || r->table_build == 5) ? 2 : (r->table_build == 4 ? 1 : 0);
+            fv.roots = (r->table_build == 0 || r->table_build >= 5) ? 2 : (r->table_build == 4 ? 1 : 0);
         }
     }
     (void)hipGetLastError();
@@ -2497,16 +2511,16 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
     return CX_OK;
 }
 
-// Route-table build input: 0 = pair planes {finger, ID slice} + two-hop
-// pairs, root-centric windows in blocks sized by distinct roots
-// (k_cz_build_roots2<PAIR>, default), 1 = row-major finger table, 2 = level
+// Route-table build input: 0 = quad planes {finger, ID slice, two-hop finger,
+// ID slice}, root-centric windows in blocks sized by distinct roots
+// (k_cz_build_roots2<7, 2>, default), 1 = row-major finger table, 2 = level
 // planes only, 3 = level + two-hop planes, one lane per entry (k_cz_build, the
 // round-2 build), 4 = root-centric windows in 256-row blocks
-// (k_cz_build_roots, round 3), 5 = as 0 on 4-B planes (no pairs).  All give
-// the same table.  Takes effect at the next finger build.
+// (k_cz_build_roots, round 3), 5 = as 0 on 4-B planes, 6 = as 0 on pair
+// planes.  All give the same table.  Takes effect at the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 5, CX_E_INVALID, "variant must be 0 .. 5");
+    CX_CHECK(variant >= 0 && variant <= 6, CX_E_INVALID, "variant must be 0 .. 6");
     ring->table_build = variant;
     return CX_OK;
 }

@@ -2424,6 +2424,31 @@ __global__ void k_fingers_pairs2(const uint32_t *FT, const uint32_t *rs, uint32_
     }
 }
 
+// Quad planes: the pair and the two-hop pair of one (level, peer) side by
+// side, Q[k][x] = {F, rs[F], C2, rs[C2]} (16 B; the two-hop half of level L is
+// {CX_NONE, 0}).  A window gathers both children of a node that the build
+// needs at one level in one 16-B load (10 loads per window instead of 15).
+__global__ void k_fingers_quads(const uint32_t *FT, const uint32_t *rs, uint32_t n, int nl,
+                                uint4 *Q) {
+    const size_t k = blockIdx.y;
+    const uint32_t *up = FT + k * (size_t)n;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+        const uint32_t y = up[x];
+        const uint32_t z = (k && y < n) ? FT[(k - 1) * (size_t)n + y] : CX_NONE;
+        const v4u q = {y, y < n ? rs[y] : 0u, z, z < n ? rs[z] : 0u};
+        __builtin_nontemporal_store(q, reinterpret_cast<v4u *>(Q + k * (size_t)n + x));
+    }
+}
+
+hipError_t fingers_quads(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint4 *Q,
+                         hipStream_t s) {
+    if (n == 0 || nl < 2) return hipSuccess;
+    k_fingers_quads<<<dim3(cx_grid(n, 256, 4096), (unsigned)nl), 256, 0, s>>>(FT, rs, (uint32_t)n,
+                                                                              nl, Q);
+    return hipGetLastError();
+}
+
 hipError_t fingers_pairs2(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint2 *P,
                           uint2 *P2, hipStream_t s) {
     if (n == 0 || nl < 2) return hipSuccess;
@@ -3215,7 +3240,9 @@ __device__ __forceinline__ uint32_t cz2_nb(int l, int gl256, uint64_t nbt) {
 // items == nullptr: the main launch (blocks from the plan); else block b
 // takes overflow item b = {first row j, level | rows << 8}.  Either appends
 // its own overflow to ovf.
-template <int WPE, bool PAIR>
+// LAY: 0 = 4-B planes + ID slices gathered apart, 1 = pair planes, 2 = quad
+// planes (fingers_pairs2 / fingers_quads)
+template <int WPE, int LAY>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
                        uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
@@ -3238,10 +3265,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     __shared__ uint16_t ridx[CZ2_RMAX];
     __shared__ uint32_t wcnt[8];
     __shared__ uint32_t sbad;  // CZ_NONE words written by the block (rare)
-    // PAIR: the slices of each window's root and of its A1, kept for W1
-    __shared__ uint32_t rsR[PAIR ? 256 : 1], ra1s[PAIR ? 256 : 1];
+    // (LAY != 0): the slices of each window's root and of its A1, kept for W1
+    __shared__ uint32_t rsR[(LAY != 0) ? 256 : 1], ra1s[(LAY != 0) ? 256 : 1];
     uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
-    uint32_t *stS = win + 2 * CZ2_RMAX, *stS1 = win + 3 * CZ2_RMAX;  // PAIR: their slices
+    uint32_t *stS = win + 2 * CZ2_RMAX, *stS1 = win + 3 * CZ2_RMAX;  // (LAY != 0): their slices
     uint32_t j0, rows;
     int lvl;
     if (items) {
@@ -3281,13 +3308,28 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     auto c2 = [&](uint32_t x, int l) -> uint32_t {
         return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
     };
-    // PAIR: {finger, its ID slice} in one 8-B gather (uniform plane base plus a
+    // (LAY != 0): {finger, its ID slice} in one 8-B gather (uniform plane base plus a
     // 32-bit byte offset, x < n < 2^29)
     auto ld64 = [](const uint2 *base, uint32_t x) -> uint2 {
         return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + x * 8u);
     };
-    auto fatp = [&](uint32_t x, int l) -> uint2 { return ld64(fv.P + (size_t)(l - fv.L) * n, x); };
-    auto c2p = [&](uint32_t x, int l) -> uint2 { return ld64(fv.P2 + (size_t)(l - fv.L - 1) * n, x); };
+    // LAY 2 (quads): {F, rs[F], C2, rs[C2]} of (l, x) in 16 B; its halves
+    // alone as 8-B loads where the window needs only one child
+    auto ldq = [&](uint32_t x, int l) -> uint4 {
+        return *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(fv.Q + (size_t)(l - fv.L) * n) + x * 16u);
+    };
+    auto fatp = [&](uint32_t x, int l) -> uint2 {
+        if constexpr (LAY == 2)
+            return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(fv.Q + (size_t)(l - fv.L) * n) + x * 16u);
+        else
+            return ld64(fv.P + (size_t)(l - fv.L) * n, x);
+    };
+    auto c2p = [&](uint32_t x, int l) -> uint2 {
+        if constexpr (LAY == 2)
+            return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(fv.Q + (size_t)(l - fv.L) * n) + x * 16u + 8u);
+        else
+            return ld64(fv.P2 + (size_t)(l - fv.L - 1) * n, x);
+    };
     bool oob = false;
     auto chk = [&](uint32_t x) -> uint32_t {
         if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
@@ -3303,7 +3345,14 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             if (pw >= n) pw -= n;
             const uint32_t p = (uint32_t)pw;
             uint32_t A, A1, sA;
-            if constexpr (PAIR) {
+            if constexpr (LAY == 2) {
+                const uint4 q = ldq(p, i);
+                A = chk(q.x);
+                A1 = chk(q.z);
+                sA = q.y;
+                stS[r] = q.y;
+                stS1[r] = q.w;
+            } else if constexpr (LAY == 1) {
                 const uint2 a = fatp(p, i), a1 = c2p(p, i);
                 A = chk(a.x);
                 A1 = chk(a1.x);
@@ -3333,7 +3382,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         const bool v = r < rows;
         A[k] = v ? stA[r] : 0u;
         A1[k] = v ? stA1[r] : 0u;
-        if constexpr (PAIR) {
+        if constexpr ((LAY != 0)) {
             S[k] = v ? stS[r] : 0u;
             S1[k] = v ? stS1[r] : 0u;
         }
@@ -3360,7 +3409,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (first[0]) {
         stA[rk0] = A[0];
         stA1[rk0] = A1[0];
-        if constexpr (PAIR) {
+        if constexpr ((LAY != 0)) {
             stS[rk0] = S[0];
             stS1[rk0] = S1[0];
         }
@@ -3368,7 +3417,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (first[1]) {
         stA[rk1] = A[1];
         stA1[rk1] = A1[1];
-        if constexpr (PAIR) {
+        if constexpr ((LAY != 0)) {
             stS[rk1] = S[1];
             stS1[rk1] = S1[1];
         }
@@ -3396,7 +3445,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (wl) {
         R = stA[t];
         RA1 = stA1[t];
-        if constexpr (PAIR) {
+        if constexpr ((LAY != 0)) {
             SR = stS[t];
             SRA1 = stS1[t];
         }
@@ -3412,11 +3461,33 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         uint32_t wbad = 0;
         uint32_t nd[16], hv[16];
         nd[0] = R;
-        if constexpr (PAIR) {
+        if constexpr ((LAY != 0)) {
             rsR[t] = SR;
             ra1s[t] = SRA1;
             hv[0] = SR;
             uint2 q[16];
+            if constexpr (LAY == 2) {
+                const uint4 a = ldq(R, i - 2), b = ldq(R, i - 3), c = ldq(R, i - 4);
+                q[1] = make_uint2(a.x, a.y);
+                q[3] = make_uint2(a.z, a.w);
+                q[2] = make_uint2(b.x, b.y);
+                q[6] = make_uint2(b.z, b.w);
+                q[4] = make_uint2(c.x, c.y);
+                q[12] = make_uint2(c.z, c.w);
+                q[8] = fatp(R, i - 5);
+                nd[1] = chk(q[1].x);
+                nd[2] = chk(q[2].x);
+                nd[3] = chk(q[3].x);
+                const uint4 e = ldq(nd[1], i - 4), f = ldq(nd[3], i - 4);
+                q[5] = make_uint2(e.x, e.y);
+                q[13] = make_uint2(e.z, e.w);
+                q[7] = make_uint2(f.x, f.y);
+                q[15] = make_uint2(f.z, f.w);
+                q[9] = fatp(nd[1], i - 5);
+                q[10] = fatp(nd[2], i - 5);
+                q[11] = fatp(nd[3], i - 5);
+                q[14] = c2p(nd[2], i - 4);
+            } else {
             q[1] = fatp(R, i - 2);
             q[2] = fatp(R, i - 3);
             q[3] = c2p(R, i - 2);
@@ -3435,6 +3506,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             q[13] = c2p(nd[1], i - 4);
             q[14] = c2p(nd[2], i - 4);
             q[15] = c2p(nd[3], i - 4);
+            }
 #pragma unroll
             for (int v = 1; v < 16; ++v) {
                 nd[v] = chk(q[v].x);
@@ -3504,10 +3576,31 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         uint32_t nd[15], hv[15];
         uint32_t hR;
         nd[0] = ra1[t] & 0x3FFFFFFFu;
-        if constexpr (PAIR) {
+        if constexpr ((LAY != 0)) {
             hR = rsR[t];
             hv[0] = ra1s[t];
             uint2 q[15];
+            if constexpr (LAY == 2) {
+                const uint4 a = ldq(nd[0], i - 2), b = ldq(nd[0], i - 3), c = ldq(nd[0], i - 4);
+                q[1] = make_uint2(a.x, a.y);
+                q[3] = make_uint2(a.z, a.w);
+                q[2] = make_uint2(b.x, b.y);
+                q[6] = make_uint2(b.z, b.w);
+                q[4] = make_uint2(c.x, c.y);
+                q[12] = make_uint2(c.z, c.w);
+                q[8] = fatp(nd[0], i - 5);
+                nd[1] = chk(q[1].x);
+                nd[2] = chk(q[2].x);
+                nd[3] = chk(q[3].x);
+                const uint4 e = ldq(nd[1], i - 4);
+                q[5] = make_uint2(e.x, e.y);
+                q[13] = make_uint2(e.z, e.w);
+                q[7] = fatp(nd[3], i - 4);
+                q[9] = fatp(nd[1], i - 5);
+                q[10] = fatp(nd[2], i - 5);
+                q[11] = fatp(nd[3], i - 5);
+                q[14] = c2p(nd[2], i - 4);
+            } else {
             q[1] = fatp(nd[0], i - 2);
             q[2] = fatp(nd[0], i - 3);
             q[3] = c2p(nd[0], i - 2);
@@ -3525,6 +3618,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             q[11] = fatp(nd[3], i - 5);
             q[13] = c2p(nd[1], i - 4);
             q[14] = c2p(nd[2], i - 4);
+            }
 #pragma unroll
             for (int v = 1; v < 15; ++v) {
                 nd[v] = chk(q[v].x);
@@ -3690,8 +3784,10 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         const char *e = getenv("CX_CZ_PAIR");
         return e ? atoi(e) : 0;
     }();
-    if (fv.P && !(ws && fv.rs && fv.P2)) return hipErrorInvalidValue;  // pairs: roots2 only
-    if (planes && (fv.C2 || fv.P2) && fv.roots == 2 && fv.rs && ws) {
+    // pair / quad planes: roots2 only
+    if ((fv.P || fv.Q) && !(ws && fv.rs && (fv.P2 || fv.Q))) return hipErrorInvalidValue;
+    if (fv.Q && n >= (1u << 28)) return hipErrorInvalidValue;  // 32-bit byte offsets
+    if (planes && (fv.C2 || fv.P2 || fv.Q) && fv.roots == 2 && fv.rs && ws) {
         int gl256;
         uint64_t nbt;
         cz2_plan(n, gl256, nbt);
@@ -3710,18 +3806,22 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             return ev && atoi(ev) == 8;
         }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
-            if (fv.P && fv.P2)  // pair planes (the default when they fit)
-                k_cz_build_roots2<7, true><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
-                                                                nlev, p_first, M, gs, out, esc,
-                                                                gl256, nbt, it, oc, ov, cap);
+            if (fv.Q)  // quad planes
+                k_cz_build_roots2<7, 2><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                             p_first, M, gs, out, esc, gl256, nbt, it,
+                                                             oc, ov, cap);
+            else if (fv.P && fv.P2)  // pair planes
+                k_cz_build_roots2<7, 1><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                             p_first, M, gs, out, esc, gl256, nbt, it,
+                                                             oc, ov, cap);
             else if (wpe8)
-                k_cz_build_roots2<8, false><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
-                                                                 nlev, p_first, M, gs, out, esc,
-                                                                 gl256, nbt, it, oc, ov, cap);
+                k_cz_build_roots2<8, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                             p_first, M, gs, out, esc, gl256, nbt, it,
+                                                             oc, ov, cap);
             else
-                k_cz_build_roots2<7, false><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
-                                                                 nlev, p_first, M, gs, out, esc,
-                                                                 gl256, nbt, it, oc, ov, cap);
+                k_cz_build_roots2<7, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                             p_first, M, gs, out, esc, gl256, nbt, it,
+                                                             oc, ov, cap);
         };
         launch((unsigned)blocks, nullptr, ws, list[0]);
         if ((e = hipGetLastError()) != hipSuccess) return e;

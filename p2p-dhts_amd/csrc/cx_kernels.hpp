@@ -155,6 +155,8 @@ struct FingerView {
     // planes; with them the build reads each window node and its slice in one
     // gather (C2 may then be null)
     const uint2 *P = nullptr, *P2 = nullptr;
+    // or quad planes (fingers_quads): Q[(l - L) n + x] = {P[l][x], P2[l][x]}
+    const uint4 *Q = nullptr;
     __host__ __device__ uint32_t at(uint32_t x, int l) const {
         return F[(size_t)x * sx + (size_t)(l - L) * sl];
     }
@@ -190,6 +192,9 @@ hipError_t successor_eyt16(const EytView &ev, const uint32_t *rank, const cell12
 // pairs of levels L + 1 .. (FingerView::P / P2), from level planes FT.
 hipError_t fingers_pairs2(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint2 *P,
                           uint2 *P2, hipStream_t s);
+// Quad planes {F, rs[F], C2, rs[C2]} of levels L .. L + nl - 1 (FingerView::Q).
+hipError_t fingers_quads(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint4 *Q,
+                         hipStream_t s);
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s);
 // C2 planes (nl - 1 of them) from the level planes FT.
