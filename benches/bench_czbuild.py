@@ -49,14 +49,15 @@ def main():
     out = {"log2_peers": lg, "table_builds": tbs, "rounds": rounds,
            "variant_env": {k: os.environ.get(k) for k in
                            ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE", "CX_CZ_ROOTS_MODE",
-                            "CX_CZ2_WPE")},
+                            "CX_CZ2_WPE", "CX_CZ2_MODE")},
            "fingers_and_table_ms": ts,
            "median_ms": {tb: sorted(v)[len(v) // 2] for tb, v in ts.items()},
            "route_table_hash": hashes, "hashes_equal": len(set(hashes.values())) == 1,
            "route_variant": v, "escapes": esc}
     # probes (stores-only / compute-only) leave an unspecified table: no route
     if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1") and \
-            os.environ.get("CX_CZ_ROOTS_MODE", "0") == "0":
+            os.environ.get("CX_CZ_ROOTS_MODE", "0") == "0" and \
+            os.environ.get("CX_CZ2_MODE", "0") == "0":
         q = 1 << 22
         keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
         chordx.fill_splitmix(keys, 0x5EED0008)

@@ -3247,7 +3247,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
                        uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
                        int gl256, uint64_t nbt, const uint2 *items, uint32_t *ovf_cnt,
-                       uint2 *ovf, uint32_t cap) {
+                       uint2 *ovf, uint32_t cap, int mode) {
+    // mode (A/B probes, CX_CZ2_MODE; 0 = the build): 1 = compute only (no
+    // table stores), 2 = stores only (no window gathers; the words stored are
+    // whatever LDS holds), 3 = stores only without the row gathers (every two
+    // rows share a dummy root)
     auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
     };
@@ -3291,7 +3295,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             nbl = cz2_nb(lvl_base + lvl, gl256, nbt);
         }
         const uint32_t xm = nbl >> 3, xr = nbl & 7, xx = rem & 7;
-        const uint32_t lbl = xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
+        const uint32_t lbl = (mode & 8) ? rem : xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
         const uint32_t RB = (CZ2_CHUNK + nbl - 1) / nbl;
         const uint32_t c0 = lbl * RB;
         if (c0 >= CZ2_CHUNK) return;  // block-uniform
@@ -3340,7 +3344,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const uint32_t r = (uint32_t)t + 256u * k;
-        if (r < rows) {
+        if (r < rows && (mode & 3) == 3) {
+            stA[r] = r >> 1;
+            stA1[r] = 0;
+        } else if (r < rows) {
             uint64_t pw = (uint64_t)p_first + j0 + r;
             if (pw >= n) pw -= n;
             const uint32_t p = (uint32_t)pw;
@@ -3440,7 +3447,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         nr = cap;
         if (t == 0) ovf[atomicAdd(ovf_cnt, 1u)] = make_uint2(j0 + rhi, (uint32_t)lvl | (rows - rhi) << 8);
     }
-    const bool wl = (uint32_t)t < nr;
+    const bool wl = (uint32_t)t < nr && (mode & 3) < 2;
     uint32_t R = 0, RA1 = 0, SR = 0, SRA1 = 0;
     if (wl) {
         R = stA[t];
@@ -3557,14 +3564,14 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         }
     }
     // plane 0: rows [0, rhi) x 4 chunks of 16 B, whole lines per store
-    for (uint32_t c = t; c < 4u * rhi; c += 256u) {
+    for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
         const uint32_t e = c >> 2, qq = c & 3u;
         const uint32_t *w = win + ridx[e] * 16;
         uint32_t u[4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
             const uint32_t word = qq * 4u + (uint32_t)x;
-            u[x] = word == 0 ? e0s[e] : w[word - 1];
+            u[x] = (mode & 4) ? word : (word == 0 ? e0s[e] : w[word - 1]);
         }
         const v4u wv4 = {u[0], u[1], u[2], u[3]};
         __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + e) * 4) + qq);
@@ -3666,14 +3673,14 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         }
     }
     // plane 1: word 15 = the row's own word
-    for (uint32_t c = t; c < 4u * rhi; c += 256u) {
+    for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
         const uint32_t e = c >> 2, qq = c & 3u;
         const uint32_t *w = win + ridx[e] * 16;
         uint32_t u[4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
             const uint32_t word = qq * 4u + (uint32_t)x;
-            u[x] = word == 15 ? e0s[e] : w[word];
+            u[x] = (mode & 4) ? word : (word == 15 ? e0s[e] : w[word]);
         }
         const v4u wv4 = {u[0], u[1], u[2], u[3]};
         __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + M + e) * 4) + qq);
@@ -3805,23 +3812,27 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             const char *ev = getenv("CX_CZ2_WPE");
             return ev && atoi(ev) == 8;
         }();
+        static const int mode = [] {
+            const char *ev = getenv("CX_CZ2_MODE");
+            return ev ? (atoi(ev) & 15) : 0;
+        }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
             if (fv.Q)  // quad planes
                 k_cz_build_roots2<7, 2><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap);
+                                                             oc, ov, cap, mode);
             else if (fv.P && fv.P2)  // pair planes
                 k_cz_build_roots2<7, 1><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap);
+                                                             oc, ov, cap, mode);
             else if (wpe8)
                 k_cz_build_roots2<8, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap);
+                                                             oc, ov, cap, mode);
             else
                 k_cz_build_roots2<7, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap);
+                                                             oc, ov, cap, mode);
         };
         launch((unsigned)blocks, nullptr, ws, list[0]);
         if ((e = hipGetLastError()) != hipSuccess) return e;
