@@ -701,11 +701,13 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
     // default build: pair planes {finger, ID slice} and two-hop pairs (one 8-B
     // gather per window node instead of two 4-B ones); table_build 5 keeps the
     // 4-B planes for A/B
-    // default build: quad planes {finger, ID slice, two-hop finger, ID slice}
-    // of one (level, peer) in 16 B (table_build 0), or pair planes (6): a
+    // A/B (round 4): quad planes {finger, ID slice, two-hop finger, ID slice}
+    // of one (level, peer) in 16 B (table_build 7) or pair planes (6): a
     // window node and its slice in one gather instead of two, both children
-    // of a node at one level in one; table_build 5 keeps the 4-B planes (A/B)
-    if (have_planes && slices && r->table_build == 0 && pp && r->n < ((size_t)1 << 28) &&
+    // of a node at one level in one.  The build itself is 2-4 % faster on
+    // them, but making them costs 2.6-3 ms more than the 4-B two-hop planes
+    // (profiles/r04/build_modes/), so the default keeps 4-B planes
+    if (have_planes && slices && r->table_build == 7 && pp && r->n < ((size_t)1 << 28) &&
         pp->alloc_pooled((size_t)nl * r->n * sizeof(uint4), s) == hipSuccess) {
         e = cxk::fingers_quads(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint4>(), s);
         if (e != hipSuccess) return e;
@@ -715,7 +717,7 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         return hipSuccess;
     }
     (void)hipGetLastError();
-    if (have_planes && slices && (r->table_build == 0 || r->table_build == 6) && pp &&
+    if (have_planes && slices && r->table_build == 6 && pp &&
         pp->alloc_pooled((size_t)nl * r->n * sizeof(uint2), s) == hipSuccess &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint2), s) == hipSuccess) {
         e = cxk::fingers_pairs2(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint2>(), c2.as<uint2>(), s);
@@ -2511,16 +2513,16 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
     return CX_OK;
 }
 
-// Route-table build input: 0 = quad planes {finger, ID slice, two-hop finger,
-// ID slice}, root-centric windows in blocks sized by distinct roots
-// (k_cz_build_roots2<7, 2>, default), 1 = row-major finger table, 2 = level
-// planes only, 3 = level + two-hop planes, one lane per entry (k_cz_build, the
-// round-2 build), 4 = root-centric windows in 256-row blocks
-// (k_cz_build_roots, round 3), 5 = as 0 on 4-B planes, 6 = as 0 on pair
-// planes.  All give the same table.  Takes effect at the next finger build.
+// Route-table build input: 0 = level + two-hop planes, root-centric windows
+// in blocks sized by distinct roots (k_cz_build_roots2<7, 0>, default), 1 =
+// row-major finger table, 2 = level planes only, 3 = level + two-hop planes,
+// one lane per entry (k_cz_build, the round-2 build), 4 = root-centric windows
+// in 256-row blocks (k_cz_build_roots, round 3), 5 = the same as 0, 6 = as 0
+// on pair planes, 7 = as 0 on quad planes.  All give the same table.  Takes
+// effect at the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 6, CX_E_INVALID, "variant must be 0 .. 6");
+    CX_CHECK(variant >= 0 && variant <= 7, CX_E_INVALID, "variant must be 0 .. 7");
     ring->table_build = variant;
     return CX_OK;
 }

@@ -3222,8 +3222,10 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
 // first 256 roots and appends the rest (< 256 rows, so < 256 roots) to an
 // overflow list that a second launch of the same kernel finishes.  LDS stays
 // under 20 KB (8 blocks per CU): the windows' buffer also stages the rows'
-// roots before the window phase, and each window's 16th word carries its root
-// into the W1 phase (with the window's CZ_NONE count in the spare top bits).
+// roots before the window phase, and each window's word 0 (slot 0 of the b = 0
+// entry is the row's own word) carries its root into the W1 phase, with the
+// window's CZ_NONE count in the spare top bits; the stores assemble each 16-B
+// chunk with one LDS read.
 // Same table, bit for bit (route_table_hash against every other build).
 constexpr int CZ2_RMAX = 464;
 constexpr uint32_t CZ2_CHUNK = 4096;  // rows of a dispatch chunk (all levels)
@@ -3259,8 +3261,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     auto enc = [&](uint32_t par, uint32_t hpar, int l, uint32_t x, uint32_t hx) -> uint32_t {
         return cz_encode_s(n, gs, par, hpar, l, x, hx, ring);
     };
-    // win: 256 windows x 16 words (15 W0 or W1 words + the root for W1 / the
-    // W1 CZ_NONE count); before the window phase its first 2 x CZ2_RMAX words
+    // win: 256 windows x 16 words (W0: the root, slots 1..15; W1: slots 0..14,
+    // its CZ_NONE count); before the window phase its first 2 x CZ2_RMAX words
     // stage the rows' roots A and two-hop roots A1 (compacted in place to the
     // distinct roots)
     __shared__ uint32_t win[256 * 16];
@@ -3268,7 +3270,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     __shared__ uint32_t e0s[CZ2_RMAX];
     __shared__ uint16_t ridx[CZ2_RMAX];
     __shared__ uint32_t wcnt[8];
-    __shared__ uint32_t sbad;  // CZ_NONE words written by the block (rare)
+    __shared__ uint32_t sbad;    // CZ_NONE words written by the block (rare)
+    __shared__ uint32_t anybad;  // some window of the block holds one
     // (LAY != 0): the slices of each window's root and of its A1, kept for W1
     __shared__ uint32_t rsR[(LAY != 0) ? 256 : 1], ra1s[(LAY != 0) ? 256 : 1];
     uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
@@ -3339,7 +3342,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
         return x < n ? x : 0u;
     };
-    if (t == 0) sbad = 0;
+    if (t == 0) {
+        sbad = 0;
+        anybad = 0;
+    }
     // ---- rows (two per lane): roots, two-hop roots, the row's own word ----
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -3464,7 +3470,6 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
     if (wl) {
         ra1[t] = RA1;
-        wr[15] = R;  // the root rides in word 15 into the W1 phase (R < n < 2^30)
         uint32_t wbad = 0;
         uint32_t nd[16], hv[16];
         nd[0] = R;
@@ -3538,42 +3543,54 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
 #pragma unroll
             for (int v = 0; v < 16; ++v) hv[v] = hiw(nd[v]);
         }
+        // word 0 (slot 0 is the row's own word) carries the root into W1, with
+        // the window's CZ_NONE count (rare) in its spare top bits (the high two
+        // beside A1); the 16 words leave as four 16-B LDS writes (a lane's
+        // window is 64 contiguous bytes: four b128 writes per lane instead of
+        // sixteen b32 writes 64 B apart, which hit two banks per wave)
+        uint4 *w4 = reinterpret_cast<uint4 *>(wr);
 #pragma unroll
-        for (int v = 1; v < 16; ++v) {
-            const int hb = 31 - __builtin_clz((unsigned)v);
-            const int pv = v & ~(1 << hb);
-            const uint32_t o = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
-            wbad += o == CZ_NONE;
-            wr[v - 1] = o;
+        for (int g = 0; g < 4; ++g) {  // four words at a time, written when done
+            uint32_t ov[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int v = 4 * g + u;
+                if (v == 0) {
+                    ov[u] = R;
+                    continue;
+                }
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pv = v & ~(1 << hb);
+                ov[u] = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
+                wbad += ov[u] == CZ_NONE;
+            }
+            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
         }
-        // the window's CZ_NONE count (rare) in the spare top bits: the low two
-        // beside the root, the high two beside A1
-        if (wbad) {
-            wr[15] |= (wbad & 3u) << 30;
+        if (wbad) {  // rare: read back beside the root and A1
+            wr[0] |= (wbad & 3u) << 30;
             ra1[t] |= (wbad >> 2) << 30;
+            anybad = 1;
         }
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k) {  // every row carries its root's W0 words
         const uint32_t r = (uint32_t)t + 256u * k;
-        if (r < rhi) {
+        if (anybad && r < rhi) {
             const uint32_t x = ridx[r];
-            const uint32_t wb = (win[x * 16 + 15] >> 30) | (ra1[x] >> 30) << 2;
+            const uint32_t wb = (win[x * 16] >> 30) | (ra1[x] >> 30) << 2;
             if (wb) atomicAdd(&sbad, wb);
         }
     }
     // plane 0: rows [0, rhi) x 4 chunks of 16 B, whole lines per store
     for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
         const uint32_t e = c >> 2, qq = c & 3u;
-        const uint32_t *w = win + ridx[e] * 16;
-        uint32_t u[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            const uint32_t word = qq * 4u + (uint32_t)x;
-            u[x] = (mode & 4) ? word : (word == 0 ? e0s[e] : w[word - 1]);
-        }
-        const v4u wv4 = {u[0], u[1], u[2], u[3]};
+        // one 16-B LDS read per chunk (the window's words sit at their slots;
+        // a lane pair of entries covers 32 banks): slot 0 is the row's own word
+        uint4 u = *reinterpret_cast<const uint4 *>(win + ridx[e] * 16 + qq * 4);
+        if (qq == 0) u.x = e0s[e];
+        if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
+        const v4u wv4 = {u.x, u.y, u.z, u.w};
         __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + e) * 4) + qq);
     }
     __syncthreads();  // plane 0 has read every W0 word
@@ -3632,7 +3649,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
                 hv[v] = q[v].y;
             }
         } else {
-            hR = hiw(wr[15] & 0x3FFFFFFFu);  // the root itself is re-read below
+            hR = hiw(wr[0] & 0x3FFFFFFFu);  // the root itself is re-read below
             nd[1] = chk(fat(nd[0], i - 2));
             nd[2] = chk(fat(nd[0], i - 3));
             nd[3] = chk(c2(nd[0], i - 2));
@@ -3650,24 +3667,36 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
 #pragma unroll
             for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
         }
-        const uint32_t o0 = enc(wr[15] & 0x3FFFFFFFu, hR, i - 1, nd[0], hv[0]);
-        wbad += o0 == CZ_NONE;
-        wr[0] = o0;
+        const uint32_t Rw = wr[0] & 0x3FFFFFFFu;
+        uint4 *w4 = reinterpret_cast<uint4 *>(wr);
 #pragma unroll
-        for (int v = 1; v < 15; ++v) {
-            const int hb = 31 - __builtin_clz((unsigned)v);
-            const int pv = v & ~(1 << hb);
-            const uint32_t o = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
-            wbad += o == CZ_NONE;
-            wr[v] = o;
+        for (int g = 0; g < 4; ++g) {
+            uint32_t ov[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int v = 4 * g + u;
+                if (v == 15) {
+                    ov[u] = wbad;
+                    continue;
+                }
+                if (v == 0) {
+                    ov[u] = enc(Rw, hR, i - 1, nd[0], hv[0]);
+                } else {
+                    const int hb = 31 - __builtin_clz((unsigned)v);
+                    const int pv = v & ~(1 << hb);
+                    ov[u] = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
+                }
+                wbad += ov[u] == CZ_NONE;
+            }
+            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
         }
-        wr[15] = wbad;
+        if (wbad) anybad = 1;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k) {  // ... and its W1 words
         const uint32_t r = (uint32_t)t + 256u * k;
-        if (r < rhi) {
+        if (anybad && r < rhi) {
             const uint32_t wb = win[ridx[r] * 16 + 15];
             if (wb) atomicAdd(&sbad, wb);
         }
@@ -3675,14 +3704,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     // plane 1: word 15 = the row's own word
     for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
         const uint32_t e = c >> 2, qq = c & 3u;
-        const uint32_t *w = win + ridx[e] * 16;
-        uint32_t u[4];
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-            const uint32_t word = qq * 4u + (uint32_t)x;
-            u[x] = (mode & 4) ? word : (word == 15 ? e0s[e] : w[word]);
-        }
-        const v4u wv4 = {u[0], u[1], u[2], u[3]};
+        uint4 u = *reinterpret_cast<const uint4 *>(win + ridx[e] * 16 + qq * 4);
+        if (qq == 3) u.w = e0s[e];  // slot 15 is the row's own word
+        if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
+        const v4u wv4 = {u.x, u.y, u.z, u.w};
         __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + M + e) * 4) + qq);
     }
     if (oob) atomicOr(esc + 1, 1u);
@@ -3699,6 +3724,17 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
 static void cz2_plan(size_t n, int &gl256, uint64_t &nbt) {
     const double gl = 128.0 - log2((double)n);
     gl256 = (int)lround(gl * 256.0);
+    // CX_CZ2_NB (A/B): the same block count for every level (16 = 256 rows)
+    static const int nb_env = [] {
+        const char *e = getenv("CX_CZ2_NB");
+        const int v = e ? atoi(e) : 0;
+        return v >= 9 && v <= 255 ? v : 0;
+    }();
+    if (nb_env) {
+        nbt = 0;
+        for (int k = 0; k < 8; ++k) nbt |= (uint64_t)nb_env << (8 * k);
+        return;
+    }
     // bucket k covers floor(l - gl) = k - 6 (k = 0: <= -6, k = 7: >= 1)
     static const double frac[8] = {0.97, 0.94, 0.89, 0.80, 0.685, 0.57, 0.51, 0.50};
     nbt = 0;
