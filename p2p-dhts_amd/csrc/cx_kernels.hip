@@ -3253,7 +3253,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     // mode (A/B probes, CX_CZ2_MODE; 0 = the build): 1 = compute only (no
     // table stores), 2 = stores only (no window gathers; the words stored are
     // whatever LDS holds), 3 = stores only without the row gathers (every two
-    // rows share a dummy root)
+    // rows share a dummy root); + 16: every store lands in the table's first
+    // 128 MiB (the write stream stays on chip)
     auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
     };
@@ -3591,7 +3592,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         if (qq == 0) u.x = e0s[e];
         if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
         const v4u wv4 = {u.x, u.y, u.z, u.w};
-        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + e) * 4) + qq);
+        const size_t ent0 = (mode & 16) ? ((tp0 + e) & ((1u << 21) - 1)) : tp0 + e;
+        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent0 * 4) + qq);
     }
     __syncthreads();  // plane 0 has read every W0 word
     // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
@@ -3708,7 +3710,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         if (qq == 3) u.w = e0s[e];  // slot 15 is the row's own word
         if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
         const v4u wv4 = {u.x, u.y, u.z, u.w};
-        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + M + e) * 4) + qq);
+        const size_t ent1 = (mode & 16) ? ((tp0 + M + e) & ((1u << 21) - 1)) : tp0 + M + e;
+        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent1 * 4) + qq);
     }
     if (oob) atomicOr(esc + 1, 1u);
     __syncthreads();
@@ -3850,7 +3853,7 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         }();
         static const int mode = [] {
             const char *ev = getenv("CX_CZ2_MODE");
-            return ev ? (atoi(ev) & 15) : 0;
+            return ev ? (atoi(ev) & 31) : 0;
         }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
             if (fv.Q)  // quad planes
