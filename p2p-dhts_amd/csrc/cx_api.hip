@@ -736,7 +736,9 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
             fv.C2 = c2.as<uint32_t>();
             // 0: blocks sized by distinct roots, 4: 256-row root blocks (round 3),
             // 3: one lane per entry (round 2)
-            fv.roots = (r->table_build == 0 || r->table_build >= 5) ? 2 : (r->table_build == 4 ? 1 : 0);
+            fv.roots = r->table_build == 8 ? 3
+                       : (r->table_build == 0 || r->table_build >= 5) ? 2
+                       : (r->table_build == 4 ? 1 : 0);
         }
     }
     (void)hipGetLastError();
@@ -774,7 +776,7 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
             }
             CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre, &pp));
             DBuf ws;  // the default build's overflow list
-            if (fv.roots == 2)
+            if (fv.roots >= 2)
                 CX_HIP(ws.alloc_pooled(cxk::cz_build_ws_words(r->n, r->rt_l0, r->rt_R, (uint32_t)r->n) *
                                            sizeof(uint32_t), s));
             CX_HIP(cxk::cz_build(fv, r->d_ring, hi.as<uint64_t>(), r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_cz,
@@ -2088,7 +2090,7 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
         cxk::FingerView fv;
         CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s, nullptr, &pp));
         DBuf ws;  // the default build's overflow list (sized for the larger part)
-        if (fv.roots == 2) {
+        if (fv.roots >= 2) {
             const size_t w0 = cxk::cz_build_ws_words(n, Lh, (int)CX_FINGERS - Lh, (uint32_t)n);
             const size_t w1 = cxk::cz_build_ws_words(n, l0, Lh - l0, M);
             CX_HIP(ws.alloc_pooled((w0 > w1 ? w0 : w1) * sizeof(uint32_t), s));
@@ -2518,11 +2520,12 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
 // row-major finger table, 2 = level planes only, 3 = level + two-hop planes,
 // one lane per entry (k_cz_build, the round-2 build), 4 = root-centric windows
 // in 256-row blocks (k_cz_build_roots, round 3), 5 = the same as 0, 6 = as 0
-// on pair planes, 7 = as 0 on quad planes.  All give the same table.  Takes
-// effect at the next finger build.
+// on pair planes, 7 = as 0 on quad planes, 8 = both windows of a root at once,
+// stores last (k_cz_build_roots3).  All give the same table.  Takes effect at
+// the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 7, CX_E_INVALID, "variant must be 0 .. 7");
+    CX_CHECK(variant >= 0 && variant <= 8, CX_E_INVALID, "variant must be 0 .. 8");
     ring->table_build = variant;
     return CX_OK;
 }

@@ -3228,6 +3228,7 @@ void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, ui
 // chunk with one LDS read.
 // Same table, bit for bit (route_table_hash against every other build).
 constexpr int CZ2_RMAX = 464;
+constexpr double CZ3_TARGET = 115.0;  // k_cz_build_roots3: roots per block (of 128)
 constexpr uint32_t CZ2_CHUNK = 4096;  // rows of a dispatch chunk (all levels)
 
 // Blocks per level per chunk: level l's bucket is clamp(floor(l - gl) + 6, 0,
@@ -3718,13 +3719,288 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (t == 0 && sbad) atomicAdd(esc, sbad);
 }
 
+// Both windows of a root at once, stores last (table_build 8, A/B): a block
+// takes up to 128 distinct roots (its rows sized per level as in
+// k_cz_build_roots2, for 115 roots), lanes 0..127 compute W0 of root t and
+// lanes 128..255 W1 of root t - 128 (waves 0-1 and 2-3: no divergence), and
+// both planes leave after the window phase.  A wave's loads and stores share
+// one in-order vmcnt queue, so in k_cz_build_roots2 the W1 gathers wait
+// behind the plane-0 stores (the build's halves add: compute 12.8 + stores
+// 9.7 ms, profiles/r04/build_writes/); here no wave issues a gather after a
+// store, and a block's dependent chain is one window instead of two.
+template <int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_cz_build_roots3(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
+                       uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
+                       int gl256, uint64_t nbt, const uint2 *items, uint32_t *ovf_cnt,
+                       uint2 *ovf, uint32_t cap) {
+    auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
+        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
+    };
+    auto hiw = [&](uint32_t x) -> uint32_t { return ld32(fv.rs, x); };
+    auto enc = [&](uint32_t par, uint32_t hpar, int l, uint32_t x, uint32_t hx) -> uint32_t {
+        return cz_encode_s(n, gs, par, hpar, l, x, hx, ring);
+    };
+    // win: W0 windows of roots 0..127 (the row's own word slot holds the
+    // window's CZ_NONE count), then W1 windows (slot 15 holds it); before the
+    // window phase its first 2 x CZ2_RMAX words stage the rows' roots / A1
+    __shared__ uint32_t win[256 * 16];
+    __shared__ uint32_t e0s[CZ2_RMAX];
+    __shared__ uint16_t ridx[CZ2_RMAX];
+    __shared__ uint32_t wcnt[8];
+    __shared__ uint32_t sbad, anybad;
+    uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
+    uint32_t j0, rows;
+    int lvl;
+    if (items) {
+        const uint2 it = items[blockIdx.x];
+        j0 = it.x;
+        lvl = (int)(it.y & 0xFFu);
+        rows = it.y >> 8;
+    } else {
+        uint32_t TB = 0;
+        for (int l = 0; l < nlev; ++l) TB += cz2_nb(lvl_base + l, gl256, nbt);
+        const uint32_t chunk = blockIdx.x / TB;
+        uint32_t rem = blockIdx.x - chunk * TB;
+        lvl = 0;
+        uint32_t nbl = cz2_nb(lvl_base, gl256, nbt);
+        while (rem >= nbl) {
+            rem -= nbl;
+            ++lvl;
+            nbl = cz2_nb(lvl_base + lvl, gl256, nbt);
+        }
+        const uint32_t xm = nbl >> 3, xr = nbl & 7, xx = rem & 7;
+        const uint32_t lbl = xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
+        const uint32_t RB = (CZ2_CHUNK + nbl - 1) / nbl;
+        const uint32_t c0 = lbl * RB;
+        if (c0 >= CZ2_CHUNK) return;  // block-uniform
+        j0 = chunk * CZ2_CHUNK + c0;
+        if (j0 >= M) return;
+        rows = CZ2_CHUNK - c0 < RB ? CZ2_CHUNK - c0 : RB;
+        if (M - j0 < rows) rows = M - j0;
+    }
+    const int i = lvl_base + lvl;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    auto fat = [&](uint32_t x, int l) -> uint32_t {
+        return ld32(fv.F + (size_t)(l - fv.L) * fv.sl, x);
+    };
+    auto c2 = [&](uint32_t x, int l) -> uint32_t {
+        return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
+    };
+    bool oob = false;
+    auto chk = [&](uint32_t x) -> uint32_t {
+        if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
+        return x < n ? x : 0u;
+    };
+    if (t == 0) {
+        sbad = 0;
+        anybad = 0;
+    }
+    // ---- rows (two per lane): roots, two-hop roots, the row's own word ----
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t r = (uint32_t)t + 256u * k;
+        if (r < rows) {
+            uint64_t pw = (uint64_t)p_first + j0 + r;
+            if (pw >= n) pw -= n;
+            const uint32_t p = (uint32_t)pw;
+            const uint32_t A = chk(fat(p, i));
+            const uint32_t A1 = chk(c2(p, i));
+            const uint32_t e0 = enc(p, hiw(p), i, A, hiw(A));
+            e0s[r] = e0;
+            if (e0 == CZ_NONE) atomicAdd(&sbad, 2u);
+            stA[r] = A;
+            stA1[r] = A1;
+        }
+    }
+    __syncthreads();
+    uint32_t A[2], A1[2];
+    bool first[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t r = (uint32_t)t + 256u * k;
+        const bool v = r < rows;
+        A[k] = v ? stA[r] : 0u;
+        A1[k] = v ? stA1[r] : 0u;
+        first[k] = v && (r == 0 || stA[r - 1] != A[k]);
+    }
+    const uint64_t fm0 = __ballot(first[0]), fm1 = __ballot(first[1]);
+    if (lane == 0) {
+        wcnt[wv] = (uint32_t)__popcll(fm0);
+        wcnt[4 + wv] = (uint32_t)__popcll(fm1);
+    }
+    __syncthreads();
+    uint32_t nr = 0, b0 = 0, b1 = 0;
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t c = wcnt[w];
+        b0 += w < wv ? c : 0u;
+        b1 += w < 4 + wv ? c : 0u;
+        nr += c;
+    }
+    const uint32_t rk0 = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm0 >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)fm0, 0u));
+    const uint32_t rk1 = b1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm1 >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)fm1, 0u));
+    __syncthreads();
+    if (first[0]) {
+        stA[rk0] = A[0];
+        stA1[rk0] = A1[0];
+    }
+    if (first[1]) {
+        stA[rk1] = A[1];
+        stA1[rk1] = A1[1];
+    }
+    if ((uint32_t)t < rows) ridx[t] = (uint16_t)(rk0 + first[0] - 1);
+    if ((uint32_t)t + 256u < rows) ridx[t + 256] = (uint16_t)(rk1 + first[1] - 1);
+    __syncthreads();
+    const uint32_t capb = cap < 128u ? cap : 128u;
+    uint32_t rhi = rows;
+    if (nr > capb) {  // block-uniform
+        uint32_t lo = 0, hi = rows;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ridx[mid] < capb) lo = mid + 1;
+            else hi = mid;
+        }
+        rhi = lo;
+        nr = capb;
+        if (t == 0) ovf[atomicAdd(ovf_cnt, 1u)] = make_uint2(j0 + rhi, (uint32_t)lvl | (rows - rhi) << 8);
+    }
+    // lanes 0..127: W0 of root t; lanes 128..255: W1 of root t - 128
+    const bool w1 = t >= 128;
+    const uint32_t rt = w1 ? (uint32_t)t - 128u : (uint32_t)t;
+    const bool wl = rt < nr;
+    uint32_t R = 0, RA1 = 0;
+    if (wl) {
+        R = stA[rt];
+        RA1 = stA1[rt];
+    }
+    __syncthreads();  // the staged roots are read before win is written
+    uint4 *w4 = reinterpret_cast<uint4 *>(win + t * 16);
+    if (wl && !w1) {  // W0: the window below R (slots 1..15; nd[0] = R)
+        uint32_t wbad = 0;
+        uint32_t nd[16], hv[16];
+        nd[0] = R;
+        nd[1] = chk(fat(R, i - 2));
+        nd[2] = chk(fat(R, i - 3));
+        nd[3] = chk(c2(R, i - 2));
+        nd[4] = chk(fat(R, i - 4));
+        nd[6] = chk(c2(R, i - 3));
+        nd[8] = chk(fat(R, i - 5));
+        nd[12] = chk(c2(R, i - 4));
+        nd[5] = chk(fat(nd[1], i - 4));
+        nd[7] = chk(fat(nd[3], i - 4));
+        nd[9] = chk(fat(nd[1], i - 5));
+        nd[10] = chk(fat(nd[2], i - 5));
+        nd[11] = chk(fat(nd[3], i - 5));
+        nd[13] = chk(c2(nd[1], i - 4));
+        nd[14] = chk(c2(nd[2], i - 4));
+        nd[15] = chk(c2(nd[3], i - 4));
+#pragma unroll
+        for (int v = 0; v < 16; ++v) hv[v] = hiw(nd[v]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            uint32_t ov[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int v = 4 * g + u;
+                if (v == 0) {
+                    ov[u] = 0;
+                    continue;
+                }
+                const int hb = 31 - __builtin_clz((unsigned)v);
+                const int pv = v & ~(1 << hb);
+                ov[u] = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
+                wbad += ov[u] == CZ_NONE;
+            }
+            if (g == 0) ov[0] = wbad;  // (the stores put the row's own word there)
+            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+        }
+        if (wbad) {
+            win[t * 16] = wbad;  // the count of all fifteen words
+            anybad = 1;
+        }
+    } else if (wl) {  // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
+        uint32_t wbad = 0;
+        uint32_t nd[15], hv[15];
+        nd[0] = RA1;
+        const uint32_t hR = hiw(R);
+        nd[1] = chk(fat(nd[0], i - 2));
+        nd[2] = chk(fat(nd[0], i - 3));
+        nd[3] = chk(c2(nd[0], i - 2));
+        nd[4] = chk(fat(nd[0], i - 4));
+        nd[6] = chk(c2(nd[0], i - 3));
+        nd[8] = chk(fat(nd[0], i - 5));
+        nd[12] = chk(c2(nd[0], i - 4));
+        nd[5] = chk(fat(nd[1], i - 4));
+        nd[7] = chk(fat(nd[3], i - 4));
+        nd[9] = chk(fat(nd[1], i - 5));
+        nd[10] = chk(fat(nd[2], i - 5));
+        nd[11] = chk(fat(nd[3], i - 5));
+        nd[13] = chk(c2(nd[1], i - 4));
+        nd[14] = chk(c2(nd[2], i - 4));
+#pragma unroll
+        for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            uint32_t ov[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int v = 4 * g + u;
+                if (v == 15) {
+                    ov[u] = wbad;
+                    continue;
+                }
+                if (v == 0) {
+                    ov[u] = enc(R, hR, i - 1, nd[0], hv[0]);
+                } else {
+                    const int hb = 31 - __builtin_clz((unsigned)v);
+                    const int pv = v & ~(1 << hb);
+                    ov[u] = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
+                }
+                wbad += ov[u] == CZ_NONE;
+            }
+            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+        }
+        if (wbad) anybad = 1;
+    }
+    __syncthreads();
+    if (anybad) {  // rare: every row carries its root's CZ_NONE words
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t r = (uint32_t)t + 256u * k;
+            if (r < rhi) {
+                const uint32_t x = ridx[r];
+                const uint32_t wb = win[x * 16] + win[(128 + x) * 16 + 15];
+                if (wb) atomicAdd(&sbad, wb);
+            }
+        }
+    }
+    // both planes: rows [0, rhi) x 4 chunks of 16 B each, whole lines per store
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const size_t tp0 = (size_t)(2 * lvl) * M + j0;
+    const uint32_t nc = 4u * rhi;
+    for (uint32_t c = t; c < 2u * nc; c += 256u) {
+        const uint32_t pl = c >= nc, cc = pl ? c - nc : c;
+        const uint32_t e = cc >> 2, qq = cc & 3u;
+        uint4 u = *reinterpret_cast<const uint4 *>(win + (pl * 128u + ridx[e]) * 16 + qq * 4);
+        if (!pl && qq == 0) u.x = e0s[e];   // slot 0 of the b = 0 entry
+        if (pl && qq == 3) u.w = e0s[e];    // slot 15 of the b = 1 entry
+        const v4u wv4 = {u.x, u.y, u.z, u.w};
+        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + pl * (size_t)M + e) * 4) + qq);
+    }
+    if (oob) atomicOr(esc + 1, 1u);
+    __syncthreads();
+    if (t == 0 && sbad) atomicAdd(esc, sbad);
+}
+
 // Block counts of k_cz_build_roots2 (cz2_nb): rows per block ~ 230 /
 // (expected distinct-root fraction of the level), from the level's finger
 // distance 2^i against the ring's mean gap 2^128 / n (uniform ring, by
 // simulation: 0.94 at 2^-4 of the mean gap, 0.89 at 2^-3, 0.80 at 2^-2, 0.685
 // at 2^-1, 0.57 at 1x, 0.51 at 2x, 0.50 from 4x up); a block with more than
 // 256 roots computes them in batches, so the estimate only sizes the blocks.
-static void cz2_plan(size_t n, int &gl256, uint64_t &nbt) {
+static void cz2_plan(size_t n, int &gl256, uint64_t &nbt, double target = 230.0) {
     const double gl = 128.0 - log2((double)n);
     gl256 = (int)lround(gl * 256.0);
     // CX_CZ2_NB (A/B): the same block count for every level (16 = 256 rows)
@@ -3742,8 +4018,9 @@ static void cz2_plan(size_t n, int &gl256, uint64_t &nbt) {
     static const double frac[8] = {0.97, 0.94, 0.89, 0.80, 0.685, 0.57, 0.51, 0.50};
     nbt = 0;
     for (int k = 0; k < 8; ++k) {
-        uint32_t rb = (uint32_t)(230.0 / frac[k]);
-        if (rb < 256) rb = 256;
+        uint32_t rb = (uint32_t)(target / frac[k]);
+        const uint32_t rmin = target > 128.0 ? 256u : 128u;
+        if (rb < rmin) rb = rmin;
         if (rb > (uint32_t)CZ2_RMAX) rb = CZ2_RMAX;
         uint32_t nb = (CZ2_CHUNK + rb - 1) / rb;
         while ((CZ2_CHUNK + nb - 1) / nb > (uint32_t)CZ2_RMAX) ++nb;
@@ -3758,10 +4035,10 @@ hipError_t cz_build(const FingerView &fv, const cell128 *ring, const uint64_t *r
 }
 
 // Blocks of the main k_cz_build_roots2 launch.
-static uint64_t cz2_blocks(size_t n, int lvl_base, int nlev, uint32_t M) {
+static uint64_t cz2_blocks(size_t n, int lvl_base, int nlev, uint32_t M, double target = 230.0) {
     int gl256;
     uint64_t nbt;
-    cz2_plan(n, gl256, nbt);
+    cz2_plan(n, gl256, nbt, target);
     uint64_t TB = 0;
     for (int l = 0; l < nlev; ++l) {
         int k = (((lvl_base + l) * 256 - gl256) >> 8) + 6;
@@ -3775,7 +4052,8 @@ static uint64_t cz2_blocks(size_t n, int lvl_base, int nlev, uint32_t M) {
 // lists of one uint2 per block.
 size_t cz_build_ws_words(size_t n, int lvl_base, int nlev, uint32_t M) {
     if (n == 0 || M == 0 || nlev <= 0) return 4;
-    return 4 + 4 * (size_t)cz2_blocks(n, lvl_base, nlev, M);
+    const uint64_t b2 = cz2_blocks(n, lvl_base, nlev, M), b3 = cz2_blocks(n, lvl_base, nlev, M, CZ3_TARGET);
+    return 4 + 4 * (size_t)(b2 > b3 ? b2 : b3);
 }
 
 // Roots per block of k_cz_build_roots2 before it defers rows to an overflow
@@ -3833,11 +4111,13 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     // pair / quad planes: roots2 only
     if ((fv.P || fv.Q) && !(ws && fv.rs && (fv.P2 || fv.Q))) return hipErrorInvalidValue;
     if (fv.Q && n >= (1u << 28)) return hipErrorInvalidValue;  // 32-bit byte offsets
-    if (planes && (fv.C2 || fv.P2 || fv.Q) && fv.roots == 2 && fv.rs && ws) {
+    if (planes && (fv.C2 || fv.P2 || fv.Q) && fv.roots >= 2 && fv.rs && ws) {
+        const bool par = fv.roots == 3 && fv.C2 && !fv.P && !fv.Q;  // k_cz_build_roots3
+        const double target = par ? CZ3_TARGET : 230.0;
         int gl256;
         uint64_t nbt;
-        cz2_plan(n, gl256, nbt);
-        const uint64_t blocks = cz2_blocks(n, lvl_base, nlev, M);
+        cz2_plan(n, gl256, nbt, target);
+        const uint64_t blocks = cz2_blocks(n, lvl_base, nlev, M, target);
         if (blocks >= (1ull << 31) || nlev > 255) return hipErrorInvalidValue;
         // two overflow lists (ping-pong), counters in ws[0], ws[1]
         uint2 *list[2] = {reinterpret_cast<uint2 *>(ws + 4),  // 16-B aligned
@@ -3856,7 +4136,11 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
             return ev ? (atoi(ev) & 31) : 0;
         }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
-            if (fv.Q)  // quad planes
+            if (par)
+                k_cz_build_roots3<7><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
+                                                          p_first, M, gs, out, esc, gl256, nbt, it,
+                                                          oc, ov, cap);
+            else if (fv.Q)  // quad planes
                 k_cz_build_roots2<7, 2><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,
                                                              oc, ov, cap, mode);

@@ -628,6 +628,15 @@ def test_route_table_from_level_planes_identical(lg):
     ring.set_table_build(7)  # ... on quad planes
     ring.build_fingers()
     h_quads = ring.route_table_hash()
+    ring.set_table_build(8)  # both windows of a root at once, stores last
+    ring.build_fingers()
+    h_par = ring.route_table_hash()
+    _lib.set_fault(2)  # ... with overflow launches
+    try:
+        ring.build_fingers()
+    finally:
+        _lib.set_fault(0)
+    h_par_ovf = ring.route_table_hash()
     # the default (blocks sized by distinct roots) with most rows deferred to
     # overflow launches (48 roots per block instead of 256)
     from chordx import _lib
@@ -638,7 +647,7 @@ def test_route_table_from_level_planes_identical(lg):
     finally:
         _lib.set_fault(0)
     h_overflow = ring.route_table_hash()
-    assert h_planes == h_rows == h_planes_only == h_entry == h_roots256 == h_overflow == h_nopairs == h_pairs == h_quads
+    assert h_planes == h_rows == h_planes_only == h_entry == h_roots256 == h_overflow == h_nopairs == h_pairs == h_quads == h_par == h_par_ovf
     assert h_planes != 0
 
 
@@ -711,6 +720,9 @@ def test_route_table_builds_edge_rings(cx, O, kind):
     ring.set_table_build(7)  # ... on quad planes
     ring.build_fingers()
     h8, e8 = ring.route_table_hash(), ring.route_info()[1]
+    ring.set_table_build(8)  # both windows of a root at once, stores last
+    ring.build_fingers()
+    h9, e9 = ring.route_table_hash(), ring.route_info()[1]
     from chordx import _lib
     ring.set_table_build(0)
     _lib.set_fault(2)  # the default with overflow launches (48 roots per block)
@@ -719,8 +731,8 @@ def test_route_table_builds_edge_rings(cx, O, kind):
     finally:
         _lib.set_fault(0)
     h5, e5 = ring.route_table_hash(), ring.route_info()[1]
-    assert h0 == h2 == h3 == h4 == h5 == h6 == h7 == h8 and h0 != 0
-    assert e0 == e2 == e3 == e4 == e5 == e6 == e7 == e8
+    assert h0 == h2 == h3 == h4 == h5 == h6 == h7 == h8 == h9 and h0 != 0
+    assert e0 == e2 == e3 == e4 == e5 == e6 == e7 == e8 == e9
     ring.set_table_build(0)
     ring.build_fingers()
     want = O.ring_build(ids)
