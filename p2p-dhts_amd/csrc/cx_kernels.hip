@@ -3274,10 +3274,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     __shared__ uint32_t wcnt[8];
     __shared__ uint32_t sbad;    // CZ_NONE words written by the block (rare)
     __shared__ uint32_t anybad;  // some window of the block holds one
-    // (LAY != 0): the slices of each window's root and of its A1, kept for W1
+    // pair / quad planes: the slices of each window's root and of its A1, kept for W1
     __shared__ uint32_t rsR[(LAY != 0) ? 256 : 1], ra1s[(LAY != 0) ? 256 : 1];
     uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
-    uint32_t *stS = win + 2 * CZ2_RMAX, *stS1 = win + 3 * CZ2_RMAX;  // (LAY != 0): their slices
+    uint32_t *stS = win + 2 * CZ2_RMAX, *stS1 = win + 3 * CZ2_RMAX;  // pair / quad planes: their slices
     uint32_t j0, rows;
     int lvl;
     if (items) {
@@ -3317,7 +3317,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     auto c2 = [&](uint32_t x, int l) -> uint32_t {
         return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
     };
-    // (LAY != 0): {finger, its ID slice} in one 8-B gather (uniform plane base plus a
+    // pair planes: {finger, its ID slice} in one 8-B gather (uniform plane base plus a
     // 32-bit byte offset, x < n < 2^29)
     auto ld64 = [](const uint2 *base, uint32_t x) -> uint2 {
         return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + x * 8u);
@@ -3397,7 +3397,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         const bool v = r < rows;
         A[k] = v ? stA[r] : 0u;
         A1[k] = v ? stA1[r] : 0u;
-        if constexpr ((LAY != 0)) {
+        if constexpr (LAY != 0) {
             S[k] = v ? stS[r] : 0u;
             S1[k] = v ? stS1[r] : 0u;
         }
@@ -3424,7 +3424,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (first[0]) {
         stA[rk0] = A[0];
         stA1[rk0] = A1[0];
-        if constexpr ((LAY != 0)) {
+        if constexpr (LAY != 0) {
             stS[rk0] = S[0];
             stS1[rk0] = S1[0];
         }
@@ -3432,7 +3432,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (first[1]) {
         stA[rk1] = A[1];
         stA1[rk1] = A1[1];
-        if constexpr ((LAY != 0)) {
+        if constexpr (LAY != 0) {
             stS[rk1] = S[1];
             stS1[rk1] = S1[1];
         }
@@ -3460,7 +3460,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (wl) {
         R = stA[t];
         RA1 = stA1[t];
-        if constexpr ((LAY != 0)) {
+        if constexpr (LAY != 0) {
             SR = stS[t];
             SRA1 = stS1[t];
         }
@@ -3475,7 +3475,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         uint32_t wbad = 0;
         uint32_t nd[16], hv[16];
         nd[0] = R;
-        if constexpr ((LAY != 0)) {
+        if constexpr (LAY != 0) {
             rsR[t] = SR;
             ra1s[t] = SRA1;
             hv[0] = SR;
@@ -3603,7 +3603,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         uint32_t nd[15], hv[15];
         uint32_t hR;
         nd[0] = ra1[t] & 0x3FFFFFFFu;
-        if constexpr ((LAY != 0)) {
+        if constexpr (LAY != 0) {
             hR = rsR[t];
             hv[0] = ra1s[t];
             uint2 q[15];
