@@ -309,7 +309,10 @@ class Ring:
         """Internal A/B switch for the route-table build: 0 = level + two-hop
         planes, root-centric windows (default), 1 = the row-major finger
         table, 2 = level planes only, 3 = level + two-hop planes, one lane per
-        entry (the round-2 build).  All build the same table."""
+        entry (the round-2 build), 4 = root-centric in 256-row blocks (round
+        3), 5 = alias of 0, 6 / 7 = as 0 on pair / quad planes, 8 = both
+        windows of a root at once, 9 = as 0 with plane 0 stored after the W1
+        gathers.  All build the same table."""
         f = L.lib().cxi_set_table_build
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))

@@ -736,7 +736,8 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
             fv.C2 = c2.as<uint32_t>();
             // 0: blocks sized by distinct roots, 4: 256-row root blocks (round 3),
             // 3: one lane per entry (round 2)
-            fv.roots = r->table_build == 8 ? 3
+            fv.roots = r->table_build == 9 ? 4
+                       : r->table_build == 8 ? 3
                        : (r->table_build == 0 || r->table_build >= 5) ? 2
                        : (r->table_build == 4 ? 1 : 0);
         }
@@ -2521,11 +2522,12 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
 // one lane per entry (k_cz_build, the round-2 build), 4 = root-centric windows
 // in 256-row blocks (k_cz_build_roots, round 3), 5 = the same as 0, 6 = as 0
 // on pair planes, 7 = as 0 on quad planes, 8 = both windows of a root at once,
-// stores last (k_cz_build_roots3).  All give the same table.  Takes effect at
-// the next finger build.
+// stores last (k_cz_build_roots3), 9 = as 0 with plane 0 stored after the W1
+// gathers (k_cz_build_roots2<7, 0, true>).  All give the same table.  Takes
+// effect at the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 8, CX_E_INVALID, "variant must be 0 .. 8");
+    CX_CHECK(variant >= 0 && variant <= 9, CX_E_INVALID, "variant must be 0 .. 9");
     ring->table_build = variant;
     return CX_OK;
 }

@@ -3245,7 +3245,11 @@ __device__ __forceinline__ uint32_t cz2_nb(int l, int gl256, uint64_t nbt) {
 // its own overflow to ovf.
 // LAY: 0 = 4-B planes + ID slices gathered apart, 1 = pair planes, 2 = quad
 // planes (fingers_pairs2 / fingers_quads)
-template <int WPE, int LAY>
+// SL (table_build 9, A/B): plane 0 leaves after the W1 gathers instead of
+// before them.  A wave's loads and stores share one in-order vmcnt queue, so
+// with SL false every W1 gather also waits for the plane-0 stores' acks; with
+// SL the W1 words wait in registers (16) while plane 0 drains from LDS.
+template <int WPE, int LAY, bool SL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
                        uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
@@ -3585,18 +3589,25 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         }
     }
     // plane 0: rows [0, rhi) x 4 chunks of 16 B, whole lines per store
-    for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
-        const uint32_t e = c >> 2, qq = c & 3u;
-        // one 16-B LDS read per chunk (the window's words sit at their slots;
-        // a lane pair of entries covers 32 banks): slot 0 is the row's own word
-        uint4 u = *reinterpret_cast<const uint4 *>(win + ridx[e] * 16 + qq * 4);
-        if (qq == 0) u.x = e0s[e];
-        if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
-        const v4u wv4 = {u.x, u.y, u.z, u.w};
-        const size_t ent0 = (mode & 16) ? ((tp0 + e) & ((1u << 21) - 1)) : tp0 + e;
-        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent0 * 4) + qq);
+    auto plane0 = [&]() {
+        for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
+            const uint32_t e = c >> 2, qq = c & 3u;
+            // one 16-B LDS read per chunk (the window's words sit at their
+            // slots; a lane pair of entries covers 32 banks): slot 0 is the
+            // row's own word
+            uint4 u = *reinterpret_cast<const uint4 *>(win + ridx[e] * 16 + qq * 4);
+            if (qq == 0) u.x = e0s[e];
+            if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
+            const v4u wv4 = {u.x, u.y, u.z, u.w};
+            const size_t ent0 = (mode & 16) ? ((tp0 + e) & ((1u << 21) - 1)) : tp0 + e;
+            __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent0 * 4) + qq);
+        }
+    };
+    if constexpr (!SL) {
+        plane0();
+        __syncthreads();  // plane 0 has read every W0 word
     }
-    __syncthreads();  // plane 0 has read every W0 word
+    uint4 o1[4];  // SL: the W1 words until plane 0 has left
     // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
     if (wl) {
         uint32_t wbad = 0;
@@ -3691,9 +3702,19 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
                 }
                 wbad += ov[u] == CZ_NONE;
             }
-            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+            if constexpr (SL) o1[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+            else w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
         }
         if (wbad) anybad = 1;
+    }
+    if constexpr (SL) {
+        plane0();
+        __syncthreads();  // plane 0 has read every W0 word
+        if (wl) {
+            uint4 *w4 = reinterpret_cast<uint4 *>(wr);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) w4[g] = o1[g];
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -4148,6 +4169,10 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
                 k_cz_build_roots2<7, 1><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,
                                                              oc, ov, cap, mode);
+            else if (fv.roots == 4)  // plane 0 after the W1 gathers
+                k_cz_build_roots2<7, 0, true><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
+                                                                   nlev, p_first, M, gs, out, esc,
+                                                                   gl256, nbt, it, oc, ov, cap, mode);
             else if (wpe8)
                 k_cz_build_roots2<8, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
                                                              p_first, M, gs, out, esc, gl256, nbt, it,

@@ -144,7 +144,9 @@ struct FingerView {
     const uint32_t *C2 = nullptr;
     // host-side build choice: 1 = root-centric windows, 256 rows per block
     // (k_cz_build_roots); 2 = blocks sized by distinct roots (k_cz_build_roots2,
-    // needs rs; without it the build falls back to 1); both need C2
+    // needs rs; without it the build falls back to 1); 3 = both windows of a
+    // root at once (k_cz_build_roots3); 4 = as 2, plane 0 stored after the W1
+    // gathers; all need C2
     int roots = 0;
     // root-centric build, optional: 32-bit ID slices (ring_codes) for the gap
     // codes instead of the 64-bit high words; only when every ring gap is

@@ -631,23 +631,25 @@ def test_route_table_from_level_planes_identical(lg):
     ring.set_table_build(8)  # both windows of a root at once, stores last
     ring.build_fingers()
     h_par = ring.route_table_hash()
-    _lib.set_fault(2)  # ... with overflow launches
-    try:
-        ring.build_fingers()
-    finally:
-        _lib.set_fault(0)
-    h_par_ovf = ring.route_table_hash()
-    # the default (blocks sized by distinct roots) with most rows deferred to
-    # overflow launches (48 roots per block instead of 256)
+    ring.set_table_build(9)  # plane 0 stored after the W1 gathers
+    ring.build_fingers()
+    h_sl = ring.route_table_hash()
     from chordx import _lib
-    ring.set_table_build(0)
-    _lib.set_fault(2)
-    try:
-        ring.build_fingers()
-    finally:
-        _lib.set_fault(0)
-    h_overflow = ring.route_table_hash()
-    assert h_planes == h_rows == h_planes_only == h_entry == h_roots256 == h_overflow == h_nopairs == h_pairs == h_quads == h_par == h_par_ovf
+
+    def with_overflow(tb):
+        # most rows deferred to overflow launches (48 roots per block)
+        ring.set_table_build(tb)
+        _lib.set_fault(2)
+        try:
+            ring.build_fingers()
+        finally:
+            _lib.set_fault(0)
+        return ring.route_table_hash()
+
+    h_ovf = [with_overflow(tb) for tb in (8, 9, 0)]  # the default last
+    assert h_planes == h_rows == h_planes_only == h_entry == h_roots256 == h_nopairs
+    assert h_planes == h_pairs == h_quads == h_par == h_sl
+    assert h_ovf == [h_planes] * 3
     assert h_planes != 0
 
 
