@@ -5403,20 +5403,47 @@ constexpr int ROW_BLOCK = 256;
 
 template <class T>
 __device__ __forceinline__ void flush_rows(const T *stage, T *out, size_t base, int cnt, int w) {
+    static_assert(16 % sizeof(T) == 0, "16-B chunks of whole elements");
     const int total = cnt * w;
     T *dst = out + base * (size_t)w;
     int t0 = 0;
-    if (sizeof(T) == 4 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(stage)) & 15) == 0) {
         // 16-B streaming stores for the bulk (rows are written once, read by
         // the caller later): the block's range is contiguous and LDS-staged
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-        const int nv = total >> 2;
+        constexpr int per = 16 / (int)sizeof(T);
+        const int nv = total / per;
         const v4u *sv = reinterpret_cast<const v4u *>(stage);
         v4u *dv = reinterpret_cast<v4u *>(dst);
         for (int t = threadIdx.x; t < nv; t += blockDim.x) __builtin_nontemporal_store(sv[t], dv + t);
-        t0 = nv << 2;
+        t0 = nv * per;
     }
     for (int t = t0 + threadIdx.x; t < total; t += blockDim.x) dst[t] = stage[t];
+}
+
+// flush_rows for the target rows, which then refills the stage with 0xFF
+// (no target) for the next tile: each lane refills what it stored.
+__device__ __forceinline__ void flush_rows_refill(uint8_t *stage, uint8_t *out, size_t base,
+                                                  int cnt, int w) {
+    const int total = cnt * w;
+    uint8_t *dst = out + base * (size_t)w;
+    int t0 = 0;
+    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(stage)) & 15) == 0) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const int nv = total >> 4;
+        v4u *sv = reinterpret_cast<v4u *>(stage);
+        v4u *dv = reinterpret_cast<v4u *>(dst);
+        const v4u none = {~0u, ~0u, ~0u, ~0u};
+        for (int t = threadIdx.x; t < nv; t += blockDim.x) {
+            __builtin_nontemporal_store(sv[t], dv + t);
+            sv[t] = none;
+        }
+        t0 = nv << 4;
+    }
+    for (int t = t0 + threadIdx.x; t < total; t += blockDim.x) {
+        dst[t] = stage[t];
+        stage[t] = 0xFF;
+    }
 }
 
 // Rows of `w` ring indices (s[k] + j) mod N for j < nvalid, CX_NONE after, for
@@ -5437,15 +5464,26 @@ __device__ __forceinline__ void flush_window(const uint32_t *s, uint32_t *out, s
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         const int nv = total >> 2;
         v4u *dv = reinterpret_cast<v4u *>(dst);
+        // (row k, column j) of word 4t, advanced by 4 blockDim words a step
+        // (one division per call instead of one per store)
+        const int step = 4 * (int)blockDim.x, dk = step / w, dj = step - dk * w;
+        int k = (4 * (int)threadIdx.x) / w, j = 4 * (int)threadIdx.x - k * w;
         for (int t = threadIdx.x; t < nv; t += blockDim.x) {
-            int k = (4 * t) / w, j = 4 * t - k * w;
+            const int k0 = k, j0 = j;
+            k += dk;
+            j += dj;
+            if (j >= w) {
+                j -= w;
+                ++k;
+            }
+            int kk = k0, jj = j0;
             uint32_t x[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                x[u] = val(k, j);
-                if (++j == w) {
-                    j = 0;
-                    ++k;
+                x[u] = val(kk, jj);
+                if (++jj == w) {
+                    jj = 0;
+                    ++kk;
                 }
             }
             const v4u xv = {x[0], x[1], x[2], x[3]};
@@ -5640,8 +5678,9 @@ hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 
 // the tags after m -- a survivor at old rank j holds new rank r = #new entries
 // from m before it, a departed one is CX_NONE (dhash_peer.cpp:322-328 on the
 // mapping cx_churn returns).  Bucket b (top kb bits, load factor <= 1/2) is
-// one 32-B entry: {hint0 | so_b | sn_b}, {tags of m_b .. m_b + 31 | hint1 |
-// cnt} with m_b = the bucket's first merged entry, hint = ID bits
+// one 32-B entry: {hint0 | so_b | sn_b}, {old mask | new mask | hint1 | cnt}
+// with m_b = the bucket's first merged entry, bit k of the old / new mask =
+// merged entry m_b + k is an old / new ring entry (its tag's two bits), hint = ID bits
 // [64 - kb, 128 - kb) (hint1's low two bits hold cnt = entries in the bucket,
 // capped at 3).  One 32-B gather replaces two directory searches and the
 // 64-B window of old_to_new entries; keys it cannot settle (a third entry in
@@ -5662,6 +5701,32 @@ __device__ __forceinline__ void cd_fetch(const ChurnDir &c, u128 key, uint4 &A, 
     B = c.cd[2 * b + 1];
 }
 
+// Bit mask of positions 0 .. k.
+__device__ __forceinline__ uint32_t cd_upto(int k) { return k >= 31 ? 0xFFFFFFFFu : (2u << k) - 1u; }
+
+// Position of the c-th (1-based) set bit of M, which has at least c: k rises
+// to c - 1 + (clear bits of M in [0, k]) until it stops (each step skips the
+// clear bits found; a window has few).
+__device__ __forceinline__ int cd_nth_bit(uint32_t M, int c) {
+    int k = c - 1;
+    for (;;) {
+        const int nk = c - 1 + __popc(~M & cd_upto(k));
+        if (nk == k) return k;
+        k = nk;
+    }
+}
+
+// x without the bit positions of Z (higher bits move down); x is clear at Z.
+__device__ __forceinline__ uint32_t cd_drop(uint32_t x, uint32_t Z) {
+    while (Z) {  // highest first, so the lower positions stay valid
+        const int p = 31 - __builtin_clz(Z);
+        Z ^= 1u << p;
+        const uint32_t lo = (1u << p) - 1u;
+        x = (x & lo) | ((x >> 1) & ~lo);
+    }
+    return x;
+}
+
 // 1 = settled (so, sn, has, mis set), 0 = take the search path.  A, B = the
 // key's bucket entry (cd_fetch).
 __device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, const uint4 A,
@@ -5670,61 +5735,59 @@ __device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, const uint
                                          uint32_t &mis) {
     const uint64_t xf = (uint64_t)(key >> (64 - c.kb));
     const uint64_t h0 = ((uint64_t)A.y << 32) | A.x;
-    uint64_t tg = ((uint64_t)B.y << 32) | B.x;
+    uint32_t O = B.x, N = B.y;  // bit k: merged entry m + k is old / new
     const uint64_t h1c = ((uint64_t)B.w << 32) | B.z;
     const int cnt = (int)(h1c & 3);
     uint32_t o = A.z, w = A.w;  // so / sn at the bucket's first merged entry
     int t = 0;
     if (cnt >= 1) {
         if (xf == h0) {  // exact compare with the first entry's ID
-            const u128 id = (tg & 1) ? ld128(c.ring_old + o) : ld128(c.ring_new + w);
+            const u128 id = (O & 1) ? ld128(c.ring_old + o) : ld128(c.ring_new + w);
             t = key > id;
         } else {
             t = xf > h0;
         }
         if (t) {
-            o += (uint32_t)(tg & 1);
-            w += (uint32_t)((tg >> 1) & 1);
+            o += O & 1u;
+            w += N & 1u;
             if (o >= n_old) o -= n_old;
             if (w >= n_new) w -= n_new;
-            tg >>= 2;
+            O >>= 1;
+            N >>= 1;
             if (cnt >= 2) {
                 int t2;
                 if ((xf >> 2) == (h1c >> 2)) {
-                    const u128 id = (tg & 1) ? ld128(c.ring_old + o) : ld128(c.ring_new + w);
+                    const u128 id = (O & 1) ? ld128(c.ring_old + o) : ld128(c.ring_new + w);
                     t2 = key > id;
                 } else {
                     t2 = (xf >> 2) > (h1c >> 2);
                 }
                 if (t2) {
                     if (cnt == 3) return 0;  // a third entry may precede the key
-                    o += (uint32_t)(tg & 1);
-                    w += (uint32_t)((tg >> 1) & 1);
+                    o += O & 1u;
+                    w += N & 1u;
                     if (o >= n_old) o -= n_old;
                     if (w >= n_new) w -= n_new;
-                    tg >>= 2;
+                    O >>= 1;
+                    N >>= 1;
                 }
             }
         }
     }
     so = o;
     sn = w;
-    uint32_t j = 0, r = 0, hs = 0, ms = 0;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const uint32_t g = (uint32_t)(tg >> (2 * k)) & 3u;
-        if ((int)j < no) {
-            if (g == 3u) {
-                if ((int)r < nn) hs |= 1u << r;
-                else ms |= 1u << j;
-            }
-            j += g & 1u;
-            r += g >> 1;
-        }
-    }
-    if ((int)j < no) return 0;  // window ran out of tags (shifted-in zeros)
-    has = hs;
-    mis = ms;
+    // The old window is the first no old entries from the key on (positions
+    // up to the no-th set bit of O).  A survivor (old and new) at position k
+    // has old rank j = |O below k| and new rank r = |N below k|: it already
+    // holds the key's new-list rank r when r < nn (positions up to the nn-th
+    // new entry), else holder j is misplaced.  r and j are the survivor's
+    // index once the positions without a new (old) entry are dropped.
+    if (__popc(O) < no) return 0;  // the window ran out of tags
+    const uint32_t act = cd_upto(cd_nth_bit(O, no));
+    const uint32_t S = O & N & act;
+    const uint32_t early = __popc(N & act) >= nn ? cd_upto(cd_nth_bit(N, nn)) : 0xFFFFFFFFu;
+    has = cd_drop(S & early, ~N & act);
+    mis = cd_drop(S & ~early, ~O & act);
     return 1;
 }
 
@@ -5748,7 +5811,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
     __shared__ uint32_t s_sn[ROW_BLOCK], s_so[ROW_BLOCK];  // the tile's successors
-    __shared__ uint8_t stage_t[ROW_BLOCK * CX_MAX_NSUCC];
+    __shared__ __attribute__((aligned(16))) uint8_t stage_t[ROW_BLOCK * CX_MAX_NSUCC];
     Searcher<DIR>::stage(sv_new, lds_new);
     if (CHURN) Searcher<DIR>::stage(sv_old, lds_old);
     const uint32_t n_new = sv_new.ev.n;
@@ -5760,15 +5823,29 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
     const bool o2n_al = CHURN && ((uintptr_t)old_to_new & 15) == 0;
     const bool use_cd = CD && *cd.ok;  // wave-uniform
     static_assert(CX_MAX_NSUCC <= 17, "five 16-B o2n loads cover 17 entries");
-    for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q;
-         base += (size_t)gridDim.x * ROW_BLOCK) {
+    static_assert(ROW_BLOCK * CX_MAX_NSUCC % 16 == 0, "stage_t in 16-B chunks");
+    for (int t = threadIdx.x; t < ROW_BLOCK * CX_MAX_NSUCC / 16; t += blockDim.x)
+        reinterpret_cast<uint4 *>(stage_t)[t] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    __syncthreads();
+    // software pipeline: the next tile's key is loaded when a tile starts and
+    // its churn-directory entry before the tile's rows are flushed, so neither
+    // gather sits between one tile's stores and the next tile's search
+    const size_t stride = (size_t)gridDim.x * ROW_BLOCK;
+    u128 key_n = 0;
+    uint4 A_n = {0, 0, 0, 0}, B_n = {0, 0, 0, 0};
+    if ((size_t)blockIdx.x * ROW_BLOCK + threadIdx.x < q) {
+        key_n = ld128(keys + (size_t)blockIdx.x * ROW_BLOCK + threadIdx.x);
+        if (use_cd) cd_fetch(cd, key_n, A_n, B_n);
+    }
+    for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q; base += stride) {
         const size_t i = base + threadIdx.x;
         const int cnt = (q - base < (size_t)ROW_BLOCK) ? (int)(q - base) : ROW_BLOCK;
+        const u128 key = key_n;
+        const uint4 A = A_n, B = B_n;
+        const bool more = i + stride < q;
+        if (more) key_n = ld128(keys + i + stride);
         if (i < q) {
-            const u128 key = ld128(keys + i);
             uint32_t sn = 0, so = 0, has = 0, m = 0;
-            uint4 A = {0, 0, 0, 0}, B = {0, 0, 0, 0};
-            if (use_cd) cd_fetch(cd, key, A, B);
             const bool settled =
                 use_cd && cd_lookup(cd, key, A, B, n_old, n_new, no, nn, so, sn, has, m);
             if (!settled) {
@@ -5838,30 +5915,24 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
             s_so[threadIdx.x] = so;
             count[i] = (uint8_t)nn;
             if (CHURN && old_lists) old_count[i] = (uint8_t)no;
-            // pass 2: misplaced holders in rank order take the first lacking rank
+            // pass 2: misplaced holders in rank order take the first lacking
+            // ranks (the row is 0xFF already: most keys have none)
             uint8_t *tg = stage_t + threadIdx.x * nslots;
-#pragma unroll
-            for (int j = 0; j < CX_MAX_NSUCC; ++j) {
-                if (j >= nslots) break;
-                uint8_t t = 0xFF;
-                if ((m >> j) & 1u) {
-                    const uint32_t free_ranks = ~has & full;
-                    if (free_ranks) {
-                        const int rr = __builtin_ctz(free_ranks);
-                        has |= 1u << rr;
-                        t = (uint8_t)rr;
-                    }
-                }
-                tg[j] = t;
+            uint32_t mm = m, free_ranks = ~has & full;
+            while (mm && free_ranks) {
+                tg[__builtin_ctz(mm)] = (uint8_t)__builtin_ctz(free_ranks);
+                mm &= mm - 1u;
+                free_ranks &= free_ranks - 1u;
             }
             mask[i] = (uint16_t)m;
         }
+        if (use_cd && more) cd_fetch(cd, key_n, A_n, B_n);
         __syncthreads();
         // new lists (sn + j mod n_new, j < nn) and old lists (so + j mod
         // n_old, j < no <= n_old: one wrap at most) straight from the successors
         flush_window(s_sn, new_lists, base, cnt, nlist, nn, n_new);
         if (CHURN && old_lists) flush_window(s_so, old_lists, base, cnt, nlist, no, n_old);
-        flush_rows(stage_t, target, base, cnt, nslots);
+        flush_rows_refill(stage_t, target, base, cnt, nslots);
         __syncthreads();
     }
 }
@@ -5964,16 +6035,17 @@ __global__ void k_cd_pack(const cell128 *mid, const uint32_t *mso, const uint32_
         const uint32_t m0 = a < M ? a : 0;
         const uint64_t h0 = cnt >= 1 ? (uint64_t)(ld128(mid + a) >> (64 - kb)) : 0;
         const uint64_t h1 = cnt >= 2 ? (uint64_t)(ld128(mid + a + 1) >> (64 - kb)) : 0;
-        uint64_t tags = 0;
+        uint32_t om = 0, nm = 0;  // old / new masks of the 32 merged entries
         uint32_t m = m0;
         for (int j = 0; j < 32; ++j) {
-            tags |= (uint64_t)mtag[m] << (2 * j);
+            const uint32_t g = mtag[m];
+            om |= (g & 1u) << j;
+            nm |= (g >> 1) << j;
             if (++m == M) m = 0;
         }
         const uint64_t h1c = (h1 & ~3ull) | cnt;
         cd[2 * b] = make_uint4((uint32_t)h0, (uint32_t)(h0 >> 32), mso[m0], msn[m0]);
-        cd[2 * b + 1] = make_uint4((uint32_t)tags, (uint32_t)(tags >> 32), (uint32_t)h1c,
-                                   (uint32_t)(h1c >> 32));
+        cd[2 * b + 1] = make_uint4(om, nm, (uint32_t)h1c, (uint32_t)(h1c >> 32));
     }
 }
 
