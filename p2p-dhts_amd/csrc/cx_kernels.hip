@@ -5799,7 +5799,7 @@ __device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, const uint
 // old_lists / old_count (CHURN, may be null): the keys' old n-successor lists
 // as cx_nsucc on the old ring gives them -- the scan already holds the old
 // successor, so DHash placement + maintenance share one pass over the keys.
-template <bool CHURN, bool DIR, bool CD = false>
+template <bool CHURN, bool DIR, bool CD = false, int PROBE = 0>
 __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, SearchView sv_old,
                                                          const uint32_t *old_to_new,
                                                          const uint32_t *holders, int nh,
@@ -5808,6 +5808,8 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                                                          uint16_t *mask, uint8_t *target,
                                                          ChurnDir cd, uint32_t *old_lists = nullptr,
                                                          uint8_t *old_count = nullptr) {
+    // PROBE (A/B, CX_MISPLACED_PROBE; 0 = the scan): 1 = no row flush (the
+    // search half), 2 = no search (the flush half: rows from the tile index)
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
     __shared__ uint32_t s_sn[ROW_BLOCK], s_so[ROW_BLOCK];  // the tile's successors
@@ -5847,7 +5849,8 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
         if (i < q) {
             uint32_t sn = 0, so = 0, has = 0, m = 0;
             const bool settled =
-                use_cd && cd_lookup(cd, key, A, B, n_old, n_new, no, nn, so, sn, has, m);
+                PROBE == 2 ? (sn = so = (uint32_t)(i % n_new), true)
+                           : use_cd && cd_lookup(cd, key, A, B, n_old, n_new, no, nn, so, sn, has, m);
             if (!settled) {
                 // Both searches are issued together: deriving the new successor
                 // from a verified old->new mapping saves a search for ~98 % of
@@ -5926,13 +5929,15 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
             }
             mask[i] = (uint16_t)m;
         }
-        if (use_cd && more) cd_fetch(cd, key_n, A_n, B_n);
+        if (use_cd && more && PROBE != 2) cd_fetch(cd, key_n, A_n, B_n);
         __syncthreads();
-        // new lists (sn + j mod n_new, j < nn) and old lists (so + j mod
-        // n_old, j < no <= n_old: one wrap at most) straight from the successors
-        flush_window(s_sn, new_lists, base, cnt, nlist, nn, n_new);
-        if (CHURN && old_lists) flush_window(s_so, old_lists, base, cnt, nlist, no, n_old);
-        flush_rows_refill(stage_t, target, base, cnt, nslots);
+        if (PROBE != 1) {
+            // new lists (sn + j mod n_new, j < nn) and old lists (so + j mod
+            // n_old, j < no <= n_old: one wrap at most) straight from the successors
+            flush_window(s_sn, new_lists, base, cnt, nlist, nn, n_new);
+            if (CHURN && old_lists) flush_window(s_so, old_lists, base, cnt, nlist, no, n_old);
+            flush_rows_refill(stage_t, target, base, cnt, nslots);
+        }
         __syncthreads();
     }
 }
@@ -5946,8 +5951,21 @@ hipError_t misplaced_churn(const SearchView &sv_old, const SearchView &sv_new,
     if ((old_lists == nullptr) != (old_count == nullptr)) return hipErrorInvalidValue;
     ChurnDir cd = {};
     if (cda) cd = ChurnDir{cda->cd, cda->kb, sv_old.ring, sv_new.ring, cda->ok};
-    if (cda && sv_new.dir && sv_old.dir)
-        k_misplaced<true, true, true><<<cx_grid(q, ROW_BLOCK, 8192), ROW_BLOCK, 0, s>>>(
+    static const int probe = [] {
+        const char *e = getenv("CX_MISPLACED_PROBE");
+        return e ? (atoi(e) & 3) : 0;
+    }();
+    const unsigned g = cx_grid(q, ROW_BLOCK, 8192);
+    if (cda && sv_new.dir && sv_old.dir && probe == 1)
+        k_misplaced<true, true, true, 1><<<g, ROW_BLOCK, 0, s>>>(
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
+            old_lists, old_count);
+    else if (cda && sv_new.dir && sv_old.dir && probe == 2)
+        k_misplaced<true, true, true, 2><<<g, ROW_BLOCK, 0, s>>>(
+            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
+            old_lists, old_count);
+    else if (cda && sv_new.dir && sv_old.dir)
+        k_misplaced<true, true, true><<<g, ROW_BLOCK, 0, s>>>(
             sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
             old_lists, old_count);
     else if (sv_new.dir && sv_old.dir)
