@@ -5401,28 +5401,9 @@ hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128
 // block and written as one contiguous, coalesced range.
 constexpr int ROW_BLOCK = 256;
 
-template <class T>
-__device__ __forceinline__ void flush_rows(const T *stage, T *out, size_t base, int cnt, int w) {
-    static_assert(16 % sizeof(T) == 0, "16-B chunks of whole elements");
-    const int total = cnt * w;
-    T *dst = out + base * (size_t)w;
-    int t0 = 0;
-    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(stage)) & 15) == 0) {
-        // 16-B streaming stores for the bulk (rows are written once, read by
-        // the caller later): the block's range is contiguous and LDS-staged
-        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-        constexpr int per = 16 / (int)sizeof(T);
-        const int nv = total / per;
-        const v4u *sv = reinterpret_cast<const v4u *>(stage);
-        v4u *dv = reinterpret_cast<v4u *>(dst);
-        for (int t = threadIdx.x; t < nv; t += blockDim.x) __builtin_nontemporal_store(sv[t], dv + t);
-        t0 = nv * per;
-    }
-    for (int t = t0 + threadIdx.x; t < total; t += blockDim.x) dst[t] = stage[t];
-}
-
-// flush_rows for the target rows, which then refills the stage with 0xFF
-// (no target) for the next tile: each lane refills what it stored.
+// Rows of `w` bytes (the target rows), staged in LDS, leave in 16-B streaming
+// stores as one contiguous range; the stage is refilled with 0xFF (no target)
+// for the next tile, each lane refilling what it stored.
 __device__ __forceinline__ void flush_rows_refill(uint8_t *stage, uint8_t *out, size_t base,
                                                   int cnt, int w) {
     const int total = cnt * w;
