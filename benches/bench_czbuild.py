@@ -57,7 +57,7 @@ def main():
     # probes (stores-only / compute-only) leave an unspecified table: no route
     if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1") and \
             os.environ.get("CX_CZ_ROOTS_MODE", "0") == "0" and \
-            os.environ.get("CX_CZ2_MODE", "0") == "0":
+            os.environ.get("CX_CZ2_MODE", "0") in ("0", "32"):  # 32: streaming stores
         q = 1 << 22
         keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
         chordx.fill_splitmix(keys, 0x5EED0008)

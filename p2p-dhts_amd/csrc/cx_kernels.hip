@@ -3259,7 +3259,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     // table stores), 2 = stores only (no window gathers; the words stored are
     // whatever LDS holds), 3 = stores only without the row gathers (every two
     // rows share a dummy root); + 16: every store lands in the table's first
-    // 128 MiB (the write stream stays on chip)
+    // 128 MiB (the write stream stays on chip); + 32: streaming (non-temporal)
+    // table stores instead of write-back ones (1.6 % slower, profiles/r04/store_ab)
     auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
     };
@@ -3600,7 +3601,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
             const v4u wv4 = {u.x, u.y, u.z, u.w};
             const size_t ent0 = (mode & 16) ? ((tp0 + e) & ((1u << 21) - 1)) : tp0 + e;
-            __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent0 * 4) + qq);
+            if (mode & 32) __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent0 * 4) + qq);
+            else reinterpret_cast<v4u *>(cz + ent0 * 4)[qq] = wv4;  // write-back (faster here)
         }
     };
     if constexpr (!SL) {
@@ -3733,7 +3735,8 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
         const v4u wv4 = {u.x, u.y, u.z, u.w};
         const size_t ent1 = (mode & 16) ? ((tp0 + M + e) & ((1u << 21) - 1)) : tp0 + M + e;
-        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent1 * 4) + qq);
+        if (mode & 32) __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent1 * 4) + qq);
+        else reinterpret_cast<v4u *>(cz + ent1 * 4)[qq] = wv4;
     }
     if (oob) atomicOr(esc + 1, 1u);
     __syncthreads();
@@ -4154,7 +4157,7 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         }();
         static const int mode = [] {
             const char *ev = getenv("CX_CZ2_MODE");
-            return ev ? (atoi(ev) & 31) : 0;
+            return ev ? (atoi(ev) & 63) : 0;
         }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
             if (par)
