@@ -4663,10 +4663,18 @@ void k_route_tree(TreeIO io) {
         const uint64_t a0 = addr_all[quad0], a1 = addr_all[quad0 + 1], a2 = addr_all[quad0 + 2],
                        a3 = addr_all[quad0 + 3];
         uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0, c3 = c0;
-        if (a0) c0 = io.tree[(a0 - 1) * 4 + qs];
-        if (a1) c1 = io.tree[(a1 - 1) * 4 + qs];
-        if (a2) c2 = io.tree[(a2 - 1) * 4 + qs];
-        if (a3) c3 = io.tree[(a3 - 1) * 4 + qs];
+        // non-temporal: a table entry is rarely read twice before it leaves L2
+        // (1.4 % faster per launch than ordinary loads, profiles/r04/ntload_ab)
+        typedef unsigned int v4n __attribute__((ext_vector_type(4)));
+        auto ld_entry = [&](uint64_t a) -> uint4 {
+            const v4n v = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.tree) +
+                                                     (a - 1) * 4 + qs);
+            return make_uint4(v.x, v.y, v.z, v.w);
+        };
+        if (a0) c0 = ld_entry(a0);
+        if (a1) c1 = ld_entry(a1);
+        if (a2) c2 = ld_entry(a2);
+        if (a3) c3 = ld_entry(a3);
         u128 xa = 0, xb = 0;
         if (mode == A_FIXC) {
             xa = ld128(io.ring + cur);
