@@ -34,6 +34,12 @@ __device__ __forceinline__ u128 ld128(const cell128 *p) {
     const uint4 v = *reinterpret_cast<const uint4 *>(p);
     return ((u128)(((uint64_t)v.w << 32) | v.z) << 64) | (((uint64_t)v.y << 32) | v.x);
 }
+// ... non-temporal (read once, nothing to keep in L2 for)
+__device__ __forceinline__ u128 ld128_nt(const cell128 *p) {
+    typedef unsigned int v4n __attribute__((ext_vector_type(4)));
+    const v4n v = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(p));
+    return ((u128)(((uint64_t)v.w << 32) | v.z) << 64) | (((uint64_t)v.y << 32) | v.x);
+}
 __device__ __forceinline__ void st128(cell128 *p, u128 x) {
     uint4 v;
     v.x = (uint32_t)x;

@@ -4696,8 +4696,9 @@ void k_route_tree(TreeIO io) {
             if (KF && io.dh) {
                 // the origin resolved the start: no source pair to load
             } else if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
-                if (pkind == ARC_NEW) pa = ld128(io.ring_ext + psrc);  // pred: local check only
-                pb = ld128(io.ring_ext + psrc + 1);
+                // non-temporal (0.5 %, profiles/r04/ntload_ab/source_pair)
+                if (pkind == ARC_NEW) pa = ld128_nt(io.ring_ext + psrc);  // pred: local check only
+                pb = ld128_nt(io.ring_ext + psrc + 1);
             }
             bst = B_PAIR;
         }
