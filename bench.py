@@ -825,7 +825,8 @@ def main():
               "exact_hops": xc, "rank": 0,
               "note": "random 64-B requests the walk issued (counting build, same batch) per "
                       "second of kernel time, vs dependent quad-cooperative 64-B gathers/s "
-                      "measured on the same route table in this run (rank 0)"}
+                      "(non-temporal, as the walk's) measured on the same route table in this "
+                      "run (rank 0)"}
 
     if rank == 0:
         total = world * Q * args.steps

@@ -7235,7 +7235,9 @@ __global__ __launch_bounds__(256) void k_gather_probe(const uint4 *t, uint64_t s
     uint64_t x = probe_mix(tid / 4 + 777);
     for (int h = 0; h < hops; ++h) {
         const uint64_t slot = x % slots;
-        const uint4 a = t[slot * 4 + sub];
+        // non-temporal, as the walk's table gathers
+        typedef unsigned int v4n __attribute__((ext_vector_type(4)));
+        const v4n a = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(t) + slot * 4 + sub);
         uint64_t v = ((uint64_t)a.y << 32 | a.x) ^ a.z;
         v = __shfl(v, (threadIdx.x & 63) & ~3, 64);
         x = probe_mix(v + x);
