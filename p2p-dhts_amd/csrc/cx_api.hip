@@ -303,6 +303,8 @@ struct PlaneSet {
     ~PlaneSet() { table_free(device, p, bytes); }  // holders synchronise first
 };
 
+static bool g_old_walk = false;  // cxi_ab_old_walk (round-5 A/B)
+
 struct cx_ring {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -1414,7 +1416,11 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     }
     SearchView dsv = ring->sv();
     dsv.dir = ring->d_dir;
-    if (v == 5 && ring->cz_valid)
+    if (v == 5 && ring->cz_valid && !g_old_walk)
+        CX_HIP(cxk::route_walk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
+                               ring->pk_ib, dsv, dsrc, reinterpret_cast<const cell128 *>(dk), q,
+                               dow, dh, dst, ring->counting ? ring->d_stats : nullptr, s));
+    else if (v == 5 && ring->cz_valid)
         CX_HIP(cxk::route_cz(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
                              ring->rt_R, ring->pk_ib, ring->rows_deferred ? nullptr : ring->d_fingers,
                              dsv, dsrc,
@@ -2376,6 +2382,12 @@ int cxi_pool_stats(uint64_t *out) {
 // ---- internal: fault injection for tests (bit 0: the route-table build's
 // finger-plane allocation fails; bit 1: the default route-table build defers
 // the rows past 48 distinct roots per block to overflow launches).
+// A/B during round 5 only: 1 = the round-4 walk (k_route_tree<false, true>)
+extern "C" int cxi_ab_old_walk(int on) {
+    g_old_walk = on != 0;
+    return CX_OK;
+}
+
 int cxi_set_fault(int mask) {
     g_fault.store(mask);
     cxk::cz2_set_cap(mask & 2 ? 48u : 256u);

@@ -223,6 +223,12 @@ hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, cons
                     int l0, int R, int ib, const uint32_t *F, const SearchView &sv,
                     const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
                     uint8_t *hops, uint8_t *status, unsigned long long *stats, hipStream_t s);
+// The default walk (cx_walk.hip): straight-line window steps over the same
+// table; n < 2^30, gs = cz_shift(ib) >= 64.
+hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                      int l0, int ib, const SearchView &sv, const uint32_t *src,
+                      const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                      uint8_t *status, unsigned long long *stats, hipStream_t s);
 // Dependent random gathers of 64-B entries (four lanes, one 16-B load each),
 // the walk's access pattern, over `bytes` of `table` (read only): entries/s.
 hipError_t gather_probe(const void *table, size_t bytes, int lanes, int hops, double *rate,

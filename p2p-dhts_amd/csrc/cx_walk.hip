@@ -1,0 +1,422 @@
+// cx_walk.hip -- the default finger-routed walk with hop counts: cx_route on a
+// converged ring of <= 2^24 peers over the pattern-keyed window table
+// (DESIGN.md 4.1).  SURVEY 8(a) rows a5, a7, a8, a9 (converged, all alive):
+//   AbstractChordPeer::GetSuccessor   abstract_chord_peer.cpp:318-337
+//   StoredLocally                     abstract_chord_peer.cpp:720-725
+//   ChordPeer::ForwardRequest         chord_peer.cpp:185-211 (one hop = one GET_SUCC)
+//   FingerTable::Lookup               finger_table.h:115-130 (level = msb(key - id))
+//
+// One lane walks one lookup; a wave keeps 64 walks in flight and advances all
+// of them by one memory round per loop iteration.  The table stores, per
+// (level i, pattern bit b, peer p), 16 relative nodes: the root A = f(p, i) and
+// the nodes reached from A (b = 0) or from A' = f(A, i - 1) (b = 1) by every
+// subset of hops at levels i-2 .. i-5 (cx_kernels.hip, k_cz_build*).  After a
+// gather the lane takes the root hop and then steps the window's levels
+// i-1 .. i-5 in a fixed, fully unrolled order: a hop at level l is due iff
+// d >= 2^l, and d < 2^(l+1) holds at every step (a hop at l leaves d < 2^l).
+// All lanes run the same straight-line steps -- no data-dependent loop -- so a
+// round costs the same VALU work whatever mix of hops the wave's lanes take.
+//
+// Distances are kept in units u = 2^gs as an interval [dmin, dmax] (the gap
+// codes are floor(gap / u)): a decision the interval cannot take exactly
+// fetches the exact IDs (M_FIX: id(cur); M_FIXT: id(cur), id(next)).  Levels
+// below the table, below gs, and nodes the format could not represent take
+// exact hops (M_EXACT: id(cur), id(cur + 1), the directory if the finger is
+// not the next peer).
+#include "cx_kernels.hpp"
+
+namespace cxk {
+namespace {
+
+constexpr int WK_BLOCK = 256;
+constexpr int WK_RES = 256;  // staged results per wave (LDS ring, 64-result flushes)
+constexpr int WK_ENT = 18;   // LDS dwords per lane's entry: 16 nodes + 2 (ds_read_b32 2-way banks)
+constexpr uint32_t WK_NONE = 0xFFFFFFFFu;
+constexpr uint32_t WK_CZ_NONE = 0xFFFFFFFFu;  // a node the 4-B format cannot hold (CZ_NONE)
+
+enum { M_NONE = 0, M_HOP = 1, M_FIX = 2, M_EXACT = 3, M_FIXT = 4 };
+enum { B_EMPTY = 0, B_KEYS = 1, B_READY = 2 };
+enum { P_WALK = 0, P_LOCAL = 1, P_BAD = 2 };
+
+struct WalkIO {
+    const cell128 *ring_ext;  // [ring[n-1], ring[0..n-1]]: (pred, self) of p at p, p + 1
+    const cell128 *ring;
+    uint32_t n;
+    const uint4 *cz;  // [R][2][n] entries of 64 B (level-major)
+    int l0, gs;
+    SearchView sv;
+    const uint32_t *src;
+    const cell128 *keys;
+    size_t q, chunk;
+    uint32_t *owner;
+    uint8_t *hops, *status;
+    // counting build: [0] table gathers, [1] exact 16-B ID gathers, [2] exact
+    // hops through the directory (a directory entry + an ID each), [3] lookups
+    unsigned long long *stats;
+};
+
+// E(l) = round(n 2^(l - 128)), the expected index advance of a level-l finger
+// (n < 2^30: 32-bit arithmetic is exact).
+__device__ __forceinline__ uint32_t wk_expect(uint32_t n, int l) {
+    const int sh = 128 - l;
+    return sh >= 32 ? 0u : (n + (1u << (sh - 1))) >> sh;
+}
+
+// Node word -> peer index: cur + E(l) + advance (stored + 2^15); Etab[l] =
+// E(l) - 2^15.  t lies in (-n/2, 2n): one of t, t + n, t - n is in [0, n),
+// and as u32 it is the smallest of the three (n < 2^30).
+__device__ __forceinline__ uint32_t wk_next(const uint32_t *Etab, uint32_t n, uint32_t cur, int l,
+                                            uint32_t wd) {
+    const uint32_t t = cur + Etab[l] + (wd & 0xFFFFu);
+    return min(t, min(t + n, t - n));
+}
+
+// floor(x / 2^gs) for gs >= 64 (ib <= 24 -> gs >= 92).
+__device__ __forceinline__ uint64_t wk_units(u128 x, int gs) {
+    return (uint64_t)(x >> 64) >> (gs - 64);
+}
+
+__device__ __forceinline__ uint64_t wk_pack(uint32_t own, uint32_t h, uint32_t st) {
+    return (1ull << 63) | ((uint64_t)st << 40) | ((uint64_t)(h & 0xFF) << 32) | own;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(WK_BLOCK) void k_walk(WalkIO io) {
+    __shared__ uint64_t res_all[WK_BLOCK / 64][WK_RES];
+    __shared__ uint32_t ent_all[WK_BLOCK * WK_ENT];
+    __shared__ uint32_t Etab[CX_FINGERS];  // E(l) - 2^15 per level
+    const uint32_t n = io.n;
+    for (int l = threadIdx.x; l < (int)CX_FINGERS; l += WK_BLOCK) Etab[l] = wk_expect(n, l) - 32768u;
+    __syncthreads();
+    const int l0 = io.l0, gs = io.gs;
+    const int lane = threadIdx.x & 63, qs = threadIdx.x & 3;
+    const uint32_t quad0 = threadIdx.x & ~3u;
+    uint64_t *res = res_all[threadIdx.x >> 6];
+    const uint32_t *ent = ent_all + threadIdx.x * WK_ENT;
+    for (int j = lane; j < WK_RES; j += 64) res[j] = 0;
+    const size_t wave = (blockIdx.x * (size_t)WK_BLOCK + threadIdx.x) >> 6;
+    const size_t base = wave * io.chunk;
+    if (base >= io.q) return;  // wave-uniform
+    const size_t end = (base + io.chunk < io.q) ? base + io.chunk : io.q;
+    size_t head = base, flushed = base;
+
+    // slot A: the lookup being walked
+    int mode = M_NONE, lvl = 0, rb = 0;
+    uint32_t cur = 0, h = 0, pn = 0;
+    uint64_t dmin = 0, dmax = 0;
+    u128 key = 0;
+    size_t qi = 0;
+    // slot B: the next lookup (key + source, then the source's ID pair)
+    int bst = B_EMPTY, pst = P_WALK;
+    size_t pq = 0;
+    u128 pkey = 0;
+    uint32_t psrc = 0;
+    uint64_t pd = 0;
+    uint32_t n_g64 = 0, n_r16 = 0, n_xc = 0, n_q = 0;
+
+    for (;;) {
+        if (__ballot(mode != M_NONE || bst != B_EMPTY) == 0 && head >= end && flushed >= end)
+            break;  // wave-uniform: every lookup delivered and written
+
+        // ---- memory round: every load of the round, one wait ----
+        const uint32_t eidx =
+            mode == M_HOP ? (uint32_t)((lvl - l0) * 2 + rb) * n + cur : WK_NONE;
+        if (STATS) {
+            n_g64 += mode == M_HOP;
+            n_r16 += mode == M_FIX ? 1u : (mode >= M_EXACT ? 2u : 0u);
+        }
+        // quad-cooperative 64-B gathers: lane qs of each quad loads 16 B of
+        // the four entries its quad wants (one load instruction = 16 lines)
+        // (quad_perm broadcast of lane k: dpp_ctrl = k * 0x55)
+        const uint32_t ek[4] = {(uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x00, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x55, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xAA, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xFF, 0xF, 0xF, false)};
+        typedef unsigned int v4n __attribute__((ext_vector_type(4)));
+        v4n ck[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (ek[k] != WK_NONE)
+                ck[k] = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.cz) +
+                                                   (size_t)ek[k] * 4 + qs);
+        u128 xa = 0, xb = 0;
+        if (mode >= M_FIX) {
+            xa = ld128(io.ring + cur);
+            if (mode != M_FIX) xb = ld128(io.ring + (mode == M_FIXT ? pn : (cur + 1 == n ? 0u : cur + 1)));
+        }
+        const bool pair_now = bst == B_KEYS;
+        u128 pa = 0, pb = 0;
+        if (pair_now && psrc < n) {  // the source's (pred, self) IDs: one 32-B pair
+            pa = ld128_nt(io.ring_ext + psrc);
+            pb = ld128_nt(io.ring_ext + psrc + 1);
+        }
+        {  // refill slot B in lookup order (results flush in 64-lookup runs)
+            size_t lim = end;
+            if (flushed + WK_RES < end) lim = flushed + WK_RES;
+            const size_t avail = lim > head ? lim - head : 0;
+            const uint64_t want = __ballot(bst == B_EMPTY);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+            if (bst == B_EMPTY && rank < avail) {
+                pq = head + rank;
+                pkey = ld128(io.keys + pq);
+                psrc = io.src[pq];
+                bst = B_KEYS;
+            }
+            const size_t took = (size_t)__popcll(want);
+            head += took < avail ? took : avail;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (ek[k] != WK_NONE) {
+                uint2 *d = reinterpret_cast<uint2 *>(ent_all + (quad0 + k) * WK_ENT + qs * 4);
+                d[0] = make_uint2(ck[k].x, ck[k].y);
+                d[1] = make_uint2(ck[k].z, ck[k].w);
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        // ---- slot B: StoredLocally at the source, or the start distance ----
+        if (pair_now) {
+            if (psrc >= n) {
+                pst = P_BAD;
+            } else if (n == 1 || (pkey - pa - 1) <= (pb - pa - 1)) {
+                pst = P_LOCAL;  // key in (pred, src]: 0 hops
+            } else {
+                pst = P_WALK;
+                pd = wk_units(pkey - pb, gs);
+            }
+            bst = B_READY;
+        }
+
+        uint32_t own = CX_NONE, st = CX_Q_OK;
+        bool fin = false, plan = false;
+        // ---- exact IDs arrived (rare) ----
+        if (mode >= M_FIX) {
+            const u128 d = key - xa;
+            if (mode == M_FIX) {
+                dmin = dmax = wk_units(d, gs);
+                plan = true;
+            } else if (mode == M_FIXT) {  // the undecided StoredLocally(pn), exactly
+                if (d <= xb - xa) {
+                    fin = true;
+                    own = pn;
+                } else {
+                    cur = pn;
+                    dmin = dmax = wk_units(key - xb, gs);
+                    plan = true;
+                }
+            } else {  // M_EXACT: the exact finger at level msb(d) = succ(id + 2^i)
+                const int i = msb128(d);
+                const u128 step = (u128)1 << i;
+                uint32_t nxt;
+                u128 idn;
+                if (step <= xb - xa) {  // the next peer
+                    nxt = cur + 1 == n ? 0u : cur + 1;
+                    idn = xb;
+                } else {
+                    nxt = dir_successor(io.sv, xa + step);
+                    idn = ld128(io.ring + nxt);
+                    if (STATS) ++n_xc;
+                }
+                ++h;
+                if (d <= idn - xa) {
+                    fin = true;
+                    own = nxt;
+                } else {
+                    cur = nxt;
+                    dmin = dmax = wk_units(key - idn, gs);
+                    plan = true;
+                }
+            }
+        }
+
+        // ---- table entry arrived: root hop, then the window's five levels ----
+        // Straight-line, branch-free steps (selects): every lane runs the same
+        // instructions whatever hops it takes.  No hop cap here: on a converged
+        // ring each hop strictly lowers msb(d) (d' = d - (id_nxt - id_cur) <
+        // 2^i), so a walk takes <= 128 < CX_HOP_CAP hops.
+        int cs = -1, ri = 0;  // cs: window subset the lane stands on (16: root A of b = 1)
+        if (mode == M_HOP) {
+            const uint32_t wd = ent[rb ? 15 : 0];
+            ri = lvl;
+            if (wd == WK_CZ_NONE) {
+                mode = M_EXACT;  // the root is not representable: exact finger next round
+            } else {
+                const uint64_t e = (1ull << (lvl - gs)) + (wd >> 16);
+                const uint32_t nxt = wk_next(Etab, n, cur, lvl, wd);
+                ++h;
+                if (dmax < e) {
+                    fin = true;
+                    own = nxt;
+                } else if (dmin <= e) {
+                    mode = M_FIXT;
+                    pn = nxt;
+                } else {
+                    cur = nxt;
+                    dmin -= e + 1;
+                    dmax -= e;
+                    cs = rb ? 16 : 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 1; o <= 5; ++o) {
+            const int l = ri - o;
+            const bool act = cs >= 0 && l >= gs;
+            const uint64_t T = 1ull << ((l - gs) & 63);  // d >= 2^l <=> floor(d/u) >= T
+            const bool need = act && dmax >= T;           // a hop at level l is due (or undecided)
+            int v;
+            bool vv;
+            if (o == 1) {
+                v = 0;
+                vv = cs == 16;  // b = 1: A -> A' (slot 0)
+            } else {
+                v = (cs & 15) | (1 << (o - 2));
+                vv = cs < 16 && !(rb && v == 15);  // slot 15 of a b = 1 entry is A
+            }
+            const uint32_t wd = ent[v];
+            const bool ok = need && vv && dmin >= T && wd != WK_CZ_NONE;
+            const uint64_t e = T + (wd >> 16);
+            const uint32_t nxt = wk_next(Etab, n, cur, l, wd);
+            const bool own_now = ok && dmax < e;
+            const bool und = ok && !own_now && dmin <= e;
+            const bool mv = ok && !own_now && !und;
+            h += ok ? 1u : 0u;
+            if (own_now) own = nxt;
+            fin = fin || own_now;
+            if (und) {
+                pn = nxt;
+                mode = M_FIXT;
+            }
+            cur = mv ? nxt : cur;
+            dmin = mv ? dmin - e - 1 : dmin;
+            dmax = mv ? dmax - e : dmax;
+            cs = mv ? v : ((need || !act) ? -1 : cs);  // left the window unless moved / not due
+        }
+        if (mode == M_HOP && !fin) plan = true;
+
+        // ---- deliver, promote slot B ----
+        if (fin) {
+            res[qi & (WK_RES - 1)] = wk_pack(own, h, st);
+            mode = M_NONE;
+        }
+        if (!plan && mode == M_NONE && bst == B_READY) {
+            bst = B_EMPTY;
+            qi = pq;
+            key = pkey;
+            cur = psrc;
+            h = 0;
+            if (STATS) ++n_q;
+            if (pst == P_WALK) {
+                dmin = dmax = pd;
+                plan = true;
+            } else {
+                res[qi & (WK_RES - 1)] =
+                    wk_pack(pst == P_LOCAL ? cur : CX_NONE, 0, pst == P_LOCAL ? CX_Q_OK : CX_Q_BADPEER);
+            }
+        }
+
+        // ---- plan: the next level and what it needs ----
+        if (plan) {
+            if (dmin == 0) {
+                mode = M_EXACT;  // d < 2^gs
+            } else {
+                const int ma = 63 - __builtin_clzll(dmin), mb = 63 - __builtin_clzll(dmax);
+                if (ma != mb) {
+                    mode = M_FIX;  // the level itself is undecided
+                } else if (ma + gs >= l0) {
+                    mode = M_HOP;
+                    lvl = ma + gs;
+                    rb = ma >= 1 ? (int)((dmax >> (ma - 1)) & 1) : 0;  // bit lvl-1 of d
+                } else {
+                    mode = M_EXACT;  // below the table
+                }
+            }
+        }
+
+        // ---- flush complete 64-result runs in lookup order ----
+        for (int it = 0; it < 2; ++it) {
+            if (flushed >= end) break;
+            const size_t idx = flushed + lane;
+            const bool inr = idx < end;
+            const uint64_t v = inr ? res[idx & (WK_RES - 1)] : 0ull;
+            if (__ballot(!inr || (v >> 63)) != ~0ull) break;
+            if (inr) {
+                io.owner[idx] = (uint32_t)v;
+                io.hops[idx] = (uint8_t)(v >> 32);
+                if (io.status) io.status[idx] = (uint8_t)(v >> 40);
+                res[idx & (WK_RES - 1)] = 0;
+            }
+            flushed += 64;
+        }
+    }
+    if (STATS) {
+        uint64_t v[4] = {n_g64, n_r16, n_xc, n_q};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) atomicAdd(io.stats + k, (unsigned long long)v[k]);
+    }
+}
+
+template <class K>
+unsigned walk_resident_grid(K kernel) {
+    int dev = 0, cus = 256, per = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WK_BLOCK, 0) != hipSuccess ||
+        per < 1)
+        per = 1;
+    return (unsigned)(per * cus);
+}
+
+}  // namespace
+
+hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
+                      int l0, int ib, const SearchView &sv, const uint32_t *src,
+                      const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
+                      uint8_t *status, unsigned long long *stats, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const int gs = cz_shift(ib);
+    // the walk's index and distance arithmetic: n < 2^30, u = 2^gs with gs >= 64,
+    // 32-bit entry indices (l0 - 5 >= 0 levels x 2 x n < 2^32)
+    if (n == 0 || n >= (1u << 30) || gs < 64 || l0 < 5 || (size_t)(128 - l0) * 2 * n >= WK_NONE)
+        return hipErrorInvalidValue;
+    WalkIO io = {};
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.cz = reinterpret_cast<const uint4 *>(cz);
+    io.l0 = l0;
+    io.gs = gs;
+    io.sv = sv;
+    io.src = src;
+    io.keys = keys;
+    io.q = q;
+    io.owner = owner;
+    io.hops = hops;
+    io.status = status;
+    io.stats = stats;
+    // one resident round of waves (no second, partial round of blocks); small
+    // batches: >= 1024 lookups per wave
+    static const unsigned resident = walk_resident_grid(k_walk<false>);
+    size_t waves = (size_t)resident * (WK_BLOCK / 64);
+    const size_t small = (q + 1023) / 1024;
+    if (small < waves) waves = small ? small : 1;
+    io.chunk = (q + waves - 1) / waves;
+    waves = (q + io.chunk - 1) / io.chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
+    if (stats)
+        k_walk<true><<<blocks, WK_BLOCK, 0, s>>>(io);
+    else
+        k_walk<false><<<blocks, WK_BLOCK, 0, s>>>(io);
+    return hipGetLastError();
+}
+
+}  // namespace cxk
