@@ -76,12 +76,22 @@ __device__ __forceinline__ uint64_t wk_units(u128 x, int gs) {
     return (uint64_t)(x >> 64) >> (gs - 64);
 }
 
+__device__ __forceinline__ u128 wk_u128(const unsigned int __attribute__((ext_vector_type(4))) v) {
+    return ((u128)(((uint64_t)v.w << 32) | v.z) << 64) | (((uint64_t)v.y << 32) | v.x);
+}
+
 __device__ __forceinline__ uint64_t wk_pack(uint32_t own, uint32_t h, uint32_t st) {
     return (1ull << 63) | ((uint64_t)st << 40) | ((uint64_t)(h & 0xFF) << 32) | own;
 }
 
+#ifdef CX_WALK_WPE
+#define WK_ATTR __attribute__((amdgpu_waves_per_eu(CX_WALK_WPE)))
+#else
+#define WK_ATTR
+#endif
+
 template <bool STATS>
-__global__ __launch_bounds__(WK_BLOCK) void k_walk(WalkIO io) {
+__global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     __shared__ uint64_t res_all[WK_BLOCK / 64][WK_RES];
     __shared__ uint32_t ent_all[WK_BLOCK * WK_ENT];
     __shared__ uint32_t Etab[CX_FINGERS];  // E(l) - 2^15 per level
@@ -125,30 +135,17 @@ __global__ __launch_bounds__(WK_BLOCK) void k_walk(WalkIO io) {
             n_g64 += mode == M_HOP;
             n_r16 += mode == M_FIX ? 1u : (mode >= M_EXACT ? 2u : 0u);
         }
-        // quad-cooperative 64-B gathers: lane qs of each quad loads 16 B of
-        // the four entries its quad wants (one load instruction = 16 lines)
-        // (quad_perm broadcast of lane k: dpp_ctrl = k * 0x55)
-        const uint32_t ek[4] = {(uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x00, 0xF, 0xF, false),
-                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x55, 0xF, 0xF, false),
-                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xAA, 0xF, 0xF, false),
-                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xFF, 0xF, 0xF, false)};
+        // Load order: the source pairs of the lookups refilled last round
+        // (their psrc is read before this round's refill loads overwrite it
+        // for other lanes), the refill, the table entries, exact IDs.  The
+        // pair and ID values are made opaque until every load is issued
+        // (wk_opaque), so no early wait on them splits the round's loads.
         typedef unsigned int v4n __attribute__((ext_vector_type(4)));
-        v4n ck[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (ek[k] != WK_NONE)
-                ck[k] = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.cz) +
-                                                   (size_t)ek[k] * 4 + qs);
-        u128 xa = 0, xb = 0;
-        if (mode >= M_FIX) {
-            xa = ld128(io.ring + cur);
-            if (mode != M_FIX) xb = ld128(io.ring + (mode == M_FIXT ? pn : (cur + 1 == n ? 0u : cur + 1)));
-        }
         const bool pair_now = bst == B_KEYS;
-        u128 pa = 0, pb = 0;
+        v4n pa4 = {0, 0, 0, 0}, pb4 = {0, 0, 0, 0};
         if (pair_now && psrc < n) {  // the source's (pred, self) IDs: one 32-B pair
-            pa = ld128_nt(io.ring_ext + psrc);
-            pb = ld128_nt(io.ring_ext + psrc + 1);
+            pa4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc));
+            pb4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc + 1));
         }
         {  // refill slot B in lookup order (results flush in 64-lookup runs)
             size_t lim = end;
@@ -166,6 +163,25 @@ __global__ __launch_bounds__(WK_BLOCK) void k_walk(WalkIO io) {
             const size_t took = (size_t)__popcll(want);
             head += took < avail ? took : avail;
         }
+        // quad-cooperative 64-B gathers: lane qs of each quad loads 16 B of
+        // the four entries its quad wants (one load instruction = 16 lines)
+        // (quad_perm broadcast of lane k: dpp_ctrl = k * 0x55)
+        const uint32_t ek[4] = {(uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x00, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x55, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xAA, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xFF, 0xF, 0xF, false)};
+        v4n ck[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (ek[k] != WK_NONE)
+                ck[k] = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.cz) +
+                                                   (size_t)ek[k] * 4 + qs);
+        v4n xa4 = {0, 0, 0, 0}, xb4 = {0, 0, 0, 0};
+        if (mode >= M_FIX) {
+            xa4 = *reinterpret_cast<const v4n *>(io.ring + cur);
+            if (mode != M_FIX)
+                xb4 = *reinterpret_cast<const v4n *>(io.ring + (mode == M_FIXT ? pn : (cur + 1 == n ? 0u : cur + 1)));
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (ek[k] != WK_NONE) {
@@ -176,6 +192,8 @@ __global__ __launch_bounds__(WK_BLOCK) void k_walk(WalkIO io) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        asm volatile("" : "+v"(pa4), "+v"(pb4), "+v"(xa4), "+v"(xb4));  // wk_opaque
+        const u128 pa = wk_u128(pa4), pb = wk_u128(pb4), xa = wk_u128(xa4), xb = wk_u128(xb4);
 
         // ---- slot B: StoredLocally at the source, or the start distance ----
         if (pair_now) {
