@@ -30,7 +30,6 @@ namespace {
 
 constexpr int WK_BLOCK = 256;
 constexpr int WK_RES = 256;  // staged results per wave (LDS ring, 64-result flushes)
-constexpr int WK_ENT = 18;   // LDS dwords per lane's entry: 16 nodes + 2 (ds_read_b32 2-way banks)
 constexpr uint32_t WK_NONE = 0xFFFFFFFFu;
 constexpr uint32_t WK_CZ_NONE = 0xFFFFFFFFu;  // a node the 4-B format cannot hold (CZ_NONE)
 
@@ -93,16 +92,21 @@ __device__ __forceinline__ uint64_t wk_pack(uint32_t own, uint32_t h, uint32_t s
 template <bool STATS>
 __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     __shared__ uint64_t res_all[WK_BLOCK / 64][WK_RES];
-    __shared__ uint32_t ent_all[WK_BLOCK * WK_ENT];
+    // entries land by LDS-DMA: region k of a wave = the 16-B quarters its
+    // lanes loaded in gather k, lane-linear; lane j's entry is 64 contiguous
+    // bytes in region j & 3 at (j >> 2) * 64 (regions 4 dwords apart mod 32
+    // banks: <= 4-way ds_read_b32 conflicts)
+    constexpr int RG = 260;
+    __shared__ uint32_t ent_all[WK_BLOCK / 64][4 * RG];
     __shared__ uint32_t Etab[CX_FINGERS];  // E(l) - 2^15 per level
     const uint32_t n = io.n;
     for (int l = threadIdx.x; l < (int)CX_FINGERS; l += WK_BLOCK) Etab[l] = wk_expect(n, l) - 32768u;
     __syncthreads();
     const int l0 = io.l0, gs = io.gs;
     const int lane = threadIdx.x & 63, qs = threadIdx.x & 3;
-    const uint32_t quad0 = threadIdx.x & ~3u;
     uint64_t *res = res_all[threadIdx.x >> 6];
-    const uint32_t *ent = ent_all + threadIdx.x * WK_ENT;
+    uint32_t *ent_w = ent_all[threadIdx.x >> 6];
+    const uint32_t *ent = ent_w + (lane & 3) * RG + (lane >> 2) * 16;
     for (int j = lane; j < WK_RES; j += 64) res[j] = 0;
     const size_t wave = (blockIdx.x * (size_t)WK_BLOCK + threadIdx.x) >> 6;
     const size_t base = wave * io.chunk;
@@ -163,32 +167,26 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
             const size_t took = (size_t)__popcll(want);
             head += took < avail ? took : avail;
         }
-        // quad-cooperative 64-B gathers: lane qs of each quad loads 16 B of
-        // the four entries its quad wants (one load instruction = 16 lines)
-        // (quad_perm broadcast of lane k: dpp_ctrl = k * 0x55)
+        // quad-cooperative 64-B gathers straight into LDS (LDS-DMA): lane qs of
+        // each quad loads 16 B of the four entries its quad wants, one load
+        // instruction = 16 lines (quad_perm broadcast of lane k: dpp k * 0x55)
         const uint32_t ek[4] = {(uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x00, 0xF, 0xF, false),
                                 (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0x55, 0xF, 0xF, false),
                                 (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xAA, 0xF, 0xF, false),
                                 (uint32_t)__builtin_amdgcn_mov_dpp((int)eidx, 0xFF, 0xF, 0xF, false)};
-        v4n ck[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (ek[k] != WK_NONE)
-                ck[k] = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.cz) +
-                                                   (size_t)ek[k] * 4 + qs);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(io.cz + (size_t)ek[k] * 4 + qs),
+                    (__attribute__((address_space(3))) void *)(ent_w + k * RG), 16, 0, 2 /* nt */);
         v4n xa4 = {0, 0, 0, 0}, xb4 = {0, 0, 0, 0};
         if (mode >= M_FIX) {
             xa4 = *reinterpret_cast<const v4n *>(io.ring + cur);
             if (mode != M_FIX)
                 xb4 = *reinterpret_cast<const v4n *>(io.ring + (mode == M_FIXT ? pn : (cur + 1 == n ? 0u : cur + 1)));
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (ek[k] != WK_NONE) {
-                uint2 *d = reinterpret_cast<uint2 *>(ent_all + (quad0 + k) * WK_ENT + qs * 4);
-                d[0] = make_uint2(ck[k].x, ck[k].y);
-                d[1] = make_uint2(ck[k].z, ck[k].w);
-            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA landed
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -12,7 +12,7 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fh:
         for row in csv.DictReader(fh):
-            name = row.get("Kernel_Name", "?").split("(")[0]
+            name = row.get("Kernel_Name", "?")
             acc[name][row["Counter_Name"]].append((row.get("Dispatch_Id"), float(row["Counter_Value"])))
 res = {}
 for k, ctrs in acc.items():
