@@ -1,14 +1,12 @@
 #!/usr/bin/env python3
-"""Route-table build A/B (row f2): a 2^24-peer ring (seed 0x5EED0007), the
-converged fingers + pattern-keyed table built twice (the second into mapped
-HBM), wall time and route_table_hash of the second build.  The build variant
-comes from the environment (CX_CZ_PAIR, CX_CZ_CHUNK, CX_CZ_STORE: read once
-per process), so run one process per variant under rocprofv3 --kernel-trace
---stats for per-kernel times.  With CX_CZ_PAIR in {0, 1} the hash must equal
-the default build's.
-    python benches/bench_czbuild.py [log2 peers] [table_builds, e.g. 0,4] [rounds]
-(table_build 0: root-centric, blocks sized by distinct roots (default); 4:
-root-centric, 256-row blocks; 3: one lane per entry)
+"""Route-table build timer (row f2): a 2^24-peer ring (seed 0x5EED0007), the
+converged fingers + pattern-keyed table built `rounds` times per build input
+(alternating ABAB...), wall time and route_table_hash of each; kernel-level A/Bs
+use two builds of the library (CHORDX_LIB, tools/ab_lib.sh) under rocprofv3
+--kernel-trace --stats.  Routes 2^22 keys through the result.
+    python benches/bench_czbuild.py [log2 peers] [table_builds, e.g. 0,3] [rounds]
+(table_build 0: root-centric, blocks sized by distinct roots (default); 3: one
+lane per entry; 1: from the row-major fingers; 2: level planes only)
 """
 import json
 import os
@@ -47,17 +45,12 @@ def main():
             hashes[tb] = ring.route_table_hash()
     v, esc, table_bytes = ring.route_info()
     out = {"log2_peers": lg, "table_builds": tbs, "rounds": rounds,
-           "variant_env": {k: os.environ.get(k) for k in
-                           ("CX_CZ_PAIR", "CX_CZ_CHUNK", "CX_CZ_STORE", "CX_CZ_ROOTS_MODE",
-                            "CX_CZ2_WPE", "CX_CZ2_MODE")},
+           "lib": os.environ.get("CHORDX_LIB", "in-tree"),
            "fingers_and_table_ms": ts,
            "median_ms": {tb: sorted(v)[len(v) // 2] for tb, v in ts.items()},
            "route_table_hash": hashes, "hashes_equal": len(set(hashes.values())) == 1,
            "route_variant": v, "escapes": esc}
-    # probes (stores-only / compute-only) leave an unspecified table: no route
-    if os.environ.get("CX_CZ_PAIR", "0") in ("0", "1") and \
-            os.environ.get("CX_CZ_ROOTS_MODE", "0") == "0" and \
-            os.environ.get("CX_CZ2_MODE", "0") in ("0", "32"):  # 32: streaming stores
+    if True:
         q = 1 << 22
         keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
         chordx.fill_splitmix(keys, 0x5EED0008)

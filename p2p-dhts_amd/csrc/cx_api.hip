@@ -303,8 +303,6 @@ struct PlaneSet {
     ~PlaneSet() { table_free(device, p, bytes); }  // holders synchronise first
 };
 
-static bool g_old_walk = false;  // cxi_ab_old_walk (round-5 A/B)
-
 struct cx_ring {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -330,13 +328,9 @@ struct cx_ring {
     int fingers_repair = 0;
     int planes_repaired = 0;                  // last build: planes remapped from the parent
     uint64_t repair_searched = 0;             //   fingers searched exactly in that repair
-    RtEntry *d_rt = nullptr;       // route table [n][rt_R] (converged fingers only)
     cell128 *d_ring_ext = nullptr; // [n+1] (pred, self) pairs
     int rt_l0 = 128, rt_R = 0;
     int depth_override = 0;        // cxi_set_route_depth (A/B): R levels instead of the default
-    bool rt_valid = false;         // d_rt matches the current converged fingers
-    uint64_t *d_pk = nullptr;      // packed route table [n][rt_R][2] (variants 2, 3)
-    bool pk_valid = false;
     uint64_t *d_tree = nullptr;    // lookahead-tree table [n][rt_R][8] (variant 4)
     bool tree_valid = false;
     int pk_ib = 1;                 // index bits of a packed finger
@@ -539,8 +533,6 @@ void free_ring(cx_ring *r) {
     table_free(r->device, r->d_ring_key, r->n * sizeof(uint32_t));
     const size_t ent = r->n * (size_t)r->rt_R;
     table_free(r->device, r->d_fingers, r->n * CX_FINGERS * sizeof(uint32_t));
-    table_free(r->device, r->d_rt, ent * sizeof(RtEntry));
-    table_free(r->device, r->d_pk, ent * 16);
     table_free(r->device, r->d_tree, ent * 64);
     table_free(r->device, r->d_cz, ent * 128);
     (void)hipFree(r->d_stree);
@@ -572,10 +564,6 @@ void free_ring(cx_ring *r) {
     delete r;
 }
 
-#ifndef CX_DIR_EXTRA_DEFAULT
-#define CX_DIR_EXTRA_DEFAULT 1
-#endif
-
 // Eytzinger copy of r->d_ring: only the Eytzinger searches (variants 0 and 3)
 // read it, so it is built when one of them is selected (256 MiB and 0.2 ms at
 // 2^24 that a default ring -- and every churn epoch -- no longer pays).
@@ -598,15 +586,11 @@ int build_search(cx_ring *r, hipStream_t s) {
         int rc = ensure_eyt(r, s);
         if (rc) return rc;
     }
-    // 2^k buckets, k = ceil(log2 n) + extra: a query's bucket entry resolves it
-    // unless the bucket holds >= 2 peers and the key lies past the first; each
-    // extra bit halves the load factor (fewer second gathers, 2x the bytes).
-    // CX_DIR_EXTRA (0..3) is the A/B knob; the default is the measured best.
-    static const int extra = [] {
-        const char *e = getenv("CX_DIR_EXTRA");
-        const int v = e ? atoi(e) : CX_DIR_EXTRA_DEFAULT;
-        return v < 0 ? 0 : (v > 3 ? 3 : v);
-    }();
+    // 2^k buckets, k = ceil(log2 n) + 1: a query's bucket entry resolves it
+    // unless the bucket holds >= 2 peers and the key lies past the first; the
+    // extra bit halves the load factor (fewer second gathers, 2x the bytes;
+    // the measured best of 0..3 extra bits, round 1)
+    constexpr int extra = 1;
     int k = 1;
     while (((size_t)1 << k) < m) ++k;
     k += extra;
@@ -655,19 +639,14 @@ void route_geometry(cx_ring *r) {
 // planes in `ft` when HBM allows (cxi_set_table_build(ring, 1) forces the
 // row-major table, for A/B), else the row-major table itself.
 hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv, DBuf &hi,
-                         DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr,
-                         DBuf *pp = nullptr) {
+                         DBuf &c2, hipStream_t s, const uint32_t *ft_pre = nullptr) {
     fv = cxk::FingerView::rows(r->d_fingers);
     // gap codes of the root-centric build: 32-bit ID slices when every ring gap
     // is below 2^(gs + 17) (uniform rings by far), else the 64-bit high words
-    // (CX_CZ_CODES=hi forces them, A/B)
-    static const bool hi_only = [] {
-        const char *e = getenv("CX_CZ_CODES");
-        return e && strcmp(e, "hi") == 0;
-    }();
+    // and the one-lane-per-entry build
     bool slices = false;
-    const bool roots_build = r->table_build == 0 || r->table_build >= 4;
-    if (roots_build && !hi_only) {
+    const bool roots_build = r->table_build == 0;
+    if (roots_build) {
         hipError_t e1 = hi.alloc_pooled(r->n * sizeof(uint32_t), s);
         uint32_t *d_wide = r->d_scratch + 100;
         if (e1 == hipSuccess)
@@ -700,48 +679,13 @@ hipError_t finger_planes(const cx_ring *r, int lo, DBuf &ft, cxk::FingerView &fv
         if (e != hipSuccess) return e;
         fv = cxk::FingerView::planes(ft.as<uint32_t>(), r->n, L, nl);
     }
-    // default build: pair planes {finger, ID slice} and two-hop pairs (one 8-B
-    // gather per window node instead of two 4-B ones); table_build 5 keeps the
-    // 4-B planes for A/B
-    // A/B (round 4): quad planes {finger, ID slice, two-hop finger, ID slice}
-    // of one (level, peer) in 16 B (table_build 7) or pair planes (6): a
-    // window node and its slice in one gather instead of two, both children
-    // of a node at one level in one.  The build itself is 2-4 % faster on
-    // them, but making them costs 2.6-3 ms more than the 4-B two-hop planes
-    // (profiles/r04/build_modes/), so the default keeps 4-B planes
-    if (have_planes && slices && r->table_build == 7 && pp && r->n < ((size_t)1 << 28) &&
-        pp->alloc_pooled((size_t)nl * r->n * sizeof(uint4), s) == hipSuccess) {
-        e = cxk::fingers_quads(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint4>(), s);
-        if (e != hipSuccess) return e;
-        fv.Q = pp->as<uint4>();
-        fv.roots = 2;
-        fv.rs = hi.as<uint32_t>();
-        return hipSuccess;
-    }
-    (void)hipGetLastError();
-    if (have_planes && slices && r->table_build == 6 && pp &&
-        pp->alloc_pooled((size_t)nl * r->n * sizeof(uint2), s) == hipSuccess &&
-        c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint2), s) == hipSuccess) {
-        e = cxk::fingers_pairs2(fv.F, hi.as<uint32_t>(), r->n, nl, pp->as<uint2>(), c2.as<uint2>(), s);
-        if (e != hipSuccess) return e;
-        fv.P = pp->as<uint2>();
-        fv.P2 = c2.as<uint2>();
-        fv.roots = 2;
-        fv.rs = hi.as<uint32_t>();
-        return hipSuccess;
-    }
-    (void)hipGetLastError();
     if (have_planes && (roots_build || r->table_build == 3) &&
         c2.alloc_pooled((size_t)(nl - 1) * r->n * sizeof(uint32_t), s) == hipSuccess) {
         e = cxk::fingers_pairs(fv.F, r->n, nl, c2.as<uint32_t>(), s);
         if (e == hipSuccess) {
             fv.C2 = c2.as<uint32_t>();
-            // 0: blocks sized by distinct roots, 4: 256-row root blocks (round 3),
-            // 3: one lane per entry (round 2)
-            fv.roots = r->table_build == 9 ? 4
-                       : r->table_build == 8 ? 3
-                       : (r->table_build == 0 || r->table_build >= 5) ? 2
-                       : (r->table_build == 4 ? 1 : 0);
+            // 0: root-centric blocks sized by distinct roots; 3: one lane per entry
+            fv.roots = roots_build ? 2 : 0;
         }
     }
     (void)hipGetLastError();
@@ -772,12 +716,12 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
         }
         if (r->d_cz) {
             CX_HIP(hipMemsetAsync(r->d_scratch, 0, 2 * sizeof(uint32_t), s));
-            DBuf ft, hi, c2, pp;
+            DBuf ft, hi, c2;
             cxk::FingerView fv;
             if (!ft_pre || r->table_build == 1) {  // the planes come from the rows
                 if (int rc = ensure_fingers_rows(r, s)) return rc;
             }
-            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre, &pp));
+            CX_HIP(finger_planes(r, r->rt_l0, ft, fv, hi, c2, s, ft_pre));
             DBuf ws;  // the default build's overflow list
             if (fv.roots >= 2)
                 CX_HIP(ws.alloc_pooled(cxk::cz_build_ws_words(r->n, r->rt_l0, r->rt_R, (uint32_t)r->n) *
@@ -792,22 +736,7 @@ int ensure_route_table(cx_ring *r, hipStream_t s, const uint32_t *ft_pre = nullp
             r->cz_valid = true;
         }
     }
-    if (r->variant() == 1 && !r->rt_valid) {
-        if (!r->d_rt && table_alloc((void **)&r->d_rt, ent * sizeof(RtEntry)) != hipSuccess)
-            r->d_rt = nullptr;
-        if (r->d_rt) {
-            if (int rc = ensure_fingers_rows(r, s)) return rc;
-            CX_HIP(cxk::rt_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->d_rt, r->d_ring_ext, s));
-            r->rt_valid = true;
-        }
-    } else if ((r->variant() == 2 || r->variant() == 3) && !r->pk_valid) {
-        if (!r->d_pk && table_alloc((void **)&r->d_pk, ent * 16) != hipSuccess) r->d_pk = nullptr;
-        if (r->d_pk) {
-            if (int rc = ensure_fingers_rows(r, s)) return rc;
-            CX_HIP(cxk::pk_build(r->d_fingers, r->d_ring, r->n, r->rt_l0, r->rt_R, r->pk_ib, r->d_pk, s));
-            r->pk_valid = true;
-        }
-    } else if (r->variant() == 4 && !r->tree_valid) {
+    if (r->variant() == 4 && !r->tree_valid) {
         if (!r->d_tree && table_alloc((void **)&r->d_tree, ent * 64) != hipSuccess)
             r->d_tree = nullptr;
         if (r->d_tree) {
@@ -829,17 +758,13 @@ int churn_merge(const cx_ring *old_ring, const cell128 *J0, size_t nj, const cel
     // every temporary recurs at the same size each membership epoch: through
     // the pool (plain hipMalloc / hipFree cost ~0.7 ms per churn at 2^24)
     DBuf G, A, ws, jk0, jk1, jt0, jt1, pos, keep, ringbuf;
-    // joins: bucket sort (CX_JOIN_SORT=radix for the radix sort, A/B), and the
-    // radix sort when a bucket overflowed (clustered joins)
-    static const bool radix_only = [] {
-        const char *e = getenv("CX_JOIN_SORT");
-        return e && strcmp(e, "radix") == 0;
-    }();
+    // joins: bucket sort, and the radix sort when a bucket overflowed
+    // (clustered joins)
     uint32_t *d_ovf = static_cast<uint32_t *>(r->d_scratch) + 64;
     uint32_t gone = 0, kept = 0, ovf = 0;
     const cell128 *J = J0;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        const bool radix = radix_only || attempt == 1;
+        const bool radix = attempt == 1;
         size_t sw = cxk::scan_workspace_words(n_old + 2 > nj + 1 ? n_old + 2 : nj + 1);
         const size_t rw = nj ? (radix ? cxk::sort_workspace_words(nj)
                                       : cxk::bucket_sort_workspace_words(nj)) : 0;
@@ -1073,11 +998,10 @@ namespace {
 int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, int ft_l = 0,
                         bool *ft_done = nullptr, bool rows = true) {
     // streaming per-block window build (needs the directory and the ID
-    // slices); CX_FINGERS_SEARCH=1 keeps one search per entry (A/B)
-    static const bool search_only = getenv("CX_FINGERS_SEARCH") != nullptr;
+    // slices); one search per entry without HBM for them
     SearchView fv = ring->sv();
     fv.dir = ring->d_dir;
-    if (!search_only && !ring->d_ring_key) {
+    if (!ring->d_ring_key) {
         if (table_alloc((void **)&ring->d_ring_key, ring->n * sizeof(uint32_t)) == hipSuccess)
             CX_HIP(cxk::ring_slice_build(ring->d_ring, ring->n, cxk::finger_key_shift(ring->n),
                                          ring->d_ring_key, s));
@@ -1085,7 +1009,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
             ring->d_ring_key = nullptr;  // no HBM for it: one search per entry
     }
     DBuf fws;
-    const bool streaming = !search_only && ring->d_ring_key &&
+    const bool streaming = ring->d_ring_key &&
                            fws.alloc_pooled(cxk::fingers_workspace_bytes(ring->n), s) == hipSuccess;
     // planes only (rows deferred) needs the streaming build with every plane a tile level
     if (!streaming || !ft || ft_l < cxk::FINGERS_TILE_L0 || ring->n < ((size_t)1 << 18)) rows = true;
@@ -1099,7 +1023,7 @@ int build_fingers_table(cx_ring *ring, hipStream_t s, uint32_t *ft = nullptr, in
                               ft_l, ft_done));
     ring->fingers_converged = true;
     ring->rows_deferred = !rows;
-    ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
+    ring->tree_valid = ring->cz_valid = false;
     return CX_OK;
 }
 }  // namespace
@@ -1172,19 +1096,17 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
     const size_t cnt = ring->n * CX_FINGERS;
     route_geometry(ring);
     // rows deferred (planes only) when nobody asked for them and the default
-    // route reads planes from the streaming build; CX_FINGERS_ROWS=1 writes
-    // them now (A/B)
-    static const bool eager_rows = getenv("CX_FINGERS_ROWS") != nullptr;
+    // route reads planes from the streaming build
     const int ft_l = ring->rt_l0 - 5;
-    const bool defer = !eager_rows && !fingers_out && ring->variant() == 5 &&
-                       (ring->table_build == 0 || ring->table_build >= 3) && ft_l >= 64 &&
+    const bool defer = !fingers_out && ring->variant() == 5 &&
+                       (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64 &&
                        ring->n >= ((size_t)1 << 18) && ft_l >= cxk::FINGERS_TILE_L0;
     // the default route table reads the fingers as level planes: the streaming
     // finger build writes them alongside the rows (no transpose pass), and the
     // ring keeps them for the finger repair of the next churn
     std::shared_ptr<PlaneSet> ps;
     bool ft_done = false;
-    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build >= 3) && ft_l >= 64) {
+    if (ring->variant() == 5 && (ring->table_build == 0 || ring->table_build == 3) && ft_l >= 64) {
         const int nl = (int)CX_FINGERS - ft_l;
         const size_t bytes = (size_t)nl * ring->n * sizeof(uint32_t);
         void *pp = nullptr;
@@ -1228,7 +1150,7 @@ int cx_fingers_build(cx_ring *ring, uint32_t *fingers_out, int memkind) {
                                          !defer || !ps))) {
         return rc;
     }
-    ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
+    ring->tree_valid = ring->cz_valid = false;  // tables follow the fingers
     if (!ring->d_ring_ext &&
         table_alloc((void **)&ring->d_ring_ext, (ring->n + 1) * sizeof(cell128)) != hipSuccess)
         ring->d_ring_ext = nullptr;
@@ -1280,7 +1202,7 @@ int cx_fingers_upload(cx_ring *ring, const uint32_t *fingers, int memkind) {
     staged.release();
     ring->fingers_converged = false;
     ring->rows_deferred = false;
-    ring->rt_valid = ring->pk_valid = ring->tree_valid = ring->cz_valid = false;
+    ring->tree_valid = ring->cz_valid = false;
     return CX_OK;
 }
 
@@ -1416,32 +1338,14 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     }
     SearchView dsv = ring->sv();
     dsv.dir = ring->d_dir;
-    if (v == 5 && ring->cz_valid && !g_old_walk)
+    if (v == 5 && ring->cz_valid)
         CX_HIP(cxk::route_walk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
                                ring->pk_ib, dsv, dsrc, reinterpret_cast<const cell128 *>(dk), q,
                                dow, dh, dst, ring->counting ? ring->d_stats : nullptr, s));
-    else if (v == 5 && ring->cz_valid)
-        CX_HIP(cxk::route_cz(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_cz, ring->rt_l0,
-                             ring->rt_R, ring->pk_ib, ring->rows_deferred ? nullptr : ring->d_fingers,
-                             dsv, dsrc,
-                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst,
-                             ring->counting ? ring->d_stats : nullptr, s));
     else if (v == 4 && ring->tree_valid)
         CX_HIP(cxk::route_tree(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_tree, ring->rt_l0,
                                ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
                                reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
-    else if (v == 3 && ring->pk_valid)
-        CX_HIP(cxk::route_pk3(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
-                              ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
-                              reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
-    else if (v == 2 && ring->pk_valid)
-        CX_HIP(cxk::route_pk(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_pk, ring->rt_l0,
-                             ring->rt_R, ring->pk_ib, ring->d_fingers, dsrc,
-                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
-    else if (v == 1 && ring->rt_valid)
-        CX_HIP(cxk::route_rt(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_rt, ring->rt_l0,
-                             ring->rt_R, ring->d_fingers, dsrc,
-                             reinterpret_cast<const cell128 *>(dk), q, dow, dh, dst, s));
     else
         CX_HIP(cxk::route(ring->d_ring, ring->n, ring->d_fingers, ring->d_min_keys,
                           ring->d_preds, ring->lit(), ring->literal(), dsrc,
@@ -2093,9 +1997,9 @@ int cx_arc_build(cx_ring *ring, int world, int rank, int top_levels) {
     ring->arc_bytes = (top_ent + low_ent) * 64 + 64;
     CX_HIP(hipMemsetAsync(ring->d_scratch, 0, 2 * sizeof(uint32_t), s));
     {
-        DBuf ft, hi, c2, pp;
+        DBuf ft, hi, c2;
         cxk::FingerView fv;
-        CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s, nullptr, &pp));
+        CX_HIP(finger_planes(ring, l0, ft, fv, hi, c2, s, nullptr));
         DBuf ws;  // the default build's overflow list (sized for the larger part)
         if (fv.roots >= 2) {
             const size_t w0 = cxk::cz_build_ws_words(n, Lh, (int)CX_FINGERS - Lh, (uint32_t)n);
@@ -2382,12 +2286,6 @@ int cxi_pool_stats(uint64_t *out) {
 // ---- internal: fault injection for tests (bit 0: the route-table build's
 // finger-plane allocation fails; bit 1: the default route-table build defers
 // the rows past 48 distinct roots per block to overflow launches).
-// A/B during round 5 only: 1 = the round-4 walk (k_route_tree<false, true>)
-extern "C" int cxi_ab_old_walk(int on) {
-    g_old_walk = on != 0;
-    return CX_OK;
-}
-
 int cxi_set_fault(int mask) {
     g_fault.store(mask);
     cxk::cz2_set_cap(mask & 2 ? 48u : 256u);
@@ -2397,14 +2295,14 @@ int cxi_set_fault(int mask) {
 // ---- internal (not part of chordx.h): error reporting for cx_wire.cpp
 int cxi_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
 
-// ---- internal (not part of chordx.h): kernel-variant switch for A/B benches
-// and parity tests.  0 = finger + ring gathers per hop, 1 = route table,
-// 2 = packed route table with one-level lookahead, 3 = 2 + staged results and
-// prefetched source pairs, 4 = lookahead-tree table, 5 = pattern-keyed window
-// table, -1 = automatic (default: 5 up to 2^24 peers, else 4).
+// ---- internal (not part of chordx.h): route-walk switch for parity tests and
+// benches.  0 = finger + ring gathers per hop (no table), 4 = lookahead-tree
+// table (the automatic choice above 2^24 peers), 5 = pattern-keyed window table
+// (k_walk), -1 = automatic (5 up to 2^24 peers, else 4).
 int cxi_set_route_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= -1 && variant <= 5, CX_E_INVALID, "variant must be -1 (auto) or 0..5");
+    CX_CHECK(variant == -1 || variant == 0 || variant == 4 || variant == 5, CX_E_INVALID,
+             "variant must be -1 (auto), 0, 4 or 5");
     ring->route_variant = variant;
     return CX_OK;
 }
@@ -2415,7 +2313,7 @@ int cxi_set_route_depth(cx_ring *ring, int R) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
     // the pattern-keyed build needs its lowest plane level (128 - R - 5) >= 64
     CX_CHECK(R == 0 || (R >= 16 && R <= 59), CX_E_INVALID, "R must be 0 or in [16, 59]");
-    CX_CHECK(!ring->d_cz && !ring->d_tree && !ring->d_pk && !ring->d_rt && !ring->d_arc_tree,
+    CX_CHECK(!ring->d_cz && !ring->d_tree && !ring->d_arc_tree,
              CX_E_STATE, "route depth is fixed once a route table exists");
     ring->depth_override = R;
     return CX_OK;
@@ -2432,9 +2330,7 @@ int cxi_route_info(const cx_ring *ring, int *variant, uint64_t *cz_escapes,
     *cz_escapes = ring->cz_escapes;
     *table_bytes = v == 5 && ring->cz_valid     ? ent * 128
                    : v == 4 && ring->tree_valid ? ent * 64
-                   : (v == 2 || v == 3) && ring->pk_valid ? ent * 16
-                   : v == 1 && ring->rt_valid ? ent * sizeof(RtEntry)
-                                              : 0;
+                                                : 0;
     return CX_OK;
 }
 
@@ -2528,18 +2424,16 @@ int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
     return CX_OK;
 }
 
-// Route-table build input: 0 = level + two-hop planes, root-centric windows
-// in blocks sized by distinct roots (k_cz_build_roots2<7, 0>, default), 1 =
-// row-major finger table, 2 = level planes only, 3 = level + two-hop planes,
-// one lane per entry (k_cz_build, the round-2 build), 4 = root-centric windows
-// in 256-row blocks (k_cz_build_roots, round 3), 5 = the same as 0, 6 = as 0
-// on pair planes, 7 = as 0 on quad planes, 8 = both windows of a root at once,
-// stores last (k_cz_build_roots3), 9 = as 0 with plane 0 stored after the W1
-// gathers (k_cz_build_roots2<7, 0, true>).  All give the same table.  Takes
-// effect at the next finger build.
+// Route-table build input (parity tests of the build's fallbacks): 0 = level +
+// two-hop planes, root-centric windows in blocks sized by distinct roots
+// (k_cz_build_roots2, default), 1 = row-major finger table (the fallback
+// without HBM for the planes), 2 = level planes only, 3 = level + two-hop
+// planes, one lane per entry (k_cz_build; also the build of rings with a gap
+// too wide for the 32-bit ID slices).  All give the same table.  Takes effect
+// at the next finger build.
 int cxi_set_table_build(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 9, CX_E_INVALID, "variant must be 0 .. 9");
+    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0 .. 3");
     ring->table_build = variant;
     return CX_OK;
 }

@@ -1350,41 +1350,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route_literal(
     }
 }
 
-// ---------------------------------------------------------------------------
-// Route table: the finger levels [l0, 128) of every peer with the successor's
-// ID stored beside its index, as the reference's Finger{lower, upper,
-// successor_} carries the successor RemotePeer (finger_table.h:20-28).  One
-// hop = one 32-byte gather.  ring_ext[0] = ring[n-1], ring_ext[1+p] = ring[p],
-// so (predecessor, self) of peer p is the contiguous pair ring_ext[p..p+1].
-// ---------------------------------------------------------------------------
-__global__ void k_rt_build(const uint32_t *F, const cell128 *ring, uint32_t n, int l0, int R,
-                           RtEntry *rt) {
-    const size_t total = (size_t)n * R;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-         t += (size_t)gridDim.x * blockDim.x) {
-        const size_t p = t / (unsigned)R;
-        const int j = (int)(t - p * (unsigned)R);
-        const uint32_t f = F[p * CX_FINGERS + l0 + j];
-        const u128 id = ld128(ring + f);
-        RtEntry e;
-        e.lo = (uint64_t)id;
-        e.hi = (uint64_t)(id >> 64);
-        e.idx = f;
-        e.pad0 = e.pad1 = e.pad2 = 0;
-        rt[t] = e;
-    }
-}
-
 __global__ void k_ring_ext(const cell128 *ring, uint32_t n, cell128 *ext) {
     for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t <= n;
          t += (size_t)gridDim.x * blockDim.x)
         st128(ext + t, ld128(ring + (t == 0 ? n - 1 : t - 1)));
-}
-
-hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
-                    cell128 *ring_ext, hipStream_t s) {
-    k_rt_build<<<cx_grid(n * (size_t)R, 256), 256, 0, s>>>(F, ring, (uint32_t)n, l0, R, rt);
-    return hipGetLastError();
 }
 
 hipError_t ring_ext_build(const cell128 *ring, size_t n, cell128 *ring_ext, hipStream_t s) {
@@ -1392,198 +1361,11 @@ hipError_t ring_ext_build(const cell128 *ring, size_t n, cell128 *ring_ext, hipS
     return hipGetLastError();
 }
 
-// Converged walk over the route table.  Each wave owns a contiguous chunk of
+// Converged walks over a route table.  Each wave owns a contiguous chunk of
 // queries and a scalar queue head; a lane that finishes takes the next index
 // (ballot + mbcnt), so lanes never idle behind the wave's longest walk.  Every
-// loop iteration is ONE dependent load round per lane: either the (pred, self)
-// pair of a new source peer or the route-table entry of the current hop.  The
-// (key, src) of a lane's next query are prefetched while it walks.
+// loop iteration is ONE dependent load round per lane.
 constexpr int RT_BLOCK = 256;
-
-__global__ __launch_bounds__(RT_BLOCK) void k_route_rt(
-    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const RtEntry *rt, int l0, int R,
-    const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
-    uint32_t *owner, uint8_t *hops, uint8_t *status) {
-    const int lane = threadIdx.x & 63;
-    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
-    const size_t base = wave * chunk;
-    if (base >= q) return;  // wave-uniform
-    const size_t end = (base + chunk < q) ? base + chunk : q;
-    size_t head = base + 64;  // wave-uniform queue head (after the first 64)
-
-    // current query
-    size_t qi = base + lane;
-    bool live = qi < end;
-    u128 key = 0, idc = 0;
-    uint32_t cur = 0, h = 0;
-    bool init = true;
-    if (live) {
-        key = ld128(keys + qi);
-        cur = src[qi];
-    }
-    // prefetched next query of this lane
-    size_t pq = 0;
-    bool plive = false;
-    u128 pkey = 0;
-    uint32_t psrc = 0;
-    {
-        const uint64_t want = __ballot(live);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-        if (live) {
-            pq = head + rank;
-            plive = pq < end;
-            if (plive) {
-                pkey = ld128(keys + pq);
-                psrc = src[pq];
-            }
-        }
-        head += (size_t)__popcll(want);
-    }
-
-    while (__ballot(live) != 0) {
-        // ---- one load round ----
-        u128 a = 0, b = 0, d = 0;
-        uint32_t nxt = 0;
-        if (live) {
-            if (init) {
-                if (cur < n) {
-                    a = ld128(ring_ext + cur);      // predecessor id
-                    b = ld128(ring_ext + cur + 1);  // own id
-                }
-            } else {
-                d = key - idc;
-                const int i = msb128(d);
-                if (i >= l0) {
-                    const RtEntry *e = rt + (size_t)cur * (unsigned)R + (i - l0);
-                    a = ld128(reinterpret_cast<const cell128 *>(e));
-                    nxt = e->idx;
-                } else {  // rare: level below the route table
-                    nxt = F[(size_t)cur * CX_FINGERS + i];
-                    a = ld128(ring + nxt);
-                }
-            }
-        }
-        // ---- process ----
-        bool fin = false;
-        uint32_t own = CX_NONE;
-        uint8_t st = CX_Q_OK;
-        if (live) {
-            if (init) {
-                if (cur >= n) {
-                    fin = true;
-                    st = CX_Q_BADPEER;
-                    h = 0;
-                } else if (n == 1 || (key - a - 1) <= (b - a - 1)) {
-                    fin = true;  // StoredLocally at the source: 0 hops
-                    own = cur;
-                    h = 0;
-                } else {
-                    idc = b;
-                    init = false;
-                    h = 0;
-                }
-            } else {
-                ++h;
-                if (d <= a - idc) {  // StoredLocally(nxt)
-                    fin = true;
-                    own = nxt;
-                } else if (h == CX_HOP_CAP) {
-                    fin = true;
-                    st = CX_Q_HOPCAP;
-                } else {
-                    cur = nxt;
-                    idc = a;
-                }
-            }
-            if (fin) {
-                owner[qi] = own;
-                hops[qi] = (uint8_t)h;
-                if (status) status[qi] = st;
-            }
-        }
-        // ---- refill: finished lanes start their prefetched query ----
-        const uint64_t m = __ballot(fin);
-        if (m) {
-            const uint64_t want = __ballot(fin && plive);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-            if (fin) {
-                qi = pq;
-                live = plive;
-                key = pkey;
-                cur = psrc;
-                init = true;
-                h = 0;
-                if (plive) {
-                    pq = head + rank;
-                    plive = pq < end;
-                    if (plive) {
-                        pkey = ld128(keys + pq);
-                        psrc = src[pq];
-                    }
-                }
-            }
-            head += (size_t)__popcll(want);
-        }
-    }
-}
-
-hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, const RtEntry *rt,
-                    int l0, int R, const uint32_t *F, const uint32_t *src, const cell128 *keys,
-                    size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
-    if (q == 0) return hipSuccess;
-    // ~16 queries per lane: waves enough to fill 256 CUs x 8 waves/SIMD x 4
-    const size_t max_waves = 256 * 32;
-    size_t waves = (q + 1023) / 1024;
-    if (waves > max_waves) waves = max_waves;
-    if (waves == 0) waves = 1;
-    const size_t chunk = (q + waves - 1) / waves;
-    waves = (q + chunk - 1) / chunk;
-    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    k_route_rt<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n, rt, l0, R, F, src, keys, q,
-                                           chunk, owner, hops, status);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Packed route table (variant 2).  A finger is packed into 8 bytes:
-//   pk = (id >> S) << ib | idx,   ib = ceil(log2 n) index bits, S = 64 + ib,
-// i.e. the exact peer index plus the top 64 - ib bits of its ID, so the ID is
-// known to lie in [T << S, (T << S) + 2^S - 1].  Entry (p, i), 16 B:
-//   .x = pk(finger(p, i)) = pk(nxt),  .y = pk(finger(nxt, i - 1))
-// The second half makes a hop whose level drops by exactly one free (no
-// gather).  Every decision of the walk (finger level, StoredLocally) is taken
-// on these ID intervals; if an interval straddles the decision the lane
-// fetches the exact IDs (ring[cur], ring[nxt]) and decides exactly, so
-// results are bit-exact for any ring (adversarial rings just run slower).
-// ---------------------------------------------------------------------------
-__global__ void k_pk_build(const uint32_t *F, const cell128 *ring, uint32_t n, int l0, int R,
-                           int ib, uint2 *pk_unused, uint64_t *rt) {
-    const size_t total = (size_t)n * R;
-    const int S = 64 + ib;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-         t += (size_t)gridDim.x * blockDim.x) {
-        const size_t p = t / (unsigned)R;
-        const int i = l0 + (int)(t - p * (unsigned)R);
-        const uint32_t f = F[p * CX_FINGERS + i];
-        const uint64_t a = ((uint64_t)(ld128(ring + f) >> S) << ib) | f;
-        uint64_t b = ~0ull;
-        if (i >= 1) {
-            const uint32_t g = F[(size_t)f * CX_FINGERS + i - 1];
-            b = ((uint64_t)(ld128(ring + g) >> S) << ib) | g;
-        }
-        rt[2 * t] = a;
-        rt[2 * t + 1] = b;
-    }
-}
-
-hipError_t pk_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
-                    uint64_t *rt, hipStream_t s) {
-    k_pk_build<<<cx_grid(n * (size_t)R, 256), 256, 0, s>>>(F, ring, (uint32_t)n, l0, R, ib,
-                                                           nullptr, rt);
-    return hipGetLastError();
-}
 
 // Level of the next hop, FingerTable::Lookup's first match = msb(key - id),
 // for id in [lo, lo + w]:  -1 if the interval does not decide it.
@@ -1607,237 +1389,9 @@ __device__ __forceinline__ int term_iv(u128 key, u128 clo, u128 cw, u128 nlo, u1
     return -1;
 }
 
-enum { M_INIT = 0, M_HOP = 1, M_FIXC = 2, M_FIXT = 3 };
-
-__global__ __launch_bounds__(RT_BLOCK) void k_route_pk(
-    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const uint4 *rt, int l0, int R,
-    int ib, const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
-    uint32_t *owner, uint8_t *hops, uint8_t *status) {
-    const int lane = threadIdx.x & 63;
-    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
-    const size_t base = wave * chunk;
-    if (base >= q) return;
-    const size_t end = (base + chunk < q) ? base + chunk : q;
-    size_t head = base + 64;
-    const int S = 64 + ib;
-    const uint64_t imask = (1ull << ib) - 1;
-    const u128 W = ((u128)1 << S) - 1;  // width of a packed ID interval
-
-    size_t qi = base + lane;
-    bool live = qi < end;
-    u128 key = 0, clo = 0, cw = 0;      // id(cur) in [clo, clo + cw]
-    uint32_t cur = 0, h = 0, pn = 0;
-    int mode = M_INIT, lvl = 0, la_lvl = -2;
-    uint64_t la = 0;
-    if (live) {
-        key = ld128(keys + qi);
-        cur = src[qi];
-    }
-    size_t pq = 0;
-    bool plive = false;
-    u128 pkey = 0;
-    uint32_t psrc = 0;
-    {
-        const uint64_t want = __ballot(live);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-        if (live) {
-            pq = head + rank;
-            plive = pq < end;
-            if (plive) {
-                pkey = ld128(keys + pq);
-                psrc = src[pq];
-            }
-        }
-        head += (size_t)__popcll(want);
-    }
-
-    while (__ballot(live) != 0) {
-        // ---------------- memory: one load round ----------------
-        u128 xa = 0, xb = 0;
-        uint4 e = make_uint4(0, 0, 0, 0);
-        if (live) {
-            if (mode == M_INIT) {
-                if (cur < n) {
-                    xa = ld128(ring_ext + cur);
-                    xb = ld128(ring_ext + cur + 1);
-                }
-            } else if (mode == M_HOP) {
-                e = rt[(size_t)cur * (unsigned)R + (lvl - l0)];
-            } else if (mode == M_FIXC) {
-                xa = ld128(ring + cur);
-            } else {
-                xa = ld128(ring + cur);
-                xb = ld128(ring + pn);
-            }
-        }
-        // ---------------- compute ----------------
-        bool fin = false, plan = false;
-        uint32_t own = CX_NONE;
-        uint8_t st = CX_Q_OK;
-        if (live) {
-            if (mode == M_INIT) {
-                h = 0;
-                la_lvl = -2;
-                if (cur >= n) {
-                    fin = true;
-                    st = CX_Q_BADPEER;
-                } else if (n == 1 || (key - xa - 1) <= (xb - xa - 1)) {
-                    fin = true;
-                    own = cur;
-                } else {
-                    clo = xb;
-                    cw = 0;
-                    plan = true;
-                }
-            } else if (mode == M_FIXC) {
-                clo = xa;
-                cw = 0;
-                plan = true;
-            } else if (mode == M_FIXT) {
-                // exact StoredLocally(pn) for the pending hop cur -> pn
-                if (key - xa <= xb - xa) {
-                    fin = true;
-                    own = pn;
-                } else if (h == CX_HOP_CAP) {
-                    fin = true;
-                    st = CX_Q_HOPCAP;
-                } else {
-                    cur = pn;
-                    clo = xb;
-                    cw = 0;
-                    plan = true;
-                }
-            } else {  // M_HOP: entry (cur, lvl) arrived
-                const uint64_t m0 = ((uint64_t)e.y << 32) | e.x;
-                la = ((uint64_t)e.w << 32) | e.z;
-                la_lvl = lvl - 1;
-                const uint32_t nxt = (uint32_t)(m0 & imask);
-                const u128 nlo = (u128)(m0 >> ib) << S;
-                ++h;
-                const int t = term_iv(key, clo, cw, nlo, W);
-                if (t == 1) {
-                    fin = true;
-                    own = nxt;
-                } else if (t < 0) {
-                    mode = M_FIXT;
-                    pn = nxt;
-                } else if (h == CX_HOP_CAP) {
-                    fin = true;
-                    st = CX_Q_HOPCAP;
-                } else {
-                    cur = nxt;
-                    clo = nlo;
-                    cw = W;
-                    plan = true;
-                }
-            }
-            // ---------------- plan the next load (free hops inline) ----------------
-            while (plan) {
-                plan = false;
-                const int i = level_iv(key, clo, cw);
-                if (i < 0) {
-                    mode = M_FIXC;  // id(cur) needed exactly
-                } else if (i == la_lvl) {
-                    // free hop: finger(cur, i) came with the previous entry
-                    la_lvl = -2;
-                    const uint32_t nxt = (uint32_t)(la & imask);
-                    const u128 nlo = (u128)(la >> ib) << S;
-                    ++h;
-                    const int t = term_iv(key, clo, cw, nlo, W);
-                    if (t == 1) {
-                        fin = true;
-                        own = nxt;
-                    } else if (t < 0) {
-                        mode = M_FIXT;
-                        pn = nxt;
-                    } else if (h == CX_HOP_CAP) {
-                        fin = true;
-                        st = CX_Q_HOPCAP;
-                    } else {
-                        cur = nxt;
-                        clo = nlo;
-                        cw = W;
-                        plan = true;
-                    }
-                } else if (i >= l0) {
-                    mode = M_HOP;
-                    lvl = i;
-                    la_lvl = -2;
-                } else {
-                    // rare: level below the table -> exact finger + exact ids
-                    la_lvl = -2;
-                    const uint32_t nxt = F[(size_t)cur * CX_FINGERS + i];
-                    const u128 idn = ld128(ring + nxt);
-                    const u128 idc = cw ? ld128(ring + cur) : clo;
-                    ++h;
-                    if (key - idc <= idn - idc) {
-                        fin = true;
-                        own = nxt;
-                    } else if (h == CX_HOP_CAP) {
-                        fin = true;
-                        st = CX_Q_HOPCAP;
-                    } else {
-                        cur = nxt;
-                        clo = idn;
-                        cw = 0;
-                        plan = true;
-                    }
-                }
-            }
-            if (fin) {
-                owner[qi] = own;
-                hops[qi] = (uint8_t)h;
-                if (status) status[qi] = st;
-            }
-        }
-        // ---------------- refill ----------------
-        const uint64_t m = __ballot(fin);
-        if (m) {
-            const uint64_t want = __ballot(fin && plive);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-            if (fin) {
-                qi = pq;
-                live = plive;
-                key = pkey;
-                cur = psrc;
-                mode = M_INIT;
-                h = 0;
-                if (plive) {
-                    pq = head + rank;
-                    plive = pq < end;
-                    if (plive) {
-                        pkey = ld128(keys + pq);
-                        psrc = src[pq];
-                    }
-                }
-            }
-            head += (size_t)__popcll(want);
-        }
-    }
-}
-
-hipError_t route_pk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
-                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
-                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                    uint8_t *status, hipStream_t s) {
-    if (q == 0) return hipSuccess;
-    const size_t max_waves = 256 * 32;
-    size_t waves = (q + 1023) / 1024;
-    if (waves > max_waves) waves = max_waves;
-    if (waves == 0) waves = 1;
-    const size_t chunk = (q + waves - 1) / waves;
-    waves = (q + chunk - 1) / chunk;
-    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    k_route_pk<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n,
-                                           reinterpret_cast<const uint4 *>(rt), l0, R, ib, F, src,
-                                           keys, q, chunk, owner, hops, status);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------
-// Variant 3: variant 2's packed walk plus
+// k_route_tree (the v4 lookahead-tree walk above 2^24 peers, and the arc
+// walks over the cz table):
 //  * result staging: a finished query's (owner, hops, status) goes to a
 //    per-wave LDS window; 64 consecutive results are flushed as coalesced
 //    stores (one 256-B owner store, two 64-B byte stores) instead of three
@@ -1885,264 +1439,8 @@ __device__ __forceinline__ uint32_t finger_of(const SearchView &sv, const cell12
     return (step <= ld128(ring + nx) - idp) ? nx : dir_successor(sv, idp + step);
 }
 
-// Plan the next step from cur (free hops and below-table hops run inline).
-// Returns: 0 = needs a load (mode set), 1 = finished (own/st set).
-__device__ __forceinline__ int pk_plan(const PkCtx &c, u128 key, u128 &clo, bool &cex,
-                                       uint32_t &cur, uint32_t &h, uint32_t &pn, int &mode,
-                                       int &lvl, int &la_lvl, uint64_t la, uint32_t &own,
-                                       uint8_t &st) {
-    for (;;) {
-        const u128 cw = cex ? (u128)0 : c.W;
-        const int i = level_iv(key, clo, cw);
-        if (i < 0) {
-            mode = A_FIXC;
-            return 0;
-        }
-        if (i == la_lvl) {
-            la_lvl = -2;
-            const uint32_t nxt = (uint32_t)(la & c.imask);
-            const u128 nlo = (u128)(la >> c.ib) << c.S;
-            ++h;
-            const int t = term_iv(key, clo, cw, nlo, c.W);
-            if (t == 1) {
-                own = nxt;
-                return 1;
-            }
-            if (t < 0) {
-                mode = A_FIXT;
-                pn = nxt;
-                return 0;
-            }
-            if (h == CX_HOP_CAP) {
-                own = CX_NONE;
-                st = CX_Q_HOPCAP;
-                return 1;
-            }
-            cur = nxt;
-            clo = nlo;
-            cex = false;
-            continue;
-        }
-        if (i >= c.l0) {
-            mode = A_HOP;
-            lvl = i;
-            la_lvl = -2;
-            return 0;
-        }
-        // rare: below the table -> exact finger + exact ids
-        la_lvl = -2;
-        const uint32_t nxt = c.F[(size_t)cur * CX_FINGERS + i];
-        const u128 idn = ld128(c.ring + nxt);
-        const u128 idc = cex ? clo : ld128(c.ring + cur);
-        ++h;
-        if (key - idc <= idn - idc) {
-            own = nxt;
-            return 1;
-        }
-        if (h == CX_HOP_CAP) {
-            own = CX_NONE;
-            st = CX_Q_HOPCAP;
-            return 1;
-        }
-        cur = nxt;
-        clo = idn;
-        cex = true;
-    }
-}
-
 __device__ __forceinline__ uint64_t pack_res(uint32_t own, uint32_t h, uint8_t st) {
     return (1ull << 63) | ((uint64_t)st << 40) | ((uint64_t)(h & 0xFF) << 32) | own;
-}
-
-__global__ __launch_bounds__(RT_BLOCK) void k_route_pk3(
-    const cell128 *ring_ext, const cell128 *ring, uint32_t n, const uint4 *rt, int l0, int R,
-    int ib, const uint32_t *F, const uint32_t *src, const cell128 *keys, size_t q, size_t chunk,
-    uint32_t *owner, uint8_t *hops, uint8_t *status) {
-    __shared__ uint64_t res_all[RT_BLOCK / 64][RES_WIN];
-    const int lane = threadIdx.x & 63;
-    uint64_t *res = res_all[threadIdx.x >> 6];
-    for (int j = lane; j < RES_WIN; j += 64) res[j] = 0;
-    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
-    const size_t base = wave * chunk;
-    if (base >= q) return;  // wave-uniform
-    const size_t end = (base + chunk < q) ? base + chunk : q;
-    PkCtx c;
-    c.ring = ring;
-    c.F = F;
-    c.n = n;
-    c.l0 = l0;
-    c.ib = ib;
-    c.S = 64 + ib;
-    c.imask = (1ull << ib) - 1;
-    c.W = ((u128)1 << c.S) - 1;
-    size_t head = base, flushed = base;
-
-    // slot A (walking query)
-    int mode = A_NONE, lvl = 0, la_lvl = -2;
-    size_t qi = 0;
-    u128 key = 0, clo = 0;
-    bool cex = true;
-    uint32_t cur = 0, h = 0, pn = 0;
-    uint64_t la = 0;
-    // slot B (prefetched query)
-    int bst = B_EMPTY;
-    size_t pq = 0;
-    u128 pkey = 0, pa = 0, pb = 0;
-    uint32_t psrc = 0;
-
-    for (;;) {
-        // ---- refill slot B from the wave's queue (window-limited) ----
-        {
-            const size_t lim = (end < flushed + RES_WIN) ? end : flushed + RES_WIN;
-            const size_t avail = lim > head ? lim - head : 0;
-            const uint64_t want = __ballot(bst == B_EMPTY);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-            if (bst == B_EMPTY && rank < avail) {
-                pq = head + rank;
-                pkey = ld128(keys + pq);
-                psrc = src[pq];
-                bst = B_KS;
-            }
-            const size_t took = (size_t)__popcll(want);
-            head += took < avail ? took : avail;
-        }
-        // exit when nothing is in flight, the queue is drained and every staged
-        // result is written (a flush moves at most two segments per iteration,
-        // so a slow lane can leave several complete segments behind it)
-        if (__ballot(mode != A_NONE || bst != B_EMPTY) == 0 && head >= end &&
-            flushed >= end)  // every staged result written
-            break;
-
-        // ---- memory: one round (slot A's load + slot B's pair) ----
-        u128 xa = 0, xb = 0;
-        uint4 e = make_uint4(0, 0, 0, 0);
-        if (mode == A_HOP) {
-            e = rt[(size_t)cur * (unsigned)R + (lvl - l0)];
-        } else if (mode == A_FIXC) {
-            xa = ld128(ring + cur);
-        } else if (mode == A_FIXT) {
-            xa = ld128(ring + cur);
-            xb = ld128(ring + pn);
-        }
-        if (bst == B_KS) {
-            if (psrc < n) {
-                pa = ld128(ring_ext + psrc);
-                pb = ld128(ring_ext + psrc + 1);
-            }
-            bst = B_PAIR;
-        }
-
-        // ---- compute slot A ----
-        bool fin = false, plan = false;
-        uint32_t own = CX_NONE;
-        uint8_t st = CX_Q_OK;
-        if (mode == A_HOP) {
-            const uint64_t m0 = ((uint64_t)e.y << 32) | e.x;
-            la = ((uint64_t)e.w << 32) | e.z;
-            la_lvl = lvl - 1;
-            const uint32_t nxt = (uint32_t)(m0 & c.imask);
-            const u128 nlo = (u128)(m0 >> ib) << c.S;
-            ++h;
-            const int t = term_iv(key, clo, cex ? (u128)0 : c.W, nlo, c.W);
-            if (t == 1) {
-                fin = true;
-                own = nxt;
-            } else if (t < 0) {
-                mode = A_FIXT;
-                pn = nxt;
-            } else if (h == CX_HOP_CAP) {
-                fin = true;
-                st = CX_Q_HOPCAP;
-            } else {
-                cur = nxt;
-                clo = nlo;
-                cex = false;
-                plan = true;
-            }
-        } else if (mode == A_FIXC) {
-            clo = xa;
-            cex = true;
-            plan = true;
-        } else if (mode == A_FIXT) {
-            if (key - xa <= xb - xa) {
-                fin = true;
-                own = pn;
-            } else if (h == CX_HOP_CAP) {
-                fin = true;
-                st = CX_Q_HOPCAP;
-            } else {
-                cur = pn;
-                clo = xb;
-                cex = true;
-                plan = true;
-            }
-        }
-        if (plan) fin = pk_plan(c, key, clo, cex, cur, h, pn, mode, lvl, la_lvl, la, own, st) == 1;
-        if (fin) {
-            res[qi & (RES_WIN - 1)] = pack_res(own, h, st);
-            mode = A_NONE;
-        }
-        // ---- promote slot B into an idle slot A ----
-        if (mode == A_NONE && bst == B_PAIR) {
-            bst = B_EMPTY;
-            qi = pq;
-            key = pkey;
-            cur = psrc;
-            h = 0;
-            la_lvl = -2;
-            own = CX_NONE;
-            st = CX_Q_OK;
-            bool done = true;
-            if (cur >= n) {
-                st = CX_Q_BADPEER;
-            } else if (n == 1 || (key - pa - 1) <= (pb - pa - 1)) {
-                own = cur;  // StoredLocally at the source: 0 hops
-            } else {
-                clo = pb;
-                cex = true;
-                done = pk_plan(c, key, clo, cex, cur, h, pn, mode, lvl, la_lvl, la, own, st) == 1;
-            }
-            if (done) {
-                res[qi & (RES_WIN - 1)] = pack_res(own, h, st);
-                mode = A_NONE;
-            }
-        }
-
-        // ---- flush complete 64-result segments (coalesced) ----
-        for (int it = 0; it < 2; ++it) {
-            if (flushed >= end) break;
-            const size_t idx = flushed + lane;
-            const bool inr = idx < end;
-            const uint64_t v = inr ? res[idx & (RES_WIN - 1)] : 0ull;
-            if (__ballot(!inr || (v >> 63)) != ~0ull) break;
-            if (inr) {
-                owner[idx] = (uint32_t)v;
-                hops[idx] = (uint8_t)(v >> 32);
-                if (status) status[idx] = (uint8_t)(v >> 40);
-                res[idx & (RES_WIN - 1)] = 0;
-            }
-            flushed += 64;
-        }
-    }
-}
-
-hipError_t route_pk3(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
-                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
-                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                     uint8_t *status, hipStream_t s) {
-    if (q == 0) return hipSuccess;
-    const size_t max_waves = 256 * 32;
-    size_t waves = (q + 1023) / 1024;
-    if (waves > max_waves) waves = max_waves;
-    if (waves == 0) waves = 1;
-    const size_t chunk = (q + waves - 1) / waves;
-    waves = (q + chunk - 1) / chunk;
-    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    k_route_pk3<<<blocks, RT_BLOCK, 0, s>>>(ring_ext, ring, (uint32_t)n,
-                                            reinterpret_cast<const uint4 *>(rt), l0, R, ib, F,
-                                            src, keys, q, chunk, owner, hops, status);
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -2397,66 +1695,6 @@ hipError_t fingers_pairs(const uint32_t *FT, size_t n, int nl, uint32_t *C2, hip
     return hipGetLastError();
 }
 
-// Pair planes for the default route-table build: each finger with its 32-bit
-// ID slice beside it, P[k][x] = {F[x][L + k], rs[F[x][L + k]]} (k < nl), and
-// the two-hop planes likewise, P2[k - 1][x] = {z, rs[z]} with z =
-// F[F[x][L + k]][L + k - 1] (k >= 1).  The build's cost is the number of
-// vector-memory instructions its window gathers issue (the texture addresser
-// is busy for the whole build, profiles/r04/build_pmc/): a window node and its
-// slice then come in one 8-B gather instead of two 4-B ones.  One lane per
-// (peer, level): the plane read is coalesced, the gathers land near each
-// other (the fingers of adjacent peers), the pairs leave as coalesced 8-B
-// streaming stores.
-__global__ void k_fingers_pairs2(const uint32_t *FT, const uint32_t *rs, uint32_t n, int nl,
-                                 uint2 *P, uint2 *P2) {
-    const size_t k = blockIdx.y;
-    const uint32_t *up = FT + k * (size_t)n;
-    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
-        const uint32_t y = up[x];
-        const v2u py = {y, y < n ? rs[y] : 0u};
-        __builtin_nontemporal_store(py, reinterpret_cast<v2u *>(P + k * (size_t)n + x));
-        if (k) {
-            const uint32_t z = y < n ? FT[(k - 1) * (size_t)n + y] : CX_NONE;
-            const v2u pz = {z, z < n ? rs[z] : 0u};
-            __builtin_nontemporal_store(pz, reinterpret_cast<v2u *>(P2 + (k - 1) * (size_t)n + x));
-        }
-    }
-}
-
-// Quad planes: the pair and the two-hop pair of one (level, peer) side by
-// side, Q[k][x] = {F, rs[F], C2, rs[C2]} (16 B; the two-hop half of level L is
-// {CX_NONE, 0}).  A window gathers both children of a node that the build
-// needs at one level in one 16-B load (10 loads per window instead of 15).
-__global__ void k_fingers_quads(const uint32_t *FT, const uint32_t *rs, uint32_t n, int nl,
-                                uint4 *Q) {
-    const size_t k = blockIdx.y;
-    const uint32_t *up = FT + k * (size_t)n;
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
-        const uint32_t y = up[x];
-        const uint32_t z = (k && y < n) ? FT[(k - 1) * (size_t)n + y] : CX_NONE;
-        const v4u q = {y, y < n ? rs[y] : 0u, z, z < n ? rs[z] : 0u};
-        __builtin_nontemporal_store(q, reinterpret_cast<v4u *>(Q + k * (size_t)n + x));
-    }
-}
-
-hipError_t fingers_quads(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint4 *Q,
-                         hipStream_t s) {
-    if (n == 0 || nl < 2) return hipSuccess;
-    k_fingers_quads<<<dim3(cx_grid(n, 256, 4096), (unsigned)nl), 256, 0, s>>>(FT, rs, (uint32_t)n,
-                                                                              nl, Q);
-    return hipGetLastError();
-}
-
-hipError_t fingers_pairs2(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint2 *P,
-                          uint2 *P2, hipStream_t s) {
-    if (n == 0 || nl < 2) return hipSuccess;
-    k_fingers_pairs2<<<dim3(cx_grid(n, 256, 4096), (unsigned)nl), 256, 0, s>>>(
-        FT, rs, (uint32_t)n, nl, P, P2);
-    return hipGetLastError();
-}
-
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s) {
     if (n == 0 || nl <= 0) return hipSuccess;
@@ -2590,13 +1828,13 @@ hipError_t ring_codes(const cell128 *ring, size_t n, int ib, uint32_t *rs, uint3
 // stores (95 ms); a quad of lanes per entry (four columns of the slot square)
 // issued more, less coalesced gathers (97 ms).
 // MODE 0: row-major fingers; 1: level planes; 2: level + two-hop planes.
-// STORE bit 0: streaming (non-temporal) stores; bit 1: through LDS, whole lines.
-template <int MODE, int STORE = 1>
+// The 64-B entries leave through LDS as whole-line streaming stores.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *ring,
                                                   const uint64_t *rh, uint32_t n, int lvl_base,
                                                   int nlev, uint32_t p_first, uint32_t M, int gs,
                                                   uint4 *cz, uint32_t *esc, uint32_t K) {
-    __shared__ uint4 cz_stage[(STORE & 2) ? 256 * 4 : 1];
+    __shared__ uint4 cz_stage[256 * 4];
     // K = 0: grid.y = plane (i - lvl_base) * 2 + b, x over the plane's rows
     // (plane after plane).  K > 0: 1-D grid in chunks of K row-blocks: every
     // plane of a chunk of rows is dispatched before the next chunk, so planes
@@ -2630,8 +1868,7 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
     const uint32_t j = lb * blockDim.x + threadIdx.x;
     uint32_t out[16];
     if (j < M) {
-        // level-major: t = plane * M + j (the walk's entry index)
-        const size_t t = (size_t)plane * M + j;
+        // level-major: entry plane * M + j (the walk's entry index)
         uint64_t pw = (uint64_t)p_first + j;  // p_first < n, j < M <= n
         if (pw >= n) pw -= n;
         const uint32_t p = (uint32_t)pw;
@@ -2735,20 +1972,8 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
         }  // chained path
 #pragma unroll
         for (int v = 0; v < 16; ++v) bad += out[v] == CZ_NONE;
-        if (!(STORE & 2)) {
-            uint4 *e = cz + t * 4;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-                const v4u w = {out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]};
-                if (STORE & 1)
-                    __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(e + k));
-                else
-                    *reinterpret_cast<v4u *>(e + k) = w;
-            }
-        }
     }
-    if (STORE & 2) {
+    {
         // the wave's 64 entries (4 KiB, contiguous: one plane, consecutive
         // rows) leave through LDS as 4 stores of 1 KiB each, so every store
         // instruction writes whole lines instead of 16 B of 64 lines
@@ -2770,10 +1995,7 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
                 const uint4 u = ws[c];
                 const v4u w = {u.x, u.y, u.z, u.w};
                 v4u *dst = reinterpret_cast<v4u *>(cz + t0 * 4) + c;
-                if (STORE & 1)
-                    __builtin_nontemporal_store(w, dst);
-                else
-                    *dst = w;
+                __builtin_nontemporal_store(w, dst);
             }
         }
     }
@@ -2781,454 +2003,30 @@ __global__ __launch_bounds__(256) void k_cz_build(FingerView fv, const cell128 *
     if (bad) atomicAdd(esc, bad);
 }
 
-// Two lanes per entry (A/B, CX_CZ_PAIR=1): the sixteen slots split by their
-// level-(i-2) bit into two independent subtrees -- even slots hang off nd0
-// (the window root), odd slots off nd1 = f(nd0, i-2) -- so each lane of a
-// pair computes eight nodes (half the live registers of k_cz_build: twice
-// the waves per SIMD for the same dependent-gather chain).  Both lanes gather
-// the root (one address: one request).  Dispatch order and the whole-line
-// stores through LDS are k_cz_build's (K-row-block chunks, XCD-aware); a
-// wave holds 32 entries (2 KiB).  probe: 0 = build, 1 = stores only (the
-// dispatch pattern's write ceiling), 2 = compute only (no table stores).
-__global__ __launch_bounds__(256) void k_cz_build_pair(FingerView fv, const cell128 *ring,
-                                                       const uint64_t *rh, uint32_t n,
-                                                       int lvl_base, int nlev, uint32_t p_first,
-                                                       uint32_t M, int gs, uint4 *cz,
-                                                       uint32_t *esc, uint32_t K, int probe) {
-    __shared__ uint32_t stage[256 * 8];  // 128 entries x 16 words
-    constexpr uint32_t RB = 128;         // rows (entries) per block
-    uint32_t plane, lb;
-    {
-        const uint32_t P = (uint32_t)nlev * 2, B = blockIdx.x;
-        const uint32_t chunk = B / (K * P), rem = B - chunk * K * P;
-        plane = rem / K;
-        const uint32_t sub = rem - plane * K;
-        lb = chunk * K + (sub & 7) * (K >> 3) + (sub >> 3);
-    }
-    const int b = (int)(plane & 1);
-    const int i = lvl_base + (int)(plane >> 1);
-    const int hl = (int)(threadIdx.x & 1);    // 0: even slots, 1: odd slots
-    const uint32_t e_loc = threadIdx.x >> 1;  // entry within the block
-    const uint32_t j = lb * RB + e_loc;
-    auto fat = [&](uint32_t x, int l) -> uint32_t { return fv.F[(size_t)(l - fv.L) * fv.sl + x]; };
-    auto c2 = [&](uint32_t x, int l) -> uint32_t { return fv.C2[(size_t)(l - fv.L - 1) * fv.sl + x]; };
-    uint32_t oob = 0, bad = 0;
-    auto chk = [&](uint32_t x) -> uint32_t {
-        if (x >= n) {
-            oob = 1;
-            return 0u;
-        }
-        return x;
-    };
-    uint32_t out[8];
-    if (j < M && probe != 1) {
-        uint64_t pw = (uint64_t)p_first + j;
-        if (pw >= n) pw -= n;
-        const uint32_t p = (uint32_t)pw;
-        const uint64_t ph = rh[p];
-        uint32_t A = 0, a = p, nd0;
-        int al = i;
-        if (b) {
-            A = chk(fat(p, i));
-            a = A;
-            al = i - 1;
-            nd0 = chk(c2(p, i));
-        } else {
-            nd0 = chk(fat(p, i));
-        }
-        // this lane's eight nodes: w = slot >> 1; slot = 2w + hl
-        uint32_t nd[8];
-        if (hl == 0) {
-            nd[0] = nd0;                      // slot 0
-            nd[1] = chk(fat(nd0, i - 3));     // slot 2
-            nd[2] = chk(fat(nd0, i - 4));     // slot 4
-            nd[3] = chk(c2(nd0, i - 3));      // slot 6
-            nd[4] = chk(fat(nd0, i - 5));     // slot 8
-            nd[6] = chk(c2(nd0, i - 4));      // slot 12
-            nd[5] = chk(fat(nd[1], i - 5));   // slot 10
-            nd[7] = chk(c2(nd[1], i - 4));    // slot 14
-        } else {
-            nd[0] = chk(fat(nd0, i - 2));     // slot 1
-            nd[1] = chk(c2(nd0, i - 2));      // slot 3
-            nd[2] = chk(fat(nd[0], i - 4));   // slot 5
-            nd[3] = chk(fat(nd[1], i - 4));   // slot 7
-            nd[4] = chk(fat(nd[0], i - 5));   // slot 9
-            nd[5] = chk(fat(nd[1], i - 5));   // slot 11
-            nd[6] = chk(c2(nd[0], i - 4));    // slot 13
-            nd[7] = b ? A : chk(c2(nd[1], i - 4));  // slot 15
-        }
-        uint64_t hv[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) hv[w] = rh[nd[w]];
-        if (hl == 0) {
-            const uint64_t ah = b ? rh[A] : ph;
-            out[0] = cz_encode_hi(n, gs, a, ah, al, nd[0], hv[0], ring);
-            // slot 2w's parent: the slot without its highest bit (even, this lane)
-#pragma unroll
-            for (int w = 1; w < 8; ++w) {
-                const int v = 2 * w;
-                const int hb = 31 - __builtin_clz((unsigned)v);
-                const int pw2 = (v & ~(1 << hb)) >> 1;
-                out[w] = cz_encode_hi(n, gs, nd[pw2], hv[pw2], i - 2 - hb, nd[w], hv[w], ring);
-            }
-        } else {
-            // slot 1's parent is slot 0 = nd0 (the other lane's root, gathered here too)
-            const uint64_t h0 = rh[nd0];
-            out[0] = cz_encode_hi(n, gs, nd0, h0, i - 2, nd[0], hv[0], ring);
-#pragma unroll
-            for (int w = 1; w < 8; ++w) {
-                const int v = 2 * w + 1;
-                const int hb = 31 - __builtin_clz((unsigned)v);
-                const int pv = v & ~(1 << hb);  // odd (contains bit 0)
-                out[w] = cz_encode_hi(n, gs, nd[pv >> 1], hv[pv >> 1], i - 2 - hb, nd[w], hv[w],
-                                      ring);
-            }
-            if (b) out[7] = cz_encode_hi(n, gs, p, ph, i, A, hv[7], ring);
-        }
-#pragma unroll
-        for (int w = 0; w < 8; ++w) bad += out[w] == CZ_NONE;
-    } else {
-#pragma unroll
-        for (int w = 0; w < 8; ++w) out[w] = j * 16 + 2 * w + hl;
-    }
-    if (probe == 2) {  // compute only: keep the results live, store nothing
-        uint32_t x = 0;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) x ^= out[w];
-        if (x == 0x9E3779B9u) atomicAdd(esc, 0u);
-    } else {
-        // the wave's 32 entries (2 KiB, contiguous) leave through LDS as two
-        // 1-KiB stores: every store instruction writes whole lines
-        const int lane = threadIdx.x & 63;
-        uint32_t *ws = stage + (threadIdx.x >> 6) * 512;
-        const int el = lane >> 1;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) ws[el * 16 + 2 * w + hl] = out[w];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t j0 = lb * RB + ((threadIdx.x & ~63u) >> 1);  // the wave's first entry
-        const size_t t0 = (size_t)plane * M + j0;
-        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int c = k * 64 + lane;  // 16-B chunk of the wave's 2 KiB
-            if (j0 + (c >> 2) < M) {
-                const uint4 u = reinterpret_cast<const uint4 *>(ws)[c];
-                const v4u wv = {u.x, u.y, u.z, u.w};
-                __builtin_nontemporal_store(wv, reinterpret_cast<v4u *>(cz + t0 * 4) + c);
-            }
-        }
-    }
-    if (oob) atomicOr(esc + 1, 1u);
-    if (bad) atomicAdd(esc, bad);
-}
-
-// Root-centric build (table_build 0, the default): of the two entries (p, i, 0) and
-// (p, i, 1) only one word depends on p -- enc(A rel p) with A = f(p, i),
+// Root-centric build (table_build 0, the default): of the two entries (p, i, 0)
+// and (p, i, 1) only one word depends on p -- enc(A rel p) with A = f(p, i),
 // slot 0 of the b = 0 entry and slot 15 of the b = 1 entry -- while the other
-// fifteen words of each are a function of (A, i): W0(A, i) = the window
-// below A over levels i-2..i-5 (slots 1..15), W1(A, i) = A' = f(A, i-1)
-// relative to A (slot 0) and the window below A' (slots 1..14).  A block
-// takes 256 consecutive rows of one level (both planes): the rows' roots are
-// non-decreasing along the ring (f(., i) is monotone up to one wrap), so the
-// block compacts them to their distinct values (~0.63 per row on a uniform
-// ring), computes both windows once per distinct root into LDS (30 words),
-// and writes the 2 x 256 entries as coalesced 16-B chunks assembled from LDS
-// (whole lines per store instruction, no staging copy).  Bit-identical to
-// k_cz_build (route_table_hash, tests/test_gpu_parity.py); dispatch order
-// is k_cz_build's K-row-block chunks over all levels.
-constexpr int CZR_W = 31;  // LDS words per root: W0[1..15], W1[0..14], CZ_NONE count
-// SPLIT: the two planes leave one after the other through one 16-word window
-// buffer (W0 first, W1 held in registers meanwhile): 21 instead of 37 KB of
-// LDS per block, so more blocks fit per CU when the VGPR budget (WPE waves
-// per SIMD) allows them.  The build is bound by the rows in flight per CU:
-// 4 -> 3 -> 2 resident blocks take 27.4 -> 31.0 -> 41.4 ms at 2^24
-// (profiles/r03/build_lat/).
-template <int SPLIT, int WPE, bool SLICE = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_cz_build_roots(FingerView fv, const cell128 *ring, const uint64_t *rh, uint32_t n,
-                      int lvl_base, int nlev, uint32_t p_first, uint32_t M, int gs, uint4 *cz,
-                      uint32_t *esc, uint32_t K, int mode, int a1_rows, int late_e0) {
-    // SLICE: gap codes from 32-bit ID slices (fv.rs, cz_encode_s) instead of
-    // the 64-bit high words (rh, cz_encode_hi)
-    // gathers as a wave-uniform plane base plus a 32-bit byte offset (x < n <
-    // 2^30): the scalar-base form of the load, one VGPR of address per gather
-    // instead of a 64-bit pointer
-    auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
-        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
-    };
-    using HT = typename std::conditional<SLICE, uint32_t, uint64_t>::type;
-    auto hiw = [&](uint32_t x) -> HT {
-        if constexpr (SLICE) return ld32(fv.rs, x);
-        else return rh[x];
-    };
-    auto enc = [&](uint32_t par, HT hpar, int l, uint32_t x, HT hx) -> uint32_t {
-        if constexpr (SLICE) return cz_encode_s(n, gs, par, hpar, l, x, hx, ring);
-        else return cz_encode_hi(n, gs, par, hpar, l, x, hx, ring);
-    };
-    constexpr int WS = SPLIT ? 16 : CZR_W;  // LDS words per root
-    constexpr int WC = SPLIT ? 15 : 30;     // the root's CZ_NONE count
-    __shared__ uint32_t win[256 * WS];
-    __shared__ uint32_t e0s[256];
-    __shared__ uint32_t roots[256];
-    __shared__ uint32_t roots_a1[256];  // A' = f(R, i - 1) = C2(p, i) of the root's first row
-    // rh[R] per root (high words); the slice build gathers rs[R] again instead
-    // (one more independent load beside a window's first ones), which keeps its
-    // LDS at 20 KB: 8 blocks per CU
-    __shared__ HT roots_h[SLICE ? 1 : 256];
-    __shared__ uint16_t ridx[256];
-    __shared__ uint32_t wcnt[4];
-    uint32_t lvl, lb;
-    {
-        const uint32_t B = blockIdx.x;
-        const uint32_t chunk = B / (K * (uint32_t)nlev), rem = B - chunk * K * (uint32_t)nlev;
-        lvl = rem / K;
-        const uint32_t sub = rem - lvl * K;
-        lb = chunk * K + (sub & 7) * (K >> 3) + (sub >> 3);
-    }
-    const int i = lvl_base + (int)lvl;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t j0 = lb * 256u;
-    const uint32_t rows = M > j0 ? (M - j0 < 256u ? M - j0 : 256u) : 0u;
-    if (rows == 0) return;  // block-uniform
-    // mode (A/B probes, CX_CZ_ROOTS_MODE; 0 = the build): 1 compute only, 2
-    // stores only (LDS contents unspecified), 3 = even blocks compute only, odd
-    // blocks store only (do the two halves overlap when different waves run them?)
-    const bool do_compute = mode == 0 || mode == 1 || (mode == 3 && !(lb & 1));
-    const bool do_store = mode == 0 || mode == 2 || (mode == 3 && (lb & 1));
-    auto fat = [&](uint32_t x, int l) -> uint32_t {
-        return ld32(fv.F + (size_t)(l - fv.L) * fv.sl, x);
-    };
-    auto c2 = [&](uint32_t x, int l) -> uint32_t {
-        return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
-    };
-    // a finger outside the ring (never from a converged build; reported, never
-    // followed): a wave-uniform flag (scalar), not a per-lane register
-    bool oob = false;
-    auto chk = [&](uint32_t x) -> uint32_t {
-        if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
-        return x < n ? x : 0u;
-    };
-    // W1 of root slot tt: A' = f(R, i - 1) relative to R (slot 0), the window
-    // below A' (1..14), into o (SPLIT) or wr[15..29]; returns its CZ_NONE count
-    auto w1_window = [&](uint32_t tt, uint32_t R, HT hR, uint32_t *o,
-                         uint32_t *wr) -> uint32_t {
-            uint32_t wbad = 0;
-            {
-                uint32_t nd[15];
-                nd[0] = a1_rows ? roots_a1[tt] : chk(fat(R, i - 1));
-                nd[1] = chk(fat(nd[0], i - 2));
-                nd[2] = chk(fat(nd[0], i - 3));
-                nd[3] = chk(c2(nd[0], i - 2));
-                nd[4] = chk(fat(nd[0], i - 4));
-                nd[6] = chk(c2(nd[0], i - 3));
-                nd[8] = chk(fat(nd[0], i - 5));
-                nd[12] = chk(c2(nd[0], i - 4));
-                nd[5] = chk(fat(nd[1], i - 4));
-                nd[7] = chk(fat(nd[3], i - 4));
-                nd[9] = chk(fat(nd[1], i - 5));
-                nd[10] = chk(fat(nd[2], i - 5));
-                nd[11] = chk(fat(nd[3], i - 5));
-                nd[13] = chk(c2(nd[1], i - 4));
-                nd[14] = chk(c2(nd[2], i - 4));
-                HT hv[15];
-#pragma unroll
-                for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
-                const uint32_t o0 = enc(R, hR, i - 1, nd[0], hv[0]);
-                wbad += o0 == CZ_NONE;
-                if (SPLIT)
-                    o[0] = o0;
-                else
-                    wr[15] = o0;
-#pragma unroll
-                for (int v = 1; v < 15; ++v) {
-                    const int hb = 31 - __builtin_clz((unsigned)v);
-                    const int pv = v & ~(1 << hb);
-                    const uint32_t ow = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
-                    wbad += ow == CZ_NONE;
-                    if (SPLIT)
-                        o[v] = ow;
-                    else
-                        wr[15 + v] = ow;
-                }
-            }
-            return wbad;
-    };
-    // ---- rows: root and the row's own word ----
-    const bool valid = (uint32_t)t < rows;
-    uint32_t A = 0xFFFFFFFFu, A1 = 0, p = 0;
-    HT hA = 0, hp = 0;
-    uint32_t bad = 0, nroots = 0;
-    uint32_t o1[SPLIT ? 15 : 1];  // SPLIT: the W1 words until plane 0 has left
-    if (!do_compute) {
-        if (valid) ridx[t] = 0;
-        __syncthreads();
-    } else {
-        if (valid) {
-            uint64_t pw = (uint64_t)p_first + j0 + t;
-            if (pw >= n) pw -= n;
-            p = (uint32_t)pw;
-            A = chk(fat(p, i));
-            // A' of the b = 1 entry from the row's two-hop plane: one gather beside
-            // A instead of one after it (a1_rows = 0: from A, for A/B)
-            if (a1_rows) A1 = chk(c2(p, i));
-            hp = hiw(p);
-            if (!late_e0) {
-                // late_e0: rh[A] is gathered once per distinct root in the window
-                // phase, beside its first window gathers, and the row's own word is
-                // encoded after it (one dependent gather less per block)
-                hA = hiw(A);
-                const uint32_t e0 = enc(p, hp, i, A, hA);
-                e0s[t] = e0;
-                bad += 2 * (e0 == CZ_NONE);  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
-            }
-        }
-        roots[t] = A;  // staged for the neighbour compare
-        __syncthreads();
-        const bool first = valid && (t == 0 || roots[t - 1] != A);
-        const uint64_t fm = __ballot(first);
-        if (lane == 0) wcnt[wv] = (uint32_t)__popcll(fm);
-        __syncthreads();
-        uint32_t base = 0, nr = 0;
-        for (int w = 0; w < 4; ++w) {
-            base += w < wv ? wcnt[w] : 0u;
-            nr += wcnt[w];
-        }
-        const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-        const uint32_t incl = rank + (first ? 1u : 0u);  // distinct roots up to and including t
-        __syncthreads();  // every lane has read roots[t - 1]
-        if (first) {
-        roots[rank] = A;
-        roots_a1[rank] = A1;
-        if (!SLICE) roots_h[rank] = hA;
-    }
-        if (valid) ridx[t] = (uint16_t)(incl - 1);
-        __syncthreads();
-        // ---- windows of the distinct roots (lanes 0 .. nr-1) ----
-        nroots = nr;
-        if ((uint32_t)t < nr) {
-            const uint32_t R = roots[t];
-            const HT hR = (SLICE || late_e0) ? hiw(R) : roots_h[t];
-            if (!SLICE && late_e0) roots_h[t] = hR;
-            uint32_t *wr = win + t * WS;
-            uint32_t wbad = 0;
-            // W0: the window below R (b = 0 entry, slots 1..15; nd[0] = R)
-            {
-                uint32_t nd[16];
-                nd[0] = R;
-                nd[1] = chk(fat(R, i - 2));
-                nd[2] = chk(fat(R, i - 3));
-                nd[3] = chk(c2(R, i - 2));
-                nd[4] = chk(fat(R, i - 4));
-                nd[6] = chk(c2(R, i - 3));
-                nd[8] = chk(fat(R, i - 5));
-                nd[12] = chk(c2(R, i - 4));
-                nd[5] = chk(fat(nd[1], i - 4));
-                nd[7] = chk(fat(nd[3], i - 4));
-                nd[9] = chk(fat(nd[1], i - 5));
-                nd[10] = chk(fat(nd[2], i - 5));
-                nd[11] = chk(fat(nd[3], i - 5));
-                nd[13] = chk(c2(nd[1], i - 4));
-                nd[14] = chk(c2(nd[2], i - 4));
-                nd[15] = chk(c2(nd[3], i - 4));
-                HT hv[16];
-                hv[0] = hR;
-#pragma unroll
-                for (int v = 1; v < 16; ++v) hv[v] = hiw(nd[v]);
-#pragma unroll
-                for (int v = 1; v < 16; ++v) {
-                    const int hb = 31 - __builtin_clz((unsigned)v);
-                    const int pv = v & ~(1 << hb);
-                    const uint32_t o = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
-                    wbad += o == CZ_NONE;
-                    wr[v - 1] = o;
-                }
-            }
-            // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
-            if (SPLIT != 2) wbad += w1_window(t, R, hR, o1, wr);
-            wr[WC] = wbad;
-        }
-        __syncthreads();
-        if (valid) {
-            const uint32_t rx = ridx[t];
-            bad += win[rx * WS + WC];
-            if (late_e0) {
-                const uint32_t e0 = enc(p, hp, i, A, SLICE ? hiw(A) : roots_h[rx]);
-                e0s[t] = e0;
-                bad += 2 * (e0 == CZ_NONE);
-            }
-        }
-        if (late_e0) __syncthreads();
-    }  // do_compute
-    // ---- stores: 2 planes x rows entries x 4 chunks of 16 B, assembled from LDS ----
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const size_t t0 = (size_t)(2 * lvl) * M + j0;
-    // chunk c: plane c >> 10, entry (c >> 2) & 255, 16-B quarter c & 3
-    auto store_chunk = [&](uint32_t c) {
-        const uint32_t pl = c >> 10, cc = c & 1023u, e = cc >> 2, qq = cc & 3u;
-        if (e >= rows) return;
-        const uint32_t *wr = win + ridx[e] * WS;
-        uint32_t w[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t word = qq * 4u + (uint32_t)u;
-            if (pl == 0)
-                w[u] = word == 0 ? e0s[e] : wr[word - 1];
-            else
-                w[u] = word == 15 ? e0s[e] : wr[(SPLIT ? 0 : 15) + word];
-        }
-        const v4u wv4 = {w[0], w[1], w[2], w[3]};
-        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (t0 + (size_t)pl * M + e) * 4) + qq);
-    };
-    if (!SPLIT) {
-        for (uint32_t c = t; do_store && c < 2u * 256u * 4u; c += 256u) store_chunk(c);
-    } else {
-        for (uint32_t c = t; do_store && c < 1024u; c += 256u) store_chunk(c);
-        if (do_compute) {
-            __syncthreads();  // plane 0 has read every W0 word
-            if (SPLIT == 2) {
-                // W1 only now: the window phase held one window per lane (fewer
-                // live registers), at the price of a second dependent chain
-                if ((uint32_t)t < nroots)
-                    win[t * WS + WC] = w1_window(t, roots[t], SLICE ? hiw(roots[t]) : roots_h[t],
-                                                 win + t * WS, nullptr);
-                __syncthreads();
-                if (valid) bad += win[ridx[t] * WS + WC];
-            } else if ((uint32_t)t < nroots) {
-#pragma unroll
-                for (int v = 0; v < (SPLIT ? 15 : 1); ++v) win[t * WS + v] = o1[v];
-            }
-            __syncthreads();
-        }
-        for (uint32_t c = 1024u + t; do_store && c < 2048u; c += 256u) store_chunk(c);
-    }
-    if (oob) atomicOr(esc + 1, 1u);
-    if (bad) atomicAdd(esc, bad);
-}
-
-// Root-centric build with blocks sized by distinct roots (table_build 0,
-// default since round 4; k_cz_build_roots above is table_build 4).  A block of
-// k_cz_build_roots takes 256 rows and computes one window per distinct root,
-// one lane each: on a uniform ring about half the rows of a level above the
-// mean gap share their root with the row before (the fingers of 256 adjacent
-// peers land on ~128 distinct peers), so half the lanes idle through the
-// window phase -- the dependent-gather chain that bounds the build.  Here a
-// block takes up to CZ2_RMAX rows, sized per level (host: cz2_plan) so that
-// its distinct roots come to ~90 % of the 256 lanes; the row phase runs two
-// rows per lane.  A block whose rows have more than 256 distinct roots (rare
-// on a uniform ring, frequent on a clustered one) writes the rows of its
-// first 256 roots and appends the rest (< 256 rows, so < 256 roots) to an
+// fifteen words of each are a function of (A, i): W0(A, i) = the window below
+// A over levels i-2..i-5 (slots 1..15), W1(A, i) = A' = f(A, i-1) relative to
+// A (slot 0) and the window below A' (slots 1..14).  A block takes up to
+// CZ2_RMAX consecutive rows of one level (both planes), sized per level (host:
+// cz2_plan) so that their distinct roots come to ~90 % of its 256 lanes: the
+// rows' roots are non-decreasing along the ring (f(., i) is monotone up to one
+// wrap), so the block compacts them to their distinct values (~0.5-0.97 per
+// row by level on a uniform ring), computes both windows once per distinct
+// root, one lane each, and writes the rows' entries as coalesced 16-B chunks
+// assembled from LDS (whole lines per store instruction).  The row phase runs
+// two rows per lane.  A block whose rows have more than 256 distinct roots
+// (rare on a uniform ring, frequent on a clustered one) writes the rows of
+// its first 256 roots and appends the rest (< 256 rows, so < 256 roots) to an
 // overflow list that a second launch of the same kernel finishes.  LDS stays
-// under 20 KB (8 blocks per CU): the windows' buffer also stages the rows'
-// roots before the window phase, and each window's word 0 (slot 0 of the b = 0
-// entry is the row's own word) carries its root into the W1 phase, with the
-// window's CZ_NONE count in the spare top bits; the stores assemble each 16-B
-// chunk with one LDS read.
-// Same table, bit for bit (route_table_hash against every other build).
+// under 20 KB: the windows' buffer also stages the rows' roots before the
+// window phase, and each window's word 0 (slot 0 of the b = 0 entry is the
+// row's own word) carries its root into the W1 phase, with the window's
+// CZ_NONE count in the spare top bits.  Dispatch: chunks of CZ2_CHUNK rows x
+// all levels, a level's blocks spread over the XCDs.
+// Same table, bit for bit, as k_cz_build (route_table_hash, tests/test_gpu_parity.py).
 constexpr int CZ2_RMAX = 464;
-constexpr double CZ3_TARGET = 115.0;  // k_cz_build_roots3: roots per block (of 128)
 constexpr uint32_t CZ2_CHUNK = 4096;  // rows of a dispatch chunk (all levels)
 
 // Blocks per level per chunk: level l's bucket is clamp(floor(l - gl) + 6, 0,
@@ -3243,24 +2041,13 @@ __device__ __forceinline__ uint32_t cz2_nb(int l, int gl256, uint64_t nbt) {
 // items == nullptr: the main launch (blocks from the plan); else block b
 // takes overflow item b = {first row j, level | rows << 8}.  Either appends
 // its own overflow to ovf.
-// LAY: 0 = 4-B planes + ID slices gathered apart, 1 = pair planes, 2 = quad
-// planes (fingers_pairs2 / fingers_quads)
-// SL (table_build 9, A/B): plane 0 leaves after the W1 gathers instead of
-// before them.  A wave's loads and stores share one in-order vmcnt queue, so
-// with SL false every W1 gather also waits for the plane-0 stores' acks; with
-// SL the W1 words wait in registers (16) while plane 0 drains from LDS.
-template <int WPE, int LAY, bool SL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+// 66 VGPRs: 7 waves per SIMD (8 forced spills and measured slower,
+// profiles/r04/build_modes/wpe_ab).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7)))
 void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
                        uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
                        int gl256, uint64_t nbt, const uint2 *items, uint32_t *ovf_cnt,
-                       uint2 *ovf, uint32_t cap, int mode) {
-    // mode (A/B probes, CX_CZ2_MODE; 0 = the build): 1 = compute only (no
-    // table stores), 2 = stores only (no window gathers; the words stored are
-    // whatever LDS holds), 3 = stores only without the row gathers (every two
-    // rows share a dummy root); + 16: every store lands in the table's first
-    // 128 MiB (the write stream stays on chip); + 32: streaming (non-temporal)
-    // table stores instead of write-back ones (1.6 % slower, profiles/r04/store_ab)
+                       uint2 *ovf, uint32_t cap) {
     auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
         return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
     };
@@ -3279,10 +2066,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     __shared__ uint32_t wcnt[8];
     __shared__ uint32_t sbad;    // CZ_NONE words written by the block (rare)
     __shared__ uint32_t anybad;  // some window of the block holds one
-    // pair / quad planes: the slices of each window's root and of its A1, kept for W1
-    __shared__ uint32_t rsR[(LAY != 0) ? 256 : 1], ra1s[(LAY != 0) ? 256 : 1];
     uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
-    uint32_t *stS = win + 2 * CZ2_RMAX, *stS1 = win + 3 * CZ2_RMAX;  // pair / quad planes: their slices
     uint32_t j0, rows;
     int lvl;
     if (items) {
@@ -3305,7 +2089,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
             nbl = cz2_nb(lvl_base + lvl, gl256, nbt);
         }
         const uint32_t xm = nbl >> 3, xr = nbl & 7, xx = rem & 7;
-        const uint32_t lbl = (mode & 8) ? rem : xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
+        const uint32_t lbl = xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
         const uint32_t RB = (CZ2_CHUNK + nbl - 1) / nbl;
         const uint32_t c0 = lbl * RB;
         if (c0 >= CZ2_CHUNK) return;  // block-uniform
@@ -3329,28 +2113,6 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     auto c2 = [&](uint32_t x, int l) -> uint32_t {
         return ld32nt(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
     };
-    // pair planes: {finger, its ID slice} in one 8-B gather (uniform plane base plus a
-    // 32-bit byte offset, x < n < 2^29)
-    auto ld64 = [](const uint2 *base, uint32_t x) -> uint2 {
-        return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + x * 8u);
-    };
-    // LAY 2 (quads): {F, rs[F], C2, rs[C2]} of (l, x) in 16 B; its halves
-    // alone as 8-B loads where the window needs only one child
-    auto ldq = [&](uint32_t x, int l) -> uint4 {
-        return *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(fv.Q + (size_t)(l - fv.L) * n) + x * 16u);
-    };
-    auto fatp = [&](uint32_t x, int l) -> uint2 {
-        if constexpr (LAY == 2)
-            return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(fv.Q + (size_t)(l - fv.L) * n) + x * 16u);
-        else
-            return ld64(fv.P + (size_t)(l - fv.L) * n, x);
-    };
-    auto c2p = [&](uint32_t x, int l) -> uint2 {
-        if constexpr (LAY == 2)
-            return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(fv.Q + (size_t)(l - fv.L) * n) + x * 16u + 8u);
-        else
-            return ld64(fv.P2 + (size_t)(l - fv.L - 1) * n, x);
-    };
     bool oob = false;
     auto chk = [&](uint32_t x) -> uint32_t {
         if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
@@ -3364,44 +2126,20 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const uint32_t r = (uint32_t)t + 256u * k;
-        if (r < rows && (mode & 3) == 3) {
-            stA[r] = r >> 1;
-            stA1[r] = 0;
-        } else if (r < rows) {
+        if (r < rows) {
             uint64_t pw = (uint64_t)p_first + j0 + r;
             if (pw >= n) pw -= n;
             const uint32_t p = (uint32_t)pw;
-            uint32_t A, A1, sA;
-            if constexpr (LAY == 2) {
-                const uint4 q = ldq(p, i);
-                A = chk(q.x);
-                A1 = chk(q.z);
-                sA = q.y;
-                stS[r] = q.y;
-                stS1[r] = q.w;
-            } else if constexpr (LAY == 1) {
-                const uint2 a = fatp(p, i), a1 = c2p(p, i);
-                A = chk(a.x);
-                A1 = chk(a1.x);
-                sA = a.y;
-                stS[r] = a.y;
-                stS1[r] = a1.y;
-            } else {
-                A = chk(fat(p, i));
-                A1 = chk(c2(p, i));
-                sA = hiw(A);
-            }
-            const uint32_t e0 = enc(p, hiw(p), i, A, sA);
-            e0s[r] = e0;
-            // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
-            if (e0 == CZ_NONE) atomicAdd(&sbad, 2u);
+            const uint32_t A = chk(fat(p, i)), A1 = chk(c2(p, i));
+            const uint32_t e0 = enc(p, hiw(p), i, A, hiw(A));
+            e0s[r] = e0;  // slot 0 of (p, i, 0) and slot 15 of (p, i, 1)
             stA[r] = A;
             stA1[r] = A1;
         }
     }
     __syncthreads();
     // distinct roots in row order: ballot per (row half, wave), eight counts
-    uint32_t A[2], A1[2], S[2], S1[2];
+    uint32_t A[2], A1[2];
     bool first[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -3409,10 +2147,6 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         const bool v = r < rows;
         A[k] = v ? stA[r] : 0u;
         A1[k] = v ? stA1[r] : 0u;
-        if constexpr (LAY != 0) {
-            S[k] = v ? stS[r] : 0u;
-            S1[k] = v ? stS1[r] : 0u;
-        }
         first[k] = v && (r == 0 || stA[r - 1] != A[k]);
     }
     const uint64_t fm0 = __ballot(first[0]), fm1 = __ballot(first[1]);
@@ -3436,18 +2170,10 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     if (first[0]) {
         stA[rk0] = A[0];
         stA1[rk0] = A1[0];
-        if constexpr (LAY != 0) {
-            stS[rk0] = S[0];
-            stS1[rk0] = S1[0];
-        }
     }
     if (first[1]) {
         stA[rk1] = A[1];
         stA1[rk1] = A1[1];
-        if constexpr (LAY != 0) {
-            stS[rk1] = S[1];
-            stS1[rk1] = S1[1];
-        }
     }
     if ((uint32_t)t < rows) ridx[t] = (uint16_t)(rk0 + first[0] - 1);
     if ((uint32_t)t + 256u < rows) ridx[t + 256] = (uint16_t)(rk1 + first[1] - 1);
@@ -3467,15 +2193,18 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         nr = cap;
         if (t == 0) ovf[atomicAdd(ovf_cnt, 1u)] = make_uint2(j0 + rhi, (uint32_t)lvl | (rows - rhi) << 8);
     }
-    const bool wl = (uint32_t)t < nr && (mode & 3) < 2;
-    uint32_t R = 0, RA1 = 0, SR = 0, SRA1 = 0;
+    // the row's own word, for the rows this block writes (a deferred row is
+    // counted by the overflow launch that writes it)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t r = (uint32_t)t + 256u * k;
+        if (r < rhi && e0s[r] == CZ_NONE) atomicAdd(&sbad, 2u);
+    }
+    const bool wl = (uint32_t)t < nr;
+    uint32_t R = 0, RA1 = 0;
     if (wl) {
         R = stA[t];
         RA1 = stA1[t];
-        if constexpr (LAY != 0) {
-            SR = stS[t];
-            SRA1 = stS1[t];
-        }
     }
     __syncthreads();  // the staged roots are read before win is written
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -3487,58 +2216,7 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         uint32_t wbad = 0;
         uint32_t nd[16], hv[16];
         nd[0] = R;
-        if constexpr (LAY != 0) {
-            rsR[t] = SR;
-            ra1s[t] = SRA1;
-            hv[0] = SR;
-            uint2 q[16];
-            if constexpr (LAY == 2) {
-                const uint4 a = ldq(R, i - 2), b = ldq(R, i - 3), c = ldq(R, i - 4);
-                q[1] = make_uint2(a.x, a.y);
-                q[3] = make_uint2(a.z, a.w);
-                q[2] = make_uint2(b.x, b.y);
-                q[6] = make_uint2(b.z, b.w);
-                q[4] = make_uint2(c.x, c.y);
-                q[12] = make_uint2(c.z, c.w);
-                q[8] = fatp(R, i - 5);
-                nd[1] = chk(q[1].x);
-                nd[2] = chk(q[2].x);
-                nd[3] = chk(q[3].x);
-                const uint4 e = ldq(nd[1], i - 4), f = ldq(nd[3], i - 4);
-                q[5] = make_uint2(e.x, e.y);
-                q[13] = make_uint2(e.z, e.w);
-                q[7] = make_uint2(f.x, f.y);
-                q[15] = make_uint2(f.z, f.w);
-                q[9] = fatp(nd[1], i - 5);
-                q[10] = fatp(nd[2], i - 5);
-                q[11] = fatp(nd[3], i - 5);
-                q[14] = c2p(nd[2], i - 4);
-            } else {
-            q[1] = fatp(R, i - 2);
-            q[2] = fatp(R, i - 3);
-            q[3] = c2p(R, i - 2);
-            q[4] = fatp(R, i - 4);
-            q[6] = c2p(R, i - 3);
-            q[8] = fatp(R, i - 5);
-            q[12] = c2p(R, i - 4);
-            nd[1] = chk(q[1].x);
-            nd[2] = chk(q[2].x);
-            nd[3] = chk(q[3].x);
-            q[5] = fatp(nd[1], i - 4);
-            q[7] = fatp(nd[3], i - 4);
-            q[9] = fatp(nd[1], i - 5);
-            q[10] = fatp(nd[2], i - 5);
-            q[11] = fatp(nd[3], i - 5);
-            q[13] = c2p(nd[1], i - 4);
-            q[14] = c2p(nd[2], i - 4);
-            q[15] = c2p(nd[3], i - 4);
-            }
-#pragma unroll
-            for (int v = 1; v < 16; ++v) {
-                nd[v] = chk(q[v].x);
-                hv[v] = q[v].y;
-            }
-        } else {
+        {
             nd[1] = chk(fat(R, i - 2));
             nd[2] = chk(fat(R, i - 3));
             nd[3] = chk(c2(R, i - 2));
@@ -3598,80 +2276,27 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     }
     // plane 0: rows [0, rhi) x 4 chunks of 16 B, whole lines per store
     auto plane0 = [&]() {
-        for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
+        for (uint32_t c = t; c < 4u * rhi; c += 256u) {
             const uint32_t e = c >> 2, qq = c & 3u;
             // one 16-B LDS read per chunk (the window's words sit at their
             // slots; a lane pair of entries covers 32 banks): slot 0 is the
             // row's own word
             uint4 u = *reinterpret_cast<const uint4 *>(win + ridx[e] * 16 + qq * 4);
             if (qq == 0) u.x = e0s[e];
-            if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
             const v4u wv4 = {u.x, u.y, u.z, u.w};
-            const size_t ent0 = (mode & 16) ? ((tp0 + e) & ((1u << 21) - 1)) : tp0 + e;
-            if (mode & 32) __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent0 * 4) + qq);
-            else reinterpret_cast<v4u *>(cz + ent0 * 4)[qq] = wv4;  // write-back (faster here)
+            // write-back stores (faster than streaming ones here, profiles/r04/store_ab)
+            reinterpret_cast<v4u *>(cz + (tp0 + e) * 4)[qq] = wv4;
         }
     };
-    if constexpr (!SL) {
-        plane0();
-        __syncthreads();  // plane 0 has read every W0 word
-    }
-    uint4 o1[4];  // SL: the W1 words until plane 0 has left
+    plane0();
+    __syncthreads();  // plane 0 has read every W0 word
     // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
     if (wl) {
         uint32_t wbad = 0;
         uint32_t nd[15], hv[15];
         uint32_t hR;
         nd[0] = ra1[t] & 0x3FFFFFFFu;
-        if constexpr (LAY != 0) {
-            hR = rsR[t];
-            hv[0] = ra1s[t];
-            uint2 q[15];
-            if constexpr (LAY == 2) {
-                const uint4 a = ldq(nd[0], i - 2), b = ldq(nd[0], i - 3), c = ldq(nd[0], i - 4);
-                q[1] = make_uint2(a.x, a.y);
-                q[3] = make_uint2(a.z, a.w);
-                q[2] = make_uint2(b.x, b.y);
-                q[6] = make_uint2(b.z, b.w);
-                q[4] = make_uint2(c.x, c.y);
-                q[12] = make_uint2(c.z, c.w);
-                q[8] = fatp(nd[0], i - 5);
-                nd[1] = chk(q[1].x);
-                nd[2] = chk(q[2].x);
-                nd[3] = chk(q[3].x);
-                const uint4 e = ldq(nd[1], i - 4);
-                q[5] = make_uint2(e.x, e.y);
-                q[13] = make_uint2(e.z, e.w);
-                q[7] = fatp(nd[3], i - 4);
-                q[9] = fatp(nd[1], i - 5);
-                q[10] = fatp(nd[2], i - 5);
-                q[11] = fatp(nd[3], i - 5);
-                q[14] = c2p(nd[2], i - 4);
-            } else {
-            q[1] = fatp(nd[0], i - 2);
-            q[2] = fatp(nd[0], i - 3);
-            q[3] = c2p(nd[0], i - 2);
-            q[4] = fatp(nd[0], i - 4);
-            q[6] = c2p(nd[0], i - 3);
-            q[8] = fatp(nd[0], i - 5);
-            q[12] = c2p(nd[0], i - 4);
-            nd[1] = chk(q[1].x);
-            nd[2] = chk(q[2].x);
-            nd[3] = chk(q[3].x);
-            q[5] = fatp(nd[1], i - 4);
-            q[7] = fatp(nd[3], i - 4);
-            q[9] = fatp(nd[1], i - 5);
-            q[10] = fatp(nd[2], i - 5);
-            q[11] = fatp(nd[3], i - 5);
-            q[13] = c2p(nd[1], i - 4);
-            q[14] = c2p(nd[2], i - 4);
-            }
-#pragma unroll
-            for (int v = 1; v < 15; ++v) {
-                nd[v] = chk(q[v].x);
-                hv[v] = q[v].y;
-            }
-        } else {
+        {
             hR = hiw(wr[0] & 0x3FFFFFFFu);  // the root itself is re-read below
             nd[1] = chk(fat(nd[0], i - 2));
             nd[2] = chk(fat(nd[0], i - 3));
@@ -3711,19 +2336,9 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
                 }
                 wbad += ov[u] == CZ_NONE;
             }
-            if constexpr (SL) o1[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-            else w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
         }
         if (wbad) anybad = 1;
-    }
-    if constexpr (SL) {
-        plane0();
-        __syncthreads();  // plane 0 has read every W0 word
-        if (wl) {
-            uint4 *w4 = reinterpret_cast<uint4 *>(wr);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) w4[g] = o1[g];
-        }
     }
     __syncthreads();
 #pragma unroll
@@ -3735,290 +2350,12 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
         }
     }
     // plane 1: word 15 = the row's own word
-    for (uint32_t c = t; (mode & 3) != 1 && c < 4u * rhi; c += 256u) {
+    for (uint32_t c = t; c < 4u * rhi; c += 256u) {
         const uint32_t e = c >> 2, qq = c & 3u;
         uint4 u = *reinterpret_cast<const uint4 *>(win + ridx[e] * 16 + qq * 4);
         if (qq == 3) u.w = e0s[e];  // slot 15 is the row's own word
-        if (mode & 4) u = make_uint4(qq * 4, qq * 4 + 1, qq * 4 + 2, qq * 4 + 3);
         const v4u wv4 = {u.x, u.y, u.z, u.w};
-        const size_t ent1 = (mode & 16) ? ((tp0 + M + e) & ((1u << 21) - 1)) : tp0 + M + e;
-        if (mode & 32) __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + ent1 * 4) + qq);
-        else reinterpret_cast<v4u *>(cz + ent1 * 4)[qq] = wv4;
-    }
-    if (oob) atomicOr(esc + 1, 1u);
-    __syncthreads();
-    if (t == 0 && sbad) atomicAdd(esc, sbad);
-}
-
-// Both windows of a root at once, stores last (table_build 8, A/B): a block
-// takes up to 128 distinct roots (its rows sized per level as in
-// k_cz_build_roots2, for 115 roots), lanes 0..127 compute W0 of root t and
-// lanes 128..255 W1 of root t - 128 (waves 0-1 and 2-3: no divergence), and
-// both planes leave after the window phase.  A wave's loads and stores share
-// one in-order vmcnt queue, so in k_cz_build_roots2 the W1 gathers wait
-// behind the plane-0 stores (the build's halves add: compute 12.8 + stores
-// 9.7 ms, profiles/r04/build_writes/); here no wave issues a gather after a
-// store, and a block's dependent chain is one window instead of two.
-template <int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-void k_cz_build_roots3(FingerView fv, const cell128 *ring, uint32_t n, int lvl_base, int nlev,
-                       uint32_t p_first, uint32_t M, int gs, uint4 *cz, uint32_t *esc,
-                       int gl256, uint64_t nbt, const uint2 *items, uint32_t *ovf_cnt,
-                       uint2 *ovf, uint32_t cap) {
-    auto ld32 = [](const uint32_t *base, uint32_t x) -> uint32_t {
-        return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
-    };
-    auto hiw = [&](uint32_t x) -> uint32_t { return ld32(fv.rs, x); };
-    auto enc = [&](uint32_t par, uint32_t hpar, int l, uint32_t x, uint32_t hx) -> uint32_t {
-        return cz_encode_s(n, gs, par, hpar, l, x, hx, ring);
-    };
-    // win: W0 windows of roots 0..127 (the row's own word slot holds the
-    // window's CZ_NONE count), then W1 windows (slot 15 holds it); before the
-    // window phase its first 2 x CZ2_RMAX words stage the rows' roots / A1
-    __shared__ uint32_t win[256 * 16];
-    __shared__ uint32_t e0s[CZ2_RMAX];
-    __shared__ uint16_t ridx[CZ2_RMAX];
-    __shared__ uint32_t wcnt[8];
-    __shared__ uint32_t sbad, anybad;
-    uint32_t *stA = win, *stA1 = win + CZ2_RMAX;
-    uint32_t j0, rows;
-    int lvl;
-    if (items) {
-        const uint2 it = items[blockIdx.x];
-        j0 = it.x;
-        lvl = (int)(it.y & 0xFFu);
-        rows = it.y >> 8;
-    } else {
-        uint32_t TB = 0;
-        for (int l = 0; l < nlev; ++l) TB += cz2_nb(lvl_base + l, gl256, nbt);
-        const uint32_t chunk = blockIdx.x / TB;
-        uint32_t rem = blockIdx.x - chunk * TB;
-        lvl = 0;
-        uint32_t nbl = cz2_nb(lvl_base, gl256, nbt);
-        while (rem >= nbl) {
-            rem -= nbl;
-            ++lvl;
-            nbl = cz2_nb(lvl_base + lvl, gl256, nbt);
-        }
-        const uint32_t xm = nbl >> 3, xr = nbl & 7, xx = rem & 7;
-        const uint32_t lbl = xx * xm + (xx < xr ? xx : xr) + (rem >> 3);
-        const uint32_t RB = (CZ2_CHUNK + nbl - 1) / nbl;
-        const uint32_t c0 = lbl * RB;
-        if (c0 >= CZ2_CHUNK) return;  // block-uniform
-        j0 = chunk * CZ2_CHUNK + c0;
-        if (j0 >= M) return;
-        rows = CZ2_CHUNK - c0 < RB ? CZ2_CHUNK - c0 : RB;
-        if (M - j0 < rows) rows = M - j0;
-    }
-    const int i = lvl_base + lvl;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    auto fat = [&](uint32_t x, int l) -> uint32_t {
-        return ld32(fv.F + (size_t)(l - fv.L) * fv.sl, x);
-    };
-    auto c2 = [&](uint32_t x, int l) -> uint32_t {
-        return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
-    };
-    bool oob = false;
-    auto chk = [&](uint32_t x) -> uint32_t {
-        if (__builtin_amdgcn_ballot_w64(x >= n)) oob = true;
-        return x < n ? x : 0u;
-    };
-    if (t == 0) {
-        sbad = 0;
-        anybad = 0;
-    }
-    // ---- rows (two per lane): roots, two-hop roots, the row's own word ----
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t r = (uint32_t)t + 256u * k;
-        if (r < rows) {
-            uint64_t pw = (uint64_t)p_first + j0 + r;
-            if (pw >= n) pw -= n;
-            const uint32_t p = (uint32_t)pw;
-            const uint32_t A = chk(fat(p, i));
-            const uint32_t A1 = chk(c2(p, i));
-            const uint32_t e0 = enc(p, hiw(p), i, A, hiw(A));
-            e0s[r] = e0;
-            if (e0 == CZ_NONE) atomicAdd(&sbad, 2u);
-            stA[r] = A;
-            stA1[r] = A1;
-        }
-    }
-    __syncthreads();
-    uint32_t A[2], A1[2];
-    bool first[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t r = (uint32_t)t + 256u * k;
-        const bool v = r < rows;
-        A[k] = v ? stA[r] : 0u;
-        A1[k] = v ? stA1[r] : 0u;
-        first[k] = v && (r == 0 || stA[r - 1] != A[k]);
-    }
-    const uint64_t fm0 = __ballot(first[0]), fm1 = __ballot(first[1]);
-    if (lane == 0) {
-        wcnt[wv] = (uint32_t)__popcll(fm0);
-        wcnt[4 + wv] = (uint32_t)__popcll(fm1);
-    }
-    __syncthreads();
-    uint32_t nr = 0, b0 = 0, b1 = 0;
-    for (int w = 0; w < 8; ++w) {
-        const uint32_t c = wcnt[w];
-        b0 += w < wv ? c : 0u;
-        b1 += w < 4 + wv ? c : 0u;
-        nr += c;
-    }
-    const uint32_t rk0 = b0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm0 >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)fm0, 0u));
-    const uint32_t rk1 = b1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm1 >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)fm1, 0u));
-    __syncthreads();
-    if (first[0]) {
-        stA[rk0] = A[0];
-        stA1[rk0] = A1[0];
-    }
-    if (first[1]) {
-        stA[rk1] = A[1];
-        stA1[rk1] = A1[1];
-    }
-    if ((uint32_t)t < rows) ridx[t] = (uint16_t)(rk0 + first[0] - 1);
-    if ((uint32_t)t + 256u < rows) ridx[t + 256] = (uint16_t)(rk1 + first[1] - 1);
-    __syncthreads();
-    const uint32_t capb = cap < 128u ? cap : 128u;
-    uint32_t rhi = rows;
-    if (nr > capb) {  // block-uniform
-        uint32_t lo = 0, hi = rows;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (ridx[mid] < capb) lo = mid + 1;
-            else hi = mid;
-        }
-        rhi = lo;
-        nr = capb;
-        if (t == 0) ovf[atomicAdd(ovf_cnt, 1u)] = make_uint2(j0 + rhi, (uint32_t)lvl | (rows - rhi) << 8);
-    }
-    // lanes 0..127: W0 of root t; lanes 128..255: W1 of root t - 128
-    const bool w1 = t >= 128;
-    const uint32_t rt = w1 ? (uint32_t)t - 128u : (uint32_t)t;
-    const bool wl = rt < nr;
-    uint32_t R = 0, RA1 = 0;
-    if (wl) {
-        R = stA[rt];
-        RA1 = stA1[rt];
-    }
-    __syncthreads();  // the staged roots are read before win is written
-    uint4 *w4 = reinterpret_cast<uint4 *>(win + t * 16);
-    if (wl && !w1) {  // W0: the window below R (slots 1..15; nd[0] = R)
-        uint32_t wbad = 0;
-        uint32_t nd[16], hv[16];
-        nd[0] = R;
-        nd[1] = chk(fat(R, i - 2));
-        nd[2] = chk(fat(R, i - 3));
-        nd[3] = chk(c2(R, i - 2));
-        nd[4] = chk(fat(R, i - 4));
-        nd[6] = chk(c2(R, i - 3));
-        nd[8] = chk(fat(R, i - 5));
-        nd[12] = chk(c2(R, i - 4));
-        nd[5] = chk(fat(nd[1], i - 4));
-        nd[7] = chk(fat(nd[3], i - 4));
-        nd[9] = chk(fat(nd[1], i - 5));
-        nd[10] = chk(fat(nd[2], i - 5));
-        nd[11] = chk(fat(nd[3], i - 5));
-        nd[13] = chk(c2(nd[1], i - 4));
-        nd[14] = chk(c2(nd[2], i - 4));
-        nd[15] = chk(c2(nd[3], i - 4));
-#pragma unroll
-        for (int v = 0; v < 16; ++v) hv[v] = hiw(nd[v]);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            uint32_t ov[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int v = 4 * g + u;
-                if (v == 0) {
-                    ov[u] = 0;
-                    continue;
-                }
-                const int hb = 31 - __builtin_clz((unsigned)v);
-                const int pv = v & ~(1 << hb);
-                ov[u] = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
-                wbad += ov[u] == CZ_NONE;
-            }
-            if (g == 0) ov[0] = wbad;  // (the stores put the row's own word there)
-            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-        }
-        if (wbad) {
-            win[t * 16] = wbad;  // the count of all fifteen words
-            anybad = 1;
-        }
-    } else if (wl) {  // W1: A' = f(R, i - 1) relative to R (slot 0), the window below A' (1..14)
-        uint32_t wbad = 0;
-        uint32_t nd[15], hv[15];
-        nd[0] = RA1;
-        const uint32_t hR = hiw(R);
-        nd[1] = chk(fat(nd[0], i - 2));
-        nd[2] = chk(fat(nd[0], i - 3));
-        nd[3] = chk(c2(nd[0], i - 2));
-        nd[4] = chk(fat(nd[0], i - 4));
-        nd[6] = chk(c2(nd[0], i - 3));
-        nd[8] = chk(fat(nd[0], i - 5));
-        nd[12] = chk(c2(nd[0], i - 4));
-        nd[5] = chk(fat(nd[1], i - 4));
-        nd[7] = chk(fat(nd[3], i - 4));
-        nd[9] = chk(fat(nd[1], i - 5));
-        nd[10] = chk(fat(nd[2], i - 5));
-        nd[11] = chk(fat(nd[3], i - 5));
-        nd[13] = chk(c2(nd[1], i - 4));
-        nd[14] = chk(c2(nd[2], i - 4));
-#pragma unroll
-        for (int v = 0; v < 15; ++v) hv[v] = hiw(nd[v]);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            uint32_t ov[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int v = 4 * g + u;
-                if (v == 15) {
-                    ov[u] = wbad;
-                    continue;
-                }
-                if (v == 0) {
-                    ov[u] = enc(R, hR, i - 1, nd[0], hv[0]);
-                } else {
-                    const int hb = 31 - __builtin_clz((unsigned)v);
-                    const int pv = v & ~(1 << hb);
-                    ov[u] = enc(nd[pv], hv[pv], i - 2 - hb, nd[v], hv[v]);
-                }
-                wbad += ov[u] == CZ_NONE;
-            }
-            w4[g] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-        }
-        if (wbad) anybad = 1;
-    }
-    __syncthreads();
-    if (anybad) {  // rare: every row carries its root's CZ_NONE words
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t r = (uint32_t)t + 256u * k;
-            if (r < rhi) {
-                const uint32_t x = ridx[r];
-                const uint32_t wb = win[x * 16] + win[(128 + x) * 16 + 15];
-                if (wb) atomicAdd(&sbad, wb);
-            }
-        }
-    }
-    // both planes: rows [0, rhi) x 4 chunks of 16 B each, whole lines per store
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const size_t tp0 = (size_t)(2 * lvl) * M + j0;
-    const uint32_t nc = 4u * rhi;
-    for (uint32_t c = t; c < 2u * nc; c += 256u) {
-        const uint32_t pl = c >= nc, cc = pl ? c - nc : c;
-        const uint32_t e = cc >> 2, qq = cc & 3u;
-        uint4 u = *reinterpret_cast<const uint4 *>(win + (pl * 128u + ridx[e]) * 16 + qq * 4);
-        if (!pl && qq == 0) u.x = e0s[e];   // slot 0 of the b = 0 entry
-        if (pl && qq == 3) u.w = e0s[e];    // slot 15 of the b = 1 entry
-        const v4u wv4 = {u.x, u.y, u.z, u.w};
-        __builtin_nontemporal_store(wv4, reinterpret_cast<v4u *>(cz + (tp0 + pl * (size_t)M + e) * 4) + qq);
+        reinterpret_cast<v4u *>(cz + (tp0 + M + e) * 4)[qq] = wv4;
     }
     if (oob) atomicOr(esc + 1, 1u);
     __syncthreads();
@@ -4034,17 +2371,6 @@ void k_cz_build_roots3(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
 static void cz2_plan(size_t n, int &gl256, uint64_t &nbt, double target = 230.0) {
     const double gl = 128.0 - log2((double)n);
     gl256 = (int)lround(gl * 256.0);
-    // CX_CZ2_NB (A/B): the same block count for every level (16 = 256 rows)
-    static const int nb_env = [] {
-        const char *e = getenv("CX_CZ2_NB");
-        const int v = e ? atoi(e) : 0;
-        return v >= 9 && v <= 255 ? v : 0;
-    }();
-    if (nb_env) {
-        nbt = 0;
-        for (int k = 0; k < 8; ++k) nbt |= (uint64_t)nb_env << (8 * k);
-        return;
-    }
     // bucket k covers floor(l - gl) = k - 6 (k = 0: <= -6, k = 7: >= 1)
     static const double frac[8] = {0.97, 0.94, 0.89, 0.80, 0.685, 0.57, 0.51, 0.50};
     nbt = 0;
@@ -4083,8 +2409,7 @@ static uint64_t cz2_blocks(size_t n, int lvl_base, int nlev, uint32_t M, double 
 // lists of one uint2 per block.
 size_t cz_build_ws_words(size_t n, int lvl_base, int nlev, uint32_t M) {
     if (n == 0 || M == 0 || nlev <= 0) return 4;
-    const uint64_t b2 = cz2_blocks(n, lvl_base, nlev, M), b3 = cz2_blocks(n, lvl_base, nlev, M, CZ3_TARGET);
-    return 4 + 4 * (size_t)(b2 > b3 ? b2 : b3);
+    return 4 + 4 * (size_t)cz2_blocks(n, lvl_base, nlev, M);
 }
 
 // Roots per block of k_cz_build_roots2 before it defers rows to an overflow
@@ -4101,23 +2426,6 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     // the high-word gap codes need every level >= 64 and gs >= 64
     if (lvl_base - 5 < 64 || cz_shift(ib) < 65) return hipErrorInvalidValue;
     if (p_first >= n || M > n || nlev * 2 > 65535) return hipErrorInvalidValue;
-    // row-blocks per chunk: 16 (4096 rows x all planes, ~1000 blocks: about one
-    // resident round); CX_CZ_CHUNK overrides for A/B (0 = plane after plane).
-    // At 2^24 with two-hop planes: 48.5 ms plane order, 44.1 / 37.6 / 41.7 /
-    // 39.8 / 38.3 ms for 8 / 16 / 24 / 32 / 64 (profiles/r02/cz_build/).
-    static const uint32_t K = [] {
-        const char *e = getenv("CX_CZ_CHUNK");
-        const int v = e ? atoi(e) : 16;
-        return (uint32_t)(v > 0 ? (v + 7) / 8 * 8 : 0);
-    }();
-    const uint32_t per = (uint32_t)((M + 256 * 8 - 1) / (256 * 8));
-    dim3 grid(per * 8, nlev * 2);
-    if (K) {
-        const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + K - 1) / K;
-        const uint64_t blocks = chunks * K * (uint64_t)nlev * 2;
-        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
-        grid = dim3((unsigned)blocks, 1);
-    }
     if (n >= (1u << 30)) return hipErrorInvalidValue;
     const bool planes = fv.sx == 1;
     if (!planes && (fv.sx != CX_FINGERS || fv.sl != 1 || fv.L != 0 || fv.C2))
@@ -4125,30 +2433,12 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
     if (planes && fv.sl != n) return hipErrorInvalidValue;
     uint4 *out = reinterpret_cast<uint4 *>(cz);
     const int gs = cz_shift(ib);
-    // stores: whole lines through LDS, streaming (3, default); CX_CZ_STORE A/B at
-    // 2^24: 37.7 ms direct plain, 37-41 ms direct streaming (16 B of 64 lines
-    // per instruction: WRITE_SIZE 1.44 x the table), 33.4 ms via LDS plain,
-    // 31.8 ms via LDS streaming (profiles/r02/cz_build/store_ab/)
-    static const int store = [] {
-        const char *e = getenv("CX_CZ_STORE");
-        return e ? (atoi(e) & 3) : 3;
-    }();
-    // CX_CZ_PAIR: 1 = two lanes per entry (k_cz_build_pair); 2 / 3 = its
-    // stores-only / compute-only probes (A/B of the build's two halves)
-    static const int pair = [] {
-        const char *e = getenv("CX_CZ_PAIR");
-        return e ? atoi(e) : 0;
-    }();
-    // pair / quad planes: roots2 only
-    if ((fv.P || fv.Q) && !(ws && fv.rs && (fv.P2 || fv.Q))) return hipErrorInvalidValue;
-    if (fv.Q && n >= (1u << 28)) return hipErrorInvalidValue;  // 32-bit byte offsets
-    if (planes && (fv.C2 || fv.P2 || fv.Q) && fv.roots >= 2 && fv.rs && ws) {
-        const bool par = fv.roots == 3 && fv.C2 && !fv.P && !fv.Q;  // k_cz_build_roots3
-        const double target = par ? CZ3_TARGET : 230.0;
+    if (planes && fv.C2 && fv.roots && fv.rs && ws) {
+        // default: root-centric blocks sized by distinct roots (k_cz_build_roots2)
         int gl256;
         uint64_t nbt;
-        cz2_plan(n, gl256, nbt, target);
-        const uint64_t blocks = cz2_blocks(n, lvl_base, nlev, M, target);
+        cz2_plan(n, gl256, nbt);
+        const uint64_t blocks = cz2_blocks(n, lvl_base, nlev, M);
         if (blocks >= (1ull << 31) || nlev > 255) return hipErrorInvalidValue;
         // two overflow lists (ping-pong), counters in ws[0], ws[1]
         uint2 *list[2] = {reinterpret_cast<uint2 *>(ws + 4),  // 16-B aligned
@@ -4156,41 +2446,9 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         hipError_t e = hipMemsetAsync(ws, 0, 2 * sizeof(uint32_t), s);
         if (e != hipSuccess) return e;
         const uint32_t cap = cz2_cap();
-        // 66 VGPRs unconstrained: 7 waves per SIMD; CX_CZ2_WPE=8 forces 8 with
-        // 5 spilled VGPRs (A/B)
-        static const int wpe8 = [] {
-            const char *ev = getenv("CX_CZ2_WPE");
-            return ev && atoi(ev) == 8;
-        }();
-        static const int mode = [] {
-            const char *ev = getenv("CX_CZ2_MODE");
-            return ev ? (atoi(ev) & 63) : 0;
-        }();
         auto launch = [&](unsigned grid, const uint2 *it, uint32_t *oc, uint2 *ov) {
-            if (par)
-                k_cz_build_roots3<7><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                          p_first, M, gs, out, esc, gl256, nbt, it,
-                                                          oc, ov, cap);
-            else if (fv.Q)  // quad planes
-                k_cz_build_roots2<7, 2><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                             p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap, mode);
-            else if (fv.P && fv.P2)  // pair planes
-                k_cz_build_roots2<7, 1><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                             p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap, mode);
-            else if (fv.roots == 4)  // plane 0 after the W1 gathers
-                k_cz_build_roots2<7, 0, true><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base,
-                                                                   nlev, p_first, M, gs, out, esc,
-                                                                   gl256, nbt, it, oc, ov, cap, mode);
-            else if (wpe8)
-                k_cz_build_roots2<8, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                             p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap, mode);
-            else
-                k_cz_build_roots2<7, 0><<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev,
-                                                             p_first, M, gs, out, esc, gl256, nbt, it,
-                                                             oc, ov, cap, mode);
+            k_cz_build_roots2<<<grid, 256, 0, s>>>(fv, ring, (uint32_t)n, lvl_base, nlev, p_first, M,
+                                                   gs, out, esc, gl256, nbt, it, oc, ov, cap);
         };
         launch((unsigned)blocks, nullptr, ws, list[0]);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -4212,95 +2470,16 @@ hipError_t cz_build_part(const FingerView &fv, const cell128 *ring, const uint64
         }
         return hipSuccess;
     }
-    if (planes && fv.C2 && fv.roots) {
-        static const int mode = [] {
-            const char *e = getenv("CX_CZ_ROOTS_MODE");
-            return e ? (atoi(e) & 3) : 0;
-        }();
-        static const int a1_rows = [] {
-            const char *e = getenv("CX_CZ_ROOTS_A1");
-            return e ? (atoi(e) != 0) : 1;
-        }();
-        static const int late_e0 = [] {
-            const char *e = getenv("CX_CZ_ROOTS_LATE");
-            return e ? (atoi(e) != 0) : 0;
-        }();
-        // probe: extra dynamic LDS per block (fewer resident blocks per CU), to
-        // measure how the build scales with the rows in flight
-        static const unsigned lds_pad = [] {
-            const char *e = getenv("CX_CZ_LDS_PAD");
-            const int v = e ? atoi(e) : 0;
-            return (unsigned)(v > 0 && v <= 65536 ? v : 0);
-        }();
-        // chunk of 16 row-blocks x all levels (CX_CZ_CHUNK overrides).  At 7
-        // blocks per CU 32 measured best (22.6 vs 22.8-24.6 ms,
-        // profiles/r03/codes/chunk_summary.txt); at 8 blocks per CU (64 VGPRs)
-        // 16 is: 22.9 vs 24.1-24.5 ms (occ8_summary.txt)
-        const uint32_t Kr = K ? K : 16;
-        const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + Kr - 1) / Kr;
-        const uint64_t blocks = chunks * Kr * (uint64_t)nlev;
-        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
-        // CX_CZ_ROOTS_SPLIT (A/B): 1 = LDS split, 2 = LDS split + W1 after plane 0
-        // default: W1 after plane 0 through the split LDS at 5 waves per SIMD
-        // with the 32-bit slice codes (88 VGPRs, 21 KB: 5 blocks per CU; 24.4-25.0
-        // vs 26.7-26.9 ms at 2^24), the one-pass kernel at 4 with the high words
-        static const int split_env = [] {
-            const char *e = getenv("CX_CZ_ROOTS_SPLIT");
-            return e ? atoi(e) : -1;
-        }();
-        const int split = split_env >= 0 ? split_env : (fv.rs ? 2 : 0);
-#define CX_ROOTS_LAUNCH(SP, W)                                                                   \
-    do {                                                                                         \
-        if (fv.rs)                                                                               \
-            k_cz_build_roots<SP, W, true><<<(unsigned)blocks, 256, lds_pad, s>>>(                \
-                fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode,   \
-                a1_rows, late_e0);                                                                \
-        else                                                                                     \
-            k_cz_build_roots<SP, W, false><<<(unsigned)blocks, 256, lds_pad, s>>>(               \
-                fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M, gs, out, esc, Kr, mode,   \
-                a1_rows, late_e0);                                                                \
-    } while (0)
-        // kept A/Bs (profiles/r03/build_lat/): the split at 4 waves per SIMD and
-        // the sequential W1 at 5; the forced 5 / 6 / 8-wave variants of either
-        // spilled (44-55 ms) with 64-bit high words and were removed; with the
-        // 32-bit slice codes the split is tried at 5 / 6 waves (3 / 4)
-        if (!split)
-            CX_ROOTS_LAUNCH(0, 4);
-        else if (split == 2)
-            CX_ROOTS_LAUNCH(2, 5);
-        else if (split == 3)
-            CX_ROOTS_LAUNCH(1, 5);
-        else if (split == 4)
-            CX_ROOTS_LAUNCH(1, 6);
-        else if (split == 5)
-            CX_ROOTS_LAUNCH(2, 6);
-        else if (split == 6)
-            CX_ROOTS_LAUNCH(2, 8);
-        else
-            CX_ROOTS_LAUNCH(1, 4);
-#undef CX_ROOTS_LAUNCH
-        return hipGetLastError();
-    }
-    if (planes && fv.C2 && pair >= 1 && pair <= 3) {
-        const uint32_t Kp = K ? K : 16;
-        const uint64_t nrb = ((uint64_t)M + 127) / 128, chunks = (nrb + Kp - 1) / Kp;
-        const uint64_t blocks = chunks * Kp * (uint64_t)nlev * 2;
-        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
-        k_cz_build_pair<<<(unsigned)blocks, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                         p_first, M, gs, out, esc, Kp, pair - 1);
-        return hipGetLastError();
-    }
-    if (planes && fv.C2 && store != 1) {
-        if (store == 0)
-            k_cz_build<2, 0><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                  p_first, M, gs, out, esc, K);
-        else if (store == 2)
-            k_cz_build<2, 2><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                  p_first, M, gs, out, esc, K);
-        else
-            k_cz_build<2, 3><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev,
-                                                  p_first, M, gs, out, esc, K);
-    } else if (planes && fv.C2)
+    // one lane per entry (rings with a gap too wide for the 32-bit slices, or
+    // no HBM for the two-hop planes / level planes): 1-D grid in chunks of 16
+    // row-blocks x all planes, whole-line streaming stores through LDS
+    // (37.6 ms at 2^24 with two-hop planes)
+    constexpr uint32_t K = 16;
+    const uint64_t nrb = ((uint64_t)M + 255) / 256, chunks = (nrb + K - 1) / K;
+    const uint64_t blocks = chunks * K * (uint64_t)nlev * 2;
+    if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)blocks, 1);
+    if (planes && fv.C2)
         k_cz_build<2><<<grid, 256, 0, s>>>(fv, ring, rh, (uint32_t)n, lvl_base, nlev, p_first, M,
                                            gs, out, esc, K);
     else if (planes)
@@ -4955,43 +3134,6 @@ hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
 
 template <class K>
 static unsigned resident_grid(K kernel, int block);
-
-hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
-                    int l0, int R, int ib, const uint32_t *F, const SearchView &sv,
-                    const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
-                    uint8_t *hops, uint8_t *status, unsigned long long *stats, hipStream_t s) {
-    if (q == 0) return hipSuccess;
-    TreeIO io = {};
-    io.ring_ext = ring_ext;
-    io.ring = ring;
-    io.n = (uint32_t)n;
-    io.stats = stats;
-    io.sv = sv;  // exact hops when F is null (rows not materialised)
-    io.tree = reinterpret_cast<const uint4 *>(cz);
-    io.l0 = l0;
-    io.R = R;
-    io.ib = ib;
-    io.F = F;
-    io.src = src;
-    io.keys = keys;
-    io.q = q;
-    io.owner = owner;
-    io.hops = hops;
-    io.status = status;
-    // one resident round of waves (no second, partial round of blocks)
-    static const unsigned resident = resident_grid(k_route_tree<false, true>, RT_BLOCK);
-    size_t waves = (size_t)resident * (RT_BLOCK / 64);
-    const size_t small = (q + 1023) / 1024;
-    if (small < waves) waves = small ? small : 1;
-    io.chunk = (q + waves - 1) / waves;
-    waves = (q + io.chunk - 1) / io.chunk;
-    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    if (stats)
-        k_route_tree<false, true, true><<<blocks, RT_BLOCK, 0, s>>>(io);
-    else
-        k_route_tree<false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
-    return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------
 // Arc-sharded mode (SURVEY 8e layout 2), two phases per lookup.  Every rank
@@ -5799,7 +3941,7 @@ __device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, const uint
 // old_lists / old_count (CHURN, may be null): the keys' old n-successor lists
 // as cx_nsucc on the old ring gives them -- the scan already holds the old
 // successor, so DHash placement + maintenance share one pass over the keys.
-template <bool CHURN, bool DIR, bool CD = false, int PROBE = 0>
+template <bool CHURN, bool DIR, bool CD = false>
 __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, SearchView sv_old,
                                                          const uint32_t *old_to_new,
                                                          const uint32_t *holders, int nh,
@@ -5808,8 +3950,6 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
                                                          uint16_t *mask, uint8_t *target,
                                                          ChurnDir cd, uint32_t *old_lists = nullptr,
                                                          uint8_t *old_count = nullptr) {
-    // PROBE (A/B, CX_MISPLACED_PROBE; 0 = the scan): 1 = no row flush (the
-    // search half), 2 = no search (the flush half: rows from the tile index)
     __shared__ u128 lds_new[Searcher<DIR>::LDS];
     __shared__ u128 lds_old[CHURN ? Searcher<DIR>::LDS : 1];
     __shared__ uint32_t s_sn[ROW_BLOCK], s_so[ROW_BLOCK];  // the tile's successors
@@ -5849,8 +3989,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
         if (i < q) {
             uint32_t sn = 0, so = 0, has = 0, m = 0;
             const bool settled =
-                PROBE == 2 ? (sn = so = (uint32_t)(i % n_new), true)
-                           : use_cd && cd_lookup(cd, key, A, B, n_old, n_new, no, nn, so, sn, has, m);
+                use_cd && cd_lookup(cd, key, A, B, n_old, n_new, no, nn, so, sn, has, m);
             if (!settled) {
                 // Both searches are issued together: deriving the new successor
                 // from a verified old->new mapping saves a search for ~98 % of
@@ -5929,15 +4068,13 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
             }
             mask[i] = (uint16_t)m;
         }
-        if (use_cd && more && PROBE != 2) cd_fetch(cd, key_n, A_n, B_n);
+        if (use_cd && more) cd_fetch(cd, key_n, A_n, B_n);
         __syncthreads();
-        if (PROBE != 1) {
-            // new lists (sn + j mod n_new, j < nn) and old lists (so + j mod
-            // n_old, j < no <= n_old: one wrap at most) straight from the successors
-            flush_window(s_sn, new_lists, base, cnt, nlist, nn, n_new);
-            if (CHURN && old_lists) flush_window(s_so, old_lists, base, cnt, nlist, no, n_old);
-            flush_rows_refill(stage_t, target, base, cnt, nslots);
-        }
+        // new lists (sn + j mod n_new, j < nn) and old lists (so + j mod
+        // n_old, j < no <= n_old: one wrap at most) straight from the successors
+        flush_window(s_sn, new_lists, base, cnt, nlist, nn, n_new);
+        if (CHURN && old_lists) flush_window(s_so, old_lists, base, cnt, nlist, no, n_old);
+        flush_rows_refill(stage_t, target, base, cnt, nslots);
         __syncthreads();
     }
 }
@@ -5951,20 +4088,8 @@ hipError_t misplaced_churn(const SearchView &sv_old, const SearchView &sv_new,
     if ((old_lists == nullptr) != (old_count == nullptr)) return hipErrorInvalidValue;
     ChurnDir cd = {};
     if (cda) cd = ChurnDir{cda->cd, cda->kb, sv_old.ring, sv_new.ring, cda->ok};
-    static const int probe = [] {
-        const char *e = getenv("CX_MISPLACED_PROBE");
-        return e ? (atoi(e) & 3) : 0;
-    }();
     const unsigned g = cx_grid(q, ROW_BLOCK, 8192);
-    if (cda && sv_new.dir && sv_old.dir && probe == 1)
-        k_misplaced<true, true, true, 1><<<g, ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
-            old_lists, old_count);
-    else if (cda && sv_new.dir && sv_old.dir && probe == 2)
-        k_misplaced<true, true, true, 2><<<g, ROW_BLOCK, 0, s>>>(
-            sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
-            old_lists, old_count);
-    else if (cda && sv_new.dir && sv_old.dir)
+    if (cda && sv_new.dir && sv_old.dir)
         k_misplaced<true, true, true><<<g, ROW_BLOCK, 0, s>>>(
             sv_new, sv_old, old_to_new, nullptr, 0, keys, q, n, lists, count, mask, target, cd,
             old_lists, old_count);
@@ -6421,16 +4546,6 @@ __device__ __forceinline__ uint32_t modp_fast(uint32_t x, uint32_t p, float inv_
     const uint32_t q = (uint32_t)__builtin_fmaf((float)x, inv_p, -0.5f);  // < 0 -> 0
     const uint32_t r = x - __umul24(q, p);
     return r < r - p ? r : r - p;
-}
-
-// Segment g's block, for the 64 consecutive segments of one wave chunk: one
-// binary search for the chunk's first segment (uniform), then a short forward
-// scan per lane (blocks of a chunk are consecutive in seg order).
-__device__ __forceinline__ size_t chunk_block(const uint64_t *seg, size_t blocks, uint64_t g0,
-                                              uint64_t g) {
-    size_t b = seg_block(seg, blocks, g0);
-    while (seg[b + 1] <= g) ++b;
-    return b;
 }
 
 typedef unsigned short cx_us2 __attribute__((ext_vector_type(2)));
@@ -7074,15 +5189,12 @@ static void ida_encode_launch(const uint8_t *data, const uint64_t *offs, const u
                                               1.0f / p, frags);
 }
 
-static int ida_depth(const char *var, int dflt);
-
 hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t *seg,
                       size_t blocks, int n, int m, int p, uint16_t *frags, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
-    static const int D = ida_depth("CX_IDA_ENC_D", 3);
-    static const int FD = ida_depth("CX_IDA_ENCF_D", 1);
-    static const bool fixed_on = !getenv("CX_IDA_GENERIC");
-    if (fixed_on && n == 14 && m > 8 && m <= 12) {  // DHash (14, 10) and neighbours
+    // pipeline depths (chunks in flight per wave): the measured best, 1 for the
+    // fixed-shape kernel and 3 for the generic one (profiles/r02)
+    if (n == 14 && m > 8 && m <= 12) {  // DHash (14, 10) and neighbours
         IdaEncTab tab = {};
         for (int i = 0; i < n; ++i) {
             uint32_t e = 1;
@@ -7106,23 +5218,15 @@ hipError_t ida_encode(const uint8_t *data, const uint64_t *offs, const uint64_t 
                                                             (uint32_t)p, 1.0f / p, frags,    \
                                                             tab);                            \
     } while (0)
-        if (p257 && FD == 1) CX_ENC_FIXED(1, true);
-        else if (p257) CX_ENC_FIXED(2, true);
-        else if (FD == 1) CX_ENC_FIXED(1, false);
-        else CX_ENC_FIXED(2, false);
+        if (p257) CX_ENC_FIXED(1, true);
+        else CX_ENC_FIXED(1, false);
 #undef CX_ENC_FIXED
         return hipGetLastError();
     }
     if (16 * m + 1 > 64 * 3)
         ida_encode_launch<8, 2>(data, offs, seg, blocks, n, m, p, frags, s);
-    else if (D == 1)
-        ida_encode_launch<3, 1>(data, offs, seg, blocks, n, m, p, frags, s);
-    else if (D == 2)
-        ida_encode_launch<3, 2>(data, offs, seg, blocks, n, m, p, frags, s);
-    else if (D == 3)
-        ida_encode_launch<3, 3>(data, offs, seg, blocks, n, m, p, frags, s);
     else
-        ida_encode_launch<3, 4>(data, offs, seg, blocks, n, m, p, frags, s);
+        ida_encode_launch<3, 3>(data, offs, seg, blocks, n, m, p, frags, s);
     return hipGetLastError();
 }
 
@@ -7160,40 +5264,23 @@ static void ida_decode_launch(const uint16_t *frags, const uint64_t *seg, size_t
         reinterpret_cast<unsigned long long *>(out_len), err);
 }
 
-// A/B knob for the pipeline depths (chunks in flight per wave): CX_IDA_ENC_D,
-// CX_IDA_DEC_D in {1, 2, 3, 4}; defaults are the measured best.
-static int ida_depth(const char *var, int dflt) {
-    const char *e = getenv(var);
-    const int d = e ? atoi(e) : dflt;
-    return d >= 1 && d <= 4 ? d : dflt;
-}
-
 hipError_t ida_decode(const uint16_t *frags, const uint64_t *seg, size_t blocks, int m, int p,
                       const int32_t *inv, const uint32_t *run_of, size_t runs, const uint8_t *okf,
                       uint16_t *out, uint64_t *out_len, uint32_t *err, hipStream_t s) {
     if (blocks == 0) return hipSuccess;
     const bool wide = (uint64_t)m * (p - 1) * 65535ull >= (1ull << 32);
-    static const int D = ida_depth("CX_IDA_DEC_D", 2);
+    // two chunks in flight per wave (the measured best, profiles/r02)
     if (wide)
         ida_decode_launch<true, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
                                               out_len, err, s);
-    else if (m == 10 && !getenv("CX_IDA_GENERIC") && D == 1)  // DHash (14, 10)
-        ida_decode_launch<false, 12, 1, 10>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
-                                            out_len, err, s);
-    else if (m == 10 && !getenv("CX_IDA_GENERIC"))
+    else if (m == 10)  // DHash (14, 10)
         ida_decode_launch<false, 12, 2, 10>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
                                             out_len, err, s);
     else if (m > 12)
         ida_decode_launch<false, IDA_MAX_N, 1>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out,
                                                out_len, err, s);
-    else if (D == 1)
-        ida_decode_launch<false, 12, 1>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
-    else if (D == 2)
-        ida_decode_launch<false, 12, 2>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
-    else if (D == 3)
-        ida_decode_launch<false, 12, 3>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
     else
-        ida_decode_launch<false, 12, 4>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
+        ida_decode_launch<false, 12, 2>(frags, seg, blocks, m, p, inv, run_of, runs, okf, out, out_len, err, s);
     return hipGetLastError();
 }
 

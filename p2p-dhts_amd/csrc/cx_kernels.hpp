@@ -7,14 +7,6 @@
 // are old ring indices.
 #define CX_TAG_JOIN 0x80000000u
 
-// Route-table entry: successor id + index of one finger (32-B aligned so one
-// hop is a single gather inside one 64-B granule).
-struct alignas(32) RtEntry {
-    uint64_t lo, hi;
-    uint32_t idx, pad0, pad1, pad2;
-};
-static_assert(sizeof(RtEntry) == 32, "RtEntry is 32 B");
-
 // In-flight record of the arc-sharded walk (32 B, the unit exchanged between
 // ranks).  qid = origin rank << ARC_ORIGIN_SHIFT | index at the origin.
 struct alignas(16) ArcRec {
@@ -110,22 +102,7 @@ hipError_t route(const cell128 *ring, size_t n, const uint32_t *F, const cell128
                  const uint32_t *preds, const LitState &ls, bool literal, const uint32_t *src,
                  const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status,
                  hipStream_t s);
-hipError_t rt_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, RtEntry *rt,
-                    cell128 *ring_ext, hipStream_t s);
 hipError_t ring_ext_build(const cell128 *ring, size_t n, cell128 *ring_ext, hipStream_t s);
-hipError_t route_rt(const cell128 *ring_ext, const cell128 *ring, size_t n, const RtEntry *rt,
-                    int l0, int R, const uint32_t *F, const uint32_t *src, const cell128 *keys,
-                    size_t q, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
-hipError_t pk_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
-                    uint64_t *rt, hipStream_t s);
-hipError_t route_pk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
-                    int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
-                    const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                    uint8_t *status, hipStream_t s);
-hipError_t route_pk3(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *rt,
-                     int l0, int R, int ib, const uint32_t *F, const uint32_t *src,
-                     const cell128 *keys, size_t q, uint32_t *owner, uint8_t *hops,
-                     uint8_t *status, hipStream_t s);
 hipError_t tree_build(const uint32_t *F, const cell128 *ring, size_t n, int l0, int R, int ib,
                       uint64_t *tree, hipStream_t s);
 hipError_t route_tree(const cell128 *ring_ext, const cell128 *ring, size_t n,
@@ -219,10 +196,6 @@ size_t cz_build_ws_words(size_t n, int lvl_base, int nlev, uint32_t M);
 // overflow launch (256; tests only: lower, to exercise that path).
 uint32_t cz2_cap();
 void cz2_set_cap(uint32_t cap);
-hipError_t route_cz(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
-                    int l0, int R, int ib, const uint32_t *F, const SearchView &sv,
-                    const uint32_t *src, const cell128 *keys, size_t q, uint32_t *owner,
-                    uint8_t *hops, uint8_t *status, unsigned long long *stats, hipStream_t s);
 // The default walk (cx_walk.hip): straight-line window steps over the same
 // table; n < 2^30, gs = cz_shift(ib) >= 64.
 hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,

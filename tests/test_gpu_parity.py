@@ -101,7 +101,7 @@ def test_fingers_c2_ring(cx, O):
 
 
 # ---------------------------------------------------------------- a7-a9 route
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 4, 5])
 def test_route_c1_golden(cx, O, c1truth, variant):
     """Config C1 ground truth (8 peers, key0..key999 from every peer)."""
     ids = O.keys_from_ints([O.uuid5_key(p) for p in c1truth["peers"]])
@@ -117,7 +117,7 @@ def test_route_c1_golden(cx, O, c1truth, variant):
     assert (status == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 4, 5])
 @pytest.mark.parametrize("n", [1, 2, 3, 9, 1000, 20000])
 def test_route_converged(cx, O, n, variant):
     ids = edge_ring(O, n, 900 + n)
@@ -170,7 +170,7 @@ def test_route_from_finger_table(cx, O, refvec):
 
 def clustered_ring(O, n, seed, spread_bits):
     """IDs packed within 2^spread_bits of a few centres: every packed-ID
-    interval straddles decisions, forcing the exact-ID fallbacks of variant 2."""
+    interval straddles decisions, forcing the exact-ID fallbacks of the table walks."""
     rng = np.random.default_rng(seed)
     centres = [int.from_bytes(rng.bytes(16), "big") for _ in range(4)] + [MAX - 5, 3]
     vals = []
@@ -201,7 +201,7 @@ def test_successor_clustered_rings(cx, O, search, spread):
     assert (lists == wl).all() and (count == wc).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 4, 5])
 @pytest.mark.parametrize("spread", [8, 40, 90, 100])
 def test_route_clustered_rings(cx, O, variant, spread):
     ids = clustered_ring(O, 3000, spread, spread)
@@ -270,7 +270,7 @@ def test_route_literal_random_edits(cx, O):
     assert (status == 1).any()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 4, 5])
 def test_route_bad_src_is_flagged(cx, O, variant):
     ring = cx.Ring(O.splitmix_keys(3, 50))
     ring.build_fingers()
@@ -616,40 +616,16 @@ def test_route_table_from_level_planes_identical(lg):
     ring.set_table_build(3)  # one lane per entry (the default is root-centric)
     ring.build_fingers()
     h_entry = ring.route_table_hash()
-    ring.set_table_build(4)  # root-centric in 256-row blocks (round 3)
-    ring.build_fingers()
-    h_roots256 = ring.route_table_hash()
-    ring.set_table_build(5)  # the default's alias (4-B planes)
-    ring.build_fingers()
-    h_nopairs = ring.route_table_hash()
-    ring.set_table_build(6)  # ... on pair planes
-    ring.build_fingers()
-    h_pairs = ring.route_table_hash()
-    ring.set_table_build(7)  # ... on quad planes
-    ring.build_fingers()
-    h_quads = ring.route_table_hash()
-    ring.set_table_build(8)  # both windows of a root at once, stores last
-    ring.build_fingers()
-    h_par = ring.route_table_hash()
-    ring.set_table_build(9)  # plane 0 stored after the W1 gathers
-    ring.build_fingers()
-    h_sl = ring.route_table_hash()
     from chordx import _lib
-
-    def with_overflow(tb):
-        # most rows deferred to overflow launches (48 roots per block)
-        ring.set_table_build(tb)
-        _lib.set_fault(2)
-        try:
-            ring.build_fingers()
-        finally:
-            _lib.set_fault(0)
-        return ring.route_table_hash()
-
-    h_ovf = [with_overflow(tb) for tb in (8, 9, 0)]  # the default last
-    assert h_planes == h_rows == h_planes_only == h_entry == h_roots256 == h_nopairs
-    assert h_planes == h_pairs == h_quads == h_par == h_sl
-    assert h_ovf == [h_planes] * 3
+    # the default with most rows deferred to overflow launches (48 roots per block)
+    ring.set_table_build(0)
+    _lib.set_fault(2)
+    try:
+        ring.build_fingers()
+    finally:
+        _lib.set_fault(0)
+    h_ovf = ring.route_table_hash()
+    assert h_planes == h_rows == h_planes_only == h_entry == h_ovf
     assert h_planes != 0
 
 
@@ -704,27 +680,15 @@ def test_route_table_builds_edge_rings(cx, O, kind):
     ring.build_fingers()
     assert ring.route_info()[0] == 5
     h0, e0 = ring.route_table_hash(), ring.route_info()[1]
+    ring.set_table_build(1)  # row-major fingers
+    ring.build_fingers()
+    h1, e1 = ring.route_table_hash(), ring.route_info()[1]
     ring.set_table_build(2)
     ring.build_fingers()
     h2, e2 = ring.route_table_hash(), ring.route_info()[1]
     ring.set_table_build(3)  # one lane per entry (the default is root-centric)
     ring.build_fingers()
     h3, e3 = ring.route_table_hash(), ring.route_info()[1]
-    ring.set_table_build(4)  # root-centric in 256-row blocks (round 3)
-    ring.build_fingers()
-    h4, e4 = ring.route_table_hash(), ring.route_info()[1]
-    ring.set_table_build(5)  # the default's alias (4-B planes)
-    ring.build_fingers()
-    h6, e6 = ring.route_table_hash(), ring.route_info()[1]
-    ring.set_table_build(6)  # ... on pair planes
-    ring.build_fingers()
-    h7, e7 = ring.route_table_hash(), ring.route_info()[1]
-    ring.set_table_build(7)  # ... on quad planes
-    ring.build_fingers()
-    h8, e8 = ring.route_table_hash(), ring.route_info()[1]
-    ring.set_table_build(8)  # both windows of a root at once, stores last
-    ring.build_fingers()
-    h9, e9 = ring.route_table_hash(), ring.route_info()[1]
     from chordx import _lib
     ring.set_table_build(0)
     _lib.set_fault(2)  # the default with overflow launches (48 roots per block)
@@ -733,13 +697,51 @@ def test_route_table_builds_edge_rings(cx, O, kind):
     finally:
         _lib.set_fault(0)
     h5, e5 = ring.route_table_hash(), ring.route_info()[1]
-    assert h0 == h2 == h3 == h4 == h5 == h6 == h7 == h8 == h9 and h0 != 0
-    assert e0 == e2 == e3 == e4 == e5 == e6 == e7 == e8 == e9
+    assert h0 == h1 == h2 == h3 == h5 and h0 != 0
+    assert e0 == e1 == e2 == e3 == e5
     ring.set_table_build(0)
     ring.build_fingers()
     want = O.ring_build(ids)
     keys = edge_keys(O, want, 0xB2, 5000)
     src = rng.integers(0, len(want), len(keys)).astype(np.uint32)
+    got = ring.route(src, keys)
+    exp = O.route(O.Peers(want, O.fingers(want)), src, keys)
+    for a, b in zip(got, exp):
+        assert (a == b).all()
+
+
+def test_route_table_escape_count_with_overflow(cx, O):
+    """Escape accounting of the default build when rows are deferred to
+    overflow launches: a ring of four dense clusters plus a few
+    uniform IDs has many nodes the 4-B format cannot hold -- row words
+    included (fingers that land in the empty space between clusters) -- and,
+    with 48 roots per block (fault 2), most rows go to overflow launches.  The
+    count must equal the one-lane-per-entry build's, which has no overflow."""
+    vals = []
+    for c in range(4):
+        base = int(O.ints_from_keys(O.splitmix_keys(0xE5C0 + c, 1))[0])
+        vals += [(base + i * 104729) % (1 << 128) for i in range(2500)]
+    vals += O.ints_from_keys(O.splitmix_keys(0xE5C9, 700))
+    ids = O.keys_from_ints(vals)
+    from chordx import _lib
+    ring = cx.Ring(ids)
+    ring.set_table_build(3)  # one lane per entry: no overflow path
+    ring.build_fingers()
+    h3, e3 = ring.route_table_hash(), ring.route_info()[1]
+    ring.set_table_build(0)
+    ring.build_fingers()
+    h0, e0 = ring.route_table_hash(), ring.route_info()[1]
+    _lib.set_fault(2)
+    try:
+        ring.build_fingers()
+    finally:
+        _lib.set_fault(0)
+    h5, e5 = ring.route_table_hash(), ring.route_info()[1]
+    assert e3 > 0
+    assert h0 == h3 == h5 and e0 == e3 == e5
+    want = O.ring_build(ids)
+    keys = edge_keys(O, want, 0xE5CA, 4000)
+    src = (np.arange(len(keys)) * 7 % len(want)).astype(np.uint32)
     got = ring.route(src, keys)
     exp = O.route(O.Peers(want, O.fingers(want)), src, keys)
     for a, b in zip(got, exp):

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Route walk PMC (round 5): SQ / TA counters of the default walk (k_walk<false>)
-# on the C4 batch (benches/bench_walk_ab.py), one rocprofv3 pass per counter group.
+# on the C4 batch (benches/bench_walk.py), one rocprofv3 pass per counter group.
 #   bash tools/r05_walk_pmc.sh <tag> [kernel-regex]
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -9,7 +9,7 @@ O=$R/gpurun_out/${1:-r05_walk_pmc}
 RX=${2:-k_walk<false>}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/benches/bench_walk_ab.py 2 1"
+B="python3 $R/benches/bench_walk.py 2 1"
 i=0
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
          "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH" \
