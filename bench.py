@@ -77,6 +77,10 @@ GRANULE = 64  # one dependent random gather
 # SURVEY 8(d) reference-work model: 25 B streamed + 64 B source-peer record +
 # 128 B per hop (finger granule + ring granule).
 REF_STREAM, REF_SRC, REF_HOP = 25, 64, 128
+# C2 / C3 (configs[1], configs[2]): SURVEY 8(d) seeds
+SEED_C2_RING, SEED_C2_KEYS = 0x5EED0001, 0x5EED0002
+SEED_C3_RING, SEED_C3_KEYS = 0x5EED0003, 0x5EED0004
+CX_FINGERS_B = 128
 # C5 (configs[4]): a second ring and key stream (SURVEY 8d seeds)
 SEED_C5_RING, SEED_C5_KEYS = 0x5EED0007, 0x5EED0008
 C5_N = 14
@@ -103,6 +107,11 @@ def parse():
     ap.add_argument("--c5-keys-log2", type=int, default=26, help="C5 keys (all ranks)")
     ap.add_argument("--c5-oracle-keys", type=int, default=1 << 20,
                     help="C5 keys checked against the oracle (rank 0)")
+    ap.add_argument("--c5-cpu-keys", type=int, default=1 << 17,
+                    help="C5 CPU baseline: largest key sample (routed lists, rank 0; 0 = skip)")
+    ap.add_argument("--c5-cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 exact-successor leg")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 fingers + routes leg")
     ap.add_argument("--mode", choices=("replicated", "arc"), default="replicated",
                     help="replicated: every rank holds the whole route table and routes its "
                          "own keys (default; the arc layout is still measured as the `arc` "
@@ -562,6 +571,39 @@ def c5_leg(args, world, rank, dev, backend):
                       and (mask[:m].cpu().numpy().view(np.uint16) == wm).all()
                       and (target[:m].cpu().numpy() == wt).all())
         t_or = time.perf_counter() - t0
+    cpu = None
+    if rank == 0 and args.c5_cpu_keys:
+        # SURVEY 8(d)'s CPU baseline: the lists by routed lookups, exactly like
+        # GetNSuccessors, on the old ring (placement) and the new ring
+        # (maintenance), then the misplaced check (or_maintenance_routed)
+        import oracle as O
+        th = host_threads()
+        Fs = []
+        for r in (old, new):
+            r.set_route_variant(0)  # the finger rows only: no route table
+            r.build_fingers()
+            Fs.append(r.fingers_device().cpu().numpy().view(np.uint32))
+            r.set_route_variant(-1)
+        Po, Pn = O.Peers(old.ids(), Fs[0]), O.Peers(new.ids(), Fs[1])
+        mc = min(args.c5_cpu_keys, q)
+        kc = keys[:mc].cpu().numpy().view(np.uint64)
+        o2n_h = o2n.cpu().numpy().view(np.uint32)
+        va, v1, qa, q1, rr, dta, dt1 = _cpu_timed(
+            lambda qq, t: O.maintenance_routed(Po, Pn, o2n_h, kc[:qq], n, threads=t), 256, mc,
+            args.c5_cpu_seconds, th, q_min=min(mc, 1 << 16))
+        gpu = (old_lists[:qa].cpu().numpy().view(np.uint32), old_count[:qa].cpu().numpy(),
+               lists[:qa].cpu().numpy().view(np.uint32), count[:qa].cpu().numpy(),
+               mask[:qa].cpu().numpy().view(np.uint16), target[:qa].cpu().numpy())
+        cpu = {"value": va, "unit": "keys/s", "cores": th, "kind": "port", "value_1core": v1,
+               "sample": f"first {qa} keys of the rank-0 shard on {th} threads ({dta:.1f} s), "
+                         f"{q1} on 1 thread ({dt1:.1f} s): per key 14 routed GetSuccessor "
+                         "lookups on the old ring (placement) and 14 on the new ring "
+                         "(maintenance) from peer q mod n, then the misplaced check; "
+                         "oracle/chord_oracle.c or_maintenance_routed (or_nsucc, "
+                         "misplaced_from_list)",
+               "equals_gpu_on_sample": all(bool((a == b).all()) for a, b in zip(rr, gpu)),
+               "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+        del Fs, Po, Pn, gpu, rr
     dist.barrier(world)
     per_step = dt_max / args.steps
     out = {
@@ -591,12 +633,209 @@ def c5_leg(args, world, rank, dev, backend):
         "keys_with_misplaced_holder": n_mis,
         "churn_equals_oracle": churn_ok,
         "parity_on_sample": parity, "oracle_sample_keys": m, "oracle_s": t_or,
+        "cpu_baseline": cpu,
         "note": "both rings whole on every rank (IDs all-gathered, the same churn everywhere); "
                 "no collective in the step; oracle: oracle/chord_oracle.c or_churn + "
                 "or_misplaced (dhash_peer.cpp:298-348)"}
     old.close()
     new.close()
     return out
+
+
+def _cpu_timed(fn, q_cal, q_max, budget_s, threads, q_min=0):
+    """Calibrate fn(q, threads) on q_cal items (1 thread), then time it on a
+    sample sized for ~budget_s / 3 on one core and ~2 budget_s / 3 on all
+    `threads`; (items/s all cores, items/s one core, q all, q one, result)."""
+    t0 = time.perf_counter()
+    fn(q_cal, 1)
+    per1 = (time.perf_counter() - t0) / q_cal
+    q1 = int(min(q_max, max(q_cal, budget_s / 3 / max(per1, 1e-12))))
+    t0 = time.perf_counter()
+    fn(q1, 1)
+    dt1 = time.perf_counter() - t0
+    qa = int(min(q_max, max(q1, q_min, budget_s * 2 / 3 * threads / max(per1, 1e-12))))
+    t0 = time.perf_counter()
+    res = fn(qa, threads)
+    dta = time.perf_counter() - t0
+    return qa / dta, q1 / dt1, qa, q1, res, dta, dt1
+
+
+def c2_leg(args, world, rank, dev):
+    """BASELINE config C2 (configs[1]): exact successor resolution
+    (StoredLocally / owner = lower_bound with wrap, abstract_chord_peer.cpp:720-725)
+    of 2^20 uniform keys (splitmix 0x5EED0002) on a 2^16-peer ring (0x5EED0001),
+    one cx_successor launch per step; every rank its own 2^20 keys (weak).
+    Roofline on SURVEY 8(d)'s 20 B/query + 16 B/peer; parity on every key."""
+    import oracle as O
+    N, Q = 1 << 16, 1 << 20
+    ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(ids, SEED_C2_RING)
+    ring = chordx.Ring(ids, device=dev.index or 0)
+    keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(keys, SEED_C2_KEYS, offset=rank * Q)
+    out = torch.empty(Q, dtype=torch.int32, device=dev)
+    steps = max(args.steps, 100)  # ~10 us kernels: enough launches to time
+    for _ in range(max(args.warmup, 10)):
+        ring.successor(keys, out=out)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dist.barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        ring.successor(keys, out=out)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier(world)
+    dt_max = dist.max_over_ranks(time.perf_counter() - t0, world, dev)
+    ev_ms = dist.max_over_ranks(ev0.elapsed_time(ev1) / steps, world, dev)
+    ring_np = ring.ids()
+    keys_np = keys.cpu().numpy().view(np.uint64)
+    want = O.successor(ring_np, keys_np, threads=host_threads())
+    parity = dist.all_over_ranks(bool((out.cpu().numpy().view(np.uint32) == want).all()), world, dev)
+    cpu = None
+    if rank == 0:
+        th = host_threads()
+        va, v1, qa, q1, _, dta, dt1 = _cpu_timed(
+            lambda q, t: O.successor(ring_np, keys_np[:q], threads=t), 4096, Q, 3.0, th)
+        cpu = {"value": va, "unit": "lookups/s", "cores": th, "kind": "port", "value_1core": v1,
+               "sample": f"first {qa} keys on {th} threads ({dta:.2f} s), {q1} on 1 ({dt1:.2f} s); "
+                         "oracle/chord_oracle.c or_successor_batch (binary search of the sorted ring)",
+               "cpu_model": cpu_model()}
+    algo = Q * 20 + N * 16
+    ring.close()
+    total = world * Q * steps
+    return {"metric": "C2 exact successor lookups/s (whole node)", "unit": "lookups/s",
+            "value": total / dt_max, "ms_per_step": dt_max * 1e3 / steps, "steps": steps,
+            "kernel_ms_per_step": ev_ms, "lookups_per_s_event_timed": world * Q / (ev_ms * 1e-3),
+            "scaling": "weak",
+            "config": {"workload": "C2: 2^16-peer ring (splitmix 0x5EED0001), 2^20 keys per GPU "
+                                   "(0x5EED0002), cx_successor (bucket directory search)",
+                       "peers": N, "keys_per_gpu": Q},
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK * world / 1e9,
+                         "achieved": world * algo / (ev_ms * 1e-3) / 1e9,
+                         "frac": world * algo / (ev_ms * 1e-3) / (HBM_PEAK * world),
+                         "model": "SURVEY 8(d): 20 B per query (16 key + 4 owner) + 16 B per peer "
+                                  "once per batch, over the event-timed step (launch gaps "
+                                  "included; the kernel alone: profiles/r05)"},
+            "parity_on_sample": parity, "oracle_sample_keys": Q, "cpu_baseline": cpu}
+
+
+def c3_leg(args, world, rank, dev):
+    """BASELINE config C3 (configs[2]): a 2^20-peer ring (0x5EED0003), the full
+    m = 128 finger table (PopulateFingerTable converged, abstract_chord_peer.cpp:564-613)
+    and 2^24 finger-routed lookups with hop counts (0x5EED0004, src = q mod N;
+    GetSuccessor + ForwardRequest, abstract_chord_peer.cpp:318-337,
+    chord_peer.cpp:185-211) per GPU.  Times: the finger build alone (route
+    variant 0: rows only, no route table), fingers + route table (route-ready),
+    and the default walk over K steps.  Parity: the whole finger table and the
+    owners/hops of a 2^18-key sample against the oracle."""
+    import oracle as O
+    N, Q = 1 << 20, 1 << 24
+    ids = torch.empty((N, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(ids, SEED_C3_RING)
+    ring = chordx.Ring(ids, device=dev.index or 0)
+    del ids
+
+    def wall(fn, reps=3):
+        best = None
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            fn()
+            ring.sync()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return best
+    ring.set_route_variant(0)  # fingers only: rows, no route table
+    F = ring.build_fingers(copy_out=True)
+    t_fing = wall(ring.build_fingers)
+    ring.set_route_variant(-1)
+    ring.build_fingers()
+    t_ready = wall(ring.build_fingers)
+    keys = torch.empty((Q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(keys, SEED_C3_KEYS, offset=rank * Q)
+    src = (torch.arange(Q, device=dev, dtype=torch.int64) % N).to(torch.int32)
+    out = (torch.empty(Q, dtype=torch.int32, device=dev), torch.empty(Q, dtype=torch.uint8, device=dev),
+           torch.empty(Q, dtype=torch.uint8, device=dev))
+    for _ in range(args.warmup):
+        ring.route(src, keys, out=out)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dist.barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        ring.route(src, keys, out=out)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier(world)
+    dt_max = dist.max_over_ranks(time.perf_counter() - t0, world, dev)
+    kern_ms = dist.max_over_ranks(ev0.elapsed_time(ev1) / args.steps, world, dev)
+    ring.route_counters(True)
+    ring.route(src, keys, out=out)
+    g64, r16, xc, _ = ring.route_counters(False)
+    gathers = g64 + r16 + 2 * xc
+    sum_hops = int(out[1].to(torch.int64).sum().item())
+    owner_eq = bool((ring.successor(keys) == out[0]).all().item()) and int((out[2] != 0).sum()) == 0
+    ring_np = ring.ids()
+    th = host_threads()
+    Fw = O.fingers(ring_np, threads=th)
+    fingers_ok = bool((F == Fw).all())
+    m = 1 << 18
+    P = O.Peers(ring_np, Fw)
+    keys_np = keys[:m].cpu().numpy().view(np.uint64)
+    src_np = src[:m].cpu().numpy().view(np.uint32)
+    wo, wh, ws = O.route(P, src_np, keys_np, threads=th)
+    parity = fingers_ok and bool((out[0][:m].cpu().numpy().view(np.uint32) == wo).all()
+                                 and (out[1][:m].cpu().numpy() == wh).all() and (ws == 0).all())
+    parity = dist.all_over_ranks(parity, world, dev)
+    owner_eq = dist.all_over_ranks(owner_eq, world, dev)
+    cpu = None
+    if rank == 0:
+        fa, f1, _, _, _, dfa, df1 = _cpu_timed(
+            lambda q, t: O.fingers(ring_np, threads=t, rows=(0, q)), 4096, N, 3.0, th)
+        ra, r1, qa, q1, _, dra, dr1 = _cpu_timed(
+            lambda q, t: O.route(P, src_np[:q], keys_np[:q], threads=t), 2048, m, 6.0, th)
+        cpu = {"fingers_peers_per_s": fa, "fingers_peers_per_s_1core": f1,
+               "value": ra, "unit": "lookups/s", "value_1core": r1, "cores": th, "kind": "port",
+               "sample": f"fingers: or_fingers_build rows ({dfa:.2f} s on {th} threads, {df1:.2f} s "
+                         f"on 1); routes: or_route on the first {qa} keys ({dra:.2f} s on {th} "
+                         f"threads), {q1} on 1 ({dr1:.2f} s)",
+               "cpu_model": cpu_model()}
+    del F, Fw, P
+    ring.close()
+    fing_bytes = N * (CX_FINGERS_B * 4 + 16)
+    algo = Q * BYTES_STREAM + GRANULE * gathers
+    ref = Q * (REF_STREAM + REF_SRC) + REF_HOP * sum_hops
+    total = world * Q * args.steps
+    return {"metric": "C3 finger-routed lookups/s with hop counts (whole node)",
+            "unit": "lookups/s", "value": total / dt_max, "ms_per_step": dt_max * 1e3 / args.steps,
+            "steps": args.steps, "kernel_ms": kern_ms, "scaling": "weak",
+            "config": {"workload": "C3: 2^20-peer ring (splitmix 0x5EED0003), m = 128 fingers, "
+                                   "2^24 keys per GPU (0x5EED0004), src = q mod N",
+                       "peers": N, "keys_per_gpu": Q},
+            "fingers_build_ms": t_fing * 1e3, "fingers_and_route_table_ms": t_ready * 1e3,
+            "fingers_roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK / 1e9,
+                                 "achieved": fing_bytes / t_fing / 1e9,
+                                 "frac": fing_bytes / t_fing / HBM_PEAK,
+                                 "model": "SURVEY 8(d): 528 B per peer (128 x 4 B written + 16 B "
+                                          "read), over the wall time of cx_fingers_build (rows "
+                                          "only, one GPU)"},
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK * world / 1e9,
+                         "achieved": world * algo / (kern_ms * 1e-3) / 1e9,
+                         "frac": world * algo / (kern_ms * 1e-3) / (HBM_PEAK * world),
+                         "algo_bytes_per_launch": algo, "gathers_per_lookup": gathers / Q,
+                         "model": f"{BYTES_STREAM} B streams per lookup + {GRANULE} B per random "
+                                  "gather issued (counted), as the headline"},
+            "reference_work_model": {"bytes_per_launch": ref,
+                                     "GBps": ref / (kern_ms * 1e-3) / 1e9,
+                                     "note": "SURVEY 8(d): 25 + 64 B + 128 B per hop"},
+            "mean_hops": sum_hops / Q, "route_owner_equals_successor": owner_eq,
+            "parity_on_sample": parity, "fingers_equal_oracle": fingers_ok,
+            "oracle_sample_keys": m, "cpu_baseline": cpu}
 
 
 def main_arc(args):
@@ -701,7 +940,7 @@ def main():
     out = (owner, hops, status)
 
     route_variant, cz_escapes, table_bytes = ring.route_info()
-    kernel_name = {5: "k_route_tree<false, true>", 4: "k_route_tree<false, false>"}.get(
+    kernel_name = {5: "k_walk<false>", 4: "k_route_tree<false, false>"}.get(
         route_variant, f"route variant {route_variant}")
 
     # ---- warmup ----
@@ -782,6 +1021,16 @@ def main():
         churn["alloc_retries_all_ranks"] = dist.sum_over_ranks(
             sum(e["alloc"]["retries"] for e in churn["epochs"]), world, dev)
         churn["table_hash_equal"] = dist.all_over_ranks(churn["table_hash_equal"], world, dev)
+        # one warm membership epoch (churn -> route-ready) amortized over K
+        # timed batches of the headline: K Q / (route_ready + K t_batch)
+        rr = churn["route_ready_ms_max_over_ranks"]["warm"]
+        churn["epoch_amortized"] = {
+            f"K{k}": {"lookups_per_s": world * k * Q / ((rr + k * dt_max * 1e3 / args.steps) * 1e-3),
+                      "vs_headline": (k * dt_max * 1e3 / args.steps) / (rr + k * dt_max * 1e3 / args.steps)}
+            for k in (1, 8)}
+        churn["epoch_amortized"]["note"] = (
+            "a warm 1 %/1 % churn epoch's route-ready time (max over ranks) plus K timed batches "
+            "of the headline (2^25 lookups per GPU each), whole node")
         if "table_depth_ab" in churn:
             st = churn["table_depth_ab"]
             st["results_equal_default"] = dist.all_over_ranks(st["results_equal_default"], world, dev)
@@ -811,6 +1060,14 @@ def main():
         ring.close()
         chordx.pool_trim()
         c5 = c5_leg(args, world, rank, dev, backend)
+        chordx.pool_trim()
+
+    # ---- C2 / C3 (configs[1], configs[2]): small rings, after the bench ring ----
+    c2 = c3 = None
+    if not args.no_c2:
+        c2 = c2_leg(args, world, rank, dev)
+    if not args.no_c3:
+        c3 = c3_leg(args, world, rank, dev)
         chordx.pool_trim()
 
     traffic = None
@@ -860,6 +1117,8 @@ def main():
             "arc": arc,
             "churn_route_ready": churn,
             "c5": c5,
+            "c2": c2,
+            "c3": c3,
             "gather_roofline": gather,
             "route_variant": route_variant,
             "route_table_bytes": table_bytes,

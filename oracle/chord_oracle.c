@@ -549,17 +549,23 @@ size_t or_churn(const or_key *old_ring, size_t n_old, const or_key *joins, size_
     return k;
 }
 
-/* Core of the scan for one key: holders h[0..nh) are ring indices (OR_NONE =
- * departed / empty slot), in the order their maintenance passes run. */
-static void misplaced_one(const or_key *ring, size_t n_ring, or_key key, const uint32_t *holder,
-                          int nh, int n, uint32_t *nl, uint8_t *count, uint16_t *mask,
-                          uint8_t *tg) {
-    int nn = (int)(n_ring < (size_t)n ? n_ring : (size_t)n);
-    uint32_t sn = n_ring ? or_successor(ring, n_ring, key) : 0;
-    /* GetNSuccessors(key, n_) on the converged ring (a10) */
-    for (int j = 0; j < n; ++j) nl[j] = j < nn ? (uint32_t)((sn + j) % n_ring) : OR_NONE;
+/* Misplaced holders of one key given its new successor list nl[0..nn)
+ * (dhash_peer.cpp:298-348).  holder[0..nh) are ring indices (OR_NONE =
+ * departed / empty slot).
+ *
+ * ORDERING ASSUMPTION (parity-unpinned): when several holders of a key are
+ * misplaced, they are applied in list order -- holder j's pass runs after
+ * holders 0..j-1 have handed the key over, so has[] already records the
+ * successors they filled.  In the reference every holder runs its own 5-s
+ * maintenance thread (DHashPeer::MaintenanceLoop, dhash_peer.cpp:271-296);
+ * which holder hands the key to which lacking successor first depends on
+ * thread timing there.  The reference's own test pins only the single-holder
+ * case (DHashGlobalMaintenance.MisplacedKeys, dhash_test.cpp:123-149); the
+ * multi-holder target assignment is this restatement's contract
+ * (tests/test_gpu_parity.py::test_misplaced_multi_holder_order). */
+static void misplaced_from_list(const uint32_t *nl, int nn, const uint32_t *holder, int nh,
+                                uint16_t *mask, uint8_t *tg) {
     for (int j = 0; j < nh; ++j) tg[j] = 0xFF;
-    *count = (uint8_t)nn;
     uint8_t has[256];
     for (int r = 0; r < nn; ++r) {
         has[r] = 0;
@@ -579,6 +585,18 @@ static void misplaced_one(const or_key *ring, size_t n_ring, or_key key, const u
             if (!has[r]) { has[r] = 1; tg[j] = (uint8_t)r; break; }
     }
     *mask = m;
+}
+
+/* Core of the scan for one key on the converged ring: the new list is the
+ * n-window of the key's successor (GetNSuccessors, a10). */
+static void misplaced_one(const or_key *ring, size_t n_ring, or_key key, const uint32_t *holder,
+                          int nh, int n, uint32_t *nl, uint8_t *count, uint16_t *mask,
+                          uint8_t *tg) {
+    int nn = (int)(n_ring < (size_t)n ? n_ring : (size_t)n);
+    uint32_t sn = n_ring ? or_successor(ring, n_ring, key) : 0;
+    for (int j = 0; j < n; ++j) nl[j] = j < nn ? (uint32_t)((sn + j) % n_ring) : OR_NONE;
+    *count = (uint8_t)nn;
+    misplaced_from_list(nl, nn, holder, nh, mask, tg);
 }
 
 typedef struct {
@@ -624,6 +642,44 @@ void or_misplaced(const or_key *old_ring, size_t n_old, const or_key *new_ring, 
     mis_ctx c = {new_ring, n_new, keys, NULL, n, n, old_ring, n_old, old_to_new,
                  new_lists, count, mask, target};
     parallel_for(q, nthreads, mis_range, &c);
+}
+
+/* C5's CPU baseline: DHash maintenance computed as the
+ * reference computes it, by routed lookups.  Per key: the placement list on
+ * the old ring, GetNSuccessors(key, n) = n routed GetSuccessor lookups
+ * (or_nsucc, abstract_chord_peer.cpp:345-373; DHashPeer::Create,
+ * dhash_peer.cpp:103-129); its holders mapped to the new ring (old_to_new,
+ * departed -> OR_NONE); the new list by the same routed GetNSuccessors on the
+ * new ring; and the misplaced check of RunGlobalMaintenance
+ * (dhash_peer.cpp:298-348) against it.  Lookups start at peer q mod n of each
+ * ring.  Outputs as or_misplaced's plus the old lists and counts. */
+typedef struct {
+    const or_peers *Po, *Pn; const uint32_t *o2n; const or_key *keys; int n;
+    uint32_t *old_lists; uint8_t *old_count; uint32_t *new_lists; uint8_t *count;
+    uint16_t *mask; uint8_t *target;
+} mroute_ctx;
+static void mroute_range(void *c, size_t b, size_t e) {
+    mroute_ctx *x = (mroute_ctx *)c;
+    uint32_t hb[256];
+    for (size_t q = b; q < e; ++q) {
+        uint32_t *ol = x->old_lists + q * (size_t)x->n, *nl = x->new_lists + q * (size_t)x->n;
+        int no = or_nsucc(x->Po, (uint32_t)(q % x->Po->n), x->keys[q], x->n, ol);
+        for (int j = no; j < x->n; ++j) ol[j] = OR_NONE;
+        x->old_count[q] = (uint8_t)no;
+        for (int j = 0; j < x->n; ++j) hb[j] = j < no ? x->o2n[ol[j]] : OR_NONE;
+        int nn = or_nsucc(x->Pn, (uint32_t)(q % x->Pn->n), x->keys[q], x->n, nl);
+        for (int j = nn; j < x->n; ++j) nl[j] = OR_NONE;
+        x->count[q] = (uint8_t)nn;
+        misplaced_from_list(nl, nn, hb, x->n, x->mask + q, x->target + q * (size_t)x->n);
+    }
+}
+void or_maintenance_routed(const or_peers *P_old, const or_peers *P_new, const uint32_t *old_to_new,
+                           const or_key *keys, size_t q, int n, uint32_t *old_lists,
+                           uint8_t *old_count, uint32_t *new_lists, uint8_t *count,
+                           uint16_t *mask, uint8_t *target, int nthreads) {
+    mroute_ctx c = {P_old, P_new, old_to_new, keys, n, old_lists, old_count, new_lists, count,
+                    mask, target};
+    parallel_for(q, nthreads, mroute_range, &c);
 }
 
 /* ------------------------------------------------------------------------

@@ -155,6 +155,12 @@ void or_misplaced(const or_key *old_ring, size_t n_old, const or_key *new_ring, 
 /* General form: explicit holders (q x nh ring indices, OR_NONE = empty), as in
  * DHashGlobalMaintenance.MisplacedKeys (dhash_test.cpp:123-149) where keys are
  * inserted straight into a non-owner's db.  nh <= 16 (mask is 16-bit). */
+/* C5 CPU baseline: placement and maintenance lists by routed GetNSuccessors
+ * on the old and new rings (lookups from peer q mod n), misplaced check. */
+void or_maintenance_routed(const or_peers *P_old, const or_peers *P_new, const uint32_t *old_to_new,
+                           const or_key *keys, size_t q, int n, uint32_t *old_lists,
+                           uint8_t *old_count, uint32_t *new_lists, uint8_t *count,
+                           uint16_t *mask, uint8_t *target, int nthreads);
 void or_misplaced_holders(const or_key *ring, size_t n_ring, const or_key *keys, size_t q,
                           const uint32_t *holders, int nh, int n, uint32_t *new_lists,
                           uint8_t *count, uint16_t *mask, uint8_t *target, int nthreads);

@@ -181,6 +181,8 @@ def lib():
         L.or_churn.argtypes = [vp, sz, vp, sz, vp, sz, vp, vp]
         L.or_misplaced.argtypes = [vp, sz, vp, sz, vp, vp, sz, i, vp, vp, vp, vp, i]
         L.or_misplaced_holders.argtypes = [vp, sz, vp, sz, vp, i, i, vp, vp, vp, vp, i]
+        L.or_maintenance_routed.argtypes = [ctypes.POINTER(_Peers), ctypes.POINTER(_Peers), vp, vp,
+                                            sz, i, vp, vp, vp, vp, vp, vp, i]
         L.or_splitmix_keys.argtypes = [ctypes.c_uint64, sz, sz, vp]
         L.or_ida_encoding_matrix.argtypes = [i, i, i, vp]
         L.or_ida_vandermonde_inverse.restype = i
@@ -352,6 +354,24 @@ def misplaced(old_ring, new_ring, o2n, keys, n, threads=None):
                        _p(keys), q, n, _p(lists), _p(count), _p(mask), _p(target),
                        threads or default_threads())
     return lists, count, mask, target
+
+
+def maintenance_routed(P_old: Peers, P_new: Peers, o2n, keys, n, threads=None):
+    """C5 by routed lookups (or_maintenance_routed): (old_lists, old_count,
+    new_lists, count, mask, target), lookups from peer q mod n of each ring."""
+    keys = _keys(keys)
+    o2n = np.ascontiguousarray(o2n, dtype=np.uint32)
+    q = len(keys)
+    old_lists = np.empty((q, n), dtype=np.uint32)
+    old_count = np.empty(q, dtype=np.uint8)
+    lists = np.empty((q, n), dtype=np.uint32)
+    count = np.empty(q, dtype=np.uint8)
+    mask = np.empty(q, dtype=np.uint16)
+    target = np.empty((q, n), dtype=np.uint8)
+    lib().or_maintenance_routed(ctypes.byref(P_old.s), ctypes.byref(P_new.s), _p(o2n), _p(keys), q,
+                                n, _p(old_lists), _p(old_count), _p(lists), _p(count), _p(mask),
+                                _p(target), threads or default_threads())
+    return old_lists, old_count, lists, count, mask, target
 
 
 def misplaced_holders(ring, keys, holders, n, threads=None):

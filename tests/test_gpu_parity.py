@@ -428,6 +428,49 @@ def test_misplaced_holders_random(cx, O):
         assert (a == b).all()
 
 
+def test_misplaced_multi_holder_order(cx, O):
+    """Several misplaced holders of one key (round-4 verdict item 7): holders
+    are applied in list order, each handing the key to the first successor in
+    list order that still lacks it (chord_oracle.c misplaced_from_list: the
+    ordering assumption, parity-unpinned -- in the reference each holder's own
+    maintenance thread runs RunGlobalMaintenance, dhash_peer.cpp:271-348, and
+    thread timing decides).  Hand-derived on a 40-peer ring, n = 4; GPU equals
+    the oracle and the hand derivation."""
+    ids = O.splitmix_keys(0x0DE1, 40)
+    want = O.ring_build(ids)
+    ring = cx.Ring(ids)
+    keys = O.splitmix_keys(0x0DE2, 64)
+    s = O.successor(want, keys).astype(np.int64)
+    n, N = 4, len(want)
+    w = lambda k, j: (s[k] + j) % N  # noqa: E731  rank j of key k's new list
+    holders = np.empty((64, 5), dtype=np.uint32)
+    exp_mask = np.zeros(64, dtype=np.uint16)
+    exp_tg = np.full((64, 5), 0xFF, dtype=np.uint8)
+    for k in range(64):
+        far = [(s[k] + 10 + 3 * j) % N for j in range(3)]  # never in the 4-window
+        case = k % 4
+        if case == 0:   # two misplaced holders, ranks 1 and 2 held: targets ranks 0, 3
+            h = [far[0], w(k, 2), far[1], w(k, 1), 0xFFFFFFFF]
+            exp_mask[k], exp_tg[k, 0], exp_tg[k, 2] = 0b101, 0, 3
+        elif case == 1:  # three misplaced, nothing held: targets 0, 1, 2 in list order
+            h = [far[2], far[0], 0xFFFFFFFF, far[1], w(k, 3)]
+            exp_mask[k], exp_tg[k, 0], exp_tg[k, 1], exp_tg[k, 3] = 0b1011, 0, 1, 2
+        elif case == 2:  # every rank held: misplaced holders keep the key (no target)
+            h = [w(k, 0), far[0], w(k, 1), w(k, 2), w(k, 3)]
+            exp_mask[k] = 0b10
+        else:           # five misplaced, four ranks: the fifth finds none left
+            h = [far[0], far[1], far[2], (s[k] + 20) % N, (s[k] + 25) % N]
+            exp_mask[k] = 0b11111
+            exp_tg[k, :4] = [0, 1, 2, 3]
+        holders[k] = h
+    got = ring.misplaced_holders(keys, holders, n)
+    exp = O.misplaced_holders(want, keys, holders, n)
+    for a, b in zip(got, exp):
+        assert (a == b).all()
+    assert (got[2].view(np.uint16) == exp_mask).all()
+    assert (got[3] == exp_tg).all()
+
+
 # ---------------------------------------------------------------- a2 InBetween
 def test_in_between_gpu(cx, O, refvec):
     def u256(v):

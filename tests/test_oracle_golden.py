@@ -427,3 +427,22 @@ def test_get_pred_lone_peer_is_itself(O):
     (abstract_chord_peer.cpp:383-385; ChordGetPred.LocalKey's one-peer ring)."""
     ring = _ring(O, [0xfffffffffffffffffffffffffffffff])
     assert (O.predecessor(ring, O.keys_from_ints([1 << 120, 0, 5])) == 0).all()
+
+
+def test_maintenance_routed_equals_window_restatement(O):
+    """C5's CPU baseline (or_maintenance_routed: placement and maintenance
+    lists by routed GetNSuccessors, abstract_chord_peer.cpp:345-373, then
+    RunGlobalMaintenance's check, dhash_peer.cpp:298-348) equals the
+    converged-window restatement the GPU parity tests use (or_misplaced,
+    or_nsucc) on a churned ring."""
+    old = O.ring_build(O.splitmix_keys(0xC5A0, 3000))
+    joins, leaves = O.splitmix_keys(0xC5A1, 60), old[::50][:60]
+    new, o2n = O.churn(old, joins, leaves)
+    keys = O.splitmix_keys(0xC5A2, 4000)
+    Po, Pn = O.Peers(old, O.fingers(old)), O.Peers(new, O.fingers(new))
+    ol, oc, nl, nc, mask, tg = O.maintenance_routed(Po, Pn, o2n, keys, 14)
+    wl, wc, wm, wt = O.misplaced(old, new, o2n, keys, 14)
+    xl, xc = O.nsucc(Po, keys, 14)
+    assert (nl == wl).all() and (nc == wc).all() and (mask == wm).all() and (tg == wt).all()
+    assert (ol == xl).all() and (oc == xc).all()
+    assert int((mask != 0).sum()) > 0
