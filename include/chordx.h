@@ -410,6 +410,16 @@ int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src
                              const cx_u128 *keys, size_t q, uint64_t cap, cx_u128 *send_keys,
                              uint32_t *send_src, uint64_t *send_hint, uint32_t *perm,
                              uint64_t *counts);
+/* cx_arc_partition_regions without a host synchronisation: counts_dev
+ * (device, world + 1 int64) receives counts[0..world) and, at [world], 1 if
+ * some destination received more than cap lookups (then that destination's
+ * region holds nothing and the caller re-partitions with cx_arc_partition).
+ * Everything runs asynchronously on the ring's stream, so a caller can
+ * partition several pieces and exchange all their counts in one collective. */
+int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_t *src,
+                                   const cx_u128 *keys, size_t q, uint64_t cap,
+                                   cx_u128 *send_keys, uint32_t *send_src, uint64_t *send_hint,
+                                   uint32_t *perm, int64_t *counts_dev);
 int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
                  uint64_t *res);
 /* cx_arc_route with the origins' source hints (cx_arc_partition_regions

@@ -188,35 +188,78 @@ class ArcRouter:
         # origin-resolved source hints ride along (8 B) when the engine has
         # them: the arc rank's walk then needs no source IDs (a random gather)
         hints = regions and self.hints and getattr(eng, "arc_hints", False)
+        dev = self.comm_device if self.comm_device is not None else keys.device
+        # counts stay on the device (RCCL): every piece's partition writes its
+        # counts and overflow flag into one row, one all_gather carries them
+        # all, one pinned copy brings the gathered matrix to the host
+        on_dev = regions and hasattr(eng, "arc_partition_regions_async") and \
+            torch.device(dev).type == "cuda" and keys.is_cuda
+        W = G + 1  # per piece: G counts + overflow flag
+        row = torch.zeros(1 + kmax * W, dtype=torch.int64, device=dev)
         parts, caps = [], []
+
+        def piece_cap(c):
+            qc = cut[c + 1] - cut[c]
+            return max(1, qc // G + qc // (4 * G) + 4096)
+
         for c in range(k):
             ps, pk = src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]]
             part = None
-            if regions:
-                qc = cut[c + 1] - cut[c]
-                cap = max(1, qc // G + qc // (4 * G) + 4096)
+            cap = 0
+            if on_dev:
+                cap = piece_cap(c)
+                part = eng.arc_partition_regions_async(G, ps, pk, cap, row[1 + c * W: 1 + (c + 1) * W],
+                                                       hints=hints)
+                part = part[:3] + (None,) + part[3:]  # counts: after the gather
+            elif regions:
+                cap = piece_cap(c)
                 part = eng.arc_partition_regions(G, ps, pk, cap, hints=hints) if hints else \
                     eng.arc_partition_regions(G, ps, pk, cap)
             if part is None:
                 part, cap = eng.arc_partition(G, ps, pk), 0
+            if part[3] is not None:
+                row[1 + c * W: 1 + c * W + G] = torch.tensor(part[3], dtype=torch.int64)
             parts.append(part)
             caps.append(cap)
-        hinted = [len(p) > 4 for p in parts]
-        dev = self.comm_device if self.comm_device is not None else parts[0][0].device
-        my_h = bool(hints) and all(hinted)
-        row = [k | (int(my_h) << 20)] + [x for p in parts for x in p[3]] + [0] * ((kmax - k) * G)
-        mine = torch.tensor(row, dtype=torch.int64, device=dev)
-        mat = torch.empty((G, 1 + kmax * G), dtype=torch.int64, device=dev)
-        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
-        if mat.is_cuda:
-            if self._mat_host is None or self._mat_host.shape != mat.shape:
-                self._mat_host = torch.empty(mat.shape, dtype=torch.int64, pin_memory=True)
-            self._mat_host.copy_(mat, non_blocking=True)
-            torch.cuda.current_stream(mat.device).synchronize()
-            mat = self._mat_host
+
+        def gather(row):
+            mat = torch.empty((G, row.numel()), dtype=torch.int64, device=row.device)
+            tdist.all_gather_into_tensor(mat.view(-1), row, group=self.group)
+            if mat.is_cuda:
+                if self._mat_host is None or self._mat_host.shape != mat.shape:
+                    self._mat_host = torch.empty(mat.shape, dtype=torch.int64, pin_memory=True)
+                self._mat_host.copy_(mat, non_blocking=True)
+                torch.cuda.current_stream(mat.device).synchronize()
+                return self._mat_host
+            return mat
+
+        my_h = bool(hints) and all(len(p) > 4 for p in parts)
+        row[0] = k | (int(my_h) << 20)
+        mat = gather(row)
+        ovf = [[int(mat[r, 1 + c * W + G]) for c in range(kmax)] for r in range(G)]
+        if any(any(o) for o in ovf):
+            # a piece crowded one destination past its region: that rank
+            # partitions it again in two passes (host counts) and every rank
+            # gathers the rows once more (all ranks see the same flags)
+            for c in range(k):
+                if ovf[self.rank][c]:
+                    ps, pk = src[cut[c]:cut[c + 1]], keys[cut[c]:cut[c + 1]]
+                    parts[c], caps[c] = eng.arc_partition(G, ps, pk), 0
+            row = mat[self.rank].clone()
+            for c in range(k):
+                if ovf[self.rank][c]:
+                    row[1 + c * W: 1 + c * W + G] = torch.tensor(parts[c][3], dtype=torch.int64)
+                row[1 + c * W + G] = 0
+            my_h = bool(hints) and all(len(p) > 4 for p in parts)
+            row[0] = k | (int(my_h) << 20)
+            mat = gather(row.to(dev))
+        for c in range(k):  # this rank's counts, as host lists (the send splits)
+            if parts[c][3] is None:
+                parts[c] = parts[c][:3] + ([int(x) for x in mat[self.rank, 1 + c * W: 1 + c * W + G]],) \
+                    + parts[c][4:]
         kg = int((mat[:, 0] & 0xFFFFF).max())  # pieces every rank runs
         use_h = bool(int((mat[:, 0] >> 20).min()))  # every rank's pieces carry hints
-        recv = [[int(mat[r, 1 + c * G + self.rank]) for r in range(G)] for c in range(kg)]
+        recv = [[int(mat[r, 1 + c * W + self.rank]) for r in range(G)] for c in range(kg)]
         if kg > k:  # this rank's extra pieces are empty
             e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=keys.device),
                  [0] * G, torch.empty(0, dtype=torch.int64, device=keys.device))

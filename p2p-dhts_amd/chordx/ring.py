@@ -567,6 +567,30 @@ class Ring:
         out = (skeys, ssrc, perm, [int(c) for c in counts])
         return out + (shint,) if hints else out
 
+    def arc_partition_regions_async(self, world: int, src, keys, cap: int, counts,
+                                    hints: bool = False):
+        """cx_arc_partition_regions_async: as arc_partition_regions, but the
+        counts (and, at counts[world], the overflow flag) land in `counts`, a
+        device int64 tensor of world + 1 elements, with no host
+        synchronisation; (send_keys, send_src, perm[, send_hint])."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src) and _is_dev(counts)):
+            raise TypeError("arc routing takes device tensors")
+        if not (counts.dtype == torch.int64 and counts.is_contiguous()
+                and counts.numel() == world + 1):
+            raise TypeError("counts: a contiguous int64 device tensor of world + 1 elements")
+        q = keys.shape[0]
+        skeys = torch.empty((world * cap, 2), dtype=torch.int64, device=keys.device)
+        ssrc = torch.empty(world * cap, dtype=torch.int32, device=keys.device)
+        perm = torch.empty(q, dtype=torch.int32, device=keys.device)
+        shint = torch.empty(world * cap, dtype=torch.int64, device=keys.device) if hints else None
+        self._arc_stream()
+        L.check(L.lib().cx_arc_partition_regions_async(self._h, world, _ptr(src), _ptr(keys), q,
+                                                       cap, _ptr(skeys), _ptr(ssrc), _ptr(shint),
+                                                       _ptr(perm), _ptr(counts)))
+        return (skeys, ssrc, perm, shint) if hints else (skeys, ssrc, perm)
+
     def arc_route(self, src, keys, res=None, hint=None):
         """Packed results (int64: owner | hops << 32 | status << 40 | 1 << 63)
         of lookups received from every rank, in input order (cx_arc_route;

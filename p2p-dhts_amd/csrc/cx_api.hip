@@ -2224,6 +2224,34 @@ int cx_arc_partition_regions(const cx_ring *ring, int world, const uint32_t *src
     return CX_OK;
 }
 
+int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_t *src,
+                                   const cx_u128 *keys, size_t q, uint64_t cap,
+                                   cx_u128 *send_keys, uint32_t *send_src, uint64_t *send_hint,
+                                   uint32_t *perm, int64_t *counts_dev) {
+    CX_CHECK(ring && counts_dev, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(q == 0 || (src && keys && send_keys && send_src && perm), CX_E_INVALID,
+             "null buffer");
+    CX_CHECK(cap >= 1 && (uint64_t)world * cap < (1ull << 32) && q < (1ull << 32), CX_E_INVALID,
+             "cap must be >= 1 with world * cap < 2^32");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    CX_CHECK(!send_hint || ring->d_ring_ext, CX_E_STATE, "arc not built (cx_arc_build)");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    hipStream_t s = ring->stream;
+    uint32_t *dcur = ring->d_scratch + CX_ARC_MAX_RANKS, *dovf = ring->d_scratch + 2 * CX_ARC_MAX_RANKS;
+    CX_HIP(cxk::arc_cursor_init(dcur, dovf, world, (uint32_t)cap, s));
+    CX_HIP(cxk::arc_partition_regions(src, reinterpret_cast<const cell128 *>(keys), q,
+                                      ring->d_arc_bounds, ring->arc_nb, world, (uint32_t)cap,
+                                      dcur, dovf, reinterpret_cast<cell128 *>(send_keys),
+                                      send_src, perm, send_hint, ring->d_ring_ext, ring->n,
+                                      ring->pk_ib, s));
+    CX_HIP(cxk::arc_counts_out(dcur, dovf, world, (uint32_t)cap, counts_dev, s));
+    return CX_OK;
+}
+
 int cx_arc_route_hinted(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
                         const uint64_t *hint, size_t q, uint64_t *res) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
@@ -2234,10 +2262,10 @@ int cx_arc_route_hinted(const cx_ring *ring, const uint32_t *src, const cx_u128 
     if (rc) return rc;
     SearchView v = ring->sv();
     v.dir = ring->d_dir;
-    CX_HIP(cxk::route_arc_kf(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
-                             ring->rt_l0, ring->rt_R, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
-                             ring->arc_M, src, reinterpret_cast<const cell128 *>(keys), q, res,
-                             ring->stream, hint));
+    CX_HIP(cxk::route_walk_arc(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
+                               ring->rt_l0, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
+                               ring->arc_M, src, reinterpret_cast<const cell128 *>(keys), q, hint,
+                               res, ring->stream));
     return CX_OK;
 }
 
@@ -2251,10 +2279,10 @@ int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, 
     if (rc) return rc;
     SearchView v = ring->sv();
     v.dir = ring->d_dir;  // exact below-table fingers by directory search
-    CX_HIP(cxk::route_arc_kf(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
-                             ring->rt_l0, ring->rt_R, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
-                             ring->arc_M, src, reinterpret_cast<const cell128 *>(keys), q, res,
-                             ring->stream));
+    CX_HIP(cxk::route_walk_arc(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
+                               ring->rt_l0, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
+                               ring->arc_M, src, reinterpret_cast<const cell128 *>(keys), q,
+                               nullptr, res, ring->stream));
     return CX_OK;
 }
 

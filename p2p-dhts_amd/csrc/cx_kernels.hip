@@ -1594,7 +1594,6 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
 // interval, and an undecided one fetches the exact IDs (A_FIXC / A_FIXT).
 // ---------------------------------------------------------------------------
 constexpr uint32_t CZ_NONE = 0xFFFFFFFFu;
-constexpr uint8_t CX_QI_ARC_MISS = 0xFE;  // key-first arc walk left the rank's rows (never on a correct layout)
 constexpr int CZ_RES_WIN = 256;  // 26 KB of LDS per 256-lane block: 6 blocks per CU
 constexpr int CZ_WAVES = 5;      // waves per SIMD the VGPR budget allows (88 VGPRs; 6 spills)
 
@@ -2686,28 +2685,17 @@ struct TreeIO {
     uint32_t *owner;
     uint8_t *hops;
     uint8_t *status;
-    uint64_t *res_out;   // key-first arc walk: packed results in input order
-    const uint64_t *dh;  // key-first arc walk: the origin's source hints (or null)
-    // STATS build only: [0] 64-B table gathers, [1] exact 16-B ring gathers,
-    // [2] exact hops (one F + one ring gather each), [3] lookups started
-    unsigned long long *stats;
 };
 
-// STATS: the same walk, additionally counting the random gathers it issues
-// (bench.py's algorithmic-bytes model and request-rate roofline); the timed
-// kernel is the STATS = false instantiation.
-// KF (key-first arc walk): arc-mode tables (replicated top planes + this
-// rank's rows), replicated-mode I/O: lookups (src, keys) in, one packed result
-// per lookup out in input order (io.res_out).  Every lookup finishes here
-// (records were sent to the rank of their key's arc); a row that is not local
-// would be a layout bug and reports CX_QI_ARC_MISS.
-template <bool ARC, bool CZ, bool STATS = false, bool KF = false>
+// Instantiations: <false, false> the lookahead-tree walk (rings above 2^24
+// peers), <true, true> the record protocol's arc walk (chordx.arc "records";
+// the default key-first arc walk is k_walk<false, true>, cx_walk.hip).
+template <bool ARC, bool CZ>
 __global__ __launch_bounds__(RT_BLOCK) __attribute__((amdgpu_waves_per_eu(CZ ? CZ_WAVES : 1)))
 void k_route_tree(TreeIO io) {
     constexpr int RW = CZ ? CZ_RES_WIN : RES_WIN;  // cz: smaller window, more waves per CU
     static_assert(!ARC || CZ, "arc mode walks pattern-keyed (cz) rows");
-    static_assert(!KF || ARC, "key-first walks arc tables");
-    constexpr bool RIO = !ARC || KF;  // results staged per wave, written in input order
+    constexpr bool RIO = !ARC;  // results staged per wave, written in input order
     __shared__ uint64_t res_all[RIO ? RT_BLOCK / 64 : 1][RIO ? RW : 1];
     __shared__ uint4 ent_all[RT_BLOCK][4];       // each lane's current 64-B entry
     __shared__ uint64_t addr_all[RT_BLOCK];      // entry index + 1 wanted by each lane (0: none)
@@ -2754,9 +2742,7 @@ void k_route_tree(TreeIO io) {
     uint64_t pqid = 0;
     u128 pkey = 0, pa = 0, pb = 0;
     uint32_t psrc = 0, ph = 0;
-    uint64_t pdh = 0;          // KF with hints: the origin's source hint
-    uint32_t n_g64 = 0, n_r16 = 0, n_xc = 0, n_q = 0;  // STATS counters
-    uint32_t *xcp = STATS ? &n_xc : nullptr;
+    uint32_t *xcp = nullptr;
 
     // outcome of a finished query (ARC: local delivery or a result record)
     auto deliver = [&](size_t idx, uint64_t id, uint32_t o, uint32_t hh, uint8_t stt) {
@@ -2795,7 +2781,7 @@ void k_route_tree(TreeIO io) {
                 (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
             if (bst == B_EMPTY && rank < avail) {
                 pq = head + rank;
-                if (ARC && !KF && io.in) {
+                if (ARC && io.in) {
                     const ArcRec r = io.in[pq];
                     pkey = ((u128)r.w1 << 64) | r.w0;
                     pqid = r.qid;
@@ -2805,8 +2791,7 @@ void k_route_tree(TreeIO io) {
                 } else {  // a new lookup (arc mode: issued on this rank)
                     pkey = ld128(io.keys + pq);
                     psrc = io.src[pq];
-                    if (KF && io.dh) pdh = io.dh[pq];
-                    pqid = (ARC && !KF) ? ((uint64_t)io.self << ARC_ORIGIN_SHIFT) | pq : pq;
+                    pqid = ARC ? ((uint64_t)io.self << ARC_ORIGIN_SHIFT) | pq : pq;
                     ph = 0;
                     pkind = ARC_NEW;
                 }
@@ -2838,10 +2823,6 @@ void k_route_tree(TreeIO io) {
                     (uint64_t)((lvl - l0) * 2 + rb) * io.M + j;
             }
             addr_all[threadIdx.x] = mode == A_HOP ? e + 1 : 0;
-            if (STATS) {
-                n_g64 += mode == A_HOP;
-                n_r16 += mode == A_FIXC ? 1u : ((mode == A_FIXT || mode == A_EXACT) ? 2u : 0u);
-            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -2872,9 +2853,7 @@ void k_route_tree(TreeIO io) {
             xb = ld128(io.ring + (cur + 1 == n ? 0u : cur + 1));
         }
         if (bst == B_KS) {
-            if (KF && io.dh) {
-                // the origin resolved the start: no source pair to load
-            } else if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
+            if (pkind != ARC_RESULT && pkind != ARC_NONE && psrc < n) {
                 // non-temporal (0.5 %, profiles/r04/ntload_ab/source_pair)
                 if (pkind == ARC_NEW) pa = ld128_nt(io.ring_ext + psrc);  // pred: local check only
                 pb = ld128_nt(io.ring_ext + psrc + 1);
@@ -2913,7 +2892,6 @@ void k_route_tree(TreeIO io) {
                 if (!cex) {  // rare: exact id of cur for the exact hop
                     clo = ld128(io.ring + cur);
                     cex = true;
-                    if (STATS) ++n_r16;
                 }
                 if (cz_exact(c, key, clo, dmin, dmax, cur, h, lvl, own, st, xcp))
                     fin = true;
@@ -2969,11 +2947,7 @@ void k_route_tree(TreeIO io) {
                              own, st, xcp, mode == A_EXACT, xb)
                    : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own, st);
             if (r == 1) fin = true;
-            if (KF && r == 2) {
-                fin = true;
-                own = CX_NONE;
-                st = CX_QI_ARC_MISS;
-            } else if (ARC && r == 2) {  // continue on the rank of the key's arc
+            if (ARC && r == 2) {  // continue on the rank of the key's arc
                 ArcRec o;
                 o.w0 = (uint64_t)key;
                 o.w1 = (uint64_t)(key >> 64);
@@ -2999,7 +2973,6 @@ void k_route_tree(TreeIO io) {
             cs = -1;
             own = CX_NONE;
             st = CX_Q_OK;
-            if (STATS) ++n_q;
             int done = 1;
             if (ARC && pkind == ARC_RESULT) {
                 // a result coming home: deliver it (w0 = owner | status << 32)
@@ -3013,22 +2986,6 @@ void k_route_tree(TreeIO io) {
                 done = 0;
             } else if (cur >= n) {
                 st = CX_Q_BADPEER;
-            } else if (KF && io.dh) {
-                if (pdh == ARC_HINT_LOCAL) {
-                    own = cur;  // StoredLocally at the source (the origin checked it)
-                } else {
-                    // d = key - id_src in units of 2^gs from the origin; id_src is
-                    // fetched (A_FIXC) only if a decision needs it exactly
-                    cex = false;
-                    dmin = dmax = pdh;
-                    done = cz_plan(c, key, clo, cex, dmin, dmax, cur, h, pn, mode, lvl, rb, cs, ri,
-                                   ent32, own, st, xcp);
-                    if (done == 2) {
-                        own = CX_NONE;
-                        st = CX_QI_ARC_MISS;
-                        done = 1;
-                    }
-                }
             } else if (pkind == ARC_NEW && (n == 1 || (key - pa - 1) <= (pb - pa - 1))) {
                 own = cur;  // StoredLocally at the source: 0 hops
             } else {
@@ -3039,11 +2996,7 @@ void k_route_tree(TreeIO io) {
                                     ri, ent32, own, st, xcp)
                           : tree_plan(c, key, clo, cex, cur, h, pn, mode, lvl, cs, ri, ent, own,
                                       st);
-                if (KF && done == 2) {
-                    own = CX_NONE;
-                    st = CX_QI_ARC_MISS;
-                    done = 1;
-                } else if (ARC && done == 2) {
+                if (ARC && done == 2) {
                     ArcRec o;
                     o.w0 = (uint64_t)key;
                     o.w1 = (uint64_t)(key >> 64);
@@ -3070,29 +3023,14 @@ void k_route_tree(TreeIO io) {
                 const uint64_t v = inr ? res[idx & (RW - 1)] : 0ull;
                 if (__ballot(!inr || (v >> 63)) != ~0ull) break;
                 if (inr) {
-                    if (KF) {
-                        __builtin_nontemporal_store(v, io.res_out + idx);
-                    } else {
-                        io.owner[idx] = (uint32_t)v;
-                        io.hops[idx] = (uint8_t)(v >> 32);
-                        if (io.status) io.status[idx] = (uint8_t)(v >> 40);
-                    }
+                    io.owner[idx] = (uint32_t)v;
+                    io.hops[idx] = (uint8_t)(v >> 32);
+                    if (io.status) io.status[idx] = (uint8_t)(v >> 40);
                     res[idx & (RW - 1)] = 0;
                 }
                 flushed += 64;
             }
         }
-    }
-    if (STATS) {
-        uint64_t v[4] = {n_g64, n_r16, n_xc, n_q};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
-        }
-        if (lane == 0)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) atomicAdd(io.stats + k, (unsigned long long)v[k]);
     }
 }
 
@@ -3180,43 +3118,6 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
     k_route_tree<true, true><<<blocks, RT_BLOCK, 0, s>>>(io);
-    return hipGetLastError();
-}
-
-// Key-first arc walk (k_route_tree<true, true, false, true>): lookups received
-// from every rank, walked from their sources over the replicated top planes
-// and this rank's rows; packed results (owner | hops << 32 | status << 40 |
-// 1 << 63) in input order.
-hipError_t route_arc_kf(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
-                        int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo,
-                        uint32_t M, const uint32_t *src, const cell128 *keys, size_t q,
-                        uint64_t *res, hipStream_t s, const uint64_t *dh) {
-    if (q == 0) return hipSuccess;
-    TreeIO io = {};
-    io.dh = dh;
-    io.src = src;
-    io.keys = keys;
-    io.ring_ext = ring_ext;
-    io.ring = ring;
-    io.n = (uint32_t)n;
-    io.tree = reinterpret_cast<const uint4 *>(cz);
-    io.l0 = l0;
-    io.R = R;
-    io.ib = ib;
-    io.sv = sv;
-    io.Lh = Lh;
-    io.plo = plo;
-    io.M = M;
-    io.q = q;
-    io.res_out = res;
-    static const unsigned resident = resident_grid(k_route_tree<true, true, false, true>, RT_BLOCK);
-    size_t waves = (size_t)resident * (RT_BLOCK / 64);
-    const size_t small = (q + 1023) / 1024;
-    if (small < waves) waves = small ? small : 1;
-    io.chunk = (q + waves - 1) / waves;
-    waves = (q + io.chunk - 1) / io.chunk;
-    const unsigned blocks = (unsigned)((waves * 64 + RT_BLOCK - 1) / RT_BLOCK);
-    k_route_tree<true, true, false, true><<<blocks, RT_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 
@@ -3516,6 +3417,33 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
         in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, cap, ovf, sd, ring_ext,
         (uint32_t)n, cz_shift(ib));
+    return hipGetLastError();
+}
+
+// Region cursors of the single-pass partition (cursor[g] = g cap) and its
+// overflow flag, set on the device (no host copy in the partition path).
+__global__ void k_arc_cursor_init(uint32_t *cursor, uint32_t *ovf, int G, uint32_t cap) {
+    const int g = threadIdx.x;
+    if (g < G) cursor[g] = (uint32_t)g * cap;
+    if (g == 0) *ovf = 0;
+}
+
+// counts[g] = cursor[g] - g cap (int64, a collective's input), counts[G] = overflow.
+__global__ void k_arc_counts_out(const uint32_t *cursor, const uint32_t *ovf, int G, uint32_t cap,
+                                 int64_t *counts) {
+    const int g = threadIdx.x;
+    if (g < G) counts[g] = (int64_t)(cursor[g] - (uint32_t)g * cap);
+    if (g == 0) counts[G] = *ovf ? 1 : 0;
+}
+
+hipError_t arc_cursor_init(uint32_t *cursor, uint32_t *ovf, int G, uint32_t cap, hipStream_t s) {
+    k_arc_cursor_init<<<1, 64, 0, s>>>(cursor, ovf, G, cap);
+    return hipGetLastError();
+}
+
+hipError_t arc_counts_out(const uint32_t *cursor, const uint32_t *ovf, int G, uint32_t cap,
+                          int64_t *counts, hipStream_t s) {
+    k_arc_counts_out<<<1, 64, 0, s>>>(cursor, ovf, G, cap, counts);
     return hipGetLastError();
 }
 

@@ -213,11 +213,13 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
                      int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo, uint32_t M,
                      int self, const ArcRec *in, const uint32_t *src, const cell128 *keys, size_t q,
                      ArcRec *out, uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
-// Key-first SoA protocol (cx_arc_partition / cx_arc_route / cx_arc_deliver).
-hipError_t route_arc_kf(const cell128 *ring_ext, const cell128 *ring, size_t n, const uint64_t *cz,
-                        int l0, int R, int ib, const SearchView &sv, int Lh, uint32_t plo,
-                        uint32_t M, const uint32_t *src, const cell128 *keys, size_t q,
-                        uint64_t *res, hipStream_t s, const uint64_t *dh = nullptr);
+// Key-first SoA protocol (cx_arc_partition / cx_arc_route / cx_arc_deliver):
+// the straight-line walk (cx_walk.hip) over the rank's arc table, packed
+// results in input order; dh = the origin's source hints or null.
+hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n,
+                          const uint64_t *arc_tree, int l0, int ib, const SearchView &sv, int Lh,
+                          uint32_t plo, uint32_t M, const uint32_t *src, const cell128 *keys,
+                          size_t q, const uint64_t *dh, uint64_t *res, hipStream_t s);
 hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
                          const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
                          uint32_t *cursor_dev, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
@@ -227,6 +229,10 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
                                  uint32_t *cursor_dev, uint32_t *ovf, cell128 *skeys,
                                  uint32_t *ssrc, uint32_t *perm, uint64_t *sd,
                                  const cell128 *ring_ext, size_t n, int ib, hipStream_t s);
+// Device-side region cursors / counts of the single-pass partition (G <= 64).
+hipError_t arc_cursor_init(uint32_t *cursor, uint32_t *ovf, int G, uint32_t cap, hipStream_t s);
+hipError_t arc_counts_out(const uint32_t *cursor, const uint32_t *ovf, int G, uint32_t cap,
+                          int64_t *counts, hipStream_t s);
 hipError_t arc_deliver(const uint64_t *res, const uint32_t *perm, size_t q, uint32_t *owner,
                        uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t arc_seed(const uint32_t *src, const cell128 *keys, size_t q, int self, ArcRec *out,

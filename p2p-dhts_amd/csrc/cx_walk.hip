@@ -32,6 +32,7 @@ constexpr int WK_BLOCK = 256;
 constexpr int WK_RES = 256;  // staged results per wave (LDS ring, 64-result flushes)
 constexpr uint32_t WK_NONE = 0xFFFFFFFFu;
 constexpr uint32_t WK_CZ_NONE = 0xFFFFFFFFu;  // a node the 4-B format cannot hold (CZ_NONE)
+constexpr uint32_t CX_QI_ARC_MISS = 0xFE;     // key-first arc walk left the rank's rows
 
 enum { M_NONE = 0, M_HOP = 1, M_FIX = 2, M_EXACT = 3, M_FIXT = 4 };
 enum { B_EMPTY = 0, B_KEYS = 1, B_READY = 2 };
@@ -52,6 +53,14 @@ struct WalkIO {
     // counting build: [0] table gathers, [1] exact 16-B ID gathers, [2] exact
     // hops through the directory (a directory entry + an ID each), [3] lookups
     unsigned long long *stats;
+    // key-first arc walk (KF): the rank's arc table = the replicated planes of
+    // levels [Lh, 128) for all n peers, then the planes of levels [l0, Lh) for
+    // the M peers plo, plo + 1, ... (cyclic: the arc and its halo); lookups
+    // start from the origin's hint dh; packed results in input order (res_out)
+    int Lh;
+    uint32_t plo, M;
+    const uint64_t *dh;
+    uint64_t *res_out;
 };
 
 // E(l) = round(n 2^(l - 128)), the expected index advance of a level-l finger
@@ -89,7 +98,7 @@ __device__ __forceinline__ uint64_t wk_pack(uint32_t own, uint32_t h, uint32_t s
 #define WK_ATTR
 #endif
 
-template <bool STATS>
+template <bool STATS, bool KF>
 __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     __shared__ uint64_t res_all[WK_BLOCK / 64][WK_RES];
     // entries land by LDS-DMA: region k of a wave = the 16-B quarters its
@@ -127,14 +136,23 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     uint32_t psrc = 0;
     uint64_t pd = 0;
     uint32_t n_g64 = 0, n_r16 = 0, n_xc = 0, n_q = 0;
+    const uint32_t arc_top = KF ? (uint32_t)(CX_FINGERS - io.Lh) * 2u * n : 0u;  // KF: local rows
 
     for (;;) {
         if (__ballot(mode != M_NONE || bst != B_EMPTY) == 0 && head >= end && flushed >= end)
             break;  // wave-uniform: every lookup delivered and written
 
         // ---- memory round: every load of the round, one wait ----
-        const uint32_t eidx =
-            mode == M_HOP ? (uint32_t)((lvl - l0) * 2 + rb) * n + cur : WK_NONE;
+        uint32_t eidx = WK_NONE;
+        if (mode == M_HOP) {
+            if (!KF)
+                eidx = (uint32_t)((lvl - l0) * 2 + rb) * n + cur;
+            else if (lvl >= io.Lh)  // replicated top planes, all peers
+                eidx = (uint32_t)((lvl - io.Lh) * 2 + rb) * n + cur;
+            else  // this rank's rows (checked local by the plan)
+                eidx = arc_top + (uint32_t)((lvl - l0) * 2 + rb) * io.M +
+                       (cur >= io.plo ? cur - io.plo : cur + n - io.plo);
+        }
         if (STATS) {
             n_g64 += mode == M_HOP;
             n_r16 += mode == M_FIX ? 1u : (mode >= M_EXACT ? 2u : 0u);
@@ -147,7 +165,7 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
         typedef unsigned int v4n __attribute__((ext_vector_type(4)));
         const bool pair_now = bst == B_KEYS;
         v4n pa4 = {0, 0, 0, 0}, pb4 = {0, 0, 0, 0};
-        if (pair_now && psrc < n) {  // the source's (pred, self) IDs: one 32-B pair
+        if ((!KF || !io.dh) && pair_now && psrc < n) {  // the source's (pred, self) IDs: one 32-B pair
             pa4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc));
             pb4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc + 1));
         }
@@ -162,6 +180,7 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
                 pq = head + rank;
                 pkey = ld128(io.keys + pq);
                 psrc = io.src[pq];
+                if (KF && io.dh) pd = io.dh[pq];  // the origin's start: d >> gs, or LOCAL / BAD
                 bst = B_KEYS;
             }
             const size_t took = (size_t)__popcll(want);
@@ -194,7 +213,10 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
         const u128 pa = wk_u128(pa4), pb = wk_u128(pb4), xa = wk_u128(xa4), xb = wk_u128(xb4);
 
         // ---- slot B: StoredLocally at the source, or the start distance ----
-        if (pair_now) {
+        if (KF && io.dh && pair_now) {  // the origin resolved the start (k_arc_scatter_soa)
+            pst = psrc >= n || pd == ARC_HINT_BAD ? P_BAD : (pd == ARC_HINT_LOCAL ? P_LOCAL : P_WALK);
+            bst = B_READY;
+        } else if (pair_now) {
             if (psrc >= n) {
                 pst = P_BAD;
             } else if (n == 1 || (pkey - pa - 1) <= (pb - pa - 1)) {
@@ -346,6 +368,12 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
                     mode = M_HOP;
                     lvl = ma + gs;
                     rb = ma >= 1 ? (int)((dmax >> (ma - 1)) & 1) : 0;  // bit lvl-1 of d
+                    if (KF && lvl < io.Lh && (cur >= io.plo ? cur - io.plo : cur + n - io.plo) >= io.M) {
+                        // a row outside the rank's arc + halo: a layout bug (the
+                        // lookup was sent to its key's arc), reported, never seen
+                        mode = M_NONE;
+                        res[qi & (WK_RES - 1)] = wk_pack(CX_NONE, h, CX_QI_ARC_MISS);
+                    }
                 } else {
                     mode = M_EXACT;  // below the table
                 }
@@ -360,9 +388,13 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
             const uint64_t v = inr ? res[idx & (WK_RES - 1)] : 0ull;
             if (__ballot(!inr || (v >> 63)) != ~0ull) break;
             if (inr) {
-                io.owner[idx] = (uint32_t)v;
-                io.hops[idx] = (uint8_t)(v >> 32);
-                if (io.status) io.status[idx] = (uint8_t)(v >> 40);
+                if (KF) {
+                    __builtin_nontemporal_store(v, io.res_out + idx);
+                } else {
+                    io.owner[idx] = (uint32_t)v;
+                    io.hops[idx] = (uint8_t)(v >> 32);
+                    if (io.status) io.status[idx] = (uint8_t)(v >> 40);
+                }
                 res[idx & (WK_RES - 1)] = 0;
             }
             flushed += 64;
@@ -421,7 +453,7 @@ hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, co
     io.stats = stats;
     // one resident round of waves (no second, partial round of blocks); small
     // batches: >= 1024 lookups per wave
-    static const unsigned resident = walk_resident_grid(k_walk<false>);
+    static const unsigned resident = walk_resident_grid(k_walk<false, false>);
     size_t waves = (size_t)resident * (WK_BLOCK / 64);
     const size_t small = (q + 1023) / 1024;
     if (small < waves) waves = small ? small : 1;
@@ -429,9 +461,52 @@ hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, co
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
     if (stats)
-        k_walk<true><<<blocks, WK_BLOCK, 0, s>>>(io);
+        k_walk<true, false><<<blocks, WK_BLOCK, 0, s>>>(io);
     else
-        k_walk<false><<<blocks, WK_BLOCK, 0, s>>>(io);
+        k_walk<false, false><<<blocks, WK_BLOCK, 0, s>>>(io);
+    return hipGetLastError();
+}
+
+// Key-first arc walk (chordx.arc.ArcRouter's default protocol): the
+// lookups this rank received for its arc, walked from their sources over the
+// replicated top planes [Lh, 128) and its own rows below, started from the
+// origin's hints (dh: d >> gs, ARC_HINT_LOCAL, ARC_HINT_BAD; or, without
+// dh, from the source's (pred, self) IDs like the replicated walk); one packed
+// result (owner | hops << 32 | status << 40 | 1 << 63) per lookup in input
+// order.
+hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n,
+                          const uint64_t *arc_tree, int l0, int ib, const SearchView &sv, int Lh,
+                          uint32_t plo, uint32_t M, const uint32_t *src, const cell128 *keys,
+                          size_t q, const uint64_t *dh, uint64_t *res, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const int gs = cz_shift(ib);
+    if (n == 0 || n >= (1u << 30) || gs < 64 || l0 < 5 || Lh < l0 || Lh > (int)CX_FINGERS ||
+        M > n || (size_t)(CX_FINGERS - Lh) * 2 * n + (size_t)(Lh - l0) * 2 * M >= WK_NONE)
+        return hipErrorInvalidValue;
+    WalkIO io = {};
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.cz = reinterpret_cast<const uint4 *>(arc_tree);
+    io.l0 = l0;
+    io.gs = gs;
+    io.sv = sv;
+    io.src = src;
+    io.keys = keys;
+    io.q = q;
+    io.Lh = Lh;
+    io.plo = plo;
+    io.M = M;
+    io.dh = dh;
+    io.res_out = res;
+    static const unsigned resident = walk_resident_grid(k_walk<false, true>);
+    size_t waves = (size_t)resident * (WK_BLOCK / 64);
+    const size_t small = (q + 1023) / 1024;
+    if (small < waves) waves = small ? small : 1;
+    io.chunk = (q + waves - 1) / waves;
+    waves = (q + io.chunk - 1) / io.chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
+    k_walk<false, true><<<blocks, WK_BLOCK, 0, s>>>(io);
     return hipGetLastError();
 }
 
