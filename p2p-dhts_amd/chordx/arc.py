@@ -73,6 +73,7 @@ class ArcRouter:
         self.chunks = None     # route_soa pipeline depth (None: by batch size)
         self.regions = True    # single-pass partition into destination regions
         self.hints = True      # origin-resolved source hints with the lookups
+        self.region_cap = None  # tests: (piece size, world) -> region cap (overflow path)
         # exchange_always: a single rank still partitions, exchanges (with
         # itself, through the process group's collectives) and delivers -- the
         # general path, so a one-GPU run executes and times what N ranks run
@@ -200,6 +201,8 @@ class ArcRouter:
 
         def piece_cap(c):
             qc = cut[c + 1] - cut[c]
+            if self.region_cap is not None:
+                return max(1, int(self.region_cap(qc, G)))
             return max(1, qc // G + qc // (4 * G) + 4096)
 
         for c in range(k):

@@ -2103,8 +2103,13 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     // reads; 0.7 % faster, profiles/r04/store_ab/nt_gathers); the ID slices
     // (64 MiB, re-read) stay cached
     auto ld32nt = [](const uint32_t *base, uint32_t x) -> uint32_t {
-        return __builtin_nontemporal_load(
-            reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u));
+        const uint32_t *a =
+            reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
+#if CX_AB_PLANE_CACHED  // A/B build only (libchordx_ab): ordinary plane gathers
+        return *a;
+#else
+        return __builtin_nontemporal_load(a);
+#endif
     };
     auto fat = [&](uint32_t x, int l) -> uint32_t {
         return ld32nt(fv.F + (size_t)(l - fv.L) * fv.sl, x);

@@ -341,6 +341,36 @@ def test_arc_soa_regions_equals_replicated(cx, O, n, G, hints):
     assert r.arc_partition_regions(G, srcs[0], keys[0], 1) is None
 
 
+@pytest.mark.parametrize("n,G", [(5000, 2), (1 << 16, 8), (70001, 5), (3, 4)])
+def test_arc_partition_async_device_counts(cx, O, n, G):
+    """cx_arc_partition_regions_async (counts and overflow flag left on the
+    device for one all_gather of every piece): the same send arrays, slots,
+    hints and counts as the synchronous call, and the overflow flag raised
+    (nothing of the crowded destination written) when cap is too small."""
+    import torch
+    q = 4096
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA2F0 + n + G)
+    cap = q if n < 10 else q // G + q // (4 * G) + 64
+    r = cx.Ring(ids_dev)
+    r.arc_build(G, 0)
+    sk, ss, perm, counts, sh = r.arc_partition_regions(G, srcs[0], keys[0], cap, hints=True)
+    dev_counts = torch.full((G + 1,), -5, dtype=torch.int64, device="cuda")
+    ak, as_, aperm, ah = r.arc_partition_regions_async(G, srcs[0], keys[0], cap, dev_counts,
+                                                       hints=True)
+    torch.cuda.synchronize()
+    assert dev_counts[:G].tolist() == counts and int(dev_counts[G]) == 0
+    assert torch.equal(perm, aperm)
+    for d in range(G):
+        rows = slice(d * cap, d * cap + counts[d])
+        assert torch.equal(sk[rows], ak[rows]) and torch.equal(ss[rows], as_[rows])
+        assert torch.equal(sh[rows], ah[rows])
+    if n >= 10:
+        small = torch.zeros(G + 1, dtype=torch.int64, device="cuda")
+        r.arc_partition_regions_async(G, srcs[0], keys[0], 1, small)
+        torch.cuda.synchronize()
+        assert int(small[G]) == 1
+
+
 def test_arc_hints_bad_sources_and_local_keys(cx, O):
     """Source hints at the edges: out-of-range sources (BADPEER at the arc
     rank), keys stored at their source (0 hops, resolved at the origin), and
@@ -501,7 +531,10 @@ def _rccl_worker(_i, n, q, chunks, out):
     src[::97] = ring.n + 3  # bad sources travel and come back as CX_Q_BADPEER
     ow, hp, st = ring.route(src, keys)
     res = []
-    for _ in range(2):  # the second call reuses the pinned count buffer
+    for it in range(3):  # the second call reuses the pinned count buffer; the third
+        # forces every piece's region to overflow (cap 64): the pieces are
+        # partitioned again in two passes and the counts gathered once more
+        router.region_cap = (lambda qc, G: 64) if it == 2 else None
         owner = torch.full((q,), -5, dtype=torch.int32, device=dev)
         hops = torch.zeros(q, dtype=torch.uint8, device=dev)
         status = torch.full((q,), 9, dtype=torch.uint8, device=dev)
