@@ -11,5 +11,6 @@ tail -3 $O/pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
 rc2=$?
+echo "bench rc=$rc2 bytes=$(wc -c < $O/bench.json)"
 tail -c 600 $O/bench.err
 exit $rc2
