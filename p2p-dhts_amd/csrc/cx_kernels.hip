@@ -1603,16 +1603,6 @@ __device__ __forceinline__ uint32_t cz_expect(uint32_t n, int l) {
     return sh > 40 ? 0u : (uint32_t)(((uint64_t)n + (1ull << (sh - 1))) >> sh);
 }
 
-__device__ __forceinline__ uint32_t cz_encode(uint32_t n, int gs, uint32_t par, u128 pid, int l,
-                                              uint32_t x, u128 xid) {
-    int64_t d = ((int64_t)x - (int64_t)par - (int64_t)cz_expect(n, l)) % (int64_t)n;
-    if (d < 0) d += n;
-    if (d > (int64_t)(n / 2)) d -= n;  // (-n/2, n/2]
-    const u128 code = (xid - pid - ((u128)1 << l)) >> gs;
-    if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
-    return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
-}
-
 __device__ __forceinline__ uint32_t cz_next(uint32_t n, uint32_t cur, int l, uint32_t wd) {
     int t = (int)cur + (int)cz_expect(n, l) + (int)(wd & 0xFFFF) - 32768;  // n < 2^30
     if (t < 0)
@@ -1720,7 +1710,7 @@ hipError_t ring_hi(const cell128 *ring, size_t n, uint64_t *hi, hipStream_t s) {
 // with gs >= 64 and l >= 64 is (D - c) >> (gs - 64), D = xhi - phi - 2^(l-64)
 // (mod 2^64), c = the borrow out of the low words (0 or 1): when D has a set
 // bit below gs - 64 the borrow cannot reach bit gs - 64, and D alone decides.
-// Otherwise (about 2^-28 of encodes) the full IDs are read.
+// Otherwise (about 2^-28 of encodes) the IDs' low words give c.
 __device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t par, uint64_t phi,
                                                  int l, uint32_t x, uint64_t xhi,
                                                  const cell128 *ring) {
@@ -1743,10 +1733,8 @@ __device__ __forceinline__ uint32_t cz_encode_hi(uint32_t n, int gs, uint32_t pa
     uint64_t code;
     if (D & ((1ull << sh) - 1)) {
         code = D >> sh;
-    } else {
-        const u128 full = ld128(ring + x) - ld128(ring + par) - ((u128)1 << l);
-        code = (uint64_t)(full >> gs);
-        if ((full >> gs) >> 64) code = ~0ull;
+    } else {  // the borrow out of the low words decides: one more load each
+        code = (D - (uint64_t)(ring[x].lo < ring[par].lo)) >> sh;
     }
     if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
     return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
@@ -1777,10 +1765,9 @@ __device__ __forceinline__ uint32_t cz_encode_s(uint32_t n, int gs, uint32_t par
     uint64_t code;
     if (D & 0x7FFFu) {
         code = D >> 15;
-    } else {
-        const u128 full = ld128(ring + x) - ld128(ring + par) - ((u128)1 << l);
-        code = (uint64_t)(full >> gs);
-        if ((full >> gs) >> 64) code = ~0ull;
+    } else {  // the full IDs (64-bit halves: no variable 128-bit shifts)
+        const cell128 cx = ring[x], cp = ring[par];
+        code = (cx.hi - cp.hi - (1ull << (l - 64)) - (uint64_t)(cx.lo < cp.lo)) >> (gs - 64);
     }
     if (d < -32768 || d > 32766 || code >= 0xFFFF) return CZ_NONE;
     return ((uint32_t)code << 16) | (uint32_t)(d + 32768);
@@ -3329,7 +3316,7 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
                     const u128 key = ((u128)r[k].w1 << 64) | r[k].w0;
                     const u128 pa = ld128(ring_ext + r[k].cur), pb = ld128(ring_ext + r[k].cur + 1);
                     dh[k] = (n == 1 || (key - pa - 1) <= (pb - pa - 1)) ? ARC_HINT_LOCAL
-                                                                         : (uint64_t)((key - pb) >> gs);
+                                                                         : (uint64_t)((key - pb) >> 64) >> (gs - 64);
                 }
             }
         }

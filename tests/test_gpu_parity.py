@@ -753,6 +753,27 @@ def test_route_table_builds_edge_rings(cx, O, kind):
         assert (a == b).all()
 
 
+def test_route_table_builds_deterministic_all_escapes(cx, O):
+    """A dense cluster alone: every finger at a table level wraps the ring, so
+    every word of the table is an escape (n * R * 16) in every build, and
+    repeated builds are bit-identical.  Round 5: the level-planes build (2)
+    took the exact-ID branch of its gap code through a variable 128-bit shift
+    whose result differed by lane and run (a few hundred slot-8 words came out
+    representable); the branch is now 64-bit arithmetic on the IDs' halves."""
+    base = 0x3C3C_5A5A_0F0F_1234 << 64
+    ids = O.keys_from_ints([base + i * 7919 for i in range(6000)])
+    ring = cx.Ring(ids)
+    seen = set()
+    for tb in (0, 1, 2, 3, 2, 1, 2):
+        ring.set_table_build(tb)
+        ring.build_fingers()
+        v, esc, nbytes = ring.route_info()
+        assert v == 5 and esc == nbytes // 4, (tb, esc, nbytes)
+        seen.add(ring.route_table_hash())
+    assert len(seen) == 1
+    ring.set_table_build(0)
+
+
 def test_route_table_escape_count_with_overflow(cx, O):
     """Escape accounting of the default build when rows are deferred to
     overflow launches: a ring of four dense clusters plus a few
