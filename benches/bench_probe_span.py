@@ -25,6 +25,7 @@ def main():
     ids = torch.empty((1 << 24, 2), dtype=torch.int64, device="cuda")
     chordx.fill_splitmix(ids, 0x5EED0005)
     base = chordx.Ring(ids)
+    base.set_route_depth(28)  # the 28-level (56 GiB) table the docstring compares against
     base.build_fingers()
     big = chordx.Ring(ids)
     big.set_route_depth(56)

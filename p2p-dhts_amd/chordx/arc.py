@@ -329,7 +329,9 @@ class ArcRouter:
         without exchange_always, which searches in place)."""
         eng = self.engine
         if self.world == 1 and not self.exchange_always:
-            owner.copy_(self._arc_ring().successor(keys).to(owner.dtype))
+            # the one arc is the whole ring: the engine's own search (no second
+            # ring holding the same IDs)
+            owner.copy_(eng.successor(keys).to(owner.dtype))
             return 0
         G = self.world
         zero = self._zeros_src(keys)

@@ -119,23 +119,14 @@ struct FingerView {
     // planes only, optional: two-hop planes C2[(l - L - 1) * sl + x] =
     // F[F[x][l]][l - 1] for l in (L, L + nl) (fingers_pairs)
     const uint32_t *C2 = nullptr;
-    // host-side build choice: 1 = root-centric windows, 256 rows per block
-    // (k_cz_build_roots); 2 = blocks sized by distinct roots (k_cz_build_roots2,
-    // needs rs; without it the build falls back to 1); 3 = both windows of a
-    // root at once (k_cz_build_roots3); 4 = as 2, plane 0 stored after the W1
-    // gathers; all need C2
+    // host-side build choice: 2 = root-centric windows in blocks sized by
+    // distinct roots (k_cz_build_roots2: needs C2 and rs), 0 = one lane per
+    // entry (k_cz_build)
     int roots = 0;
     // root-centric build, optional: 32-bit ID slices (ring_codes) for the gap
     // codes instead of the 64-bit high words; only when every ring gap is
     // below 2^(gs + 17)
     const uint32_t *rs = nullptr;
-    // root-centric build (roots == 2), optional: pair planes (fingers_pairs2):
-    // P[(l - L) n + x] = {F[x][l], rs[F[x][l]]}, P2 likewise for the two-hop
-    // planes; with them the build reads each window node and its slice in one
-    // gather (C2 may then be null)
-    const uint2 *P = nullptr, *P2 = nullptr;
-    // or quad planes (fingers_quads): Q[(l - L) n + x] = {P[l][x], P2[l][x]}
-    const uint4 *Q = nullptr;
     __host__ __device__ uint32_t at(uint32_t x, int l) const {
         return F[(size_t)x * sx + (size_t)(l - L) * sl];
     }
@@ -167,13 +158,6 @@ hipError_t successor_stree(const STreeView &st, const cell128 *keys, size_t q, u
 hipError_t eyt_rank_build(size_t n, uint32_t *rank, hipStream_t s);
 hipError_t successor_eyt16(const EytView &ev, const uint32_t *rank, const cell128 *keys, size_t q,
                            uint32_t *owner, bool pred, hipStream_t s);
-// Pair planes {finger, rs[finger]} of levels L .. L + nl - 1 and the two-hop
-// pairs of levels L + 1 .. (FingerView::P / P2), from level planes FT.
-hipError_t fingers_pairs2(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint2 *P,
-                          uint2 *P2, hipStream_t s);
-// Quad planes {F, rs[F], C2, rs[C2]} of levels L .. L + nl - 1 (FingerView::Q).
-hipError_t fingers_quads(const uint32_t *FT, const uint32_t *rs, size_t n, int nl, uint4 *Q,
-                         hipStream_t s);
 hipError_t fingers_levels(const uint32_t *F, size_t n, int L, int nl, uint32_t *FT,
                           hipStream_t s);
 // C2 planes (nl - 1 of them) from the level planes FT.

@@ -194,7 +194,10 @@ def test_device_arguments_checked(ida):
     device are refused before any pointer reaches the kernels."""
     import torch
     nb, bl = 16, 100
-    data = torch.randint(0, 256, (nb * bl,), dtype=torch.uint8, device="cuda")
+    # nonzero bytes: decode drops trailing zeros (IDA::Decode), so a block whose
+    # last byte is 0 would come back shorter than bl
+    g = torch.Generator(device="cpu").manual_seed(0x1DA)
+    data = torch.randint(1, 256, (nb * bl,), dtype=torch.uint8, generator=g).cuda()
     offs = torch.arange(0, nb * bl + 1, bl, dtype=torch.int64, device="cuda")
     frags, seg = ida.encode_flat(data, offs)
     S = (bl + 9) // 10
