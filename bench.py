@@ -319,8 +319,12 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
             "layout": f"ring IDs all-gathered; arc-sharded route planes x{world} (top {top} "
                       "levels replicated, lower levels for the arc + halo); key-first SoA "
                       "all_to_all-v with origin-resolved source hints (28 B out, 8 B back per "
-                      "lookup), single-pass region partition, pipelined pieces; at N = 1 the "
-                      "rank exchanges with itself through a one-rank RCCL group",
+                      "lookup crossing ranks); count pass whose device counts travel in one "
+                      "all_gather per step, exact-layout scatter on a side stream overlapping "
+                      "the walks of earlier pieces; each rank walks the lookups of its own arc "
+                      "in place (no collective carries them); at N = 1 the general path runs "
+                      "through a one-rank RCCL group (the count all_gather and its host read; "
+                      "no lookup crosses ranks, so no all_to_all is issued)",
             "note": "owner, hops and status of every lookup equal the replicated route's "
                     "(checked on every rank)"}
 

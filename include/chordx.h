@@ -420,6 +420,22 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
                                    const cx_u128 *keys, size_t q, uint64_t cap,
                                    cx_u128 *send_keys, uint32_t *send_src, uint64_t *send_hint,
                                    uint32_t *perm, int64_t *counts_dev);
+/* Exact-layout partition in two asynchronous passes (no capacity, no
+ * overflow, no host synchronisation): cx_arc_count_async writes the
+ * per-destination counts of the lookups' keys into counts_dev (device,
+ * world int64); cx_arc_scatter_async, given those counts (still on the
+ * device), lays destination d's lookups out at [sum_{j<d} counts[j], ...) of
+ * send_keys / send_src / send_hint (q entries each; send_hint may be NULL)
+ * with perm[i] = the slot of lookup i.  cursor_dev: world uint32 of scratch
+ * (device) per concurrent scatter.  Both run on the ring's stream, so a
+ * caller can count every piece, exchange the counts in one collective, and
+ * scatter each piece on another stream while earlier pieces are walked. */
+int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size_t q,
+                       int64_t *counts_dev);
+int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
+                         const cx_u128 *keys, size_t q, const int64_t *counts_dev,
+                         uint32_t *cursor_dev, cx_u128 *send_keys, uint32_t *send_src,
+                         uint64_t *send_hint, uint32_t *perm);
 int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
                  uint64_t *res);
 /* cx_arc_route with the origins' source hints (cx_arc_partition_regions

@@ -18,7 +18,13 @@ sources over the replicated top planes and its own rows and answers in
 receive order, 8 B per lookup; the answers come back with the splits swapped
 and land in send order, where the origin scatters them through the
 permutation it kept.  One count exchange, three all_to_alls, no origin or
-index crossing xGMI, no re-bucketing of results.
+index crossing xGMI, no re-bucketing of results.  On RCCL (route_exact) the
+partition runs in two passes: a count pass over the keys (16 B per lookup)
+whose device counts travel in the step's one all_gather while the scatter
+lays each piece out by those counts on a side stream, overlapping the walks
+of earlier pieces; a rank walks the lookups whose key lies in its own arc in
+place (they never enter a collective), and the all_to_alls carry only the
+other ranks' regions -- none at all when no lookup of any rank crosses ranks.
 
 Record protocol ("records", origin walk or key-first): one bulk-synchronous round = step (walk every record as far as this rank's
 rows reach) -> bucket by destination -> exchange: one all_gather of the G x G
@@ -74,6 +80,10 @@ class ArcRouter:
         self.regions = True    # single-pass partition into destination regions
         self.hints = True      # origin-resolved source hints with the lookups
         self.region_cap = None  # tests: (piece size, world) -> region cap (overflow path)
+        # RCCL: count pass + exact-layout scatter on a side stream, own region
+        # walked in place (route_exact); False: the single-pass region layout
+        self.exact = True
+        self._side = None      # side stream of the exact path's scatters
         # exchange_always: a single rank still partitions, exchanges (with
         # itself, through the process group's collectives) and delivers -- the
         # general path, so a one-GPU run executes and times what N ranks run
@@ -180,6 +190,9 @@ class ArcRouter:
         kmax = max(4, int(fixed)) if fixed is not None else 4  # piece slots per rank
         k = int(fixed) if fixed is not None else max(1, min(4, q >> 22))
         k = max(1, min(k, kmax, max(q, 1)))
+        dev = self.comm_device if self.comm_device is not None else keys.device
+        if self.exact and hasattr(eng, "arc_count_async") and keys.is_cuda:
+            return self.route_exact(src, keys, owner, hops, status, k, kmax)
         cut = [c * q // k for c in range(k + 1)]
         G = self.world
         # single-pass partition into per-destination regions when the engine
@@ -314,6 +327,166 @@ class ArcRouter:
             eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
                             status[sl] if status is not None else None)
             self.records_sent += int(sum(parts[c][3]))
+        self.rounds = 2
+        return 2
+
+    def _comm_cuda(self):
+        return self.comm_device is None or torch.device(self.comm_device).type == "cuda"
+
+    def _gather_row(self, row):
+        """all_gather of every rank's count row, landed on the host (RCCL: one
+        pinned copy, one wait on the current stream)."""
+        G = self.world
+        if not self._comm_cuda():  # gloo (tests): through the host
+            r = row.to(self.comm_device)
+            mat = torch.empty((G, r.numel()), dtype=torch.int64, device=r.device)
+            tdist.all_gather_into_tensor(mat.view(-1), r, group=self.group)
+            return mat
+        mat = torch.empty((G, row.numel()), dtype=torch.int64, device=row.device)
+        tdist.all_gather_into_tensor(mat.view(-1), row, group=self.group)
+        if self._mat_host is None or self._mat_host.shape != mat.shape:
+            self._mat_host = torch.empty(mat.shape, dtype=torch.int64, pin_memory=True)
+        self._mat_host.copy_(mat, non_blocking=True)
+        torch.cuda.current_stream(mat.device).synchronize()
+        return self._mat_host
+
+    def _a2a_views(self, outs, ins):
+        """all_to_all from the views `ins` (one per destination rank) into the
+        views `outs` (one per source rank): RCCL's list all_to_all,
+        asynchronous (returns its work); gloo (tests): packed through host
+        buffers on the current stream, synchronous (returns None)."""
+        if self._comm_cuda():
+            return tdist.all_to_all(outs, ins, group=self.group, async_op=True)
+        dev = self.comm_device
+        in_splits = [int(t.shape[0]) for t in ins]
+        out_splits = [int(t.shape[0]) for t in outs]
+        packed = torch.cat([t.to(dev) for t in ins])
+        got = torch.empty((sum(out_splits),) + tuple(packed.shape[1:]), dtype=packed.dtype,
+                          device=dev)
+        tdist.all_to_all_single(got, packed, output_split_sizes=out_splits,
+                                input_split_sizes=in_splits, group=self.group)
+        for t, piece in zip(outs, torch.split(got, out_splits)):
+            t.copy_(piece)
+        return None
+
+    def route_exact(self, src, keys, owner, hops, status, k, kmax) -> int:
+        """route_soa on RCCL with the exact-layout partition (module docstring).
+
+        Current stream: the count pass of every piece (arc_count_async into one
+        device row), the all_gather of that row and its one host read, then
+        per piece the walk of this rank's own region in place and of the
+        lookups the other ranks sent, the answers' return exchange and the
+        delivery.  Side stream: the scatter of each piece (arc_scatter_async,
+        reading the counts on the device), started as soon as the counts
+        exist, and each piece's outgoing exchange, which waits on that
+        scatter only.  Returns 2 (rounds of the protocol)."""
+        eng, G, me = self.engine, self.world, self.rank
+        dev = keys.device
+        q = int(keys.shape[0])
+        cut = [c * q // k for c in range(k + 1)]
+        main = torch.cuda.current_stream(dev)
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        side = self._side
+        hints = bool(self.hints and getattr(eng, "arc_hints", False))
+        row = torch.zeros(1 + kmax * G, dtype=torch.int64, device=dev)
+        row[0] = k | (int(hints) << 20)
+        for c in range(k):
+            eng.arc_count_async(G, keys[cut[c]:cut[c + 1]], row[1 + c * G: 1 + (c + 1) * G])
+        cursors = torch.empty(k * G, dtype=torch.int32, device=dev)
+        side.wait_stream(main)  # the counts (and the caller's inputs) are written
+        parts, ready = [], []
+        with torch.cuda.stream(side):
+            for c in range(k):
+                sl = slice(cut[c], cut[c + 1])
+                part = eng.arc_scatter_async(G, src[sl], keys[sl], row[1 + c * G: 1 + (c + 1) * G],
+                                             cursors[c * G: (c + 1) * G], hints=hints)
+                parts.append(part if hints else part + (None,))
+                ev = torch.cuda.Event()
+                ev.record(side)
+                ready.append(ev)
+        mat = self._gather_row(row)
+        kg = int((mat[:, 0] & 0xFFFFF).max())  # pieces every rank runs
+        use_h = bool(int((mat[:, 0] >> 20).min()))  # every rank's pieces carry hints
+        if kg > k:  # this rank's extra pieces are empty
+            e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=dev),
+                 torch.empty(0, dtype=torch.int64, device=dev))
+            parts += [e] * (kg - k)
+            ready += [None] * (kg - k)
+            cut += [q] * (kg - k)
+        cnt = [[int(mat[me, 1 + c * G + d]) for d in range(G)] for c in range(kg)]
+        recv = [[int(mat[r, 1 + c * G + me]) for r in range(G)] for c in range(kg)]
+        offs = []
+        for c in range(kg):
+            o, acc = [], 0
+            for d in range(G):
+                o.append(acc)
+                acc += cnt[c][d]
+            offs.append(o)
+        # lookups that cross ranks anywhere (the same answer on every rank):
+        # without any, no rank issues an all_to_all
+        remote = any(int(mat[r, 1 + c * G + d]) for r in range(G) for d in range(G) if r != d
+                     for c in range(kg))
+        for c in range(kg):
+            if sum(cnt[c]) != cut[c + 1] - cut[c]:
+                raise RuntimeError("arc count pass and partition disagree")
+
+        def region(t, c, d):
+            return t[offs[c][d]: offs[c][d] + cnt[c][d]] if d != me else t[:0]
+
+        def send(c):
+            """Issued on the side stream: waits for piece c's scatter only.
+            Returns ([(received, work)], event after the issue on the side
+            stream)."""
+            sk, ss, _, sh = parts[c]
+            rs = [recv[c][r] if r != me else 0 for r in range(G)]
+            out = []
+            with torch.cuda.stream(side):
+                for t in ((sk, ss, sh) if use_h else (sk, ss)):
+                    o = torch.empty((sum(rs),) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+                    w = self._a2a_views(list(torch.split(o, rs)),
+                                        [region(t, c, d) for d in range(G)])
+                    out.append((o, w))
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return out, ev
+
+        inflight = send(0) if remote else None
+        backs = []
+        for c in range(kg):
+            got = inflight
+            if remote and c + 1 < kg:
+                inflight = send(c + 1)
+            sk, ss, _, sh = parts[c]
+            back = torch.empty(cut[c + 1] - cut[c], dtype=torch.int64, device=dev)
+            if ready[c] is not None:
+                main.wait_event(ready[c])
+            o, n_ = offs[c][me], cnt[c][me]
+            if n_:  # this rank's own region: walked in place
+                eng.arc_route(ss[o:o + n_], sk[o:o + n_], res=back[o:o + n_],
+                              hint=sh[o:o + n_] if use_h else None)
+            work = None
+            if remote:
+                arrived, ev = got
+                main.wait_event(ev)
+                for _, w in arrived:
+                    if w is not None:
+                        w.wait()
+                rk, rs_ = arrived[0][0], arrived[1][0]
+                rh = arrived[2][0] if use_h else None
+                res = eng.arc_route(rs_, rk, hint=rh) if use_h else eng.arc_route(rs_, rk)
+                splits = [recv[c][r] if r != me else 0 for r in range(G)]
+                work = self._a2a_views([region(back, c, d) for d in range(G)],
+                                       list(torch.split(res, splits)))
+                self.records_sent += sum(cnt[c]) - cnt[c][me]
+            backs.append((back, work))
+        for c in range(kg):
+            back, work = backs[c]
+            if work is not None:
+                work.wait()
+            sl = slice(cut[c], cut[c + 1])
+            eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
+                            status[sl] if status is not None else None)
         self.rounds = 2
         return 2
 

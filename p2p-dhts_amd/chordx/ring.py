@@ -591,6 +591,44 @@ class Ring:
                                                        _ptr(perm), _ptr(counts)))
         return (skeys, ssrc, perm, shint) if hints else (skeys, ssrc, perm)
 
+    def arc_count_async(self, world: int, keys, counts):
+        """cx_arc_count_async: per-destination counts of the keys' arcs into
+        `counts` (device int64, world elements), no host synchronisation."""
+        keys = self._prep_keys(keys)
+        if not (_is_dev(keys) and _is_dev(counts)):
+            raise TypeError("arc routing takes device tensors")
+        if not (counts.dtype == torch.int64 and counts.is_contiguous()
+                and counts.numel() == world):
+            raise TypeError("counts: a contiguous int64 device tensor of world elements")
+        self._arc_stream()
+        L.check(L.lib().cx_arc_count_async(self._h, world, _ptr(keys), keys.shape[0],
+                                           _ptr(counts)))
+
+    def arc_scatter_async(self, world: int, src, keys, counts, cursor, hints: bool = False):
+        """cx_arc_scatter_async: the exact-layout partition of (src, keys) by the
+        device counts of arc_count_async over the same keys; cursor: device
+        int32 scratch of world elements (one per concurrent scatter).  Returns
+        (send_keys, send_src, perm[, send_hint]), destination d's lookups at
+        rows [sum(counts[:d]), sum(counts[:d + 1]))."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        for t, n, w in ((counts, world, 8), (cursor, world, 4)):
+            if not (_is_dev(t) and t.is_contiguous() and t.numel() == n and t.element_size() == w):
+                raise TypeError("counts (int64) / cursor (int32): contiguous device tensors of "
+                                "world elements")
+        if not (_is_dev(keys) and _is_dev(src)):
+            raise TypeError("arc routing takes device tensors")
+        q = keys.shape[0]
+        skeys = torch.empty((q, 2), dtype=torch.int64, device=keys.device)
+        ssrc = torch.empty(q, dtype=torch.int32, device=keys.device)
+        perm = torch.empty(q, dtype=torch.int32, device=keys.device)
+        shint = torch.empty(q, dtype=torch.int64, device=keys.device) if hints else None
+        self._arc_stream()
+        L.check(L.lib().cx_arc_scatter_async(self._h, world, _ptr(src), _ptr(keys), q,
+                                             _ptr(counts), _ptr(cursor), _ptr(skeys), _ptr(ssrc),
+                                             _ptr(shint), _ptr(perm)))
+        return (skeys, ssrc, perm, shint) if hints else (skeys, ssrc, perm)
+
     def arc_route(self, src, keys, res=None, hint=None):
         """Packed results (int64: owner | hops << 32 | status << 40 | 1 << 63)
         of lookups received from every rank, in input order (cx_arc_route;

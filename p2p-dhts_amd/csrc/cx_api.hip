@@ -2252,6 +2252,45 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
     return CX_OK;
 }
 
+int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size_t q,
+                       int64_t *counts_dev) {
+    CX_CHECK(ring && counts_dev, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(q == 0 || keys, CX_E_INVALID, "null buffer");
+    CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many lookups for one rank");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    CX_HIP(cxk::arc_count_keys(reinterpret_cast<const cell128 *>(keys), q, ring->d_arc_bounds,
+                               ring->arc_nb, world, counts_dev, ring->stream));
+    return CX_OK;
+}
+
+int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
+                         const cx_u128 *keys, size_t q, const int64_t *counts_dev,
+                         uint32_t *cursor_dev, cx_u128 *send_keys, uint32_t *send_src,
+                         uint64_t *send_hint, uint32_t *perm) {
+    CX_CHECK(ring && counts_dev && cursor_dev, CX_E_INVALID, "null argument");
+    CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
+    CX_CHECK(q == 0 || (src && keys && send_keys && send_src && perm), CX_E_INVALID,
+             "null buffer");
+    CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many lookups for one rank");
+    CX_CHECK(ring->arc_world == world && ring->d_arc_bounds, CX_E_STATE,
+             "arc not built for this world size (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    CX_CHECK(!send_hint || ring->d_ring_ext, CX_E_STATE, "arc not built (cx_arc_build)");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    CX_HIP(cxk::arc_scatter_exact(src, reinterpret_cast<const cell128 *>(keys), q,
+                                  ring->d_arc_bounds, ring->arc_nb, world, counts_dev, cursor_dev,
+                                  reinterpret_cast<cell128 *>(send_keys), send_src, perm,
+                                  send_hint, ring->d_ring_ext, ring->n, ring->pk_ib,
+                                  ring->stream));
+    return CX_OK;
+}
+
 int cx_arc_route_hinted(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
                         const uint64_t *hint, size_t q, uint64_t *res) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");

@@ -3287,10 +3287,17 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
                                                          uint32_t *ssrc, uint32_t *slot_of,
                                                          uint32_t cap, uint32_t *ovf,
                                                          uint64_t *sd, const cell128 *ring_ext,
-                                                         uint32_t n, int gs) {
-    __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS];
+                                                         uint32_t n, int gs, const int64_t *pref) {
+    __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS], off[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
+    if (threadIdx.x == 0) {  // exact layout: region d starts at the sum of counts below d
+        uint64_t acc = 0;
+        for (int j = 0; j < G; ++j) {
+            off[j] = (uint32_t)acc;
+            acc += pref ? (uint64_t)pref[j] : 0u;
+        }
+    }
     const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
     for (size_t b0 = (size_t)blockIdx.x * per; b0 < q; b0 += (size_t)gridDim.x * per) {
         for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
@@ -3324,11 +3331,14 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
         for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
         __syncthreads();
         for (int j = threadIdx.x; j < G; j += blockDim.x) {
-            basep[j] = h[j] ? atomicAdd(&cursor[j], h[j]) : 0u;
+            basep[j] = h[j] ? off[j] + atomicAdd(&cursor[j], h[j]) : 0u;
             if (cap && h[j] && (uint64_t)basep[j] + h[j] > (uint64_t)(j + 1) * cap) {
                 atomicOr(ovf, 1u);
                 basep[j] = 0xFFFFFFFFu;  // nothing of this destination is written
             }
+            // exact layout: counts that do not match these lookups (a caller's
+            // error) never write past the arrays
+            if (pref && h[j] && (uint64_t)basep[j] + h[j] > q) basep[j] = 0xFFFFFFFFu;
         }
         __syncthreads();
 #pragma unroll
@@ -3394,7 +3404,7 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
     if (e != hipSuccess || q == 0) return e;
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
         in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, 0u, nullptr, nullptr, nullptr, 0u,
-        0);
+        0, nullptr);
     return hipGetLastError();
 }
 
@@ -3408,7 +3418,70 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
     const ArcIn<true> in{nullptr, src, keys, 0};
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
         in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, cap, ovf, sd, ring_ext,
-        (uint32_t)n, cz_shift(ib));
+        (uint32_t)n, cz_shift(ib), nullptr);
+    return hipGetLastError();
+}
+
+// Count pass of the exact-layout partition: counts[d] (int64, zeroed here) =
+// lookups whose key's arc is rank d's.  Keys only (16 B per lookup); a block
+// folds 1024 lookups into its LDS histogram per pass, one global atomic per
+// (block, destination) at the end.
+__global__ __launch_bounds__(256) void k_arc_count_keys(const cell128 *keys, size_t q,
+                                                        const ArcBound *bounds, int nb, int G,
+                                                        unsigned long long *counts) {
+    __shared__ uint32_t h[ARC_MAX_RANKS];
+    __shared__ ArcBound sb[ARC_MAX_RANKS];
+    for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+    for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
+    __syncthreads();
+    const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
+    for (size_t b0 = (size_t)blockIdx.x * per; b0 < q; b0 += (size_t)gridDim.x * per) {
+        int d[ARC_SCAT_R];
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) {
+            const size_t i = b0 + (size_t)k * blockDim.x + threadIdx.x;
+            d[k] = -1;
+            if (i < q) {
+                const u128 key = ld128(keys + i);
+                ArcRec r;
+                r.w0 = (uint64_t)key;
+                r.w1 = (uint64_t)(key >> 64);
+                r.hk = ARC_NEW << 8;
+                d[k] = arc_dest(r, sb, nb, G);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) (void)arc_wave_slots(d[k], G, h);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < G; j += blockDim.x)
+        if (h[j]) atomicAdd(&counts[j], (unsigned long long)h[j]);
+}
+
+hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
+                          int64_t *counts, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(counts, 0, (size_t)G * sizeof(int64_t), s);
+    if (e != hipSuccess || q == 0) return e;
+    k_arc_count_keys<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
+        keys, q, bounds, nb, G, reinterpret_cast<unsigned long long *>(counts));
+    return hipGetLastError();
+}
+
+// Exact-layout scatter: destination d's lookups at [sum_{j<d} counts[j], ...)
+// of the send arrays (counts from arc_count_keys over the same lookups, read
+// on the device: the scatter needs no host round trip); cursor: G words of
+// the caller's, zeroed here.
+hipError_t arc_scatter_exact(const uint32_t *src, const cell128 *keys, size_t q,
+                             const ArcBound *bounds, int nb, int G, const int64_t *counts,
+                             uint32_t *cursor, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
+                             uint64_t *sd, const cell128 *ring_ext, size_t n, int ib,
+                             hipStream_t s) {
+    hipError_t e = hipMemsetAsync(cursor, 0, (size_t)G * sizeof(uint32_t), s);
+    if (e != hipSuccess || q == 0) return e;
+    const ArcIn<true> in{nullptr, src, keys, 0};
+    k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
+        in, q, bounds, nb, G, cursor, skeys, ssrc, perm, 0u, nullptr, sd, ring_ext, (uint32_t)n,
+        cz_shift(ib), counts);
     return hipGetLastError();
 }
 

@@ -214,6 +214,16 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
                                  uint32_t *ssrc, uint32_t *perm, uint64_t *sd,
                                  const cell128 *ring_ext, size_t n, int ib, hipStream_t s);
 // Device-side region cursors / counts of the single-pass partition (G <= 64).
+// Exact-layout partition (ArcRouter's device-count path): per-destination
+// counts of the lookups' keys (int64, zeroed first), then the scatter that
+// lays destination d's lookups out at the sum of the counts below d.
+hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
+                          int64_t *counts, hipStream_t s);
+hipError_t arc_scatter_exact(const uint32_t *src, const cell128 *keys, size_t q,
+                             const ArcBound *bounds, int nb, int G, const int64_t *counts,
+                             uint32_t *cursor, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
+                             uint64_t *sd, const cell128 *ring_ext, size_t n, int ib,
+                             hipStream_t s);
 hipError_t arc_cursor_init(uint32_t *cursor, uint32_t *ovf, int G, uint32_t cap, hipStream_t s);
 hipError_t arc_counts_out(const uint32_t *cursor, const uint32_t *ovf, int G, uint32_t cap,
                           int64_t *counts, hipStream_t s);

@@ -29,7 +29,6 @@ namespace cxk {
 namespace {
 
 constexpr int WK_BLOCK = 256;
-constexpr int WK_RES = 256;  // staged results per wave (LDS ring, 64-result flushes)
 constexpr uint32_t WK_NONE = 0xFFFFFFFFu;
 constexpr uint32_t WK_CZ_NONE = 0xFFFFFFFFu;  // a node the 4-B format cannot hold (CZ_NONE)
 constexpr uint32_t CX_QI_ARC_MISS = 0xFE;     // key-first arc walk left the rank's rows
@@ -100,7 +99,6 @@ __device__ __forceinline__ uint64_t wk_pack(uint32_t own, uint32_t h, uint32_t s
 
 template <bool STATS, bool KF>
 __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
-    __shared__ uint64_t res_all[WK_BLOCK / 64][WK_RES];
     // entries land by LDS-DMA: region k of a wave = the 16-B quarters its
     // lanes loaded in gather k, lane-linear; lane j's entry is 64 contiguous
     // bytes in region j & 3 at (j >> 2) * 64 (regions 4 dwords apart mod 32
@@ -113,25 +111,43 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     __syncthreads();
     const int l0 = io.l0, gs = io.gs;
     const int lane = threadIdx.x & 63, qs = threadIdx.x & 3;
-    uint64_t *res = res_all[threadIdx.x >> 6];
     uint32_t *ent_w = ent_all[threadIdx.x >> 6];
     const uint32_t *ent = ent_w + (lane & 3) * RG + (lane >> 2) * 16;
-    for (int j = lane; j < WK_RES; j += 64) res[j] = 0;
     const size_t wave = (blockIdx.x * (size_t)WK_BLOCK + threadIdx.x) >> 6;
     const size_t base = wave * io.chunk;
     if (base >= io.q) return;  // wave-uniform
-    const size_t end = (base + io.chunk < io.q) ? base + io.chunk : io.q;
-    size_t head = base, flushed = base;
+    // lookups [base, base + cnt) of the batch, by offset from base (32-bit:
+    // chunk < 2^32); results are stored as each lookup finishes (a wave's
+    // lookups finish within a few hundred of each other, so its scattered
+    // 4-B / 1-B stores fill the same few lines, merged in L2)
+    const uint32_t cnt = (uint32_t)((base + io.chunk < io.q) ? io.chunk : io.q - base);
+    uint32_t *const own_w = KF ? nullptr : io.owner + base;
+    uint8_t *const hop_w = KF ? nullptr : io.hops + base;
+    uint8_t *const st_w = KF || !io.status ? nullptr : io.status + base;
+    uint64_t *const res_w = KF ? io.res_out + base : nullptr;
+    const cell128 *const key_r = io.keys + base;
+    const uint32_t *const src_r = io.src + base;
+    const uint64_t *const dh_r = KF && io.dh ? io.dh + base : nullptr;
+    auto put = [&](uint32_t o, uint32_t ow, uint32_t hh, uint32_t st) {
+        if (KF) {
+            res_w[o] = wk_pack(ow, hh, st);
+        } else {
+            own_w[o] = ow;
+            hop_w[o] = (uint8_t)hh;
+            if (st_w) st_w[o] = (uint8_t)st;
+        }
+    };
+    uint32_t head = 0;
 
     // slot A: the lookup being walked
     int mode = M_NONE, lvl = 0, rb = 0;
     uint32_t cur = 0, h = 0, pn = 0;
     uint64_t dmin = 0, dmax = 0;
     u128 key = 0;
-    size_t qi = 0;
+    uint32_t qi = 0;
     // slot B: the next lookup (key + source, then the source's ID pair)
     int bst = B_EMPTY, pst = P_WALK;
-    size_t pq = 0;
+    uint32_t pq = 0;
     u128 pkey = 0;
     uint32_t psrc = 0;
     uint64_t pd = 0;
@@ -139,8 +155,8 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     const uint32_t arc_top = KF ? (uint32_t)(CX_FINGERS - io.Lh) * 2u * n : 0u;  // KF: local rows
 
     for (;;) {
-        if (__ballot(mode != M_NONE || bst != B_EMPTY) == 0 && head >= end && flushed >= end)
-            break;  // wave-uniform: every lookup delivered and written
+        if (__ballot(mode != M_NONE || bst != B_EMPTY) == 0 && head >= cnt)
+            break;  // wave-uniform: every lookup delivered
 
         // ---- memory round: every load of the round, one wait ----
         uint32_t eidx = WK_NONE;
@@ -169,21 +185,19 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
             pa4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc));
             pb4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc + 1));
         }
-        {  // refill slot B in lookup order (results flush in 64-lookup runs)
-            size_t lim = end;
-            if (flushed + WK_RES < end) lim = flushed + WK_RES;
-            const size_t avail = lim > head ? lim - head : 0;
+        {  // refill slot B in lookup order
+            const uint32_t avail = cnt - head;
             const uint64_t want = __ballot(bst == B_EMPTY);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
             if (bst == B_EMPTY && rank < avail) {
                 pq = head + rank;
-                pkey = ld128(io.keys + pq);
-                psrc = io.src[pq];
-                if (KF && io.dh) pd = io.dh[pq];  // the origin's start: d >> gs, or LOCAL / BAD
+                pkey = ld128(key_r + pq);
+                psrc = src_r[pq];
+                if (KF && io.dh) pd = dh_r[pq];  // the origin's start: d >> gs, or LOCAL / BAD
                 bst = B_KEYS;
             }
-            const size_t took = (size_t)__popcll(want);
+            const uint32_t took = (uint32_t)__popcll(want);
             head += took < avail ? took : avail;
         }
         // quad-cooperative 64-B gathers straight into LDS (LDS-DMA): lane qs of
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
 
         // ---- deliver, promote slot B ----
         if (fin) {
-            res[qi & (WK_RES - 1)] = wk_pack(own, h, st);
+            put(qi, own, h, st);
             mode = M_NONE;
         }
         if (!plan && mode == M_NONE && bst == B_READY) {
@@ -351,8 +365,7 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
                 dmin = dmax = pd;
                 plan = true;
             } else {
-                res[qi & (WK_RES - 1)] =
-                    wk_pack(pst == P_LOCAL ? cur : CX_NONE, 0, pst == P_LOCAL ? CX_Q_OK : CX_Q_BADPEER);
+                put(qi, pst == P_LOCAL ? cur : CX_NONE, 0, pst == P_LOCAL ? CX_Q_OK : CX_Q_BADPEER);
             }
         }
 
@@ -372,32 +385,12 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
                         // a row outside the rank's arc + halo: a layout bug (the
                         // lookup was sent to its key's arc), reported, never seen
                         mode = M_NONE;
-                        res[qi & (WK_RES - 1)] = wk_pack(CX_NONE, h, CX_QI_ARC_MISS);
+                        put(qi, CX_NONE, h, CX_QI_ARC_MISS);
                     }
                 } else {
                     mode = M_EXACT;  // below the table
                 }
             }
-        }
-
-        // ---- flush complete 64-result runs in lookup order ----
-        for (int it = 0; it < 2; ++it) {
-            if (flushed >= end) break;
-            const size_t idx = flushed + lane;
-            const bool inr = idx < end;
-            const uint64_t v = inr ? res[idx & (WK_RES - 1)] : 0ull;
-            if (__ballot(!inr || (v >> 63)) != ~0ull) break;
-            if (inr) {
-                if (KF) {
-                    __builtin_nontemporal_store(v, io.res_out + idx);
-                } else {
-                    io.owner[idx] = (uint32_t)v;
-                    io.hops[idx] = (uint8_t)(v >> 32);
-                    if (io.status) io.status[idx] = (uint8_t)(v >> 40);
-                }
-                res[idx & (WK_RES - 1)] = 0;
-            }
-            flushed += 64;
         }
     }
     if (STATS) {
@@ -458,6 +451,7 @@ hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, co
     const size_t small = (q + 1023) / 1024;
     if (small < waves) waves = small ? small : 1;
     io.chunk = (q + waves - 1) / waves;
+    if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
     if (stats)
@@ -504,6 +498,7 @@ hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n
     const size_t small = (q + 1023) / 1024;
     if (small < waves) waves = small ? small : 1;
     io.chunk = (q + waves - 1) / waves;
+    if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
     k_walk<false, true><<<blocks, WK_BLOCK, 0, s>>>(io);

@@ -375,6 +375,46 @@ def test_arc_partition_async_device_counts(cx, O, n, G):
         assert int(small[G]) == 1
 
 
+@pytest.mark.parametrize("n,G", [(5000, 2), (1 << 16, 8), (70001, 5), (3, 4), (1 << 16, 64)])
+def test_arc_count_and_exact_scatter(cx, O, n, G):
+    """cx_arc_count_async + cx_arc_scatter_async (the exact-layout partition
+    ArcRouter.route_exact runs on RCCL): the counts equal the region
+    partition's, destination d's lookups fill rows [sum(counts[:d]),
+    sum(counts[:d + 1])) exactly, and keys, sources and hints equal the
+    region partition's through each call's permutation."""
+    import torch
+    q = 4096
+    ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA3F0 + n + G)
+    r = cx.Ring(ids_dev)
+    r.arc_build(G, 0)
+    sk, ss, perm, counts, sh = r.arc_partition_regions(G, srcs[0], keys[0], q, hints=True)
+    dc = torch.full((G,), -5, dtype=torch.int64, device="cuda")
+    r.arc_count_async(G, keys[0], dc)
+    cur = torch.full((G,), 77, dtype=torch.int32, device="cuda")
+    ak, as_, aperm, ah = r.arc_scatter_async(G, srcs[0], keys[0], dc, cur, hints=True)
+    torch.cuda.synchronize()
+    assert dc.tolist() == counts and sum(counts) == q
+    p0, p1 = perm.long(), aperm.long()
+    assert torch.equal(sk[p0], ak[p1]) and torch.equal(ss[p0], as_[p1])
+    assert torch.equal(sh[p0], ah[p1])
+    assert torch.equal(torch.sort(p1).values, torch.arange(q, device="cuda"))  # a permutation
+    off = 0
+    for d in range(G):
+        inr = (p1 >= off) & (p1 < off + counts[d])
+        assert int(inr.sum()) == counts[d]
+        assert bool((p0[inr] >= d * q).all()) and bool((p0[inr] < d * q + counts[d]).all())
+        off += counts[d]
+    # no hints, an empty batch
+    bk, bs, bperm = r.arc_scatter_async(G, srcs[0], keys[0], dc, cur)
+    torch.cuda.synchronize()
+    assert torch.equal(bk[bperm.long()], keys[0])
+    z = torch.zeros(G, dtype=torch.int64, device="cuda")
+    r.arc_count_async(G, keys[0][:0], z)
+    e = r.arc_scatter_async(G, srcs[0][:0], keys[0][:0], z, cur)
+    torch.cuda.synchronize()
+    assert int(z.abs().sum()) == 0 and e[0].shape[0] == 0
+
+
 def test_arc_hints_bad_sources_and_local_keys(cx, O):
     """Source hints at the edges: out-of-range sources (BADPEER at the arc
     rank), keys stored at their source (0 hops, resolved at the origin), and
@@ -448,7 +488,7 @@ def test_arc_soa_matches_oracle_clustered(cx, O):
 # sharing the GPU over gloo (RCCL refuses two ranks on one device): owners,
 # hops and statuses equal the replicated route of the same lookups.
 # ---------------------------------------------------------------------------
-def _router_worker(rank, world, port, n, q, chunks, out):
+def _router_worker(rank, world, port, n, q, chunks, out, exact=True):
     import os
     import sys
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
@@ -466,6 +506,7 @@ def _router_worker(rank, world, port, n, q, chunks, out):
     ring = chordx.Ring(ids)
     router = ArcRouter(ring, ring.n, rank, world, comm_device="cpu")
     router.chunks = chunks
+    router.exact = exact
     keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
     chordx.fill_splitmix(keys, 0xA7C1, offset=rank * q)
     src = ((torch.arange(q, device="cuda") * 7 + rank * 13) % ring.n).to(torch.int32)
@@ -483,8 +524,8 @@ def _router_worker(rank, world, port, n, q, chunks, out):
     tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("chunks", [1, 3])
-def test_arc_router_two_ranks_on_one_gpu(cx, chunks):
+@pytest.mark.parametrize("chunks,exact", [(1, True), (3, True), (1, False), (3, False)])
+def test_arc_router_two_ranks_on_one_gpu(cx, chunks, exact):
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -493,7 +534,7 @@ def test_arc_router_two_ranks_on_one_gpu(cx, chunks):
     s.close()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.start_processes(_router_worker, args=(2, port, 40000, 30000, chunks, out), nprocs=2,
+    mp.start_processes(_router_worker, args=(2, port, 40000, 30000, chunks, out, exact), nprocs=2,
                        join=True, start_method="spawn")
     for r in range(2):
         assert out[r][:3] == (True, True, True), (r, out[r])
@@ -535,9 +576,12 @@ def _rccl_worker(_i, n, q, chunks, out):
     src[::97] = ring.n + 3  # bad sources travel and come back as CX_Q_BADPEER
     ow, hp, st = ring.route(src, keys)
     res = []
-    for it in range(3):  # the second call reuses the pinned count buffer; the third
-        # forces every piece's region to overflow (cap 64): the pieces are
-        # partitioned again in two passes and the counts gathered once more
+    for it in range(4):  # calls 0, 1: the exact-layout path (the second reuses the
+        # pinned count buffer and the side stream); 2, 3: the region layout, the
+        # third with every piece's region forced to overflow (cap 64): the
+        # pieces are partitioned again in two passes and the counts gathered
+        # once more
+        router.exact = it < 2
         router.region_cap = (lambda qc, G: 64) if it == 2 else None
         owner = torch.full((q,), -5, dtype=torch.int32, device=dev)
         hops = torch.zeros(q, dtype=torch.uint8, device=dev)
@@ -567,8 +611,8 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
                        start_method="spawn")
     backend, res, bad, succ_ok = out[0]
     assert backend == "nccl" and bad == len(range(0, q, 97))
-    for r in res:
-        assert r == (True, True, True, 2, q), r
+    for it, r in enumerate(res):  # the exact path walks its own region in place
+        assert r == (True, True, True, 2, 0 if it < 2 else q), (it, r)
     assert succ_ok == (True, 2, q)
 
 
