@@ -423,19 +423,31 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
 /* Exact-layout partition in two asynchronous passes (no capacity, no
  * overflow, no host synchronisation): cx_arc_count_async writes the
  * per-destination counts of the lookups' keys into counts_dev (device,
- * world int64); cx_arc_scatter_async, given those counts (still on the
- * device), lays destination d's lookups out at [sum_{j<d} counts[j], ...) of
- * send_keys / send_src / send_hint (q entries each; send_hint may be NULL)
- * with perm[i] = the slot of lookup i.  cursor_dev: world uint32 of scratch
- * (device) per concurrent scatter.  Both run on the ring's stream, so a
- * caller can count every piece, exchange the counts in one collective, and
- * scatter each piece on another stream while earlier pieces are walked. */
+ * world int64) and, with own_idx (device, q uint32) and own_cursor (device,
+ * one uint32 of scratch), compacts the indices of the lookups of rank `me`'s
+ * own arc into own_idx[0 .. counts[me]) (any order) for cx_arc_route_local;
+ * cx_arc_scatter_async, given those counts (still on the device), lays
+ * destination d's lookups out at [sum_{j<d} counts[j], ...) of send_keys /
+ * send_src / send_hint (q entries each; send_hint may be NULL) with perm[i] =
+ * the slot of lookup i; skip_rank >= 0 leaves that destination's lookups out
+ * (perm = 0xFFFFFFFF, their count taken as 0: the rank walks them in place).
+ * cursor_dev: world uint32 of scratch (device) per concurrent scatter.  Both
+ * run on the ring's stream, so a caller can count every piece, exchange the
+ * counts in one collective, and scatter each piece on another stream while
+ * earlier pieces are walked. */
 int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size_t q,
-                       int64_t *counts_dev);
+                       int64_t *counts_dev, int me, uint32_t *own_idx, uint32_t *own_cursor);
 int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
                          const cx_u128 *keys, size_t q, const int64_t *counts_dev,
                          uint32_t *cursor_dev, cx_u128 *send_keys, uint32_t *send_src,
-                         uint64_t *send_hint, uint32_t *perm);
+                         uint64_t *send_hint, uint32_t *perm, int skip_rank);
+/* The lookups of this rank's own arc walked in place: keys[idx[j]] issued at
+ * src[idx[j]] for j < q, over the arc planes (as cx_arc_route), started from
+ * the sources' own IDs; owner / hops / status (status may be NULL) written at
+ * idx[j] -- no exchange, no packed results, no delivery pass. */
+int cx_arc_route_local(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
+                       const uint32_t *idx, size_t q, uint32_t *owner, uint8_t *hops,
+                       uint8_t *status);
 int cx_arc_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size_t q,
                  uint64_t *res);
 /* cx_arc_route with the origins' source hints (cx_arc_partition_regions

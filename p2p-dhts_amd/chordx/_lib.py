@@ -45,7 +45,7 @@ EXPORTS = (
     "cx_arc_build", "cx_arc_info", "cx_arc_seed", "cx_arc_start", "cx_arc_step",
     "cx_arc_bucket", "cx_arc_send_ahead",
     "cx_arc_partition", "cx_arc_partition_regions", "cx_arc_partition_regions_async",
-    "cx_arc_count_async", "cx_arc_scatter_async",
+    "cx_arc_count_async", "cx_arc_scatter_async", "cx_arc_route_local",
     "cx_arc_route", "cx_arc_route_hinted",
     "cx_arc_deliver",
     "cx_hex_parse", "cx_hex_format",
@@ -132,8 +132,9 @@ def lib() -> ctypes.CDLL:
         "cx_arc_partition": ([vp, i, vp, vp, sz, vp, vp, vp, vp], i),
         "cx_arc_partition_regions": ([vp, i, vp, vp, sz, u64, vp, vp, vp, vp, vp], i),
         "cx_arc_partition_regions_async": ([vp, i, vp, vp, sz, u64, vp, vp, vp, vp, vp], i),
-        "cx_arc_count_async": ([vp, i, vp, sz, vp], i),
-        "cx_arc_scatter_async": ([vp, i, vp, vp, sz, vp, vp, vp, vp, vp, vp], i),
+        "cx_arc_count_async": ([vp, i, vp, sz, vp, i, vp, vp], i),
+        "cx_arc_scatter_async": ([vp, i, vp, vp, sz, vp, vp, vp, vp, vp, vp, i], i),
+        "cx_arc_route_local": ([vp, vp, vp, vp, sz, vp, vp, vp], i),
         "cx_arc_route_hinted": ([vp, vp, vp, vp, sz, vp], i),
         "cx_arc_route": ([vp, vp, vp, sz, vp], i),
         "cx_arc_deliver": ([vp, vp, vp, sz, vp, vp, vp], i),

@@ -373,13 +373,17 @@ class ArcRouter:
         """route_soa on RCCL with the exact-layout partition (module docstring).
 
         Current stream: the count pass of every piece (arc_count_async into one
-        device row), the all_gather of that row and its one host read, then
-        per piece the walk of this rank's own region in place and of the
-        lookups the other ranks sent, the answers' return exchange and the
-        delivery.  Side stream: the scatter of each piece (arc_scatter_async,
-        reading the counts on the device), started as soon as the counts
-        exist, and each piece's outgoing exchange, which waits on that
-        scatter only.  Returns 2 (rounds of the protocol)."""
+        device row; it also compacts the indices of the lookups of this rank's
+        own arc), the all_gather of that row and its one host read, then per
+        piece the walk of the own lookups in place (arc_route_local: outputs
+        straight into owner / hops / status), of the lookups the other ranks
+        sent, the answers' return exchange and the delivery of this rank's
+        remote lookups.  Side stream (G > 1): the scatter of each piece's
+        remote lookups (arc_scatter_async, reading the counts on the device,
+        own lookups skipped), started as soon as the counts exist, and each
+        piece's outgoing exchange, which waits on that scatter only.  A
+        one-rank group has no remote lookups: no scatter, no all_to_all, no
+        delivery.  Returns 2 (rounds of the protocol)."""
         eng, G, me = self.engine, self.world, self.rank
         dev = keys.device
         q = int(keys.shape[0])
@@ -391,45 +395,51 @@ class ArcRouter:
         hints = bool(self.hints and getattr(eng, "arc_hints", False))
         row = torch.zeros(1 + kmax * G, dtype=torch.int64, device=dev)
         row[0] = k | (int(hints) << 20)
+        own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
+        own_cur = torch.empty(k, dtype=torch.int32, device=dev)
         for c in range(k):
-            eng.arc_count_async(G, keys[cut[c]:cut[c + 1]], row[1 + c * G: 1 + (c + 1) * G])
-        cursors = torch.empty(k * G, dtype=torch.int32, device=dev)
-        side.wait_stream(main)  # the counts (and the caller's inputs) are written
+            eng.arc_count_async(G, keys[cut[c]:cut[c + 1]], row[1 + c * G: 1 + (c + 1) * G], me,
+                                own_idx[cut[c]:], own_cur[c:c + 1])
         parts, ready = [], []
-        with torch.cuda.stream(side):
-            for c in range(k):
-                sl = slice(cut[c], cut[c + 1])
-                part = eng.arc_scatter_async(G, src[sl], keys[sl], row[1 + c * G: 1 + (c + 1) * G],
-                                             cursors[c * G: (c + 1) * G], hints=hints)
-                parts.append(part if hints else part + (None,))
-                ev = torch.cuda.Event()
-                ev.record(side)
-                ready.append(ev)
+        if G > 1:
+            cursors = torch.empty(k * G, dtype=torch.int32, device=dev)
+            side.wait_stream(main)  # the counts (and the caller's inputs) are written
+            with torch.cuda.stream(side):
+                for c in range(k):
+                    sl = slice(cut[c], cut[c + 1])
+                    part = eng.arc_scatter_async(G, src[sl], keys[sl],
+                                                 row[1 + c * G: 1 + (c + 1) * G],
+                                                 cursors[c * G: (c + 1) * G], hints=hints, skip=me)
+                    parts.append(part if hints else part + (None,))
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    ready.append(ev)
         mat = self._gather_row(row)
         kg = int((mat[:, 0] & 0xFFFFF).max())  # pieces every rank runs
         use_h = bool(int((mat[:, 0] >> 20).min()))  # every rank's pieces carry hints
-        if kg > k:  # this rank's extra pieces are empty
+        if G > 1 and kg > k:  # this rank's extra pieces are empty
             e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=dev),
                  torch.empty(0, dtype=torch.int64, device=dev))
             parts += [e] * (kg - k)
             ready += [None] * (kg - k)
-            cut += [q] * (kg - k)
+        cut += [q] * (kg - k)
         cnt = [[int(mat[me, 1 + c * G + d]) for d in range(G)] for c in range(kg)]
-        recv = [[int(mat[r, 1 + c * G + me]) for r in range(G)] for c in range(kg)]
-        offs = []
+        recv = [[int(mat[r, 1 + c * G + me]) if r != me else 0 for r in range(G)]
+                for c in range(kg)]
+        for c in range(kg):
+            if sum(cnt[c]) != cut[c + 1] - cut[c]:
+                raise RuntimeError("arc count pass and partition disagree")
+        offs = []  # remote regions only (the own lookups take no slot)
         for c in range(kg):
             o, acc = [], 0
             for d in range(G):
                 o.append(acc)
-                acc += cnt[c][d]
+                acc += cnt[c][d] if d != me else 0
             offs.append(o)
         # lookups that cross ranks anywhere (the same answer on every rank):
         # without any, no rank issues an all_to_all
         remote = any(int(mat[r, 1 + c * G + d]) for r in range(G) for d in range(G) if r != d
                      for c in range(kg))
-        for c in range(kg):
-            if sum(cnt[c]) != cut[c + 1] - cut[c]:
-                raise RuntimeError("arc count pass and partition disagree")
 
         def region(t, c, d):
             return t[offs[c][d]: offs[c][d] + cnt[c][d]] if d != me else t[:0]
@@ -439,12 +449,12 @@ class ArcRouter:
             Returns ([(received, work)], event after the issue on the side
             stream)."""
             sk, ss, _, sh = parts[c]
-            rs = [recv[c][r] if r != me else 0 for r in range(G)]
             out = []
             with torch.cuda.stream(side):
                 for t in ((sk, ss, sh) if use_h else (sk, ss)):
-                    o = torch.empty((sum(rs),) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
-                    w = self._a2a_views(list(torch.split(o, rs)),
+                    o = torch.empty((sum(recv[c]),) + tuple(t.shape[1:]), dtype=t.dtype,
+                                    device=dev)
+                    w = self._a2a_views(list(torch.split(o, recv[c])),
                                         [region(t, c, d) for d in range(G)])
                     out.append((o, w))
                 ev = torch.cuda.Event()
@@ -457,16 +467,17 @@ class ArcRouter:
             got = inflight
             if remote and c + 1 < kg:
                 inflight = send(c + 1)
-            sk, ss, _, sh = parts[c]
-            back = torch.empty(cut[c + 1] - cut[c], dtype=torch.int64, device=dev)
-            if ready[c] is not None:
-                main.wait_event(ready[c])
-            o, n_ = offs[c][me], cnt[c][me]
-            if n_:  # this rank's own region: walked in place
-                eng.arc_route(ss[o:o + n_], sk[o:o + n_], res=back[o:o + n_],
-                              hint=sh[o:o + n_] if use_h else None)
-            work = None
+            sl = slice(cut[c], cut[c + 1])
+            n_own = cnt[c][me]
+            if n_own:  # this rank's own lookups: walked in place, outputs written
+                eng.arc_route_local(src[sl], keys[sl], own_idx[cut[c]: cut[c] + n_own], owner[sl],
+                                    hops[sl], status[sl] if status is not None else None)
+            back, work = None, None
             if remote:
+                n_rem = sum(cnt[c]) - n_own
+                # the piece's length (perm names slots < n_rem; arc_deliver
+                # takes a result buffer at least as long as perm)
+                back = torch.empty(cut[c + 1] - cut[c], dtype=torch.int64, device=dev)
                 arrived, ev = got
                 main.wait_event(ev)
                 for _, w in arrived:
@@ -475,18 +486,22 @@ class ArcRouter:
                 rk, rs_ = arrived[0][0], arrived[1][0]
                 rh = arrived[2][0] if use_h else None
                 res = eng.arc_route(rs_, rk, hint=rh) if use_h else eng.arc_route(rs_, rk)
-                splits = [recv[c][r] if r != me else 0 for r in range(G)]
                 work = self._a2a_views([region(back, c, d) for d in range(G)],
-                                       list(torch.split(res, splits)))
-                self.records_sent += sum(cnt[c]) - cnt[c][me]
+                                       list(torch.split(res, recv[c])))
+                self.records_sent += n_rem
             backs.append((back, work))
-        for c in range(kg):
-            back, work = backs[c]
-            if work is not None:
-                work.wait()
-            sl = slice(cut[c], cut[c + 1])
-            eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
-                            status[sl] if status is not None else None)
+        if G > 1:
+            for c in range(kg):
+                back, work = backs[c]
+                if ready[c] is not None:
+                    main.wait_event(ready[c])  # perm is written (no remote: nothing else)
+                if work is not None:
+                    work.wait()
+                if back is None:
+                    continue
+                sl = slice(cut[c], cut[c + 1])
+                eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
+                                status[sl] if status is not None else None)
         self.rounds = 2
         return 2
 

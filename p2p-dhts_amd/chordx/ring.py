@@ -591,25 +591,40 @@ class Ring:
                                                        _ptr(perm), _ptr(counts)))
         return (skeys, ssrc, perm, shint) if hints else (skeys, ssrc, perm)
 
-    def arc_count_async(self, world: int, keys, counts):
+    def arc_count_async(self, world: int, keys, counts, me: int = -1, own_idx=None,
+                        own_cursor=None):
         """cx_arc_count_async: per-destination counts of the keys' arcs into
-        `counts` (device int64, world elements), no host synchronisation."""
+        `counts` (device int64, world elements), no host synchronisation; with
+        own_idx (device int32, >= q elements) and own_cursor (device int32, one
+        element): the indices of rank `me`'s own lookups compacted into
+        own_idx[:counts[me]]."""
         keys = self._prep_keys(keys)
         if not (_is_dev(keys) and _is_dev(counts)):
             raise TypeError("arc routing takes device tensors")
         if not (counts.dtype == torch.int64 and counts.is_contiguous()
                 and counts.numel() == world):
             raise TypeError("counts: a contiguous int64 device tensor of world elements")
+        if own_idx is not None:
+            if not (0 <= me < world):
+                raise ValueError("me must be in [0, world)")
+            for t, n_ in ((own_idx, keys.shape[0]), (own_cursor, 1)):
+                if t is None or not (_is_dev(t) and t.is_contiguous() and t.element_size() == 4
+                                     and t.numel() >= n_):
+                    raise TypeError("own_idx (>= q) / own_cursor (1): contiguous 4-byte device "
+                                    "tensors")
         self._arc_stream()
         L.check(L.lib().cx_arc_count_async(self._h, world, _ptr(keys), keys.shape[0],
-                                           _ptr(counts)))
+                                           _ptr(counts), int(me), _ptr(own_idx),
+                                           _ptr(own_cursor)))
 
-    def arc_scatter_async(self, world: int, src, keys, counts, cursor, hints: bool = False):
+    def arc_scatter_async(self, world: int, src, keys, counts, cursor, hints: bool = False,
+                          skip: int = -1):
         """cx_arc_scatter_async: the exact-layout partition of (src, keys) by the
         device counts of arc_count_async over the same keys; cursor: device
-        int32 scratch of world elements (one per concurrent scatter).  Returns
-        (send_keys, send_src, perm[, send_hint]), destination d's lookups at
-        rows [sum(counts[:d]), sum(counts[:d + 1]))."""
+        int32 scratch of world elements (one per concurrent scatter); skip: a
+        destination left out (its lookups' perm = -1, its count taken as 0).
+        Returns (send_keys, send_src, perm[, send_hint]), destination d's
+        lookups at rows [sum(counts[:d]), sum(counts[:d + 1]))."""
         keys = self._prep_keys(keys)
         src = self._prep_u32(src, "src", keys.shape[0])
         for t, n, w in ((counts, world, 8), (cursor, world, 4)):
@@ -618,6 +633,8 @@ class Ring:
                                 "world elements")
         if not (_is_dev(keys) and _is_dev(src)):
             raise TypeError("arc routing takes device tensors")
+        if not -1 <= skip < world:
+            raise ValueError("skip must be -1 or a rank")
         q = keys.shape[0]
         skeys = torch.empty((q, 2), dtype=torch.int64, device=keys.device)
         ssrc = torch.empty(q, dtype=torch.int32, device=keys.device)
@@ -626,8 +643,28 @@ class Ring:
         self._arc_stream()
         L.check(L.lib().cx_arc_scatter_async(self._h, world, _ptr(src), _ptr(keys), q,
                                              _ptr(counts), _ptr(cursor), _ptr(skeys), _ptr(ssrc),
-                                             _ptr(shint), _ptr(perm)))
+                                             _ptr(shint), _ptr(perm), int(skip)))
         return (skeys, ssrc, perm, shint) if hints else (skeys, ssrc, perm)
+
+    def arc_route_local(self, src, keys, idx, owner, hops, status=None):
+        """cx_arc_route_local: the lookups keys[idx[j]] from src[idx[j]] of this
+        rank's own arc walked in place; owner / hops / status written at
+        idx[j] (status may be None)."""
+        keys = self._prep_keys(keys)
+        src = self._prep_u32(src, "src", keys.shape[0])
+        if not (_is_dev(keys) and _is_dev(src) and _is_dev(idx)):
+            raise TypeError("arc routing takes device tensors")
+        if not (idx.is_contiguous() and idx.element_size() == 4):
+            raise TypeError("idx: a contiguous 4-byte device tensor")
+        q0 = keys.shape[0]
+        for t, w, name in ((owner, 4, "owner"), (hops, 1, "hops"), (status, 1, "status")):
+            if t is not None and not (_is_dev(t) and t.element_size() == w and t.numel() >= q0
+                                      and t.is_contiguous()):
+                raise TypeError(f"{name}: contiguous device tensor of {w}-byte elements, >= "
+                                "len(keys)")
+        self._arc_stream()
+        L.check(L.lib().cx_arc_route_local(self._h, _ptr(src), _ptr(keys), _ptr(idx), idx.numel(),
+                                           _ptr(owner), _ptr(hops), _ptr(status)))
 
     def arc_route(self, src, keys, res=None, hint=None):
         """Packed results (int64: owner | hops << 32 | status << 40 | 1 << 63)

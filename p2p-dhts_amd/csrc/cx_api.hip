@@ -2253,8 +2253,10 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
 }
 
 int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size_t q,
-                       int64_t *counts_dev) {
+                       int64_t *counts_dev, int me, uint32_t *own_idx, uint32_t *own_cursor) {
     CX_CHECK(ring && counts_dev, CX_E_INVALID, "null argument");
+    CX_CHECK(!own_idx || (own_cursor && me >= 0 && me < world), CX_E_INVALID,
+             "own_idx needs own_cursor and 0 <= me < world");
     CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
     CX_CHECK(q == 0 || keys, CX_E_INVALID, "null buffer");
     CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many lookups for one rank");
@@ -2264,15 +2266,17 @@ int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size
     int rc = use_device(ring);
     if (rc) return rc;
     CX_HIP(cxk::arc_count_keys(reinterpret_cast<const cell128 *>(keys), q, ring->d_arc_bounds,
-                               ring->arc_nb, world, counts_dev, ring->stream));
+                               ring->arc_nb, world, counts_dev, me, own_idx, own_cursor,
+                               ring->stream));
     return CX_OK;
 }
 
 int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
                          const cx_u128 *keys, size_t q, const int64_t *counts_dev,
                          uint32_t *cursor_dev, cx_u128 *send_keys, uint32_t *send_src,
-                         uint64_t *send_hint, uint32_t *perm) {
+                         uint64_t *send_hint, uint32_t *perm, int skip_rank) {
     CX_CHECK(ring && counts_dev && cursor_dev, CX_E_INVALID, "null argument");
+    CX_CHECK(skip_rank >= -1 && skip_rank < world, CX_E_INVALID, "skip_rank out of range");
     CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
     CX_CHECK(q == 0 || (src && keys && send_keys && send_src && perm), CX_E_INVALID,
              "null buffer");
@@ -2286,8 +2290,27 @@ int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
     CX_HIP(cxk::arc_scatter_exact(src, reinterpret_cast<const cell128 *>(keys), q,
                                   ring->d_arc_bounds, ring->arc_nb, world, counts_dev, cursor_dev,
                                   reinterpret_cast<cell128 *>(send_keys), send_src, perm,
-                                  send_hint, ring->d_ring_ext, ring->n, ring->pk_ib,
+                                  send_hint, ring->d_ring_ext, ring->n, ring->pk_ib, skip_rank,
                                   ring->stream));
+    return CX_OK;
+}
+
+int cx_arc_route_local(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
+                       const uint32_t *idx, size_t q, uint32_t *owner, uint8_t *hops,
+                       uint8_t *status) {
+    CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
+    CX_CHECK(ring->arc_world > 0 && ring->d_arc_tree, CX_E_STATE, "arc not built (cx_arc_build)");
+    CX_CHECK(!ring->edited(), CX_E_STATE, "state uploaded after cx_arc_build: use cx_route");
+    CX_CHECK(q == 0 || (src && keys && idx && owner && hops), CX_E_INVALID, "null buffer");
+    CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many lookups for one rank");
+    int rc = use_device(ring);
+    if (rc) return rc;
+    SearchView v = ring->sv();
+    v.dir = ring->d_dir;
+    CX_HIP(cxk::route_walk_arc_local(ring->d_ring_ext, ring->d_ring, ring->n, ring->d_arc_tree,
+                                     ring->rt_l0, ring->pk_ib, v, ring->arc_Lh, ring->arc_plo,
+                                     ring->arc_M, src, reinterpret_cast<const cell128 *>(keys),
+                                     idx, q, owner, hops, status, ring->stream));
     return CX_OK;
 }
 

@@ -2086,23 +2086,16 @@ void k_cz_build_roots2(FingerView fv, const cell128 *ring, uint32_t n, int lvl_b
     }
     const int i = lvl_base + lvl;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    // plane gathers non-temporal (the planes are 4.6 GiB of mostly single
-    // reads; 0.7 % faster, profiles/r04/store_ab/nt_gathers); the ID slices
-    // (64 MiB, re-read) stay cached
-    auto ld32nt = [](const uint32_t *base, uint32_t x) -> uint32_t {
-        const uint32_t *a =
-            reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + x * 4u);
-#if CX_AB_PLANE_CACHED  // A/B build only (libchordx_ab): ordinary plane gathers
-        return *a;
-#else
-        return __builtin_nontemporal_load(a);
-#endif
-    };
+    // plane gathers through the caches: round 4 made them non-temporal (0.7 %
+    // faster then, profiles/r04/store_ab/nt_gathers); a round-5 ABBA of the
+    // current build (profiles/r05/build_ab/) has cached ones ahead, 24.5-24.7
+    // vs 26.8-27.2 ms per fingers + table build and 29.5 vs 35.2 GB fetched
+    // (neighbouring roots share plane lines in L2)
     auto fat = [&](uint32_t x, int l) -> uint32_t {
-        return ld32nt(fv.F + (size_t)(l - fv.L) * fv.sl, x);
+        return ld32(fv.F + (size_t)(l - fv.L) * fv.sl, x);
     };
     auto c2 = [&](uint32_t x, int l) -> uint32_t {
-        return ld32nt(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
+        return ld32(fv.C2 + (size_t)(l - fv.L - 1) * fv.sl, x);
     };
     bool oob = false;
     auto chk = [&](uint32_t x) -> uint32_t {
@@ -3287,7 +3280,8 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
                                                          uint32_t *ssrc, uint32_t *slot_of,
                                                          uint32_t cap, uint32_t *ovf,
                                                          uint64_t *sd, const cell128 *ring_ext,
-                                                         uint32_t n, int gs, const int64_t *pref) {
+                                                         uint32_t n, int gs, const int64_t *pref,
+                                                         int skip) {
     __shared__ uint32_t h[ARC_MAX_RANKS], basep[ARC_MAX_RANKS], off[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
@@ -3295,7 +3289,7 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
         uint64_t acc = 0;
         for (int j = 0; j < G; ++j) {
             off[j] = (uint32_t)acc;
-            acc += pref ? (uint64_t)pref[j] : 0u;
+            acc += pref && j != skip ? (uint64_t)pref[j] : 0u;
         }
     }
     const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
@@ -3312,6 +3306,10 @@ __global__ __launch_bounds__(256) void k_arc_scatter_soa(ArcIn<true> in, size_t 
             if (i < q) {
                 r[k] = in.get(i);
                 d[k] = arc_dest(r[k], sb, nb, G);
+                if (d[k] == skip) {  // walked in place by the rank itself: no slot
+                    slot_of[i] = 0xFFFFFFFFu;
+                    d[k] = -1;
+                }
             }
         }
         uint64_t dh[ARC_SCAT_R];
@@ -3361,7 +3359,9 @@ __global__ void k_arc_deliver(const uint64_t *res, const uint32_t *slot_of, size
                               uint32_t *owner, uint8_t *hops, uint8_t *status) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q;
          i += (size_t)gridDim.x * blockDim.x) {
-        const uint64_t v = res[slot_of ? slot_of[i] : i];
+        const uint32_t sl = slot_of ? slot_of[i] : (uint32_t)i;
+        if (sl == 0xFFFFFFFFu) continue;  // the origin's own lookup: answered in place
+        const uint64_t v = res[sl];
         owner[i] = (uint32_t)v;
         hops[i] = (uint8_t)(v >> 32);
         if (status) status[i] = (uint8_t)(v >> 40);
@@ -3404,7 +3404,7 @@ hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
     if (e != hipSuccess || q == 0) return e;
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
         in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, 0u, nullptr, nullptr, nullptr, 0u,
-        0, nullptr);
+        0, nullptr, -1);
     return hipGetLastError();
 }
 
@@ -3418,25 +3418,31 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
     const ArcIn<true> in{nullptr, src, keys, 0};
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
         in, q, bounds, nb, G, cursor_dev, skeys, ssrc, perm, cap, ovf, sd, ring_ext,
-        (uint32_t)n, cz_shift(ib), nullptr);
+        (uint32_t)n, cz_shift(ib), nullptr, -1);
     return hipGetLastError();
 }
 
 // Count pass of the exact-layout partition: counts[d] (int64, zeroed here) =
-// lookups whose key's arc is rank d's.  Keys only (16 B per lookup); a block
-// folds 1024 lookups into its LDS histogram per pass, one global atomic per
-// (block, destination) at the end.
+// lookups whose key's arc is rank d's, and (own_idx != nullptr) the indices of
+// the lookups of rank `me`'s own arc compacted into own_idx (any order; the
+// rank walks them in place, cx_arc_route_local).  Keys only (16 B per lookup,
+// + 4 B per own lookup); 1024 lookups per block pass, one global atomic per
+// (block, destination) at the end and one per pass for the own slots.
 __global__ __launch_bounds__(256) void k_arc_count_keys(const cell128 *keys, size_t q,
                                                         const ArcBound *bounds, int nb, int G,
-                                                        unsigned long long *counts) {
-    __shared__ uint32_t h[ARC_MAX_RANKS];
+                                                        unsigned long long *counts, int me,
+                                                        uint32_t *own_idx, uint32_t *own_cur) {
+    __shared__ uint32_t h[ARC_MAX_RANKS], tot[ARC_MAX_RANKS];
+    __shared__ uint32_t obase;
     __shared__ ArcBound sb[ARC_MAX_RANKS];
-    for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+    for (int j = threadIdx.x; j < G; j += blockDim.x) tot[j] = 0;
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
-    __syncthreads();
     const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
     for (size_t b0 = (size_t)blockIdx.x * per; b0 < q; b0 += (size_t)gridDim.x * per) {
+        for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
+        __syncthreads();
         int d[ARC_SCAT_R];
+        uint32_t slot[ARC_SCAT_R];
 #pragma unroll
         for (int k = 0; k < ARC_SCAT_R; ++k) {
             const size_t i = b0 + (size_t)k * blockDim.x + threadIdx.x;
@@ -3451,37 +3457,50 @@ __global__ __launch_bounds__(256) void k_arc_count_keys(const cell128 *keys, siz
             }
         }
 #pragma unroll
-        for (int k = 0; k < ARC_SCAT_R; ++k) (void)arc_wave_slots(d[k], G, h);
+        for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
+        __syncthreads();
+        for (int j = threadIdx.x; j < G; j += blockDim.x) tot[j] += h[j];
+        if (own_idx && threadIdx.x == 0) obase = h[me] ? atomicAdd(own_cur, h[me]) : 0u;
+        __syncthreads();
+        if (own_idx) {
+#pragma unroll
+            for (int k = 0; k < ARC_SCAT_R; ++k)
+                if (d[k] == me) own_idx[obase + slot[k]] = (uint32_t)(b0 + (size_t)k * blockDim.x + threadIdx.x);
+        }
     }
     __syncthreads();
     for (int j = threadIdx.x; j < G; j += blockDim.x)
-        if (h[j]) atomicAdd(&counts[j], (unsigned long long)h[j]);
+        if (tot[j]) atomicAdd(&counts[j], (unsigned long long)tot[j]);
 }
 
 hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
-                          int64_t *counts, hipStream_t s) {
+                          int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_cur,
+                          hipStream_t s) {
     hipError_t e = hipMemsetAsync(counts, 0, (size_t)G * sizeof(int64_t), s);
+    if (e == hipSuccess && own_idx) e = hipMemsetAsync(own_cur, 0, sizeof(uint32_t), s);
     if (e != hipSuccess || q == 0) return e;
     k_arc_count_keys<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
-        keys, q, bounds, nb, G, reinterpret_cast<unsigned long long *>(counts));
+        keys, q, bounds, nb, G, reinterpret_cast<unsigned long long *>(counts), me, own_idx,
+        own_cur);
     return hipGetLastError();
 }
 
 // Exact-layout scatter: destination d's lookups at [sum_{j<d} counts[j], ...)
 // of the send arrays (counts from arc_count_keys over the same lookups, read
 // on the device: the scatter needs no host round trip); cursor: G words of
-// the caller's, zeroed here.
+// the caller's, zeroed here.  skip >= 0: that destination's lookups (the
+// rank's own, walked in place) take no slot (perm = 0xFFFFFFFF, counted as 0).
 hipError_t arc_scatter_exact(const uint32_t *src, const cell128 *keys, size_t q,
                              const ArcBound *bounds, int nb, int G, const int64_t *counts,
                              uint32_t *cursor, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
-                             uint64_t *sd, const cell128 *ring_ext, size_t n, int ib,
+                             uint64_t *sd, const cell128 *ring_ext, size_t n, int ib, int skip,
                              hipStream_t s) {
     hipError_t e = hipMemsetAsync(cursor, 0, (size_t)G * sizeof(uint32_t), s);
     if (e != hipSuccess || q == 0) return e;
     const ArcIn<true> in{nullptr, src, keys, 0};
     k_arc_scatter_soa<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
         in, q, bounds, nb, G, cursor, skeys, ssrc, perm, 0u, nullptr, sd, ring_ext, (uint32_t)n,
-        cz_shift(ib), counts);
+        cz_shift(ib), counts, skip);
     return hipGetLastError();
 }
 

@@ -204,6 +204,13 @@ hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n
                           const uint64_t *arc_tree, int l0, int ib, const SearchView &sv, int Lh,
                           uint32_t plo, uint32_t M, const uint32_t *src, const cell128 *keys,
                           size_t q, const uint64_t *dh, uint64_t *res, hipStream_t s);
+// The arc rank's own lookups in place: keys[idx[j]] from src[idx[j]], outputs
+// at idx[j] (cx_arc_route_local).
+hipError_t route_walk_arc_local(const cell128 *ring_ext, const cell128 *ring, size_t n,
+                                const uint64_t *arc_tree, int l0, int ib, const SearchView &sv,
+                                int Lh, uint32_t plo, uint32_t M, const uint32_t *src,
+                                const cell128 *keys, const uint32_t *idx, size_t q,
+                                uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s);
 hipError_t arc_partition(const uint32_t *src, const cell128 *keys, size_t q,
                          const ArcBound *bounds, int nb, int G, uint32_t *counts_dev,
                          uint32_t *cursor_dev, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
@@ -218,11 +225,12 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
 // counts of the lookups' keys (int64, zeroed first), then the scatter that
 // lays destination d's lookups out at the sum of the counts below d.
 hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
-                          int64_t *counts, hipStream_t s);
+                          int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_cur,
+                          hipStream_t s);
 hipError_t arc_scatter_exact(const uint32_t *src, const cell128 *keys, size_t q,
                              const ArcBound *bounds, int nb, int G, const int64_t *counts,
                              uint32_t *cursor, cell128 *skeys, uint32_t *ssrc, uint32_t *perm,
-                             uint64_t *sd, const cell128 *ring_ext, size_t n, int ib,
+                             uint64_t *sd, const cell128 *ring_ext, size_t n, int ib, int skip,
                              hipStream_t s);
 hipError_t arc_cursor_init(uint32_t *cursor, uint32_t *ovf, int G, uint32_t cap, hipStream_t s);
 hipError_t arc_counts_out(const uint32_t *cursor, const uint32_t *ovf, int G, uint32_t cap,

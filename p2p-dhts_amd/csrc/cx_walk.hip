@@ -34,7 +34,7 @@ constexpr uint32_t WK_CZ_NONE = 0xFFFFFFFFu;  // a node the 4-B format cannot ho
 constexpr uint32_t CX_QI_ARC_MISS = 0xFE;     // key-first arc walk left the rank's rows
 
 enum { M_NONE = 0, M_HOP = 1, M_FIX = 2, M_EXACT = 3, M_FIXT = 4 };
-enum { B_EMPTY = 0, B_KEYS = 1, B_READY = 2 };
+enum { B_EMPTY = 0, B_KEYS = 1, B_READY = 2, B_IDX = 3 };
 enum { P_WALK = 0, P_LOCAL = 1, P_BAD = 2 };
 
 struct WalkIO {
@@ -60,6 +60,10 @@ struct WalkIO {
     uint32_t plo, M;
     const uint64_t *dh;
     uint64_t *res_out;
+    // IX: the lookups are keys[idx[j]], src[idx[j]] (j < q), their outputs
+    // owner / hops / status at idx[j] (an arc rank's own lookups, walked in
+    // place without leaving the origin's arrays)
+    const uint32_t *idx;
 };
 
 // E(l) = round(n 2^(l - 128)), the expected index advance of a level-l finger
@@ -97,8 +101,9 @@ __device__ __forceinline__ uint64_t wk_pack(uint32_t own, uint32_t h, uint32_t s
 #define WK_ATTR
 #endif
 
-template <bool STATS, bool KF>
+template <bool STATS, bool KF, bool IX = false>
 __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
+    constexpr bool PACK = KF && !IX;  // packed results in input order (res_out)
     // entries land by LDS-DMA: region k of a wave = the 16-B quarters its
     // lanes loaded in gather k, lane-linear; lane j's entry is 64 contiguous
     // bytes in region j & 3 at (j >> 2) * 64 (regions 4 dwords apart mod 32
@@ -113,7 +118,10 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     const int lane = threadIdx.x & 63, qs = threadIdx.x & 3;
     uint32_t *ent_w = ent_all[threadIdx.x >> 6];
     const uint32_t *ent = ent_w + (lane & 3) * RG + (lane >> 2) * 16;
-    const size_t wave = (blockIdx.x * (size_t)WK_BLOCK + threadIdx.x) >> 6;
+    // wave-uniform by construction; readfirstlane tells the compiler, so base
+    // and every array pointer below live in SGPRs (6 VGPRs fewer)
+    const size_t wave = __builtin_amdgcn_readfirstlane(
+        (uint32_t)((blockIdx.x * (size_t)WK_BLOCK + threadIdx.x) >> 6));
     const size_t base = wave * io.chunk;
     if (base >= io.q) return;  // wave-uniform
     // lookups [base, base + cnt) of the batch, by offset from base (32-bit:
@@ -121,15 +129,18 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     // lookups finish within a few hundred of each other, so its scattered
     // 4-B / 1-B stores fill the same few lines, merged in L2)
     const uint32_t cnt = (uint32_t)((base + io.chunk < io.q) ? io.chunk : io.q - base);
-    uint32_t *const own_w = KF ? nullptr : io.owner + base;
-    uint8_t *const hop_w = KF ? nullptr : io.hops + base;
-    uint8_t *const st_w = KF || !io.status ? nullptr : io.status + base;
-    uint64_t *const res_w = KF ? io.res_out + base : nullptr;
-    const cell128 *const key_r = io.keys + base;
-    const uint32_t *const src_r = io.src + base;
-    const uint64_t *const dh_r = KF && io.dh ? io.dh + base : nullptr;
+    // IX: lookup "offsets" are the indices idx[] names, relative to the arrays
+    const size_t ab = IX ? 0 : base;
+    uint32_t *const own_w = PACK ? nullptr : io.owner + ab;
+    uint8_t *const hop_w = PACK ? nullptr : io.hops + ab;
+    uint8_t *const st_w = PACK || !io.status ? nullptr : io.status + ab;
+    uint64_t *const res_w = PACK ? io.res_out + base : nullptr;
+    const cell128 *const key_r = io.keys + ab;
+    const uint32_t *const src_r = io.src + ab;
+    const uint64_t *const dh_r = PACK && io.dh ? io.dh + base : nullptr;
+    const uint32_t *const idx_r = IX ? io.idx + base : nullptr;
     auto put = [&](uint32_t o, uint32_t ow, uint32_t hh, uint32_t st) {
-        if (KF) {
+        if (PACK) {
             res_w[o] = wk_pack(ow, hh, st);
         } else {
             own_w[o] = ow;
@@ -181,9 +192,14 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
         typedef unsigned int v4n __attribute__((ext_vector_type(4)));
         const bool pair_now = bst == B_KEYS;
         v4n pa4 = {0, 0, 0, 0}, pb4 = {0, 0, 0, 0};
-        if ((!KF || !io.dh) && pair_now && psrc < n) {  // the source's (pred, self) IDs: one 32-B pair
+        if ((!PACK || !io.dh) && pair_now && psrc < n) {  // the source's (pred, self) IDs: one 32-B pair
             pa4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc));
             pb4 = __builtin_nontemporal_load(reinterpret_cast<const v4n *>(io.ring_ext + psrc + 1));
+        }
+        if (IX && bst == B_IDX) {  // the index arrived last round: key and source
+            pkey = ld128(key_r + pq);
+            psrc = src_r[pq];
+            bst = B_KEYS;
         }
         {  // refill slot B in lookup order
             const uint32_t avail = cnt - head;
@@ -191,11 +207,16 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
             if (bst == B_EMPTY && rank < avail) {
-                pq = head + rank;
-                pkey = ld128(key_r + pq);
-                psrc = src_r[pq];
-                if (KF && io.dh) pd = dh_r[pq];  // the origin's start: d >> gs, or LOCAL / BAD
-                bst = B_KEYS;
+                if (IX) {  // the lookup's index first (one more round of the pipeline)
+                    pq = idx_r[head + rank];
+                    bst = B_IDX;
+                } else {
+                    pq = head + rank;
+                    pkey = ld128(key_r + pq);
+                    psrc = src_r[pq];
+                    if (PACK && io.dh) pd = dh_r[pq];  // the origin's start: d >> gs, or LOCAL / BAD
+                    bst = B_KEYS;
+                }
             }
             const uint32_t took = (uint32_t)__popcll(want);
             head += took < avail ? took : avail;
@@ -227,7 +248,7 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
         const u128 pa = wk_u128(pa4), pb = wk_u128(pb4), xa = wk_u128(xa4), xb = wk_u128(xb4);
 
         // ---- slot B: StoredLocally at the source, or the start distance ----
-        if (KF && io.dh && pair_now) {  // the origin resolved the start (k_arc_scatter_soa)
+        if (PACK && io.dh && pair_now) {  // the origin resolved the start (k_arc_scatter_soa)
             pst = psrc >= n || pd == ARC_HINT_BAD ? P_BAD : (pd == ARC_HINT_LOCAL ? P_LOCAL : P_WALK);
             bst = B_READY;
         } else if (pair_now) {
@@ -406,12 +427,29 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
     }
 }
 
+// Waves per SIMD the walk runs at (one 256-thread block = one wave per SIMD
+// of a CU).  The register budget allows 8 (57 VGPRs) but 8 measured slower
+// than 7 (3.43-3.45 vs 3.27 ms, profiles/r05/walk_ab/w8_vs_w7): past ~4.6 x
+// 10^5 walks in flight the random-request latency grows faster than the
+// requests.  Dynamic LDS holds a launch to CX_WALK_WAVES blocks per CU.
+#ifndef CX_WALK_WAVES
+#define CX_WALK_WAVES 7
+#endif
+
 template <class K>
-unsigned walk_resident_grid(K kernel) {
+size_t walk_lds_pad(K kernel) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kernel)) != hipSuccess) return 0;
+    const size_t lds = 160 * 1024, cap = lds / (CX_WALK_WAVES + 1) + 256;  // > 1/(w+1) of LDS
+    return fa.sharedSizeBytes < cap ? cap - fa.sharedSizeBytes : 0;
+}
+
+template <class K>
+unsigned walk_resident_grid(K kernel, size_t pad) {
     int dev = 0, cus = 256, per = 1;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WK_BLOCK, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, WK_BLOCK, pad) != hipSuccess ||
         per < 1)
         per = 1;
     return (unsigned)(per * cus);
@@ -446,7 +484,8 @@ hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, co
     io.stats = stats;
     // one resident round of waves (no second, partial round of blocks); small
     // batches: >= 1024 lookups per wave
-    static const unsigned resident = walk_resident_grid(k_walk<false, false>);
+    static const size_t pad = walk_lds_pad(k_walk<false, false>);
+    static const unsigned resident = walk_resident_grid(k_walk<false, false>, pad);
     size_t waves = (size_t)resident * (WK_BLOCK / 64);
     const size_t small = (q + 1023) / 1024;
     if (small < waves) waves = small ? small : 1;
@@ -455,9 +494,9 @@ hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, co
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
     if (stats)
-        k_walk<true, false><<<blocks, WK_BLOCK, 0, s>>>(io);
+        k_walk<true, false><<<blocks, WK_BLOCK, pad, s>>>(io);
     else
-        k_walk<false, false><<<blocks, WK_BLOCK, 0, s>>>(io);
+        k_walk<false, false><<<blocks, WK_BLOCK, pad, s>>>(io);
     return hipGetLastError();
 }
 
@@ -493,7 +532,8 @@ hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n
     io.M = M;
     io.dh = dh;
     io.res_out = res;
-    static const unsigned resident = walk_resident_grid(k_walk<false, true>);
+    static const size_t pad = walk_lds_pad(k_walk<false, true>);
+    static const unsigned resident = walk_resident_grid(k_walk<false, true>, pad);
     size_t waves = (size_t)resident * (WK_BLOCK / 64);
     const size_t small = (q + 1023) / 1024;
     if (small < waves) waves = small ? small : 1;
@@ -501,7 +541,51 @@ hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n
     if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
     waves = (q + io.chunk - 1) / io.chunk;
     const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
-    k_walk<false, true><<<blocks, WK_BLOCK, 0, s>>>(io);
+    k_walk<false, true><<<blocks, WK_BLOCK, pad, s>>>(io);
+    return hipGetLastError();
+}
+
+// An arc rank's own lookups in place (ArcRouter.route_exact): the key-first
+// arc walk over keys[idx[j]] from src[idx[j]] (started from the source's
+// (pred, self) IDs, no hints), owner / hops / status written at idx[j].
+hipError_t route_walk_arc_local(const cell128 *ring_ext, const cell128 *ring, size_t n,
+                                const uint64_t *arc_tree, int l0, int ib, const SearchView &sv,
+                                int Lh, uint32_t plo, uint32_t M, const uint32_t *src,
+                                const cell128 *keys, const uint32_t *idx, size_t q,
+                                uint32_t *owner, uint8_t *hops, uint8_t *status, hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const int gs = cz_shift(ib);
+    if (n == 0 || n >= (1u << 30) || gs < 64 || l0 < 5 || Lh < l0 || Lh > (int)CX_FINGERS ||
+        M > n || (size_t)(CX_FINGERS - Lh) * 2 * n + (size_t)(Lh - l0) * 2 * M >= WK_NONE)
+        return hipErrorInvalidValue;
+    WalkIO io = {};
+    io.ring_ext = ring_ext;
+    io.ring = ring;
+    io.n = (uint32_t)n;
+    io.cz = reinterpret_cast<const uint4 *>(arc_tree);
+    io.l0 = l0;
+    io.gs = gs;
+    io.sv = sv;
+    io.src = src;
+    io.keys = keys;
+    io.q = q;
+    io.owner = owner;
+    io.hops = hops;
+    io.status = status;
+    io.Lh = Lh;
+    io.plo = plo;
+    io.M = M;
+    io.idx = idx;
+    static const size_t pad = walk_lds_pad(k_walk<false, true, true>);
+    static const unsigned resident = walk_resident_grid(k_walk<false, true, true>, pad);
+    size_t waves = (size_t)resident * (WK_BLOCK / 64);
+    const size_t small = (q + 1023) / 1024;
+    if (small < waves) waves = small ? small : 1;
+    io.chunk = (q + waves - 1) / waves;
+    if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
+    waves = (q + io.chunk - 1) / io.chunk;
+    const unsigned blocks = (unsigned)((waves * 64 + WK_BLOCK - 1) / WK_BLOCK);
+    k_walk<false, true, true><<<blocks, WK_BLOCK, pad, s>>>(io);
     return hipGetLastError();
 }
 

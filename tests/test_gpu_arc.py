@@ -404,6 +404,37 @@ def test_arc_count_and_exact_scatter(cx, O, n, G):
         assert int(inr.sum()) == counts[d]
         assert bool((p0[inr] >= d * q).all()) and bool((p0[inr] < d * q + counts[d]).all())
         off += counts[d]
+    # the own lookups (rank 0's arc): compacted by the count pass, left out of
+    # the scatter (perm -1, no slot), walked in place by arc_route_local
+    own = torch.full((q,), -7, dtype=torch.int32, device="cuda")
+    oc = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dc2 = torch.zeros(G, dtype=torch.int64, device="cuda")
+    r.arc_count_async(G, keys[0], dc2, 0, own, oc)
+    sk2, ss2, perm2 = r.arc_scatter_async(G, srcs[0], keys[0], dc2, cur, skip=0)
+    torch.cuda.synchronize()
+    assert dc2.tolist() == counts and int(oc) == counts[0]
+    want_own = torch.nonzero(p0 < counts[0]).flatten()  # region 0 of the region layout
+    got_own = torch.sort(own[:counts[0]].long()).values
+    assert torch.equal(got_own, want_own)
+    pm = perm2.long()
+    assert bool((pm[want_own] == -1).all())
+    rem = pm >= 0
+    assert int(rem.sum()) == q - counts[0]
+    assert torch.equal(torch.sort(pm[rem]).values, torch.arange(q - counts[0], device="cuda"))
+    assert torch.equal(sk2[pm[rem]], keys[0][rem]) and torch.equal(ss2[pm[rem]], srcs[0][rem])
+    if counts[0]:
+        ow = torch.full((q,), -3, dtype=torch.int32, device="cuda")
+        hp = torch.full((q,), 250, dtype=torch.uint8, device="cuda")
+        stt = torch.full((q,), 9, dtype=torch.uint8, device="cuda")
+        r.arc_route_local(srcs[0], keys[0], own[:counts[0]], ow, hp, stt)
+        torch.cuda.synchronize()
+        eo, eh, es = ring.route(srcs[0], keys[0])
+        oi = want_own
+        assert torch.equal(ow[oi], eo[oi]) and torch.equal(hp[oi], eh[oi])
+        assert torch.equal(stt[oi], es[oi])
+        untouched = torch.ones(q, dtype=torch.bool, device="cuda")
+        untouched[oi] = False
+        assert bool((ow[untouched] == -3).all()) and bool((stt[untouched] == 9).all())
     # no hints, an empty batch
     bk, bs, bperm = r.arc_scatter_async(G, srcs[0], keys[0], dc, cur)
     torch.cuda.synchronize()

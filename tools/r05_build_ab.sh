@@ -4,6 +4,8 @@
 # ABBA order, bench_czbuild (2^24, table_build 0, 3 builds each), then one
 # FETCH_SIZE and one WRITE_SIZE pass of k_cz_build_roots2 for each library.
 #   bash tools/r05_build_ab.sh <tag>
+# (Recorded in profiles/r05/build_ab/ before the switch: cached gathers won and
+# are the default since; B is then built with -DCX_AB_PLANE_CACHED=1, a no-op.)
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
