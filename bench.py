@@ -944,7 +944,7 @@ def main():
     out = (owner, hops, status)
 
     route_variant, cz_escapes, table_bytes = ring.route_info()
-    kernel_name = {5: "k_walk<false, false>", 4: "k_route_tree<false, false>"}.get(
+    kernel_name = {5: "k_walk<false, false, false>", 4: "k_route_tree<false, false>"}.get(
         route_variant, f"route variant {route_variant}")
 
     # ---- warmup ----

@@ -6,7 +6,7 @@ set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
 O=$R/gpurun_out/${1:-r05_walk_pmc}
-RX=${2:-k_walk<false, false>}
+RX=${2:-k_walk<false, false, false>}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 B="python3 $R/benches/bench_walk.py 2 1"

@@ -11,7 +11,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_route_tree<false, true, false, false>"
+KERNEL = "k_walk<false, false, false>"
 
 
 def main():
