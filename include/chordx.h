@@ -423,9 +423,10 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
 /* Exact-layout partition in two asynchronous passes (no capacity, no
  * overflow, no host synchronisation): cx_arc_count_async writes the
  * per-destination counts of the lookups' keys into counts_dev (device,
- * world int64) and, with own_idx (device, q uint32) and own_cursor (device,
- * one uint32 of scratch), compacts the indices of the lookups of rank `me`'s
- * own arc into own_idx[0 .. counts[me]) (any order) for cx_arc_route_local;
+ * world int64) and, with own_idx (device, q uint32) and own_ws (device
+ * scratch of 2048 + ceil(q / 4) uint32), writes the indices of the lookups of
+ * rank `me`'s own arc, ascending, into own_idx[0 .. counts[me]) for
+ * cx_arc_route_local;
  * cx_arc_scatter_async, given those counts (still on the device), lays
  * destination d's lookups out at [sum_{j<d} counts[j], ...) of send_keys /
  * send_src / send_hint (q entries each; send_hint may be NULL) with perm[i] =
@@ -436,7 +437,7 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
  * counts in one collective, and scatter each piece on another stream while
  * earlier pieces are walked. */
 int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size_t q,
-                       int64_t *counts_dev, int me, uint32_t *own_idx, uint32_t *own_cursor);
+                       int64_t *counts_dev, int me, uint32_t *own_idx, uint32_t *own_ws);
 int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
                          const cx_u128 *keys, size_t q, const int64_t *counts_dev,
                          uint32_t *cursor_dev, cx_u128 *send_keys, uint32_t *send_src,

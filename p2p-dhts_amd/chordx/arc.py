@@ -172,7 +172,8 @@ class ArcRouter:
         returns the number of exchange rounds (1 on a single rank, else 2).
 
         The batch is cut into pieces (default: one per 2^22 lookups, at most
-        4; `chunks` / self.chunks fix the count), partitioned up front; one
+        4, one on a one-rank group; `chunks` / self.chunks fix the count),
+        partitioned up front; one
         all_gather carries every piece's counts.  Piece c + 1's lookups travel
         while piece c is walked, and piece c's answers travel back while piece
         c + 1 is walked (the collectives run on RCCL's stream, the walks on the
@@ -188,7 +189,9 @@ class ArcRouter:
         q = int(keys.shape[0])
         fixed = chunks if chunks is not None else self.chunks
         kmax = max(4, int(fixed)) if fixed is not None else 4  # piece slots per rank
-        k = int(fixed) if fixed is not None else max(1, min(4, q >> 22))
+        # pieces overlap one piece's exchange with another's walk; a one-rank
+        # group exchanges nothing, so its batch is one piece unless fixed
+        k = int(fixed) if fixed is not None else (max(1, min(4, q >> 22)) if self.world > 1 else 1)
         k = max(1, min(k, kmax, max(q, 1)))
         dev = self.comm_device if self.comm_device is not None else keys.device
         if self.exact and hasattr(eng, "arc_count_async") and keys.is_cuda:
@@ -396,10 +399,11 @@ class ArcRouter:
         row = torch.zeros(1 + kmax * G, dtype=torch.int64, device=dev)
         row[0] = k | (int(hints) << 20)
         own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
-        own_cur = torch.empty(k, dtype=torch.int32, device=dev)
+        wsw = eng.arc_own_ws_words(max(cut[c + 1] - cut[c] for c in range(k)))
+        own_ws = torch.empty(k * wsw, dtype=torch.int32, device=dev)
         for c in range(k):
             eng.arc_count_async(G, keys[cut[c]:cut[c + 1]], row[1 + c * G: 1 + (c + 1) * G], me,
-                                own_idx[cut[c]:], own_cur[c:c + 1])
+                                own_idx[cut[c]:], own_ws[c * wsw: (c + 1) * wsw])
         parts, ready = [], []
         if G > 1:
             cursors = torch.empty(k * G, dtype=torch.int32, device=dev)

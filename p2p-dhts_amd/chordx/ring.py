@@ -591,13 +591,18 @@ class Ring:
                                                        _ptr(perm), _ptr(counts)))
         return (skeys, ssrc, perm, shint) if hints else (skeys, ssrc, perm)
 
+    @staticmethod
+    def arc_own_ws_words(q: int) -> int:
+        """int32 words of arc_count_async's own_ws scratch for q lookups."""
+        return 2048 + (int(q) + 3) // 4
+
     def arc_count_async(self, world: int, keys, counts, me: int = -1, own_idx=None,
-                        own_cursor=None):
+                        own_ws=None):
         """cx_arc_count_async: per-destination counts of the keys' arcs into
         `counts` (device int64, world elements), no host synchronisation; with
-        own_idx (device int32, >= q elements) and own_cursor (device int32, one
-        element): the indices of rank `me`'s own lookups compacted into
-        own_idx[:counts[me]]."""
+        own_idx (device int32, >= q elements) and own_ws (device int32 scratch,
+        >= arc_own_ws_words(q) elements): the indices of rank `me`'s own
+        lookups, ascending, in own_idx[:counts[me]]."""
         keys = self._prep_keys(keys)
         if not (_is_dev(keys) and _is_dev(counts)):
             raise TypeError("arc routing takes device tensors")
@@ -607,15 +612,15 @@ class Ring:
         if own_idx is not None:
             if not (0 <= me < world):
                 raise ValueError("me must be in [0, world)")
-            for t, n_ in ((own_idx, keys.shape[0]), (own_cursor, 1)):
+            for t, n_ in ((own_idx, keys.shape[0]), (own_ws, self.arc_own_ws_words(keys.shape[0]))):
                 if t is None or not (_is_dev(t) and t.is_contiguous() and t.element_size() == 4
                                      and t.numel() >= n_):
-                    raise TypeError("own_idx (>= q) / own_cursor (1): contiguous 4-byte device "
-                                    "tensors")
+                    raise TypeError("own_idx (>= q) / own_ws (>= arc_own_ws_words(q)): "
+                                    "contiguous 4-byte device tensors")
         self._arc_stream()
         L.check(L.lib().cx_arc_count_async(self._h, world, _ptr(keys), keys.shape[0],
                                            _ptr(counts), int(me), _ptr(own_idx),
-                                           _ptr(own_cursor)))
+                                           _ptr(own_ws)))
 
     def arc_scatter_async(self, world: int, src, keys, counts, cursor, hints: bool = False,
                           skip: int = -1):

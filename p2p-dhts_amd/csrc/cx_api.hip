@@ -2253,10 +2253,10 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
 }
 
 int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size_t q,
-                       int64_t *counts_dev, int me, uint32_t *own_idx, uint32_t *own_cursor) {
+                       int64_t *counts_dev, int me, uint32_t *own_idx, uint32_t *own_ws) {
     CX_CHECK(ring && counts_dev, CX_E_INVALID, "null argument");
-    CX_CHECK(!own_idx || (own_cursor && me >= 0 && me < world), CX_E_INVALID,
-             "own_idx needs own_cursor and 0 <= me < world");
+    CX_CHECK(!own_idx || (own_ws && me >= 0 && me < world), CX_E_INVALID,
+             "own_idx needs own_ws and 0 <= me < world");
     CX_CHECK(world >= 1 && world <= CX_ARC_MAX_RANKS, CX_E_INVALID, "world must be in [1, 64]");
     CX_CHECK(q == 0 || keys, CX_E_INVALID, "null buffer");
     CX_CHECK(q < (1ull << 32), CX_E_INVALID, "too many lookups for one rank");
@@ -2266,7 +2266,7 @@ int cx_arc_count_async(const cx_ring *ring, int world, const cx_u128 *keys, size
     int rc = use_device(ring);
     if (rc) return rc;
     CX_HIP(cxk::arc_count_keys(reinterpret_cast<const cell128 *>(keys), q, ring->d_arc_bounds,
-                               ring->arc_nb, world, counts_dev, me, own_idx, own_cursor,
+                               ring->arc_nb, world, counts_dev, me, own_idx, own_ws,
                                ring->stream));
     return CX_OK;
 }

@@ -3423,65 +3423,110 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
 }
 
 // Count pass of the exact-layout partition: counts[d] (int64, zeroed here) =
-// lookups whose key's arc is rank d's, and (own_idx != nullptr) the indices of
-// the lookups of rank `me`'s own arc compacted into own_idx (any order; the
-// rank walks them in place, cx_arc_route_local).  Keys only (16 B per lookup,
-// + 4 B per own lookup); 1024 lookups per block pass, one global atomic per
-// (block, destination) at the end and one per pass for the own slots.
+// lookups whose key's arc is rank d's.  Keys only (16 B per lookup); block b
+// takes the contiguous lookups [b per, (b + 1) per) and folds them into its
+// LDS histogram, one global atomic per (block, destination) at the end.  With
+// own_idx: each lookup's destination byte (dest) and the block's count of
+// rank `me`'s lookups (blk_own[b]) are kept for k_arc_own_compact.
+constexpr uint32_t ARC_OWN_BLOCKS = 2048;
+
 __global__ __launch_bounds__(256) void k_arc_count_keys(const cell128 *keys, size_t q,
                                                         const ArcBound *bounds, int nb, int G,
                                                         unsigned long long *counts, int me,
-                                                        uint32_t *own_idx, uint32_t *own_cur) {
-    __shared__ uint32_t h[ARC_MAX_RANKS], tot[ARC_MAX_RANKS];
-    __shared__ uint32_t obase;
+                                                        uint8_t *dest, uint32_t *blk_own,
+                                                        size_t per) {
+    __shared__ uint32_t h[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
-    for (int j = threadIdx.x; j < G; j += blockDim.x) tot[j] = 0;
+    for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
     for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
-    const size_t per = (size_t)blockDim.x * ARC_SCAT_R;
-    for (size_t b0 = (size_t)blockIdx.x * per; b0 < q; b0 += (size_t)gridDim.x * per) {
-        for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
-        __syncthreads();
+    __syncthreads();
+    const size_t lo = blockIdx.x * per, hi = lo + per < q ? lo + per : q;
+    for (size_t b0 = lo; b0 < hi; b0 += (size_t)blockDim.x * ARC_SCAT_R) {  // uniform trips
         int d[ARC_SCAT_R];
-        uint32_t slot[ARC_SCAT_R];
 #pragma unroll
         for (int k = 0; k < ARC_SCAT_R; ++k) {
             const size_t i = b0 + (size_t)k * blockDim.x + threadIdx.x;
             d[k] = -1;
-            if (i < q) {
+            if (i < hi) {
                 const u128 key = ld128(keys + i);
                 ArcRec r;
                 r.w0 = (uint64_t)key;
                 r.w1 = (uint64_t)(key >> 64);
                 r.hk = ARC_NEW << 8;
                 d[k] = arc_dest(r, sb, nb, G);
+                if (dest) dest[i] = (uint8_t)d[k];
             }
         }
 #pragma unroll
-        for (int k = 0; k < ARC_SCAT_R; ++k) slot[k] = arc_wave_slots(d[k], G, h);
-        __syncthreads();
-        for (int j = threadIdx.x; j < G; j += blockDim.x) tot[j] += h[j];
-        if (own_idx && threadIdx.x == 0) obase = h[me] ? atomicAdd(own_cur, h[me]) : 0u;
-        __syncthreads();
-        if (own_idx) {
-#pragma unroll
-            for (int k = 0; k < ARC_SCAT_R; ++k)
-                if (d[k] == me) own_idx[obase + slot[k]] = (uint32_t)(b0 + (size_t)k * blockDim.x + threadIdx.x);
-        }
+        for (int k = 0; k < ARC_SCAT_R; ++k) (void)arc_wave_slots(d[k], G, h);
     }
     __syncthreads();
     for (int j = threadIdx.x; j < G; j += blockDim.x)
-        if (tot[j]) atomicAdd(&counts[j], (unsigned long long)tot[j]);
+        if (h[j]) atomicAdd(&counts[j], (unsigned long long)h[j]);
+    if (blk_own && threadIdx.x == 0) blk_own[blockIdx.x] = h[me];
 }
 
+// The indices of rank `me`'s lookups in ascending order: block b (the same
+// lookups as in k_arc_count_keys) writes its own lookups at the sum of the
+// earlier blocks' counts, four destination bytes per thread and one block
+// scan per 1024 lookups -- no global atomics.
+__global__ __launch_bounds__(256) void k_arc_own_compact(const uint8_t *dest, size_t q, int me,
+                                                         const uint32_t *blk_own,
+                                                         uint32_t *own_idx, size_t per) {
+    __shared__ uint32_t part[256], wsum[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t acc = 0;
+    for (uint32_t j = t; j < blockIdx.x; j += blockDim.x) acc += blk_own[j];
+    part[t] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) part[t] += part[t + o];
+        __syncthreads();
+    }
+    uint32_t off = part[0];
+    const size_t lo = blockIdx.x * per, hi = lo + per < q ? lo + per : q;
+    for (size_t b0 = lo; b0 < hi; b0 += 4 * (size_t)blockDim.x) {  // uniform trips
+        const size_t i0 = b0 + 4 * (size_t)t;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i0 + k < hi && dest[i0 + k] == (uint8_t)me) bits |= 1u << k;
+        const uint32_t c = (uint32_t)__popc(bits);
+        uint32_t x = c;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t pos = off + x - c;
+        for (int j = 0; j < w; ++j) pos += wsum[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (bits & (1u << k)) own_idx[pos++] = (uint32_t)(i0 + k);
+        off += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
+
+// own_ws: ARC_OWN_BLOCKS block counts, then one destination byte per lookup.
 hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
-                          int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_cur,
+                          int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_ws,
                           hipStream_t s) {
     hipError_t e = hipMemsetAsync(counts, 0, (size_t)G * sizeof(int64_t), s);
-    if (e == hipSuccess && own_idx) e = hipMemsetAsync(own_cur, 0, sizeof(uint32_t), s);
     if (e != hipSuccess || q == 0) return e;
-    k_arc_count_keys<<<cx_grid((q + ARC_SCAT_R - 1) / ARC_SCAT_R, 256, 2048), 256, 0, s>>>(
-        keys, q, bounds, nb, G, reinterpret_cast<unsigned long long *>(counts), me, own_idx,
-        own_cur);
+    const size_t tiles = (q + 1023) / 1024;
+    const size_t grid = tiles < ARC_OWN_BLOCKS ? tiles : ARC_OWN_BLOCKS;
+    const size_t per = (tiles + grid - 1) / grid * 1024;
+    const unsigned g = (unsigned)((q + per - 1) / per);
+    uint32_t *blk = own_idx ? own_ws : nullptr;
+    uint8_t *dest = own_idx ? reinterpret_cast<uint8_t *>(own_ws + ARC_OWN_BLOCKS) : nullptr;
+    k_arc_count_keys<<<g, 256, 0, s>>>(keys, q, bounds, nb, G,
+                                       reinterpret_cast<unsigned long long *>(counts), me, dest,
+                                       blk, per);
+    if (own_idx && (e = hipGetLastError()) == hipSuccess)
+        k_arc_own_compact<<<g, 256, 0, s>>>(dest, q, me, blk, own_idx, per);
     return hipGetLastError();
 }
 

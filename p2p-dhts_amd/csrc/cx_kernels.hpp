@@ -225,7 +225,7 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
 // counts of the lookups' keys (int64, zeroed first), then the scatter that
 // lays destination d's lookups out at the sum of the counts below d.
 hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
-                          int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_cur,
+                          int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_ws,
                           hipStream_t s);
 hipError_t arc_scatter_exact(const uint32_t *src, const cell128 *keys, size_t q,
                              const ArcBound *bounds, int nb, int G, const int64_t *counts,

@@ -375,15 +375,15 @@ def test_arc_partition_async_device_counts(cx, O, n, G):
         assert int(small[G]) == 1
 
 
-@pytest.mark.parametrize("n,G", [(5000, 2), (1 << 16, 8), (70001, 5), (3, 4), (1 << 16, 64)])
-def test_arc_count_and_exact_scatter(cx, O, n, G):
+@pytest.mark.parametrize("n,G,q", [(5000, 2, 4096), (1 << 16, 8, 300001), (70001, 5, 4096),
+                                   (3, 4, 4096), (1 << 16, 64, 70000), (1 << 16, 1, 3 << 20)])
+def test_arc_count_and_exact_scatter(cx, O, n, G, q):
     """cx_arc_count_async + cx_arc_scatter_async (the exact-layout partition
     ArcRouter.route_exact runs on RCCL): the counts equal the region
     partition's, destination d's lookups fill rows [sum(counts[:d]),
     sum(counts[:d + 1])) exactly, and keys, sources and hints equal the
     region partition's through each call's permutation."""
     import torch
-    q = 4096
     ids_dev, ring, srcs, keys = _setup(cx, O, torch, n, q, G, 0xA3F0 + n + G)
     r = cx.Ring(ids_dev)
     r.arc_build(G, 0)
@@ -407,15 +407,15 @@ def test_arc_count_and_exact_scatter(cx, O, n, G):
     # the own lookups (rank 0's arc): compacted by the count pass, left out of
     # the scatter (perm -1, no slot), walked in place by arc_route_local
     own = torch.full((q,), -7, dtype=torch.int32, device="cuda")
-    oc = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ws = torch.full((r.arc_own_ws_words(q),), 5, dtype=torch.int32, device="cuda")
     dc2 = torch.zeros(G, dtype=torch.int64, device="cuda")
-    r.arc_count_async(G, keys[0], dc2, 0, own, oc)
+    r.arc_count_async(G, keys[0], dc2, 0, own, ws)
     sk2, ss2, perm2 = r.arc_scatter_async(G, srcs[0], keys[0], dc2, cur, skip=0)
     torch.cuda.synchronize()
-    assert dc2.tolist() == counts and int(oc) == counts[0]
+    assert dc2.tolist() == counts
     want_own = torch.nonzero(p0 < counts[0]).flatten()  # region 0 of the region layout
-    got_own = torch.sort(own[:counts[0]].long()).values
-    assert torch.equal(got_own, want_own)
+    assert torch.equal(own[:counts[0]].long(), want_own)  # ascending
+    assert bool((own[counts[0]:] == -7).all())
     pm = perm2.long()
     assert bool((pm[want_own] == -1).all())
     rem = pm >= 0
