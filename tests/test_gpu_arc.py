@@ -520,6 +520,8 @@ def test_arc_soa_matches_oracle_clustered(cx, O):
 # hops and statuses equal the replicated route of the same lookups.
 # ---------------------------------------------------------------------------
 def _router_worker(rank, world, port, n, q, chunks, out, exact=True):
+    if isinstance(q, (list, tuple)):  # per-rank batch sizes
+        q = q[rank]
     import os
     import sys
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
@@ -553,6 +555,28 @@ def _router_worker(rank, world, port, n, q, chunks, out, exact=True):
     out[rank] = (bool(torch.equal(ow, owner)), bool(torch.equal(hp, hops)),
                  bool(torch.equal(st, status)), rounds, router.records_sent)
     tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("chunks", [None, 3])
+def test_arc_router_three_ranks_ragged_batches(cx, chunks):
+    """Three gloo ranks on one GPU with batches of different sizes, one of them
+    empty (ranks run max-over-ranks pieces, the missing ones empty) on the
+    exact-layout path: every rank's owners, hops and statuses equal the
+    replicated route's."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    qs = [(1 << 23) + 4097, 0, 12345]  # auto pieces: 2 / 1 / 1 by size (kg = 2)
+    mp.start_processes(_router_worker, args=(3, port, 40000, qs, chunks, out, True), nprocs=3,
+                       join=True, start_method="spawn")
+    for r in range(3):
+        assert out[r][:3] == (True, True, True), (r, out[r])
+        assert out[r][3] == 2
 
 
 @pytest.mark.parametrize("chunks,exact", [(1, True), (3, True), (1, False), (3, False)])
