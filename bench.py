@@ -304,6 +304,22 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
         and int((status != 0).sum().item()) == 0
     same = dist.all_over_ranks(same, world, dev)
     total = world * Q * args.steps
+    # DHash placement lists (n = 14) in the same layout (keys to
+    # their owner's arc, windows read there from the arc + a 13-peer halo,
+    # lists back): the same keys, K steps, equal to the replicated cx_nsucc
+    lists = torch.empty((Q, 14), dtype=torch.int32, device=dev)
+    cnt = torch.empty(Q, dtype=torch.uint8, device=dev)
+    router.nsucc(keys, 14, lists, cnt)  # builds the halo ring once
+    _, dt_ns = time_steps(lambda: router.nsucc(keys, 14, lists, cnt), args.steps, world, dev)
+    wl, wc = ring.nsucc(keys, 14)
+    ns_same = dist.all_over_ranks(bool(torch.equal(lists, wl.to(torch.int32))) and
+                                  bool(torch.equal(cnt, wc)), world, dev)
+    del lists, cnt, wl, wc
+    placement = {"value": total / dt_ns, "unit": "keys/s", "ms_per_step": dt_ns * 1e3 / args.steps,
+                 "n": 14, "equals_replicated_nsucc": ns_same,
+                 "layout": "exact-successor partition (keys to their owner's arc, one "
+                           "all_to_all-v), the 14-window read from the arc plus a 13-peer halo "
+                           "ring (ArcRouter.nsucc), 15 int32 per key back (window + count)"}
     group = torch.distributed.get_backend() if torch.distributed.is_initialized() else None
     if single:
         torch.distributed.destroy_process_group()
@@ -314,6 +330,7 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
             "records_exchanged_per_lookup": sent / total,
             "rounds_per_step": router.rounds,
             "equals_replicated_route": same,
+            "dhash_placement": placement,
             "top_levels_replicated": top, "local_rows": rows,
             "route_plane_bytes_per_gpu": plane_bytes, "build_s": t_build,
             "layout": f"ring IDs all-gathered; arc-sharded route planes x{world} (top {top} "

@@ -525,7 +525,15 @@ class ArcRouter:
             # ring holding the same IDs)
             owner.copy_(eng.successor(keys).to(owner.dtype))
             return 0
-        G = self.world
+        q = int(keys.shape[0])
+        k = self._pieces_all(q, 1 << 22, keys)  # bounded collectives, as nsucc
+        cut = [c * q // k for c in range(k + 1)]
+        for c in range(k):
+            self._succ_piece(keys[cut[c]:cut[c + 1]], owner[cut[c]:cut[c + 1]])
+        return 2
+
+    def _succ_piece(self, keys, owner):
+        eng, G = self.engine, self.world
         zero = self._zeros_src(keys)
         sk, _, perm, counts = eng.arc_partition(G, zero, keys)[:4]
         dev = self.comm_device if self.comm_device is not None else sk.device
@@ -545,7 +553,97 @@ class ArcRouter:
         back = self._land(back, work, perm)
         owner.copy_(back.to(owner.device)[perm.long()].to(owner.dtype))
         self.records_sent += int(sum(counts))
+
+    def halo_ring(self, h: int):
+        """This rank's arc plus the h peers after it as a ring of its own
+        (SURVEY 8e's DHash halo: a 14-window from an owner in the arc reaches
+        13 peers past it), and the map from its indices to global ones:
+        (ring, wrap) -- local index j is global j when j < wrap (the halo
+        wrapped past the ring's end to peers 0 .. wrap - 1, the smallest IDs),
+        else lo + j - wrap.  Built once per h."""
+        cache = getattr(self, "_halo", None)
+        if cache is not None and cache[0] == h:
+            return cache[1], cache[2]
+        eng, n = self.engine, self.n
+        ids = eng.ids_device()
+        end = self.hi + h
+        wrap = max(0, min(end - n, self.lo))  # never onto the arc itself (one rank: none)
+        parts = [ids[self.lo:min(end, n)]]
+        if wrap:
+            parts.insert(0, ids[:wrap])
+        sub = type(eng)(torch.cat(parts).contiguous(), device=eng.device)
+        self._halo = (h, sub, wrap)
+        return sub, wrap
+
+    def nsucc(self, keys, n_list: int, lists, count) -> int:
+        """DHash placement lists in the arc layout ("a 14-window may
+        straddle an arc, so use a 13-peer halo"): this rank's keys go to the
+        rank whose arc holds their owner (the exact-successor partition), that
+        rank reads each key's n-successor window (GetNSuccessors on a
+        converged ring, abstract_chord_peer.cpp:345-373) from its arc plus the
+        n - 1 peers after it (halo_ring), and the windows come back as global
+        peer indices with the splits swapped: lists[i, :] / count[i] as
+        cx_nsucc on the whole ring.  Collective over the group; returns the
+        number of exchange rounds (2; 0 on a single rank without
+        exchange_always, or on a ring too small for disjoint halos, where the
+        replicated ring answers in place)."""
+        eng, G = self.engine, self.world
+        h = n_list - 1
+        if (G == 1 and not self.exchange_always) or self.n < G * (n_list + 1):
+            lo_, co_ = eng.nsucc(keys, n_list)
+            lists.copy_(lo_.to(lists.dtype))
+            count.copy_(co_.to(count.dtype))
+            return 0
+        # pieces of <= 2^22 keys (60 B per key come back: one collective of a
+        # 2^25-key batch would pass 2^31 bytes, which RCCL's all_to_all does
+        # not carry whole); every rank runs the largest rank's piece count
+        q = int(keys.shape[0])
+        k = self._pieces_all(q, 1 << 22, keys)
+        if k > 1:
+            cut = [c * q // k for c in range(k + 1)]
+            for c in range(k):
+                sl = slice(cut[c], cut[c + 1])
+                self._nsucc_piece(keys[sl], n_list, lists[sl], count[sl])
+            return 2
+        self._nsucc_piece(keys, n_list, lists, count)
         return 2
+
+    def _pieces_all(self, q: int, per: int, like) -> int:
+        """max over ranks of ceil(q / per) (one all_reduce on the comm device,
+        else on `like`'s device)."""
+        dev = self.comm_device if self.comm_device is not None else like.device
+        t = torch.tensor([max(1, -(-q // per))], dtype=torch.int64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def _nsucc_piece(self, keys, n_list, lists, count):
+        eng, G = self.engine, self.world
+        h = n_list - 1
+        zero = self._zeros_src(keys)
+        sk, _, perm, counts = eng.arc_partition(G, zero, keys)[:4]
+        dev = self.comm_device if self.comm_device is not None else sk.device
+        mine = torch.tensor(list(counts), dtype=torch.int64, device=dev)
+        mat = torch.empty((G, G), dtype=torch.int64, device=dev)
+        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
+        m = mat.cpu() if mat.is_cuda else mat
+        recv = [int(m[r, self.rank]) for r in range(G)]
+        rk, work = self._a2a(sk, recv, list(counts), dev)
+        rk = self._land(rk, work, sk)
+        W = n_list + 1  # the window's global indices, then its count
+        if rk.shape[0]:
+            sub, wrap = self.halo_ring(h)
+            ll, lc = sub.nsucc(rk, n_list)
+            ll = ll.to(torch.int64)
+            glob = torch.where(ll < wrap, ll, ll + (self.lo - wrap))
+            got = torch.cat([glob.to(torch.int32), lc.to(torch.int32).view(-1, 1)], dim=1)
+        else:
+            got = torch.empty((0, W), dtype=torch.int32, device=rk.device)
+        back, work = self._a2a(got.contiguous(), list(counts), recv, dev)
+        back = self._land(back, work, perm)
+        back = back.to(lists.device)[perm.long()]
+        lists.copy_(back[:, :n_list].to(lists.dtype))
+        count.copy_(back[:, n_list].to(count.dtype))
+        self.records_sent += int(sum(counts))
 
     def _zeros_src(self, keys):
         z = getattr(self, "_zsrc", None)

@@ -552,8 +552,14 @@ def _router_worker(rank, world, port, n, q, chunks, out, exact=True):
     ref = chordx.Ring(ids)
     ref.build_fingers()
     ow, hp, st = ref.route(src, keys)
+    # DHash placement lists in the arc layout (13-peer halo) == the whole ring's
+    lists = torch.full((q, 14), -1, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(q, dtype=torch.uint8, device="cuda")
+    nr = router.nsucc(keys, 14, lists, cnt)
+    wl, wc = ref.nsucc(keys, 14)
+    ns_ok = bool(torch.equal(lists, wl.to(torch.int32))) and bool(torch.equal(cnt, wc)) and nr == 2
     out[rank] = (bool(torch.equal(ow, owner)), bool(torch.equal(hp, hops)),
-                 bool(torch.equal(st, status)), rounds, router.records_sent)
+                 bool(torch.equal(st, status)) and ns_ok, rounds, router.records_sent)
     tdist.destroy_process_group()
 
 
@@ -653,6 +659,13 @@ def _rccl_worker(_i, n, q, chunks, out):
     rs = router.successor(keys, own)
     torch.cuda.synchronize()
     succ_ok = (bool(torch.equal(own, ring.successor(keys))), rs, router.records_sent)
+    # DHash placement lists through the same group (the halo ring of the one arc)
+    lists = torch.full((q, 14), -1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(q, dtype=torch.uint8, device=dev)
+    nr = router.nsucc(keys, 14, lists, cnt)
+    wl, wc = ring.nsucc(keys, 14)
+    succ_ok = succ_ok + (bool(torch.equal(lists, wl.to(torch.int32))) and
+                         bool(torch.equal(cnt, wc)) and nr == 2,)
     out[0] = (tdist.get_backend(), res, int((st == chordx.CX_Q_BADPEER).sum().item()), succ_ok)
     tdist.destroy_process_group()
 
@@ -668,7 +681,7 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
     assert backend == "nccl" and bad == len(range(0, q, 97))
     for it, r in enumerate(res):  # the exact path walks its own region in place
         assert r == (True, True, True, 2, 0 if it < 2 else q), (it, r)
-    assert succ_ok == (True, 2, q)
+    assert succ_ok == (True, 2, q, True)
 
 
 @pytest.mark.parametrize("G", [2, 8])
