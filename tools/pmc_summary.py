@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of the PMC passes under a tools/pmc_kernel.sh output dir."""
+"""Per-kernel averages of the PMC passes (rocprofv3 --pmc ... -o run --output-format csv)
+under an output dir, e.g. tools/r05_walk_pmc.sh's."""
 import csv
 import glob
 import json
