@@ -135,6 +135,34 @@ def test_route_converged(cx, O, n, variant):
     assert (owner == O.successor(want_ring, keys)).all()
 
 
+@pytest.mark.parametrize("q", [1, 2, 63, 64, 65, 1023, 1025, 4097, 70001])
+def test_route_batch_sizes_write_exactly_q(cx, O, q):
+    """The default walk stores each lookup's outputs as it finishes (no result
+    ring): every batch size writes owner / hops / status of exactly its q
+    lookups -- equal to the oracle -- and nothing past them."""
+    import torch
+    ids = O.splitmix_keys(0xBA7C, 20000)
+    ring = cx.Ring(ids)
+    F = ring.build_fingers(copy_out=True)
+    assert ring.route_info()[0] == 5
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, 0xBA7D, q)[:q]
+    src = (np.arange(q) * 7919 % len(want_ring)).astype(np.uint32)
+    kd = torch.from_numpy(keys.view(np.int64).copy()).cuda()
+    sd = torch.from_numpy(src.view(np.int32).copy()).cuda()
+    pad = 300
+    owner = torch.full((q + pad,), -9, dtype=torch.int32, device="cuda")
+    hops = torch.full((q + pad,), 201, dtype=torch.uint8, device="cuda")
+    status = torch.full((q + pad,), 77, dtype=torch.uint8, device="cuda")
+    ring.route(sd, kd, out=(owner[:q], hops[:q], status[:q]))
+    torch.cuda.synchronize()
+    wo, wh, ws = O.route(O.Peers(want_ring, F), src, keys)
+    assert (owner[:q].cpu().numpy().view(np.uint32) == wo).all()
+    assert (hops[:q].cpu().numpy() == wh).all() and (status[:q].cpu().numpy() == ws).all()
+    assert bool((owner[q:] == -9).all()) and bool((hops[q:] == 201).all())
+    assert bool((status[q:] == 77).all())
+
+
 def test_route_from_predecessor(cx, O, refvec):
     """ChordGetSucc.FromPredecessor: all fingers of the source point at itself."""
     g = refvec["get_succ"]["from_predecessor"]
