@@ -18,13 +18,20 @@ sources over the replicated top planes and its own rows and answers in
 receive order, 8 B per lookup; the answers come back with the splits swapped
 and land in send order, where the origin scatters them through the
 permutation it kept.  One count exchange, three all_to_alls, no origin or
-index crossing xGMI, no re-bucketing of results.  On RCCL (route_exact) the
+index crossing xGMI, no re-bucketing of results.  With a device engine
+(route_exact; gloo test runs stage the exchanges through the host) the
 partition runs in two passes: a count pass over the keys (16 B per lookup)
-whose device counts travel in the step's one all_gather while the scatter
-lays each piece out by those counts on a side stream, overlapping the walks
-of earlier pieces; a rank walks the lookups whose key lies in its own arc in
-place (they never enter a collective), and the all_to_alls carry only the
-other ranks' regions -- none at all when no lookup of any rank crosses ranks.
+whose device counts travel in the step's one all_gather -- read on the host
+once -- and which compacts the indices of the rank's own lookups, then a
+scatter that lays each piece's other lookups out by those counts on a side
+stream, overlapping the walks of earlier pieces.  A rank walks the lookups
+whose key lies in its own arc in place (arc_route_local: they never enter a
+collective), and the all_to_alls carry only the other ranks' regions -- none
+at all when no lookup of any rank crosses ranks.
+
+DHash placement lists (nsucc) and exact successors (successor) use the same
+key partition: the owner's rank reads the answer from its arc (plus a
+13-peer halo for the 14-windows) and sends it back.
 
 Record protocol ("records", origin walk or key-first): one bulk-synchronous round = step (walk every record as far as this rank's
 rows reach) -> bucket by destination -> exchange: one all_gather of the G x G
