@@ -445,7 +445,8 @@ int cx_arc_scatter_async(const cx_ring *ring, int world, const uint32_t *src,
 /* The lookups of this rank's own arc walked in place: keys[idx[j]] issued at
  * src[idx[j]] for j < q, over the arc planes (as cx_arc_route), started from
  * the sources' own IDs; owner / hops / status (status may be NULL) written at
- * idx[j] -- no exchange, no packed results, no delivery pass. */
+ * idx[j] -- no exchange, no packed results, no delivery pass.  Every idx[j]
+ * must index keys / src / owner / hops / status (device data: not checked). */
 int cx_arc_route_local(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys,
                        const uint32_t *idx, size_t q, uint32_t *owner, uint8_t *hops,
                        uint8_t *status);
