@@ -519,7 +519,7 @@ def test_arc_soa_matches_oracle_clustered(cx, O):
 # sharing the GPU over gloo (RCCL refuses two ranks on one device): owners,
 # hops and statuses equal the replicated route of the same lookups.
 # ---------------------------------------------------------------------------
-def _router_worker(rank, world, port, n, q, chunks, out, exact=True):
+def _router_worker(rank, world, port, n, q, chunks, out, exact=True, clustered=False):
     if isinstance(q, (list, tuple)):  # per-rank batch sizes
         q = q[rank]
     import os
@@ -536,6 +536,10 @@ def _router_worker(rank, world, port, n, q, chunks, out, exact=True):
     torch.cuda.set_device(0)
     ids = torch.empty((n, 2), dtype=torch.int64, device="cuda")
     chordx.fill_splitmix(ids, 0xA7C0)
+    if clustered:  # half the peers in one dense run: exact-ID steps, escapes
+        m = n // 2
+        ids[:m, 1] = 0x3C3C5A5A0F0F1234
+        ids[:m, 0] = torch.arange(m, device="cuda", dtype=torch.int64) * 7919
     ring = chordx.Ring(ids)
     router = ArcRouter(ring, ring.n, rank, world, comm_device="cpu")
     router.chunks = chunks
@@ -583,6 +587,25 @@ def test_arc_router_three_ranks_ragged_batches(cx, chunks):
     for r in range(3):
         assert out[r][:3] == (True, True, True), (r, out[r])
         assert out[r][3] == 2
+
+
+def test_arc_router_three_ranks_clustered_ring(cx):
+    """The exact-layout path on a ring with a dense cluster (half the peers
+    within 2^26 of one ID): gapped hints, exact-ID steps and escaped table
+    words at every rank; owners, hops, statuses and placement lists equal
+    the replicated ring's."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_router_worker, args=(3, port, 40000, 50000, 2, out, True, True),
+                       nprocs=3, join=True, start_method="spawn")
+    for r in range(3):
+        assert out[r][:3] == (True, True, True), (r, out[r])
 
 
 @pytest.mark.parametrize("chunks,exact", [(1, True), (3, True), (1, False), (3, False)])
