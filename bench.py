@@ -317,9 +317,12 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
     del lists, cnt, wl, wc
     placement = {"value": total / dt_ns, "unit": "keys/s", "ms_per_step": dt_ns * 1e3 / args.steps,
                  "n": 14, "equals_replicated_nsucc": ns_same,
-                 "layout": "exact-successor partition (keys to their owner's arc, one "
-                           "all_to_all-v), the 14-window read from the arc plus a 13-peer halo "
-                           "ring (ArcRouter.nsucc), 15 int32 per key back (window + count)"}
+                 "layout": "count pass (device counts, the rank's own keys' indices) and one "
+                           "all_gather; windows read from the owner's arc plus a 13-peer halo "
+                           "ring (ArcRouter.nsucc): own keys in place, the others sent to their "
+                           "owner's rank (exact-layout scatter, all_to_all-v) with 15 int32 "
+                           "per key back (window + count); at N = 1 every key is the rank's "
+                           "own"}
     group = torch.distributed.get_backend() if torch.distributed.is_initialized() else None
     if single:
         torch.distributed.destroy_process_group()

@@ -354,11 +354,14 @@ class ArcRouter:
             return mat
         mat = torch.empty((G, row.numel()), dtype=torch.int64, device=row.device)
         tdist.all_gather_into_tensor(mat.view(-1), row, group=self.group)
-        if self._mat_host is None or self._mat_host.shape != mat.shape:
-            self._mat_host = torch.empty(mat.shape, dtype=torch.int64, pin_memory=True)
-        self._mat_host.copy_(mat, non_blocking=True)
+        # one pinned landing buffer per row length (route and placement rows differ)
+        pool = self.__dict__.setdefault("_pinned", {})
+        host = pool.get(row.numel())
+        if host is None:
+            host = pool[row.numel()] = torch.empty(mat.shape, dtype=torch.int64, pin_memory=True)
+        host.copy_(mat, non_blocking=True)
         torch.cuda.current_stream(mat.device).synchronize()
-        return self._mat_host
+        return host
 
     def _a2a_views(self, outs, ins):
         """all_to_all from the views `ins` (one per destination rank) into the
@@ -605,7 +608,7 @@ class ArcRouter:
         # 2^25-key batch would pass 2^31 bytes, which RCCL's all_to_all does
         # not carry whole); every rank runs the largest rank's piece count
         q = int(keys.shape[0])
-        k = self._pieces_all(q, 1 << 22, keys)
+        k = self._pieces_all(q, 1 << 22, keys) if G > 1 else 1
         if k > 1:
             cut = [c * q // k for c in range(k + 1)]
             for c in range(k):
@@ -623,34 +626,69 @@ class ArcRouter:
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=self.group)
         return int(t.item())
 
+    def _windows(self, k, n_list, out=None):
+        """The n-windows of keys k (owners in this rank's arc) as global peer
+        indices, and their counts (halo_ring): (lists int32 (m, n), count
+        uint8 (m,)), written into out when given."""
+        m = int(k.shape[0])
+        if out is None:
+            out = (torch.empty((m, n_list), dtype=torch.int32, device=k.device),
+                   torch.empty(m, dtype=torch.uint8, device=k.device))
+        if m == 0:
+            return out
+        sub, wrap = self.halo_ring(n_list - 1)
+        ll, lc = sub.nsucc(k, n_list, out=out)
+        if self.lo != wrap:  # local index j >= wrap is global lo + j - wrap
+            ll.add_((ll >= wrap).to(ll.dtype) * (self.lo - wrap))
+        return ll, lc
+
     def _nsucc_piece(self, keys, n_list, lists, count):
-        eng, G = self.engine, self.world
-        h = n_list - 1
-        zero = self._zeros_src(keys)
-        sk, _, perm, counts = eng.arc_partition(G, zero, keys)[:4]
-        dev = self.comm_device if self.comm_device is not None else sk.device
-        mine = torch.tensor(list(counts), dtype=torch.int64, device=dev)
-        mat = torch.empty((G, G), dtype=torch.int64, device=dev)
-        tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
-        m = mat.cpu() if mat.is_cuda else mat
-        recv = [int(m[r, self.rank]) for r in range(G)]
-        rk, work = self._a2a(sk, recv, list(counts), dev)
+        """One piece: the count pass (device counts, this rank's own lookups'
+        indices) and one all_gather; the own lookups' windows are read in place
+        and written straight into the outputs, the others go out in the exact
+        layout (own skipped), their windows come back and land through perm."""
+        eng, G, me = self.engine, self.world, self.rank
+        q = int(keys.shape[0])
+        dev = keys.device
+        row = torch.zeros(G, dtype=torch.int64, device=dev)
+        own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(eng.arc_own_ws_words(q), dtype=torch.int32, device=dev)
+        eng.arc_count_async(G, keys, row, me, own_idx, ws)
+        mat = self._gather_row(row)  # (G, G): mat[r, d] = rank r's lookups for rank d
+        c_me = int(mat[me, me])
+        direct = (lists.dtype == torch.int32 and count.dtype == torch.uint8 and lists.is_cuda
+                  and lists.is_contiguous() and count.is_contiguous())
+        if c_me == q and q and direct:  # every lookup is this rank's: straight into the outputs
+            self._windows(keys, n_list, out=(lists, count))
+        elif c_me == q and q:
+            wl, wc = self._windows(keys, n_list)
+            lists.copy_(wl.to(lists.dtype))
+            count.copy_(wc.to(count.dtype))
+        elif c_me:
+            oi = own_idx[:c_me].long()
+            wl, wc = self._windows(keys[oi], n_list)
+            lists[oi] = wl.to(lists.dtype)
+            count[oi] = wc.to(count.dtype)
+        remote = any(int(mat[r, d]) for r in range(G) for d in range(G) if r != d)
+        if not remote:  # every rank sees the same matrix: all exchange or none do
+            return
+        send = [int(mat[me, d]) if d != me else 0 for d in range(G)]
+        recv = [int(mat[r, me]) if r != me else 0 for r in range(G)]
+        cursor = torch.empty(G, dtype=torch.int32, device=dev)
+        sk, _, perm = eng.arc_scatter_async(G, self._zeros_src(keys), keys, row, cursor, skip=me)
+        cdev = self.comm_device if self.comm_device is not None else dev
+        rk, work = self._a2a(sk[:sum(send)], recv, send, cdev)
         rk = self._land(rk, work, sk)
-        W = n_list + 1  # the window's global indices, then its count
-        if rk.shape[0]:
-            sub, wrap = self.halo_ring(h)
-            ll, lc = sub.nsucc(rk, n_list)
-            ll = ll.to(torch.int64)
-            glob = torch.where(ll < wrap, ll, ll + (self.lo - wrap))
-            got = torch.cat([glob.to(torch.int32), lc.to(torch.int32).view(-1, 1)], dim=1)
-        else:
-            got = torch.empty((0, W), dtype=torch.int32, device=rk.device)
-        back, work = self._a2a(got.contiguous(), list(counts), recv, dev)
-        back = self._land(back, work, perm)
-        back = back.to(lists.device)[perm.long()]
-        lists.copy_(back[:, :n_list].to(lists.dtype))
-        count.copy_(back[:, n_list].to(count.dtype))
-        self.records_sent += int(sum(counts))
+        gl, gc = self._windows(rk, n_list)
+        got = torch.cat([gl, gc.to(torch.int32).view(-1, 1)], dim=1)  # one exchange
+        back, work = self._a2a(got.contiguous(), send, recv, cdev)
+        back = self._land(back, work, perm).to(lists.device)
+        pm = perm.long()
+        sel = pm >= 0
+        rows = back[pm[sel]]
+        lists[sel] = rows[:, :n_list].to(lists.dtype)
+        count[sel] = rows[:, n_list].to(count.dtype)
+        self.records_sent += sum(send)
 
     def _zeros_src(self, keys):
         z = getattr(self, "_zsrc", None)

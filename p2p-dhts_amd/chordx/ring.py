@@ -386,11 +386,19 @@ class Ring:
         return owner, hops, status
 
     # ---- a10/a11 ---------------------------------------------------------
-    def nsucc(self, keys, n: int):
+    def nsucc(self, keys, n: int, out=None):
+        """GetNSuccessors(key, n) on the converged ring: (lists (q, n), count);
+        out = (lists, count) to write caller buffers."""
         keys = self._prep_keys(keys)
         q = keys.shape[0]
-        lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
-        count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        if out is None:
+            lists = self._empty(keys, (q, n), np.uint32, torch and torch.int32)
+            count = self._empty(keys, (q,), np.uint8, torch and torch.uint8)
+        else:
+            lists, count = out
+            self._check_out([(lists, 4, "lists"), (count, 1, "count")], q)
+            if tuple(lists.shape) != (q, n):
+                raise TypeError(f"lists: expected shape ({q}, {n})")
         mk = self._mem(keys, lists)
         L.check(L.lib().cx_nsucc(self._h, _ptr(keys), q, n, _ptr(lists), _ptr(count), mk))
         return lists, count
