@@ -315,6 +315,18 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
     ns_same = dist.all_over_ranks(bool(torch.equal(lists, wl.to(torch.int32))) and
                                   bool(torch.equal(cnt, wc)), world, dev)
     del lists, cnt, wl, wc
+    # exact-successor mode: the same keys, their owners searched on
+    # the owner's arc of the ring only
+    own = torch.empty(Q, dtype=torch.int32, device=dev)
+    router.successor(keys, own)  # builds the arc's ring once
+    _, dt_sc = time_steps(lambda: router.successor(keys, own), args.steps, world, dev)
+    sc_same = dist.all_over_ranks(bool(torch.equal(own, ring.successor(keys))), world, dev)
+    del own
+    exact_succ = {"value": total / dt_sc, "unit": "lookups/s",
+                  "ms_per_step": dt_sc * 1e3 / args.steps, "equals_replicated_successor": sc_same,
+                  "layout": "count pass and one all_gather; owners searched on the owner's arc "
+                            "of the ring (ArcRouter.successor): own keys in place, the others "
+                            "sent to their owner's rank (16 B out, 4 B back per key)"}
     placement = {"value": total / dt_ns, "unit": "keys/s", "ms_per_step": dt_ns * 1e3 / args.steps,
                  "n": 14, "equals_replicated_nsucc": ns_same,
                  "layout": "count pass (device counts, the rank's own keys' indices) and one "
@@ -334,6 +346,7 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
             "rounds_per_step": router.rounds,
             "equals_replicated_route": same,
             "dhash_placement": placement,
+            "exact_successor": exact_succ,
             "top_levels_replicated": top, "local_rows": rows,
             "route_plane_bytes_per_gpu": plane_bytes, "build_s": t_build,
             "layout": f"ring IDs all-gathered; arc-sharded route planes x{world} (top {top} "

@@ -536,13 +536,16 @@ class ArcRouter:
             owner.copy_(eng.successor(keys).to(owner.dtype))
             return 0
         q = int(keys.shape[0])
-        k = self._pieces_all(q, 1 << 22, keys)  # bounded collectives, as nsucc
+        # bounded collectives, as nsucc (one piece on a one-rank group)
+        k = self._pieces_all(q, 1 << 22, keys) if self.world > 1 else 1
         cut = [c * q // k for c in range(k + 1)]
         for c in range(k):
             self._succ_piece(keys[cut[c]:cut[c + 1]], owner[cut[c]:cut[c + 1]])
         return 2
 
     def _succ_piece(self, keys, owner):
+        if hasattr(self.engine, "arc_count_async") and keys.is_cuda:
+            return self._succ_piece_exact(keys, owner)
         eng, G = self.engine, self.world
         zero = self._zeros_src(keys)
         sk, _, perm, counts = eng.arc_partition(G, zero, keys)[:4]
@@ -563,6 +566,46 @@ class ArcRouter:
         back = self._land(back, work, perm)
         owner.copy_(back.to(owner.device)[perm.long()].to(owner.dtype))
         self.records_sent += int(sum(counts))
+
+    def _succ_piece_exact(self, keys, owner):
+        """One piece on a device engine: the count pass (device counts, this
+        rank's own keys' indices) and one all_gather; own keys are searched in
+        place on the arc's ring, the others go to their owner's rank in the
+        exact layout (own skipped) and their owners come back through perm."""
+        eng, G, me = self.engine, self.world, self.rank
+        q = int(keys.shape[0])
+        dev = keys.device
+        row = torch.zeros(G, dtype=torch.int64, device=dev)
+        own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(eng.arc_own_ws_words(q), dtype=torch.int32, device=dev)
+        eng.arc_count_async(G, keys, row, me, own_idx, ws)
+        mat = self._gather_row(row)
+        c_me = int(mat[me, me])
+
+        def search(k):  # global owner indices of keys owned in this arc
+            return (self._arc_ring().successor(k).to(torch.int64) + self.lo).to(torch.int32)
+        if c_me == q and q:
+            owner.copy_(search(keys).to(owner.dtype))
+        elif c_me:
+            oi = own_idx[:c_me].long()
+            owner[oi] = search(keys[oi]).to(owner.dtype)
+        remote = any(int(mat[r, d]) for r in range(G) for d in range(G) if r != d)
+        if not remote:
+            return
+        send = [int(mat[me, d]) if d != me else 0 for d in range(G)]
+        recv = [int(mat[r, me]) if r != me else 0 for r in range(G)]
+        cursor = torch.empty(G, dtype=torch.int32, device=dev)
+        sk, _, perm = eng.arc_scatter_async(G, self._zeros_src(keys), keys, row, cursor, skip=me)
+        cdev = self.comm_device if self.comm_device is not None else dev
+        rk, work = self._a2a(sk[:sum(send)], recv, send, cdev)
+        rk = self._land(rk, work, sk)
+        got = search(rk) if rk.shape[0] else torch.empty(0, dtype=torch.int32, device=dev)
+        back, work = self._a2a(got, send, recv, cdev)
+        back = self._land(back, work, perm).to(owner.device)
+        pm = perm.long()
+        sel = pm >= 0
+        owner[sel] = back[pm[sel]].to(owner.dtype)
+        self.records_sent += sum(send)
 
     def halo_ring(self, h: int):
         """This rank's arc plus the h peers after it as a ring of its own

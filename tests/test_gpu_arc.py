@@ -704,7 +704,7 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
     assert backend == "nccl" and bad == len(range(0, q, 97))
     for it, r in enumerate(res):  # the exact path walks its own region in place
         assert r == (True, True, True, 2, 0 if it < 2 else q), (it, r)
-    assert succ_ok == (True, 2, q, True)
+    assert succ_ok == (True, 2, 0, True)  # one rank: every key is its own, none sent
 
 
 @pytest.mark.parametrize("G", [2, 8])
