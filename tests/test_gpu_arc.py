@@ -589,6 +589,25 @@ def test_arc_router_three_ranks_ragged_batches(cx, chunks):
         assert out[r][3] == 2
 
 
+def test_arc_router_four_ranks(cx):
+    """Four gloo ranks on one GPU, the exact-layout path with three pieces per
+    rank: routes, placement lists and (through the same worker) every rank's
+    results equal the replicated ring's."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_router_worker, args=(4, port, 50000, 40000, 3, out, True),
+                       nprocs=4, join=True, start_method="spawn")
+    for r in range(4):
+        assert out[r][:3] == (True, True, True), (r, out[r])
+        assert out[r][3] == 2 and out[r][4] > 0
+
+
 def test_arc_router_three_ranks_clustered_ring(cx):
     """The exact-layout path on a ring with a dense cluster (half the peers
     within 2^26 of one ID): gapped hints, exact-ID steps and escaped table
