@@ -1547,7 +1547,10 @@ static int misplaced_impl(const cx_ring *old_ring, const cx_ring *new_ring,
         if (!nr->d_cdir) {
             const size_t Mmax = old_ring->n + new_ring->n;
             int kb = 1;
-            while (((size_t)1 << kb) < Mmax) ++kb;  // >= 2^kb / 2 >= the merged size
+            // load factor <= 1/4: a key whose bucket holds a third entry before
+            // it takes the two-search path, and at 1/2 (~0.8 % of keys) nearly half
+            // the waves waited for one (3.29 vs 3.03 ms at C5, profiles/r05/c5_cdkb/)
+            while (((size_t)1 << kb) < 2 * Mmax) ++kb;
             const size_t bytes = ((size_t)1 << kb) * 32;
             DBuf ws, lo, sw;
             CX_HIP(ws.alloc_pooled(cxk::churn_dir_workspace_bytes(old_ring->n, new_ring->n), s));

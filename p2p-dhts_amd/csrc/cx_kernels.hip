@@ -3876,7 +3876,7 @@ hipError_t copy_tagged(const cell128 *src, size_t n, uint32_t tag_base, cell128 
 // sn(m) = #new entries before m, and the old n-window's holders follow from
 // the tags after m -- a survivor at old rank j holds new rank r = #new entries
 // from m before it, a departed one is CX_NONE (dhash_peer.cpp:322-328 on the
-// mapping cx_churn returns).  Bucket b (top kb bits, load factor <= 1/2) is
+// mapping cx_churn returns).  Bucket b (top kb bits, load factor <= 1/4) is
 // one 32-B entry: {hint0 | so_b | sn_b}, {old mask | new mask | hint1 | cnt}
 // with m_b = the bucket's first merged entry, bit k of the old / new mask =
 // merged entry m_b + k is an old / new ring entry (its tag's two bits), hint = ID bits
