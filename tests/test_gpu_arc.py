@@ -708,7 +708,19 @@ def _rccl_worker(_i, n, q, chunks, out):
     wl, wc = ring.nsucc(keys, 14)
     succ_ok = succ_ok + (bool(torch.equal(lists, wl.to(torch.int32))) and
                          bool(torch.equal(cnt, wc)) and nr == 2,)
-    out[0] = (tdist.get_backend(), res, int((st == chordx.CX_Q_BADPEER).sum().item()), succ_ok)
+    # the exact path's list all_to_all on RCCL (on one rank it has no remote
+    # lookups, so route() never issues it): views into larger buffers, 1-D and
+    # 2-D, asynchronous with work.wait(), and an empty exchange
+    a2a_ok = True
+    for t in (keys[5:77], src[1000:1300], keys[:0]):
+        o = torch.full_like(t, -1)
+        w = router._a2a_views([o], [t])
+        if w is not None:
+            w.wait()
+        torch.cuda.synchronize()
+        a2a_ok = a2a_ok and bool(torch.equal(o, t))
+    out[0] = (tdist.get_backend(), res, int((st == chordx.CX_Q_BADPEER).sum().item()), succ_ok,
+              a2a_ok)
     tdist.destroy_process_group()
 
 
@@ -719,8 +731,8 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
     out = mgr.dict()
     mp.start_processes(_rccl_worker, args=(1 << 20, q, chunks, out), nprocs=1, join=True,
                        start_method="spawn")
-    backend, res, bad, succ_ok = out[0]
-    assert backend == "nccl" and bad == len(range(0, q, 97))
+    backend, res, bad, succ_ok, a2a_ok = out[0]
+    assert backend == "nccl" and bad == len(range(0, q, 97)) and a2a_ok
     for it, r in enumerate(res):  # the exact path walks its own region in place
         assert r == (True, True, True, 2, 0 if it < 2 else q), (it, r)
     assert succ_ok == (True, 2, 0, True)  # one rank: every key is its own, none sent
