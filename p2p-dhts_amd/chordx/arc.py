@@ -494,9 +494,13 @@ class ArcRouter:
                 back = torch.empty(cut[c + 1] - cut[c], dtype=torch.int64, device=dev)
                 arrived, ev = got
                 main.wait_event(ev)
-                for _, w in arrived:
+                for t, w in arrived:
                     if w is not None:
                         w.wait()
+                    # allocated on the side stream, read by this stream's walk:
+                    # the allocator must not hand the block to a later side-
+                    # stream allocation before that walk is done
+                    t.record_stream(main)
                 rk, rs_ = arrived[0][0], arrived[1][0]
                 rh = arrived[2][0] if use_h else None
                 res = eng.arc_route(rs_, rk, hint=rh) if use_h else eng.arc_route(rs_, rk)
@@ -514,6 +518,7 @@ class ArcRouter:
                 if back is None:
                     continue
                 sl = slice(cut[c], cut[c + 1])
+                parts[c][2].record_stream(main)  # perm: a side-stream block read here
                 eng.arc_deliver(back, parts[c][2], owner[sl], hops[sl],
                                 status[sl] if status is not None else None)
         self.rounds = 2
