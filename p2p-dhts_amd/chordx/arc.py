@@ -387,11 +387,13 @@ class ArcRouter:
 
         Current stream: the count pass of every piece (arc_count_async into one
         device row; it also compacts the indices of the lookups of this rank's
-        own arc), the all_gather of that row and its one host read, then per
-        piece the walk of the own lookups in place (arc_route_local: outputs
-        straight into owner / hops / status), of the lookups the other ranks
-        sent, the answers' return exchange and the delivery of this rank's
-        remote lookups.  Side stream (G > 1): the scatter of each piece's
+        own arc), the all_gather of that row and its one host read, the walk of
+        every piece's own lookups in place in ONE launch (arc_route_local:
+        outputs straight into owner / hops / status; a walk launch below ~2^21
+        lookups is latency-bound at ~0.17 ms, so G pieces' own lookups walked
+        piece by piece would pay that G times), then per piece the walk of the
+        lookups the other ranks sent, the answers' return exchange and the
+        delivery of this rank's remote lookups.  Side stream (G > 1): the scatter of each piece's
         remote lookups (arc_scatter_async, reading the counts on the device,
         own lookups skipped), started as soon as the counts exist, and each
         piece's outgoing exchange, which waits on that scatter only.  A
@@ -476,19 +478,35 @@ class ArcRouter:
             return out, ev
 
         inflight = send(0) if remote else None
+        # this rank's own lookups, every piece at once: walked in place, outputs
+        # written (the count pass left each piece's indices piece-relative at
+        # own_idx[cut[c]:])
+        n_own = [cnt[c][me] for c in range(kg)]
+        if sum(n_own):
+            if sum(1 for x in n_own if x) == 1:
+                c = next(c for c in range(kg) if n_own[c])
+                sl = slice(cut[c], cut[c + 1])
+                eng.arc_route_local(src[sl], keys[sl], own_idx[cut[c]: cut[c] + n_own[c]],
+                                    owner[sl], hops[sl],
+                                    status[sl] if status is not None else None)
+            else:
+                idx_all = torch.empty(sum(n_own), dtype=torch.int32, device=dev)
+                at = 0
+                for c in range(kg):
+                    if n_own[c]:
+                        torch.add(own_idx[cut[c]: cut[c] + n_own[c]], cut[c],
+                                  out=idx_all[at: at + n_own[c]])
+                        at += n_own[c]
+                eng.arc_route_local(src, keys, idx_all, owner, hops, status)
         backs = []
         for c in range(kg):
             got = inflight
             if remote and c + 1 < kg:
                 inflight = send(c + 1)
             sl = slice(cut[c], cut[c + 1])
-            n_own = cnt[c][me]
-            if n_own:  # this rank's own lookups: walked in place, outputs written
-                eng.arc_route_local(src[sl], keys[sl], own_idx[cut[c]: cut[c] + n_own], owner[sl],
-                                    hops[sl], status[sl] if status is not None else None)
             back, work = None, None
             if remote:
-                n_rem = sum(cnt[c]) - n_own
+                n_rem = sum(cnt[c]) - n_own[c]
                 # the piece's length (perm names slots < n_rem; arc_deliver
                 # takes a result buffer at least as long as perm)
                 back = torch.empty(cut[c + 1] - cut[c], dtype=torch.int64, device=dev)
