@@ -3021,7 +3021,9 @@ void k_route_tree(TreeIO io) {
 
 static void tree_geometry(size_t q, size_t &chunk, unsigned &blocks) {
     const size_t max_waves = 256 * 32;
-    size_t waves = (q + 1023) / 1024;
+    // >= 64 lookups per wave: a small batch spread over as many waves as it
+    // fills (a walk is a chain of dependent gathers; cx_walk.hip WK_MIN_PER_WAVE)
+    size_t waves = (q + 63) / 64;
     if (waves > max_waves) waves = max_waves;
     if (waves == 0) waves = 1;
     chunk = (q + waves - 1) / waves;
@@ -3097,7 +3099,7 @@ hipError_t route_arc(const cell128 *ring_ext, const cell128 *ring, size_t n, con
     io.status = status;
     static const unsigned resident = resident_grid(k_route_tree<true, true>, RT_BLOCK);
     size_t waves = (size_t)resident * (RT_BLOCK / 64);
-    const size_t small = (q + 1023) / 1024;
+    const size_t small = (q + 63) / 64;  // >= 64 lookups per wave (tree_geometry)
     if (small < waves) waves = small ? small : 1;
     io.chunk = (q + waves - 1) / waves;
     waves = (q + io.chunk - 1) / io.chunk;

@@ -432,6 +432,12 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
 // than 7 (3.43-3.45 vs 3.27 ms, profiles/r05/walk_ab/w8_vs_w7): past ~4.6 x
 // 10^5 walks in flight the random-request latency grows faster than the
 // requests.  Dynamic LDS holds a launch to CX_WALK_WAVES blocks per CU.
+// Fewest lookups per wave of a launch (small batches): one per lane.  A walk
+// is a chain of dependent gathers, so a batch below one resident round of
+// waves is fastest spread over as many waves as it fills; at >= 1024 per wave
+// (before round 5) a 2^16 / 2^18 / 2^20 / 2^22 batch took 159 / 167 / 175 /
+// 443 us, at 64 per wave 24 / 39 / 123 / 417 us (profiles/r05/walk_q/minq/).
+constexpr size_t WK_MIN_PER_WAVE = 64;
 #ifndef CX_WALK_WAVES
 #define CX_WALK_WAVES 7
 #endif
@@ -483,11 +489,11 @@ hipError_t route_walk(const cell128 *ring_ext, const cell128 *ring, size_t n, co
     io.status = status;
     io.stats = stats;
     // one resident round of waves (no second, partial round of blocks); small
-    // batches: >= 1024 lookups per wave
+    // batches: >= WK_MIN_PER_WAVE lookups per wave
     static const size_t pad = walk_lds_pad(k_walk<false, false>);
     static const unsigned resident = walk_resident_grid(k_walk<false, false>, pad);
     size_t waves = (size_t)resident * (WK_BLOCK / 64);
-    const size_t small = (q + 1023) / 1024;
+    const size_t small = (q + WK_MIN_PER_WAVE - 1) / WK_MIN_PER_WAVE;
     if (small < waves) waves = small ? small : 1;
     io.chunk = (q + waves - 1) / waves;
     if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
@@ -535,7 +541,7 @@ hipError_t route_walk_arc(const cell128 *ring_ext, const cell128 *ring, size_t n
     static const size_t pad = walk_lds_pad(k_walk<false, true>);
     static const unsigned resident = walk_resident_grid(k_walk<false, true>, pad);
     size_t waves = (size_t)resident * (WK_BLOCK / 64);
-    const size_t small = (q + 1023) / 1024;
+    const size_t small = (q + WK_MIN_PER_WAVE - 1) / WK_MIN_PER_WAVE;
     if (small < waves) waves = small ? small : 1;
     io.chunk = (q + waves - 1) / waves;
     if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
@@ -579,7 +585,7 @@ hipError_t route_walk_arc_local(const cell128 *ring_ext, const cell128 *ring, si
     static const size_t pad = walk_lds_pad(k_walk<false, true, true>);
     static const unsigned resident = walk_resident_grid(k_walk<false, true, true>, pad);
     size_t waves = (size_t)resident * (WK_BLOCK / 64);
-    const size_t small = (q + 1023) / 1024;
+    const size_t small = (q + WK_MIN_PER_WAVE - 1) / WK_MIN_PER_WAVE;
     if (small < waves) waves = small ? small : 1;
     io.chunk = (q + waves - 1) / waves;
     if (io.chunk >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit lookup offsets
