@@ -135,11 +135,13 @@ def test_route_converged(cx, O, n, variant):
     assert (owner == O.successor(want_ring, keys)).all()
 
 
-@pytest.mark.parametrize("q", [1, 2, 63, 64, 65, 1023, 1025, 4097, 70001])
+@pytest.mark.parametrize("q", [1, 2, 63, 64, 65, 1023, 1025, 4097, 70001, 458753, 917507])
 def test_route_batch_sizes_write_exactly_q(cx, O, q):
     """The default walk stores each lookup's outputs as it finishes (no result
     ring): every batch size writes owner / hops / status of exactly its q
-    lookups -- equal to the oracle -- and nothing past them."""
+    lookups -- equal to the oracle -- and nothing past them.  Sizes cover one
+    lookup per wave, partial waves, and the switch to one resident round of
+    waves (>= 64 lookups per wave: 7 x 4 x 256 waves fill at 458752)."""
     import torch
     ids = O.splitmix_keys(0xBA7C, 20000)
     ring = cx.Ring(ids)
