@@ -1047,6 +1047,25 @@ def main():
     owner_eq = dist.all_over_ranks(owner_eq and bool((succ == rout[0]).all().item()), world, dev)
     rsrc_bad = int((rout[2] != 0).sum().item())
     del rsrc, rout
+    # small batches (serving): one launch over the first 2^k lookups of the same
+    # batch, HIP events around 20 back-to-back launches; outputs must equal the
+    # full batch's (the walk is per lookup)
+    small = {}
+    for lk in (12, 16, 20):
+        m = 1 << lk
+        if m > Q:
+            continue
+        so = (torch.empty(m, dtype=torch.int32, device=dev), torch.empty(m, dtype=torch.uint8, device=dev),
+              torch.empty(m, dtype=torch.uint8, device=dev))
+        ring.route(src[:m], keys[:m], out=so)
+        e0.record(stream)
+        for _ in range(20):
+            ring.route(src[:m], keys[:m], out=so)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        same = bool(torch.equal(so[0], owner[:m])) and bool(torch.equal(so[1], hops[:m]))
+        small[f"2^{lk}"] = {"us_per_launch": e0.elapsed_time(e1) / 20 * 1e3, "equal_to_batch": same}
+        del so
 
     # ---- churn -> route-ready (f2), cold then warm ----
     churn = None
@@ -1170,6 +1189,7 @@ def main():
             "route_owner_equals_successor": owner_eq,
             "counting_build_same_results": counting_same,
             "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
+            "route_small_batches": small,
             "route_random_src": {"kernel_ms": rsrc_ms, "lookups_per_s": Q / (rsrc_ms * 1e-3),
                                  "bad_status": rsrc_bad,
                                  "note": "same keys and kernel, src uniform in [0, N) "
