@@ -199,13 +199,48 @@ hipError_t dev_malloc(T **p, size_t bytes) {
 }
 }  // namespace
 
+// Host-memory calls (CX_MEM_HOST) stage their inputs and outputs in device
+// buffers.  A small per-thread cache keeps those buffers from call to call:
+// a small batch's call otherwise spent more time in hipMalloc / hipFree (five
+// of each for cx_route) than on the GPU.  Blocks are power-of-two sized, at
+// most STAGE_MAX each (bigger staging is a plain hipMalloc, amortized by the
+// batch), at most STAGE_HELD held per thread; a block returns to the cache only
+// after the stream that used it has drained.  A thread's blocks are left to
+// process exit (the HIP runtime may already be gone when thread-local
+// destructors run).
+constexpr size_t STAGE_MAX = (size_t)16 << 20;
+constexpr size_t STAGE_HELD = (size_t)64 << 20;
+struct StageBlk {
+    void *p;
+    size_t cap;
+    int dev;
+};
+thread_local std::vector<StageBlk> *t_stage = nullptr;
+thread_local size_t t_stage_held = 0;
+
 struct DBuf {
     void *p = nullptr;
     size_t pooled = 0;  // > 0: a table-pool block of this size (build temporaries >= 1 GiB)
-    hipStream_t user = nullptr;  // stream whose work uses a pooled block
+    size_t staged = 0;  // > 0: a staging-cache block of this capacity (alloc_stage)
+    int dev = 0;
+    hipStream_t user = nullptr;  // stream whose work uses a pooled / staged block
     ~DBuf() { drop(); }
     void drop() {
         if (!p) return;
+        if (staged) {
+            (void)hipStreamSynchronize(user);
+            if (!t_stage) t_stage = new std::vector<StageBlk>();
+            if (t_stage_held + staged <= STAGE_HELD) {
+                t_stage->push_back(StageBlk{p, staged, dev});
+                t_stage_held += staged;
+            } else {
+                (void)hipFree(p);
+            }
+            p = nullptr;
+            staged = 0;
+            user = nullptr;
+            return;
+        }
         if (pooled) {
             // a pooled block goes back to the pool only after the work queued
             // on it has finished (hipFree would wait; the pool does not), so
@@ -225,6 +260,40 @@ struct DBuf {
     hipError_t alloc(size_t bytes) {
         drop();
         return dev_malloc(&p, bytes ? bytes : 16);
+    }
+    // staging for a host-memory call on `stream` (the per-thread cache above)
+    hipError_t alloc_stage(size_t bytes, hipStream_t stream) {
+        drop();
+        if (bytes > STAGE_MAX) return alloc(bytes);
+        int d = 0;
+        (void)hipGetDevice(&d);
+        size_t cap = 4096;
+        while (cap < bytes) cap <<= 1;
+        if (t_stage) {  // the smallest cached block of this device that fits
+            size_t best = t_stage->size();
+            for (size_t k = 0; k < t_stage->size(); ++k) {
+                const StageBlk &b = (*t_stage)[k];
+                if (b.dev == d && b.cap >= bytes && (best == t_stage->size() || b.cap < (*t_stage)[best].cap))
+                    best = k;
+            }
+            if (best < t_stage->size()) {
+                p = (*t_stage)[best].p;
+                cap = (*t_stage)[best].cap;
+                t_stage->erase(t_stage->begin() + best);
+                t_stage_held -= cap;
+                staged = cap;
+                dev = d;
+                user = stream;
+                return hipSuccess;
+            }
+        }
+        hipError_t e = dev_malloc(&p, cap);
+        if (e == hipSuccess) {
+            staged = cap;
+            dev = d;
+            user = stream;
+        }
+        return e;
     }
     // through the table pool: build temporaries of the same size recur every
     // membership epoch; `stream` is the stream the block's users run on
@@ -435,14 +504,14 @@ int stage_in(const T *src, size_t count, int memkind, DBuf &tmp, const T **dev, 
         return CX_OK;
     }
     CX_CHECK(memkind == CX_MEM_HOST, CX_E_INVALID, "bad memkind");
-    CX_HIP(tmp.alloc(count * sizeof(T)));
+    CX_HIP(tmp.alloc_stage(count * sizeof(T), s));
     CX_HIP(hipMemcpyAsync(tmp.p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
     *dev = tmp.as<T>();
     return CX_OK;
 }
 
 template <class T>
-int stage_out(T *dst, size_t count, int memkind, DBuf &tmp, T **dev) {
+int stage_out(T *dst, size_t count, int memkind, DBuf &tmp, T **dev, hipStream_t s) {
     if (count == 0) {
         *dev = dst;
         return CX_OK;
@@ -453,7 +522,7 @@ int stage_out(T *dst, size_t count, int memkind, DBuf &tmp, T **dev) {
         return CX_OK;
     }
     CX_CHECK(memkind == CX_MEM_HOST, CX_E_INVALID, "bad memkind");
-    CX_HIP(tmp.alloc(count * sizeof(T)));
+    CX_HIP(tmp.alloc_stage(count * sizeof(T), s));
     *dev = tmp.as<T>();
     return CX_OK;
 }
@@ -978,7 +1047,7 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
     const cx_u128 *dk;
     uint32_t *dout;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(owner, q, memkind, to, &dout))) return rc;
+    if ((rc = stage_out(owner, q, memkind, to, &dout, s))) return rc;
     if (ring->search_variant == 2) {
         cxk::STreeView st;
         if ((rc = stree_view(const_cast<cx_ring *>(ring), st, s))) return rc;
@@ -1073,7 +1142,7 @@ int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t 
     const cx_u128 *dk;
     uint32_t *dout;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(pred, q, memkind, to, &dout))) return rc;
+    if ((rc = stage_out(pred, q, memkind, to, &dout, s))) return rc;
     if (ring->search_variant == 2) {
         cxk::STreeView st;
         if ((rc = stree_view(const_cast<cx_ring *>(ring), st, s))) return rc;
@@ -1323,9 +1392,9 @@ int cx_route(const cx_ring *ring, const uint32_t *src, const cx_u128 *keys, size
     uint8_t *dh, *dst = nullptr;
     if ((rc = stage_in(src, q, memkind, ts, &dsrc, s))) return rc;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(owner, q, memkind, to, &dow))) return rc;
-    if ((rc = stage_out(hops, q, memkind, th, &dh))) return rc;
-    if (status && (rc = stage_out(status, q, memkind, tst, &dst))) return rc;
+    if ((rc = stage_out(owner, q, memkind, to, &dow, s))) return rc;
+    if ((rc = stage_out(hops, q, memkind, th, &dh, s))) return rc;
+    if (status && (rc = stage_out(status, q, memkind, tst, &dst, s))) return rc;
     if (!ring->literal()) {
         int e2 = ensure_route_table(const_cast<cx_ring *>(ring), s);
         if (e2) return e2;
@@ -1371,8 +1440,8 @@ int cx_nsucc(const cx_ring *ring, const cx_u128 *keys, size_t q, int n, uint32_t
     uint32_t *dl;
     uint8_t *dc;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(lists, q * (size_t)n, memkind, tl, &dl))) return rc;
-    if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
+    if ((rc = stage_out(lists, q * (size_t)n, memkind, tl, &dl, s))) return rc;
+    if ((rc = stage_out(count, q, memkind, tc, &dc, s))) return rc;
     CX_HIP(cxk::nsucc(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, n, dl, dc, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(lists, dl, q * (size_t)n * sizeof(uint32_t),
@@ -1526,13 +1595,13 @@ static int misplaced_impl(const cx_ring *old_ring, const cx_ring *new_ring,
     const bool fused = old_lists != nullptr;
     if ((rc = stage_in(old_to_new, old_ring->n, memkind, to2n, &d_o2n, s))) return rc;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl))) return rc;
-    if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
-    if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
-    if ((rc = stage_out(target, q * (size_t)n, memkind, tt, &dt))) return rc;
+    if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl, s))) return rc;
+    if ((rc = stage_out(count, q, memkind, tc, &dc, s))) return rc;
+    if ((rc = stage_out(mask, q, memkind, tm, &dm, s))) return rc;
+    if ((rc = stage_out(target, q * (size_t)n, memkind, tt, &dt, s))) return rc;
     if (fused) {
-        if ((rc = stage_out(old_lists, q * (size_t)n, memkind, tol, &dol))) return rc;
-        if ((rc = stage_out(old_count, q, memkind, toc, &doc))) return rc;
+        if ((rc = stage_out(old_lists, q * (size_t)n, memkind, tol, &dol, s))) return rc;
+        if ((rc = stage_out(old_count, q, memkind, toc, &doc, s))) return rc;
     }
     // churn directory: the new ring came from cx_churn(old_ring) and the
     // caller's mapping equals the one it returned (checked on the device)
@@ -1627,10 +1696,10 @@ int cx_misplaced_holders(const cx_ring *ring, const cx_u128 *keys, size_t q,
     uint16_t *dm;
     if ((rc = stage_in(holders, q * (size_t)nh, memkind, th, &dh, s))) return rc;
     if ((rc = stage_in(keys, q, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl))) return rc;
-    if ((rc = stage_out(count, q, memkind, tc, &dc))) return rc;
-    if ((rc = stage_out(mask, q, memkind, tm, &dm))) return rc;
-    if ((rc = stage_out(target, q * (size_t)nh, memkind, tt, &dt))) return rc;
+    if ((rc = stage_out(new_lists, q * (size_t)n, memkind, tl, &dl, s))) return rc;
+    if ((rc = stage_out(count, q, memkind, tc, &dc, s))) return rc;
+    if ((rc = stage_out(mask, q, memkind, tm, &dm, s))) return rc;
+    if ((rc = stage_out(target, q * (size_t)nh, memkind, tt, &dt, s))) return rc;
     CX_HIP(cxk::misplaced_holders(ring->sv(), dh, nh, reinterpret_cast<const cell128 *>(dk), q,
                                   n, dl, dc, dm, dt, s));
     if (memkind == CX_MEM_HOST && q) {
@@ -1656,7 +1725,7 @@ int cx_in_between(const cx_u256 *v, const cx_u256 *lb, const cx_u256 *ub, size_t
     if ((rc = stage_in(v, q, memkind, tv, &dv, s))) return rc;
     if ((rc = stage_in(lb, q, memkind, tl, &dl, s))) return rc;
     if ((rc = stage_in(ub, q, memkind, tu, &du, s))) return rc;
-    if ((rc = stage_out(out, q, memkind, to, &dout))) return rc;
+    if ((rc = stage_out(out, q, memkind, to, &dout, s))) return rc;
     CX_HIP(cxk::in_between(dv, dl, du, q, inclusive, dout, s));
     if (memkind == CX_MEM_HOST && q) {
         CX_HIP(hipMemcpyAsync(out, dout, q, hipMemcpyDeviceToHost, s));
@@ -1691,7 +1760,7 @@ int cx_uuid5_dns(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx
         CX_HIP(hipMemcpy(&nbytes, offsets + count, sizeof(nbytes), hipMemcpyDeviceToHost));
     }
     if ((rc = stage_in(bytes, (size_t)nbytes, memkind, tb, &dbytes, s))) return rc;
-    if ((rc = stage_out(out, count, memkind, tout, &dout))) return rc;
+    if ((rc = stage_out(out, count, memkind, tout, &dout, s))) return rc;
     CX_HIP(cxk::uuid5(dbytes, doff, count, reinterpret_cast<cell128 *>(dout), s));
     return finish_out(out, dout, count, memkind, s);
 }
@@ -1735,8 +1804,8 @@ int cx_hex_parse(const uint8_t *bytes, const uint64_t *offsets, size_t count, cx
         CX_HIP(hipMemcpy(&nbytes, offsets + count, sizeof(nbytes), hipMemcpyDeviceToHost));
     }
     if ((rc = stage_in(bytes, (size_t)nbytes, memkind, tb, &dbytes, s))) return rc;
-    if ((rc = stage_out(out, count, memkind, tout, &dout))) return rc;
-    if ((rc = stage_out(ok, count, memkind, tok, &dok))) return rc;
+    if ((rc = stage_out(out, count, memkind, tout, &dout, s))) return rc;
+    if ((rc = stage_out(ok, count, memkind, tok, &dok, s))) return rc;
     CX_HIP(cxk::hex_parse(dbytes, doff, count, reinterpret_cast<cell128 *>(dout), dok, s));
     if ((rc = finish_out(ok, dok, count, memkind, s))) return rc;
     return finish_out(out, dout, count, memkind, s);
@@ -1758,8 +1827,8 @@ int cx_hex_format(const cx_u128 *keys, size_t count, char *out, uint8_t *len, in
     uint8_t *dlen;
     int rc;
     if ((rc = stage_in(keys, count, memkind, tk, &dk, s))) return rc;
-    if ((rc = stage_out(out, count * 32, memkind, tout, &dout))) return rc;
-    if ((rc = stage_out(len, count, memkind, tlen, &dlen))) return rc;
+    if ((rc = stage_out(out, count * 32, memkind, tout, &dout, s))) return rc;
+    if ((rc = stage_out(len, count, memkind, tlen, &dlen, s))) return rc;
     CX_HIP(cxk::hex_format(reinterpret_cast<const cell128 *>(dk), count, dout, dlen, s));
     if ((rc = finish_out(len, dlen, count, memkind, s))) return rc;
     return finish_out(out, dout, count * 32, memkind, s);
@@ -1835,7 +1904,7 @@ int cx_ida_encode(const uint8_t *data, const uint64_t *offsets, const uint64_t *
     if ((rc = stage_in(data, (size_t)nbytes, memkind, td, &dd, s))) return rc;
     if ((rc = stage_in(offsets, blocks + 1, memkind, to, &doff, s))) return rc;
     if ((rc = stage_in(seg_offsets, blocks + 1, memkind, tseg, &dseg, s))) return rc;
-    if ((rc = stage_out(frags, (size_t)(segs * n), memkind, tf, &df))) return rc;
+    if ((rc = stage_out(frags, (size_t)(segs * n), memkind, tf, &df, s))) return rc;
     CX_HIP(cxk::ida_encode(dd, doff, dseg, blocks, n, m, p, df, s));
     return finish_out(frags, df, (size_t)(segs * n), memkind, s);
 }
@@ -1869,8 +1938,8 @@ int cx_ida_decode(const uint16_t *frags, const uint64_t *seg_offsets, const uint
         if ((rc = stage_in(frags, (size_t)(segs * m), memkind, tf, &dfr, s))) return rc;
         if ((rc = stage_in(seg_offsets, blocks + 1, memkind, tsg, &dseg, s))) return rc;
         if ((rc = stage_in(indices, blocks * (size_t)m, memkind, ti, &didx, s))) return rc;
-        if ((rc = stage_out(out, (size_t)(segs * m), memkind, tout, &dout))) return rc;
-        if ((rc = stage_out(out_len, blocks, memkind, tlen, &dlen))) return rc;
+        if ((rc = stage_out(out, (size_t)(segs * m), memkind, tout, &dout, s))) return rc;
+        if ((rc = stage_out(out_len, blocks, memkind, tlen, &dlen, s))) return rc;
     }
     // runs of equal index lists share one inverse
     IdaArena &arena = ida_arena(device);
