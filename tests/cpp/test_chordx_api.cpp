@@ -221,6 +221,7 @@ int main() {
     RUN(ChordGetSucc, FromPredecessor);
     RUN(ChordGetSucc, Failing);
     RUN(ChordGetSucc, LivelockHitsHopCap);
+    RUN(ChordGetPred, Fixtures);
     RUN(DHashPeer, InsufficientSuccs);
     RUN(Wire, GetSuccJoinFixture);
     RUN(DataBlock, EncodeDecodeVal1);
