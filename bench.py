@@ -380,6 +380,103 @@ def _route_rounds(rings, keys, srcs, dev, rounds=6, per=3):
     return {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
 
 
+def overlap_leg(serve, joins, leaves, keys, src, dev, builds=3, q_serve=1 << 23):
+    """Lookups keep running while the next membership epoch's ring builds
+    (double-buffered route tables).  `serve` is epoch e's
+    route-ready ring; a serving thread routes batches of q_serve of the bench's
+    lookups on it on a stream of its own, keeping two launches queued (a
+    server's pipeline), while this thread churns `serve` (the same 1 %/1 %
+    event set) into epoch e + 1 and builds its fingers and route table on the
+    new handle's stream -- `builds` times back to back, each new ring closed
+    after it is route-ready.  Calls on one handle are serialised by a lock
+    (the handle's stream is per-handle state: the churn call holds it, each
+    route enqueue takes it for microseconds).
+
+    Reports the serving rate alone and during the rebuilds (launches whose
+    completion was observed inside a rebuild window), each rebuild's wall time
+    under that load, and the serving outputs' equality with a reference route
+    of `serve` taken before."""
+    import threading
+    from collections import deque
+    Qs = min(q_serve, keys.shape[0])
+    ks = keys[:Qs].contiguous()
+    ss = (src[:Qs].to(torch.int64) % serve.n).to(torch.int32)
+    ref = serve.route(ss, ks)
+    torch.cuda.synchronize(dev)
+    outs = [tuple(torch.empty_like(t) for t in ref) for _ in range(2)]
+    lock = threading.Lock()
+    stop = threading.Event()
+    done = []  # host time at which each launch was seen complete
+    stream = torch.cuda.Stream(device=dev)
+    err = []
+
+    def serving():
+        try:
+            with torch.cuda.stream(stream):
+                pend, i = deque(), 0
+                while not stop.is_set():
+                    with lock:
+                        serve.route(ss, ks, out=outs[i % 2])
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    pend.append(ev)
+                    i += 1
+                    if len(pend) >= 2:
+                        pend.popleft().synchronize()
+                        done.append(time.perf_counter())
+                while pend:
+                    pend.popleft().synchronize()
+                    done.append(time.perf_counter())
+        except Exception as e:  # reported; the leg's checks then fail
+            err.append(repr(e))
+
+    def rate(t0, t1):
+        n = sum(1 for t in done if t0 < t <= t1)
+        return n * Qs / (t1 - t0)
+
+    th = threading.Thread(target=serving, daemon=True)
+    th.start()
+    time.sleep(0.25)
+    a0 = time.perf_counter()
+    time.sleep(0.3)
+    a1 = time.perf_counter()
+    recs = []
+    build_stream = torch.cuda.Stream(device=dev)
+    for b in range(builds):
+        with torch.cuda.stream(build_stream):
+            t0 = time.perf_counter()
+            with lock:
+                new, _ = serve.churn(joins, leaves)
+            new.sync()
+            t1 = time.perf_counter()
+            new.build_fingers()
+            new.sync()
+            t2 = time.perf_counter()
+        recs.append({"route_ready_ms": (t2 - t0) * 1e3, "churn_ms": (t1 - t0) * 1e3,
+                     "fingers_and_table_ms": (t2 - t1) * 1e3,
+                     "serving_lookups_per_s": rate(t0, t2)})
+        if b == builds - 1:
+            k2 = ks[: 1 << 20]
+            o, _, st = new.route((torch.arange(k2.shape[0], device=dev) % new.n).to(torch.int32), k2)
+            new_ok = bool((o == new.successor(k2)).all().item()) and int((st != 0).sum().item()) == 0
+        new.close()
+        del new
+    stop.set()
+    th.join()
+    alone = rate(a0, a1)
+    same = not err and all(bool(torch.equal(a, b)) for o in outs for a, b in zip(o, ref))
+    during = sorted(r["serving_lookups_per_s"] for r in recs)[len(recs) // 2]
+    return {"serving_lookups_per_s_alone": alone,
+            "serving_lookups_per_s_during_rebuild": during,
+            "serving_during_vs_alone": during / alone if alone else None,
+            "rebuild_ms_under_load": sorted(r["route_ready_ms"] for r in recs)[len(recs) // 2],
+            "rebuilds": recs, "serving_batch": Qs, "serving_equals_reference": same,
+            "new_ring_route_equals_successor": new_ok, "errors": err,
+            "layout": "epoch e's ring (route table and all) keeps serving on its own stream "
+                      "while epoch e + 1 is churned from it and built on the new handle's "
+                      "stream; both tables are resident (2 x 64 GiB of 288 GB)"}
+
+
 def churn_leg(ring, keys, src, dev, depth_ab=28):
     """1 % joins + 1 % leaves of the bench ring -> route-ready.  Every epoch
     states its allocation path: the table pool's counters around it
@@ -452,6 +549,8 @@ def churn_leg(ring, keys, src, dev, depth_ab=28):
         and int((st != 0).sum().item()) == 0
     out["new_ring_peers"] = a1.n
     del k2, s2, o, h, st
+    # epoch e (a1) keeps serving while epoch e + 1 builds
+    out["overlapped"] = overlap_leg(a1, joins, leaves, keys, src, dev)
     out["route_ready_ms"] = {"cold": out["cold"]["route_ready_ms"],
                              "warm": out["warm"]["route_ready_ms"]}
     r_def = out["warm"]["route_levels"]

@@ -51,6 +51,23 @@ import torch
 import torch.distributed as tdist
 
 MAX_ROUNDS = 300  # hop cap 255 + seed + result delivery, with margin
+# Largest per-peer view of one all_to_all call (bytes).  Measured on the box
+# (tools/diag_rccl_a2a.py, profiles/r06/rccl_a2a/): RCCL 2.26.6 delivers a
+# 1 GiB send/recv view whole but only the first half of one of 2,013,265,920 B
+# or more, and reports success.  Every exchange is cut into calls of at most
+# this many bytes per view (ArcRouter._rounds).
+VIEW_CAP = 1 << 30
+
+
+class _Works:
+    """The works of one exchange issued as several all_to_all calls."""
+
+    def __init__(self, works):
+        self.works = list(works)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
 
 
 def arc_bounds(n: int, world: int, g: int):
@@ -95,6 +112,35 @@ class ArcRouter:
         # itself, through the process group's collectives) and delivers -- the
         # general path, so a one-GPU run executes and times what N ranks run
         self.exchange_always = exchange_always
+        # self_exchange: the rank's own lookups / keys travel through the
+        # collectives too (to itself) instead of being answered in place -- on a
+        # one-rank group every lookup then crosses RCCL, the exchange a one-GPU
+        # run can time and check (bench `arc.exchange_selftest`).  Must agree
+        # on every rank (checked through the gathered rows).
+        self.self_exchange = False
+        # largest per-peer view of one all_to_all call (bytes); see _rounds
+        self.view_cap = VIEW_CAP
+
+    def _rounds(self, rows: int, row_bytes: int) -> int:
+        """all_to_all calls one exchange is issued as: every per-peer view of
+        each call stays at or below view_cap bytes (VIEW_CAP: RCCL copies only
+        half of a larger one).  `rows` must be the largest per-peer count of
+        the exchange over ALL ranks (from the gathered counts), so every rank
+        issues the same number of calls."""
+        return max(1, -(-int(rows) * int(row_bytes) // self.view_cap))
+
+    def _list_a2a(self, outs, ins, rounds: int = 1):
+        """RCCL list all_to_all from the views `ins` (one per destination)
+        into `outs` (one per source), as `rounds` calls over consecutive
+        slices of every view -- slice j of a view of c rows is rows [c j / R,
+        c (j + 1) / R), the same cut on the sending and the receiving side.
+        Asynchronous: returns one waitable for all of them."""
+        works = []
+        for j in range(rounds):
+            o = [t[t.shape[0] * j // rounds: t.shape[0] * (j + 1) // rounds] for t in outs]
+            i = [t[t.shape[0] * j // rounds: t.shape[0] * (j + 1) // rounds] for t in ins]
+            works.append(tdist.all_to_all(o, i, group=self.group, async_op=True))
+        return _Works(works)
 
     def _exchange(self, send, counts):
         """Returns (received records, global number of records in flight)."""
@@ -105,8 +151,8 @@ class ArcRouter:
         mat = torch.empty((self.world, self.world), dtype=torch.int64, device=dev)
         tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
         if mat.is_cuda:
-            # the splits must reach the host (all_to_all_single takes lists):
-            # one async copy into a pinned buffer, then wait on that copy only
+            # the splits must reach the host (all_to_all takes lists): one
+            # async copy into a pinned buffer, then wait on that copy only
             if self._mat_host is None or self._mat_host.shape != mat.shape:
                 self._mat_host = torch.empty((self.world, self.world), dtype=torch.int64,
                                              pin_memory=True)
@@ -121,28 +167,34 @@ class ArcRouter:
             return send[:0], 0
         s = send.to(dev) if send.device != torch.device(dev) else send
         recv = torch.empty((sum(recv_counts), s.shape[1]), dtype=s.dtype, device=dev)
-        tdist.all_to_all_single(recv, s.contiguous(), output_split_sizes=recv_counts,
-                                input_split_sizes=list(counts), group=self.group)
+        if recv.is_cuda:
+            rows = max(int(x) for x in m.flatten())
+            self._list_a2a(list(torch.split(recv, recv_counts)),
+                           list(torch.split(s.contiguous(), list(counts))),
+                           self._rounds(rows, s.shape[1] * s.element_size())).wait()
+        else:
+            tdist.all_to_all_single(recv, s.contiguous(), output_split_sizes=recv_counts,
+                                    input_split_sizes=list(counts), group=self.group)
         return (recv.to(send.device) if recv.device != send.device else recv), inflight
 
-    def _a2a(self, t, out_splits, in_splits, dev):
+    def _a2a(self, t, out_splits, in_splits, dev, rounds: int = 1):
         """Asynchronous all-to-all-v of a contiguous buffer: (output, work).
-        On RCCL every SoA exchange is a list all_to_all (split views), so all
-        ranks issue the same collective kind whether their pieces were laid
-        out in regions or packed; gloo takes all_to_all_single."""
+        On RCCL every SoA exchange is a list all_to_all (split views, `rounds`
+        calls: _list_a2a), so all ranks issue the same collective kind whether
+        their pieces were laid out in regions or packed; gloo takes
+        all_to_all_single."""
         s = t.to(dev) if t.device != torch.device(dev) else t
         out = torch.empty((sum(out_splits),) + tuple(s.shape[1:]), dtype=s.dtype, device=dev)
         if out.is_cuda:
-            work = tdist.all_to_all(list(torch.split(out, list(out_splits))),
-                                    list(torch.split(s.contiguous(), list(in_splits))),
-                                    group=self.group, async_op=True)
+            work = self._list_a2a(list(torch.split(out, list(out_splits))),
+                                  list(torch.split(s.contiguous(), list(in_splits))), rounds)
         else:
             work = tdist.all_to_all_single(out, s.contiguous(), output_split_sizes=out_splits,
                                            input_split_sizes=in_splits, group=self.group,
                                            async_op=True)
         return out, work
 
-    def _a2a_regions(self, t, counts, cap, out_splits, dev):
+    def _a2a_regions(self, t, counts, cap, out_splits, dev, rounds: int = 1):
         """Asynchronous all_to_all of destination regions: rows [d cap, d cap
         + counts[d]) of t go to rank d (no compaction on RCCL: a list
         all_to_all over region views).  gloo has no list all_to_all: the
@@ -150,12 +202,10 @@ class ArcRouter:
         views = [t[d * cap: d * cap + counts[d]] for d in range(self.world)]
         if torch.device(dev).type == "cuda" and t.is_cuda:
             out = torch.empty((sum(out_splits),) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
-            outs = list(torch.split(out, out_splits))
-            work = tdist.all_to_all(outs, views, group=self.group, async_op=True)
-            return out, work
+            return out, self._list_a2a(list(torch.split(out, out_splits)), views, rounds)
         return self._a2a(torch.cat(views), out_splits, list(counts), dev)
 
-    def _a2a_into_regions(self, t, in_splits, counts, cap, like, dev):
+    def _a2a_into_regions(self, t, in_splits, counts, cap, like, dev, rounds: int = 1):
         """Asynchronous all_to_all whose arrivals from rank d land at rows
         [d cap, d cap + counts[d]) of a world x cap buffer (the answers coming
         home to the region slots perm names)."""
@@ -163,9 +213,7 @@ class ArcRouter:
         if torch.device(dev).type == "cuda" and t.is_cuda:
             back = torch.empty((G * cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
             outs = [back[d * cap: d * cap + counts[d]] for d in range(G)]
-            work = tdist.all_to_all(outs, list(torch.split(t, in_splits)), group=self.group,
-                                    async_op=True)
-            return back, work, None
+            return back, self._list_a2a(outs, list(torch.split(t, in_splits)), rounds), None
         packed, work = self._a2a(t, list(counts), in_splits, dev)
         return packed, work, (counts, cap)
 
@@ -200,9 +248,10 @@ class ArcRouter:
         # group exchanges nothing, so its batch is one piece unless fixed
         k = int(fixed) if fixed is not None else (max(1, min(4, q >> 22)) if self.world > 1 else 1)
         k = max(1, min(k, kmax, max(q, 1)))
-        dev = self.comm_device if self.comm_device is not None else keys.device
         if self.exact and hasattr(eng, "arc_count_async") and keys.is_cuda:
             return self.route_exact(src, keys, owner, hops, status, k, kmax)
+        if self.self_exchange:
+            raise ValueError("self_exchange needs the exact protocol (a device engine)")
         cut = [c * q // k for c in range(k + 1)]
         G = self.world
         # single-pass partition into per-destination regions when the engine
@@ -260,8 +309,9 @@ class ArcRouter:
             return mat
 
         my_h = bool(hints) and all(len(p) > 4 for p in parts)
-        row[0] = k | (int(my_h) << 20)
+        row[0] = k | (int(my_h) << 20)  # bit 21 = 0: the region protocol
         mat = gather(row)
+        self._agree(mat[:, 0], 0)
         ovf = [[int(mat[r, 1 + c * W + G]) for c in range(kmax)] for r in range(G)]
         if any(any(o) for o in ovf):
             # a piece crowded one destination past its region: that rank
@@ -286,6 +336,10 @@ class ArcRouter:
         kg = int((mat[:, 0] & 0xFFFFF).max())  # pieces every rank runs
         use_h = bool(int((mat[:, 0] >> 20).min()))  # every rank's pieces carry hints
         recv = [[int(mat[r, 1 + c * W + self.rank]) for r in range(G)] for c in range(kg)]
+        # calls per exchange of piece c: its largest per-peer view on any rank
+        # (16-B keys out is the widest row; answers and hints are 8 B)
+        rnd = [self._rounds(max(int(mat[r, 1 + c * W + d]) for r in range(G) for d in range(G)),
+                            16) for c in range(kg)]
         if kg > k:  # this rank's extra pieces are empty
             e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=keys.device),
                  [0] * G, torch.empty(0, dtype=torch.int64, device=keys.device))
@@ -299,14 +353,14 @@ class ArcRouter:
         def send(c):
             sk, ss, _, cnt = parts[c][:4]
             if caps[c]:
-                out = [self._a2a_regions(sk, cnt, caps[c], recv[c], dev),
-                       self._a2a_regions(ss, cnt, caps[c], recv[c], dev)]
+                out = [self._a2a_regions(sk, cnt, caps[c], recv[c], dev, rnd[c]),
+                       self._a2a_regions(ss, cnt, caps[c], recv[c], dev, rnd[c])]
                 if use_h:
-                    out.append(self._a2a_regions(parts[c][4], cnt, caps[c], recv[c], dev))
+                    out.append(self._a2a_regions(parts[c][4], cnt, caps[c], recv[c], dev, rnd[c]))
                 return out
-            out = [self._a2a(sk, recv[c], cnt, dev), self._a2a(ss, recv[c], cnt, dev)]
+            out = [self._a2a(sk, recv[c], cnt, dev, rnd[c]), self._a2a(ss, recv[c], cnt, dev, rnd[c])]
             if use_h:  # an empty piece (kg > k) still takes part in every exchange
-                out.append(self._a2a(parts[c][4], recv[c], cnt, dev))
+                out.append(self._a2a(parts[c][4], recv[c], cnt, dev, rnd[c]))
             return out
 
         inflight = send(0)
@@ -321,9 +375,9 @@ class ArcRouter:
             res = eng.arc_route(rs, rk, hint=rh) if use_h else eng.arc_route(rs, rk)
             if caps[c]:
                 backs.append(self._a2a_into_regions(res, recv[c], parts[c][3], caps[c],
-                                                    parts[c][2], dev))
+                                                    parts[c][2], dev, rnd[c]))
             else:
-                backs.append(self._a2a(res, parts[c][3], recv[c], dev) + (None,))
+                backs.append(self._a2a(res, parts[c][3], recv[c], dev, rnd[c]) + (None,))
         for c in range(kg):
             back = self._land(backs[c][0], backs[c][1], parts[c][2])
             if backs[c][2] is not None:  # gloo: packed answers -> their regions
@@ -363,13 +417,14 @@ class ArcRouter:
         torch.cuda.current_stream(mat.device).synchronize()
         return host
 
-    def _a2a_views(self, outs, ins):
+    def _a2a_views(self, outs, ins, rounds: int = 1):
         """all_to_all from the views `ins` (one per destination rank) into the
-        views `outs` (one per source rank): RCCL's list all_to_all,
-        asynchronous (returns its work); gloo (tests): packed through host
-        buffers on the current stream, synchronous (returns None)."""
+        views `outs` (one per source rank): RCCL's list all_to_all in
+        `rounds` calls (_list_a2a), asynchronous (returns its work); gloo
+        (tests): packed through host buffers on the current stream,
+        synchronous (returns None)."""
         if self._comm_cuda():
-            return tdist.all_to_all(outs, ins, group=self.group, async_op=True)
+            return self._list_a2a(outs, ins, rounds)
         dev = self.comm_device
         in_splits = [int(t.shape[0]) for t in ins]
         out_splits = [int(t.shape[0]) for t in outs]
@@ -381,6 +436,19 @@ class ArcRouter:
         for t, piece in zip(outs, torch.split(got, out_splits)):
             t.copy_(piece)
         return None
+
+    def _agree(self, w0, proto: int):
+        """The protocol (bit 21 of the gathered rows' first words: 1 = the
+        exact layout) and self_exchange (bit 22) must be the same on every
+        rank.  Every rank sees the same gathered words, so a disagreement
+        raises on all of them instead of hanging the group in mismatched
+        collectives."""
+        words = {(int(w) >> 21) & 3 for w in w0}
+        if len(words) != 1:
+            raise RuntimeError("arc routing: ranks disagree on the protocol or self_exchange "
+                               f"(bits 21-22 of the gathered rows: {sorted(words)})")
+        if words.pop() != proto | (int(self.self_exchange) << 1):
+            raise RuntimeError("arc routing: gathered protocol word does not match this rank's")
 
     def route_exact(self, src, keys, owner, hops, status, k, kmax) -> int:
         """route_soa on RCCL with the exact-layout partition (module docstring).
@@ -398,8 +466,16 @@ class ArcRouter:
         own lookups skipped), started as soon as the counts exist, and each
         piece's outgoing exchange, which waits on that scatter only.  A
         one-rank group has no remote lookups: no scatter, no all_to_all, no
-        delivery.  Returns 2 (rounds of the protocol)."""
+        delivery -- unless self_exchange, which sends the rank's own lookups
+        through the collectives like everyone else's (own walk skipped).
+
+        The gathered row is 1 + kmax (G + 1) words, the length the region
+        protocol gathers: word 0 = piece count | hints << 20 | 1 << 21 (exact)
+        | self_exchange << 22, then kmax x G counts, then the kmax piece
+        lengths; every rank checks every rank's counts against its lengths and
+        the protocol bits, so a bad row raises on all ranks.  Returns 2."""
         eng, G, me = self.engine, self.world, self.rank
+        sx = bool(self.self_exchange)
         dev = keys.device
         q = int(keys.shape[0])
         cut = [c * q // k for c in range(k + 1)]
@@ -408,8 +484,19 @@ class ArcRouter:
             self._side = torch.cuda.Stream(dev)
         side = self._side
         hints = bool(self.hints and getattr(eng, "arc_hints", False))
-        row = torch.zeros(1 + kmax * G, dtype=torch.int64, device=dev)
-        row[0] = k | (int(hints) << 20)
+        LEN = 1 + kmax * G  # piece lengths start here
+        # the row's host-known words (flags, piece lengths) in one pinned copy;
+        # the landing buffer is free again: the previous call's row gather
+        # waited on this stream after its copy
+        pool = self.__dict__.setdefault("_rowh", {})
+        rowh = pool.get(LEN + kmax)
+        if rowh is None:
+            rowh = pool[LEN + kmax] = torch.empty(LEN + kmax, dtype=torch.int64, pin_memory=True)
+        rowh.zero_()
+        rowh[0] = k | (int(hints) << 20) | (1 << 21) | (int(sx) << 22)
+        for c in range(k):
+            rowh[LEN + c] = cut[c + 1] - cut[c]
+        row = rowh.to(dev, non_blocking=True)
         own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
         wsw = eng.arc_own_ws_words(max(cut[c + 1] - cut[c] for c in range(k)))
         own_ws = torch.empty(k * wsw, dtype=torch.int32, device=dev)
@@ -417,7 +504,8 @@ class ArcRouter:
             eng.arc_count_async(G, keys[cut[c]:cut[c + 1]], row[1 + c * G: 1 + (c + 1) * G], me,
                                 own_idx[cut[c]:], own_ws[c * wsw: (c + 1) * wsw])
         parts, ready = [], []
-        if G > 1:
+        scatter = G > 1 or sx
+        if scatter:
             cursors = torch.empty(k * G, dtype=torch.int32, device=dev)
             side.wait_stream(main)  # the counts (and the caller's inputs) are written
             with torch.cuda.stream(side):
@@ -425,40 +513,51 @@ class ArcRouter:
                     sl = slice(cut[c], cut[c + 1])
                     part = eng.arc_scatter_async(G, src[sl], keys[sl],
                                                  row[1 + c * G: 1 + (c + 1) * G],
-                                                 cursors[c * G: (c + 1) * G], hints=hints, skip=me)
+                                                 cursors[c * G: (c + 1) * G], hints=hints,
+                                                 skip=-1 if sx else me)
                     parts.append(part if hints else part + (None,))
                     ev = torch.cuda.Event()
                     ev.record(side)
                     ready.append(ev)
         mat = self._gather_row(row)
+        self._agree(mat[:, 0], 1)
         kg = int((mat[:, 0] & 0xFFFFF).max())  # pieces every rank runs
-        use_h = bool(int((mat[:, 0] >> 20).min()))  # every rank's pieces carry hints
-        if G > 1 and kg > k:  # this rank's extra pieces are empty
+        use_h = bool(int((mat[:, 0] >> 20).min() & 1))  # every rank's pieces carry hints
+        for r in range(G):  # every rank checks every row: a bad one raises everywhere
+            for c in range(kmax):
+                if sum(int(x) for x in mat[r, 1 + c * G: 1 + (c + 1) * G]) != int(mat[r, LEN + c]):
+                    raise RuntimeError(f"arc count pass and partition disagree (rank {r}, "
+                                       f"piece {c})")
+        if scatter and kg > k:  # this rank's extra pieces are empty
             e = (keys[:0], src[:0], torch.empty(0, dtype=torch.int32, device=dev),
                  torch.empty(0, dtype=torch.int64, device=dev))
             parts += [e] * (kg - k)
             ready += [None] * (kg - k)
         cut += [q] * (kg - k)
+
+        def crosses(r, d):  # lookups of rank r for rank d travel through the collective
+            return r != d or sx
         cnt = [[int(mat[me, 1 + c * G + d]) for d in range(G)] for c in range(kg)]
-        recv = [[int(mat[r, 1 + c * G + me]) if r != me else 0 for r in range(G)]
+        recv = [[int(mat[r, 1 + c * G + me]) if crosses(r, me) else 0 for r in range(G)]
                 for c in range(kg)]
-        for c in range(kg):
-            if sum(cnt[c]) != cut[c + 1] - cut[c]:
-                raise RuntimeError("arc count pass and partition disagree")
-        offs = []  # remote regions only (the own lookups take no slot)
+        offs = []  # travelling regions only (the own lookups take no slot)
         for c in range(kg):
             o, acc = [], 0
             for d in range(G):
                 o.append(acc)
-                acc += cnt[c][d] if d != me else 0
+                acc += cnt[c][d] if crosses(me, d) else 0
             offs.append(o)
+        # calls per exchange of piece c: its largest travelling per-peer view on
+        # any rank, 16-B keys being the widest row (the same on every rank)
+        rnd = [self._rounds(max([int(mat[r, 1 + c * G + d]) for r in range(G) for d in range(G)
+                                 if crosses(r, d)] + [0]), 16) for c in range(kg)]
         # lookups that cross ranks anywhere (the same answer on every rank):
         # without any, no rank issues an all_to_all
-        remote = any(int(mat[r, 1 + c * G + d]) for r in range(G) for d in range(G) if r != d
-                     for c in range(kg))
+        remote = any(int(mat[r, 1 + c * G + d]) for r in range(G) for d in range(G)
+                     if crosses(r, d) for c in range(kg))
 
         def region(t, c, d):
-            return t[offs[c][d]: offs[c][d] + cnt[c][d]] if d != me else t[:0]
+            return t[offs[c][d]: offs[c][d] + cnt[c][d]] if crosses(me, d) else t[:0]
 
         def send(c):
             """Issued on the side stream: waits for piece c's scatter only.
@@ -471,7 +570,7 @@ class ArcRouter:
                     o = torch.empty((sum(recv[c]),) + tuple(t.shape[1:]), dtype=t.dtype,
                                     device=dev)
                     w = self._a2a_views(list(torch.split(o, recv[c])),
-                                        [region(t, c, d) for d in range(G)])
+                                        [region(t, c, d) for d in range(G)], rnd[c])
                     out.append((o, w))
                 ev = torch.cuda.Event()
                 ev.record(side)
@@ -481,7 +580,7 @@ class ArcRouter:
         # this rank's own lookups, every piece at once: walked in place, outputs
         # written (the count pass left each piece's indices piece-relative at
         # own_idx[cut[c]:])
-        n_own = [cnt[c][me] for c in range(kg)]
+        n_own = [0 if sx else cnt[c][me] for c in range(kg)]
         if sum(n_own):
             if sum(1 for x in n_own if x) == 1:
                 c = next(c for c in range(kg) if n_own[c])
@@ -503,7 +602,6 @@ class ArcRouter:
             got = inflight
             if remote and c + 1 < kg:
                 inflight = send(c + 1)
-            sl = slice(cut[c], cut[c + 1])
             back, work = None, None
             if remote:
                 n_rem = sum(cnt[c]) - n_own[c]
@@ -523,10 +621,10 @@ class ArcRouter:
                 rh = arrived[2][0] if use_h else None
                 res = eng.arc_route(rs_, rk, hint=rh) if use_h else eng.arc_route(rs_, rk)
                 work = self._a2a_views([region(back, c, d) for d in range(G)],
-                                       list(torch.split(res, recv[c])))
+                                       list(torch.split(res, recv[c])), rnd[c])
                 self.records_sent += n_rem
             backs.append((back, work))
-        if G > 1:
+        if scatter:
             for c in range(kg):
                 back, work = backs[c]
                 if ready[c] is not None:
@@ -558,34 +656,43 @@ class ArcRouter:
             # ring holding the same IDs)
             owner.copy_(eng.successor(keys).to(owner.dtype))
             return 0
-        q = int(keys.shape[0])
-        # bounded collectives, as nsucc (one piece on a one-rank group)
-        k = self._pieces_all(q, 1 << 22, keys) if self.world > 1 else 1
-        cut = [c * q // k for c in range(k + 1)]
-        for c in range(k):
-            self._succ_piece(keys[cut[c]:cut[c + 1]], owner[cut[c]:cut[c + 1]])
+        # one piece: the collectives cut themselves into calls of <= view_cap
+        # bytes per view (_rounds)
+        self._succ_piece(keys, owner, self._exact_piece(keys))
         return 2
 
-    def _succ_piece(self, keys, owner):
-        if hasattr(self.engine, "arc_count_async") and keys.is_cuda:
+    def _exact_piece(self, keys) -> bool:
+        """The exact-layout piece protocol (device engine, device keys);
+        self_exchange needs it."""
+        exact = hasattr(self.engine, "arc_count_async") and keys.is_cuda
+        if self.self_exchange and not exact:
+            raise ValueError("self_exchange needs the exact protocol (a device engine)")
+        return exact
+
+    def _succ_piece(self, keys, owner, exact):
+        if exact:
             return self._succ_piece_exact(keys, owner)
         eng, G = self.engine, self.world
         zero = self._zeros_src(keys)
         sk, _, perm, counts = eng.arc_partition(G, zero, keys)[:4]
         dev = self.comm_device if self.comm_device is not None else sk.device
-        mine = torch.tensor(list(counts), dtype=torch.int64, device=dev)
-        mat = torch.empty((G, G), dtype=torch.int64, device=dev)
+        # the counts and, last, the protocol word (bits 21-22, _agree)
+        mine = torch.tensor(list(counts) + [int(self.self_exchange) << 22], dtype=torch.int64,
+                            device=dev)
+        mat = torch.empty((G, G + 1), dtype=torch.int64, device=dev)
         tdist.all_gather_into_tensor(mat.view(-1), mine, group=self.group)
         m = mat.cpu() if mat.is_cuda else mat
+        self._agree(m[:, G], 0)
         recv = [int(m[r, self.rank]) for r in range(G)]
-        rk, work = self._a2a(sk, recv, list(counts), dev)
+        nr = self._rounds(max(int(x) for x in m[:, :G].flatten()), 16)
+        rk, work = self._a2a(sk, recv, list(counts), dev, nr)
         rk = self._land(rk, work, sk)
         if rk.shape[0]:
             got = self._arc_ring().successor(rk)  # index in this rank's arc
             got = (got.to(torch.int64) + self.lo).to(torch.int32)
         else:  # nothing for this arc (or an empty arc: n < world)
             got = torch.empty(0, dtype=torch.int32, device=rk.device)
-        back, work = self._a2a(got, list(counts), recv, dev)
+        back, work = self._a2a(got, list(counts), recv, dev, nr)
         back = self._land(back, work, perm)
         owner.copy_(back.to(owner.device)[perm.long()].to(owner.dtype))
         self.records_sent += int(sum(counts))
@@ -598,12 +705,9 @@ class ArcRouter:
         eng, G, me = self.engine, self.world, self.rank
         q = int(keys.shape[0])
         dev = keys.device
-        row = torch.zeros(G, dtype=torch.int64, device=dev)
-        own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
-        ws = torch.empty(eng.arc_own_ws_words(q), dtype=torch.int32, device=dev)
-        eng.arc_count_async(G, keys, row, me, own_idx, ws)
-        mat = self._gather_row(row)
-        c_me = int(mat[me, me])
+        mat, row, own_idx = self._count_gather(keys)
+        sx = bool(self.self_exchange)
+        c_me = 0 if sx else int(mat[me, me])
 
         def search(k):  # global owner indices of keys owned in this arc
             return (self._arc_ring().successor(k).to(torch.int64) + self.lo).to(torch.int32)
@@ -612,18 +716,20 @@ class ArcRouter:
         elif c_me:
             oi = own_idx[:c_me].long()
             owner[oi] = search(keys[oi]).to(owner.dtype)
-        remote = any(int(mat[r, d]) for r in range(G) for d in range(G) if r != d)
+        remote = any(int(mat[r, d]) for r in range(G) for d in range(G) if r != d or sx)
         if not remote:
             return
-        send = [int(mat[me, d]) if d != me else 0 for d in range(G)]
-        recv = [int(mat[r, me]) if r != me else 0 for r in range(G)]
+        send = [int(mat[me, d]) if d != me or sx else 0 for d in range(G)]
+        recv = [int(mat[r, me]) if r != me or sx else 0 for r in range(G)]
+        nr = self._rounds(self._max_crossing(mat, sx), 16)
         cursor = torch.empty(G, dtype=torch.int32, device=dev)
-        sk, _, perm = eng.arc_scatter_async(G, self._zeros_src(keys), keys, row, cursor, skip=me)
+        sk, _, perm = eng.arc_scatter_async(G, self._zeros_src(keys), keys, row, cursor,
+                                            skip=-1 if sx else me)
         cdev = self.comm_device if self.comm_device is not None else dev
-        rk, work = self._a2a(sk[:sum(send)], recv, send, cdev)
+        rk, work = self._a2a(sk[:sum(send)], recv, send, cdev, nr)
         rk = self._land(rk, work, sk)
         got = search(rk) if rk.shape[0] else torch.empty(0, dtype=torch.int32, device=dev)
-        back, work = self._a2a(got, send, recv, cdev)
+        back, work = self._a2a(got, send, recv, cdev, nr)
         back = self._land(back, work, perm).to(owner.device)
         pm = perm.long()
         sel = pm >= 0
@@ -670,27 +776,35 @@ class ArcRouter:
             lists.copy_(lo_.to(lists.dtype))
             count.copy_(co_.to(count.dtype))
             return 0
-        # pieces of <= 2^22 keys (60 B per key come back: one collective of a
-        # 2^25-key batch would pass 2^31 bytes, which RCCL's all_to_all does
-        # not carry whole); every rank runs the largest rank's piece count
-        q = int(keys.shape[0])
-        k = self._pieces_all(q, 1 << 22, keys) if G > 1 else 1
-        if k > 1:
-            cut = [c * q // k for c in range(k + 1)]
-            for c in range(k):
-                sl = slice(cut[c], cut[c + 1])
-                self._nsucc_piece(keys[sl], n_list, lists[sl], count[sl])
-            return 2
+        # one piece: the collectives cut themselves into calls of <= view_cap
+        # bytes per view (_rounds; the 60-B rows back of a 2^25-key batch are
+        # 2,013,265,920 B, which one RCCL call delivers only half of)
+        if not self._exact_piece(keys):
+            raise ValueError("ArcRouter.nsucc needs a device engine and device keys")
         self._nsucc_piece(keys, n_list, lists, count)
         return 2
 
-    def _pieces_all(self, q: int, per: int, like) -> int:
-        """max over ranks of ceil(q / per) (one all_reduce on the comm device,
-        else on `like`'s device)."""
-        dev = self.comm_device if self.comm_device is not None else like.device
-        t = torch.tensor([max(1, -(-q // per))], dtype=torch.int64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=self.group)
-        return int(t.item())
+    def _count_gather(self, keys):
+        """The exact layout's count pass and its one all_gather: (gathered
+        (G, G + 1) host matrix -- counts, then the protocol word --, the
+        device counts row, own_idx).  Every rank checks the protocol words."""
+        eng, G, me = self.engine, self.world, self.rank
+        q = int(keys.shape[0])
+        dev = keys.device
+        row = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+        row[G] = (1 | (int(self.self_exchange) << 1)) << 21
+        own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(eng.arc_own_ws_words(q), dtype=torch.int32, device=dev)
+        eng.arc_count_async(G, keys, row[:G], me, own_idx, ws)
+        mat = self._gather_row(row)  # mat[r, d] = rank r's keys for rank d
+        self._agree(mat[:, G], 1)
+        return mat, row[:G], own_idx
+
+    @staticmethod
+    def _max_crossing(mat, sx):
+        """Largest count any rank sends any rank through the collectives."""
+        G = mat.shape[0]
+        return max([int(mat[r, d]) for r in range(G) for d in range(G) if r != d or sx] + [0])
 
     def _windows(self, k, n_list, out=None):
         """The n-windows of keys k (owners in this rank's arc) as global peer
@@ -716,12 +830,9 @@ class ArcRouter:
         eng, G, me = self.engine, self.world, self.rank
         q = int(keys.shape[0])
         dev = keys.device
-        row = torch.zeros(G, dtype=torch.int64, device=dev)
-        own_idx = torch.empty(max(q, 1), dtype=torch.int32, device=dev)
-        ws = torch.empty(eng.arc_own_ws_words(q), dtype=torch.int32, device=dev)
-        eng.arc_count_async(G, keys, row, me, own_idx, ws)
-        mat = self._gather_row(row)  # (G, G): mat[r, d] = rank r's lookups for rank d
-        c_me = int(mat[me, me])
+        mat, row, own_idx = self._count_gather(keys)
+        sx = bool(self.self_exchange)
+        c_me = 0 if sx else int(mat[me, me])
         direct = (lists.dtype == torch.int32 and count.dtype == torch.uint8 and lists.is_cuda
                   and lists.is_contiguous() and count.is_contiguous())
         if c_me == q and q and direct:  # every lookup is this rank's: straight into the outputs
@@ -735,19 +846,21 @@ class ArcRouter:
             wl, wc = self._windows(keys[oi], n_list)
             lists[oi] = wl.to(lists.dtype)
             count[oi] = wc.to(count.dtype)
-        remote = any(int(mat[r, d]) for r in range(G) for d in range(G) if r != d)
+        remote = any(int(mat[r, d]) for r in range(G) for d in range(G) if r != d or sx)
         if not remote:  # every rank sees the same matrix: all exchange or none do
             return
-        send = [int(mat[me, d]) if d != me else 0 for d in range(G)]
-        recv = [int(mat[r, me]) if r != me else 0 for r in range(G)]
+        send = [int(mat[me, d]) if d != me or sx else 0 for d in range(G)]
+        recv = [int(mat[r, me]) if r != me or sx else 0 for r in range(G)]
+        nr = self._rounds(self._max_crossing(mat, sx), max(16, 4 * (n_list + 1)))
         cursor = torch.empty(G, dtype=torch.int32, device=dev)
-        sk, _, perm = eng.arc_scatter_async(G, self._zeros_src(keys), keys, row, cursor, skip=me)
+        sk, _, perm = eng.arc_scatter_async(G, self._zeros_src(keys), keys, row, cursor,
+                                            skip=-1 if sx else me)
         cdev = self.comm_device if self.comm_device is not None else dev
-        rk, work = self._a2a(sk[:sum(send)], recv, send, cdev)
+        rk, work = self._a2a(sk[:sum(send)], recv, send, cdev, nr)
         rk = self._land(rk, work, sk)
         gl, gc = self._windows(rk, n_list)
         got = torch.cat([gl, gc.to(torch.int32).view(-1, 1)], dim=1)  # one exchange
-        back, work = self._a2a(got.contiguous(), send, recv, cdev)
+        back, work = self._a2a(got.contiguous(), send, recv, cdev, nr)
         back = self._land(back, work, perm).to(lists.device)
         pm = perm.long()
         sel = pm >= 0

@@ -738,6 +738,98 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
     assert succ_ok == (True, 2, 0, True)  # one rank: every key is its own, none sent
 
 
+# ---------------------------------------------------------------------------
+# Round 6: the single-piece 2^25-key placement exchange on
+# a one-rank RCCL group.  Measured cause of the round-5 "half empty" return
+# (tools/diag_rccl_a2a.py, profiles/r06/rccl_a2a/): RCCL 2.26.6 delivers only
+# the first half of a send/recv view of 2,013,265,920 B or more (1 GiB arrives
+# whole), with the work reporting success.  ArcRouter now issues every
+# exchange as calls of <= VIEW_CAP bytes per view (_rounds / _list_a2a), cut the
+# same way on every rank from the gathered counts.  self_exchange sends the
+# rank's own keys through RCCL, so this one-GPU test runs the exchange at the
+# failing size: 60-B rows back for 2^25 keys in one piece.
+# ---------------------------------------------------------------------------
+def _rccl_selfx_worker(_i, n, q, out):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "p2p-dhts_amd")]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    import torch
+    import torch.distributed as tdist
+    import chordx
+    from chordx import dist
+    from chordx.arc import ArcRouter, VIEW_CAP
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    assert dist.init_single("nccl", dev)
+    ids = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(ids, 0xA7F0)
+    ring = chordx.Ring(ids)
+    ring.build_fingers()
+    router = ArcRouter(ring, ring.n, 0, 1, exchange_always=True)
+    router.self_exchange = True
+    keys = torch.empty((q, 2), dtype=torch.int64, device=dev)
+    chordx.fill_splitmix(keys, 0xA7F1)
+    res = {}
+    # placement lists: one piece, 60 B per key back = 2,013,265,920 B at 2^25
+    lists = torch.full((q, 14), -1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(q, dtype=torch.uint8, device=dev)
+    router.records_sent = 0
+    nr = router.nsucc(keys, 14, lists, cnt)
+    wl, wc = ring.nsucc(keys, 14)
+    res["nsucc"] = (bool(torch.equal(lists, wl.to(torch.int32))) and bool(torch.equal(cnt, wc)),
+                    nr, router.records_sent, router._rounds(q, 60))
+    del lists, cnt, wl, wc
+    # exact successors and routes through the same self-exchange
+    own = torch.full((q,), -3, dtype=torch.int32, device=dev)
+    router.records_sent = 0
+    router.successor(keys, own)
+    res["successor"] = (bool(torch.equal(own, ring.successor(keys))), router.records_sent)
+    del own
+    src = ((torch.arange(q, device=dev) * 7) % ring.n).to(torch.int32)
+    ow, hp, st = ring.route(src, keys)
+    for chunks in (1, 3):
+        router.chunks = chunks
+        owner = torch.full((q,), -5, dtype=torch.int32, device=dev)
+        hops = torch.zeros(q, dtype=torch.uint8, device=dev)
+        status = torch.full((q,), 9, dtype=torch.uint8, device=dev)
+        router.records_sent = 0
+        router.route(src, keys, owner, hops, status)
+        torch.cuda.synchronize()
+        res[f"route{chunks}"] = (bool(torch.equal(ow, owner)) and bool(torch.equal(hp, hops))
+                                 and bool(torch.equal(st, status)), router.records_sent)
+    # the split exchange itself above the cap: a buffer of 2^31 + 8 MiB, 4-B rows
+    m = ((1 << 31) + (8 << 20)) // 4
+    t = (torch.arange(m, dtype=torch.int64, device=dev) * 2654435761 % 2147483629).to(torch.int32)
+    r = router._rounds(m, 4)
+    got, work = router._a2a(t, [m], [m], dev, r)
+    work.wait()
+    res["a2a_2g"] = (bool(torch.equal(got, t)), r, VIEW_CAP)
+    out[0] = res
+    tdist.destroy_process_group()
+
+
+def test_arc_rccl_self_exchange_full_size(cx):
+    """One piece of 2^25 keys through RCCL on a one-rank group (self_exchange):
+    placement lists, exact successors and routes (1 and 3 pieces) equal the
+    replicated ring's, and a 2^31 + 8 MiB exchange arrives whole."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    q = 1 << 25
+    mp.start_processes(_rccl_selfx_worker, args=(1 << 20, q, out), nprocs=1, join=True,
+                       start_method="spawn")
+    res = out[0]
+    ok, nr, sent, rounds = res["nsucc"]
+    assert ok and nr == 2 and sent == q and rounds >= 2, res["nsucc"]
+    assert res["successor"] == (True, q)
+    assert res["route1"] == (True, q) and res["route3"] == (True, q)
+    got_ok, r, cap = res["a2a_2g"]
+    assert got_ok and r == -(-((1 << 31) + (8 << 20)) // cap)
+
+
 @pytest.mark.parametrize("G", [2, 8])
 def test_arc_exact_successor_simulated_ranks(cx, O, G):
     """Exact-successor mode, G ranks simulated on one GPU: every rank's region
