@@ -257,7 +257,44 @@ def setup_ring(args, world, rank, dev, backend):
     t0 = time.perf_counter()
     ring = chordx.Ring(ids, device=dev.index or 0)
     torch.cuda.synchronize(dev)
-    return ring, t_gather, time.perf_counter() - t0
+    t_ring = time.perf_counter() - t0
+    setup_ring.sort_roofline = sort_roofline(ids)
+    return ring, t_gather, t_ring
+
+
+# Ring sort byte models per key (16-B ID + 4-B index tag).  LSD, per pass:
+# histogram 16 + scatter 20 in / 20 out = 56.  MSD (round 6) at 2^24 keys:
+# two such passes over the top bytes, the bucket bounds (the high word, 8) and
+# the LDS bucket sort (20 in / 20 out): 2 x 56 + 8 + 40 = 160.
+SORT_LSD_PASS_BYTES = 56
+SORT_MSD_BYTES = 2 * SORT_LSD_PASS_BYTES + 8 + 40
+
+
+def sort_roofline(ids):
+    """cx_ring_create's (ID, index) sort of the bench's unsorted ring IDs, both
+    variants timed with HIP events (chordx.ring.sort_time), against HBM."""
+    from chordx.ring import sort_time
+    n = ids.shape[0]
+    out = {}
+    for name, v, by in (("msd_buckets", 0, SORT_MSD_BYTES), ("lsd_16_pass", 1, 16 * SORT_LSD_PASS_BYTES)):
+        ms = []
+        ok = True
+        for _ in range(3):
+            t, good = sort_time(ids, v)
+            ms.append(t)
+            ok = ok and good
+        t = sorted(ms)[1]
+        out[name] = {"ms": t, "bytes": by * n, "GBps": by * n / (t * 1e-3) / 1e9,
+                     "frac": by * n / (t * 1e-3) / HBM_PEAK, "sorted": ok,
+                     "passes": 4 if v == 0 else 16}
+    out["keys"] = n
+    out["speedup"] = out["lsd_16_pass"]["ms"] / out["msd_buckets"]["ms"]
+    out["note"] = ("ms = the sort alone (HIP events, median of 3); bytes: MSD 160 B per key "
+                   "(two top-byte passes of 56, bucket bounds 8, LDS bucket sort 40), LSD 56 B "
+                   "per key per pass x 16; "
+                   "the default is MSD with the LSD sort (4 tag + 16 key passes) as the "
+                   "fallback for a bucket above 2048 keys")
+    return out
 
 
 def time_steps(fn, steps, world, dev):
@@ -304,6 +341,30 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
         and int((status != 0).sum().item()) == 0
     same = dist.all_over_ranks(same, world, dev)
     total = world * Q * args.steps
+    # exchange self-test: the same protocol with every rank's own lookups sent
+    # through the collectives too (self_exchange), so every lookup crosses
+    # RCCL -- at N = 1 the exchange a one-GPU run can time and check
+    router.self_exchange = True
+    for t in (owner, hops, status):
+        t.fill_(0xEE)
+    router.route(src, keys, owner, hops, status)
+    torch.cuda.synchronize(dev)
+    router.records_sent = 0
+    _, dt_x = time_steps(lambda: router.route(src, keys, owner, hops, status), args.steps,
+                         world, dev)
+    sent_x = dist.sum_over_ranks(router.records_sent, world, dev)
+    same_x = dist.all_over_ranks(
+        bool((owner == owner_ref).all().item()) and bool((hops == hops_ref).all().item())
+        and int((status != 0).sum().item()) == 0, world, dev)
+    router.self_exchange = False
+    selftest = {"value": total / dt_x, "unit": "lookups/s", "ms_per_step": dt_x * 1e3 / args.steps,
+                "records_exchanged_per_lookup": sent_x / total, "equals_replicated_route": same_x,
+                "bytes_exchanged_per_lookup": 28 + 8,
+                "layout": "ArcRouter.route with self_exchange: the exact-layout scatter of EVERY "
+                          "lookup (the rank's own included) on the side stream, keys + sources + "
+                          "hints (28 B) out and packed answers (8 B) back through RCCL list "
+                          "all_to_alls in calls of <= 1 GiB per view, walked on arrival, "
+                          "delivered through perm"}
     # DHash placement lists (n = 14) in the same layout (keys to
     # their owner's arc, windows read there from the arc + a 13-peer halo,
     # lists back): the same keys, K steps, equal to the replicated cx_nsucc
@@ -347,6 +408,7 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
             "equals_replicated_route": same,
             "dhash_placement": placement,
             "exact_successor": exact_succ,
+            "exchange_selftest": selftest,
             "top_levels_replicated": top, "local_rows": rows,
             "route_plane_bytes_per_gpu": plane_bytes, "build_s": t_build,
             "layout": f"ring IDs all-gathered; arc-sharded route planes x{world} (top {top} "
@@ -380,7 +442,7 @@ def _route_rounds(rings, keys, srcs, dev, rounds=6, per=3):
     return {d: sorted(v)[len(v) // 2] for d, v in ms.items()}
 
 
-def overlap_leg(serve, joins, leaves, keys, src, dev, builds=3, q_serve=1 << 23):
+def overlap_leg(serve, joins, leaves, keys, src, dev, builds=3, q_serve=1 << 23, priority=0):
     """Lookups keep running while the next membership epoch's ring builds
     (double-buffered route tables).  `serve` is epoch e's
     route-ready ring; a serving thread routes batches of q_serve of the bench's
@@ -407,7 +469,9 @@ def overlap_leg(serve, joins, leaves, keys, src, dev, builds=3, q_serve=1 << 23)
     lock = threading.Lock()
     stop = threading.Event()
     done = []  # host time at which each launch was seen complete
-    stream = torch.cuda.Stream(device=dev)
+    # priority < 0: the serving stream is a high-priority HIP stream (its
+    # launches' workgroups dispatch ahead of the rebuild's)
+    stream = torch.cuda.Stream(device=dev, priority=priority)
     err = []
 
     def serving():
@@ -466,7 +530,8 @@ def overlap_leg(serve, joins, leaves, keys, src, dev, builds=3, q_serve=1 << 23)
     alone = rate(a0, a1)
     same = not err and all(bool(torch.equal(a, b)) for o in outs for a, b in zip(o, ref))
     during = sorted(r["serving_lookups_per_s"] for r in recs)[len(recs) // 2]
-    return {"serving_lookups_per_s_alone": alone,
+    return {"serving_stream_priority": priority,
+            "serving_lookups_per_s_alone": alone,
             "serving_lookups_per_s_during_rebuild": during,
             "serving_during_vs_alone": during / alone if alone else None,
             "rebuild_ms_under_load": sorted(r["route_ready_ms"] for r in recs)[len(recs) // 2],
@@ -551,6 +616,9 @@ def churn_leg(ring, keys, src, dev, depth_ab=28):
     del k2, s2, o, h, st
     # epoch e (a1) keeps serving while epoch e + 1 builds
     out["overlapped"] = overlap_leg(a1, joins, leaves, keys, src, dev)
+    # the same with the serving stream at high priority
+    out["overlapped"]["high_priority_serving"] = overlap_leg(a1, joins, leaves, keys, src, dev,
+                                                             builds=2, priority=-1)
     out["route_ready_ms"] = {"cold": out["cold"]["route_ready_ms"],
                              "warm": out["warm"]["route_ready_ms"]}
     r_def = out["warm"]["route_levels"]
@@ -770,6 +838,9 @@ def c5_leg(args, world, rank, dev, backend):
         "churn_equals_oracle": churn_ok,
         "parity_on_sample": parity, "oracle_sample_keys": m, "oracle_s": t_or,
         "cpu_baseline": cpu,
+        "box_spread_record": "profiles/r06/c5_r4r5/README.md: round-4 and round-5 code in ABBA "
+                             "order on one lease, directory load factor 1/2 and 1/4 on each "
+                             "(3.29-3.30 ms at 1/4 for both, 3.44-3.45 ms at 1/2 for both)",
         "note": "both rings whole on every rank (IDs all-gathered, the same churn everywhere); "
                 "no collective in the step; oracle: oracle/chord_oracle.c or_churn + "
                 "or_misplaced (dhash_peer.cpp:298-348)"}
@@ -1294,6 +1365,7 @@ def main():
                                  "note": "same keys and kernel, src uniform in [0, N) "
                                          "(splitmix 0x5EED000A) instead of q mod N"},
             "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring,
+                        "ring_sort_roofline": getattr(setup_ring, "sort_roofline", None),
                         "fingers_build": t_fing, "fingers_build_again": t_fing_warm,
                         "alloc": setup_alloc,
                         "note": "fingers_build = converged fingers + route table on fresh "

@@ -765,6 +765,22 @@ def uuid5_dns(names, device: int = 0) -> np.ndarray:
     return out
 
 
+def sort_time(ids, variant: int = 0):
+    """Internal A/B: (ms, sorted) of cx_ring_create's (ID, index) sort over the
+    device IDs `ids` ((n, 2) int64), variant 0 = the default (MSD buckets +
+    LDS bucket sort), 1 = the 16-pass LSD sort (cxi_sort_time)."""
+    assert _is_dev(ids) and ids.dim() == 2 and ids.shape[1] == 2
+    ids = ids.contiguous()
+    f = L.lib().cxi_sort_time
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    torch.cuda.current_stream(ids.device).synchronize()
+    ms, ok = ctypes.c_double(), ctypes.c_int()
+    L.check(f(_ptr(ids), ids.shape[0], ids.device.index or 0, int(variant), ctypes.byref(ms),
+              ctypes.byref(ok)))
+    return ms.value, bool(ok.value)
+
+
 def fill_splitmix(out, seed: int, offset: int = 0):
     """Synthetic uniform 128-bit keys written on the device into `out` ((q, 2) int64)."""
     assert _is_dev(out) and out.dim() == 2 and out.shape[1] == 2

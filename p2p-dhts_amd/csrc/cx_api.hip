@@ -200,14 +200,15 @@ hipError_t dev_malloc(T **p, size_t bytes) {
 }  // namespace
 
 // Host-memory calls (CX_MEM_HOST) stage their inputs and outputs in device
-// buffers.  A small per-thread cache keeps those buffers from call to call:
+// buffers.  A small process-wide cache keeps those buffers from call to call:
 // a small batch's call otherwise spent more time in hipMalloc / hipFree (five
 // of each for cx_route) than on the GPU.  Blocks are power-of-two sized, at
 // most STAGE_MAX each (bigger staging is a plain hipMalloc, amortized by the
-// batch), at most STAGE_HELD held per thread; a block returns to the cache only
-// after the stream that used it has drained.  A thread's blocks are left to
-// process exit (the HIP runtime may already be gone when thread-local
-// destructors run).
+// batch), at most STAGE_HELD idle in the whole process (any number of calling
+// threads: the cache is shared behind a mutex); a block returns to the cache
+// only after the stream that used it has drained.  cx_pool_trim frees the idle
+// blocks; the rest are left to process exit (the HIP runtime may already be
+// gone when static destructors run).
 constexpr size_t STAGE_MAX = (size_t)16 << 20;
 constexpr size_t STAGE_HELD = (size_t)64 << 20;
 struct StageBlk {
@@ -215,8 +216,22 @@ struct StageBlk {
     size_t cap;
     int dev;
 };
-thread_local std::vector<StageBlk> *t_stage = nullptr;
-thread_local size_t t_stage_held = 0;
+std::mutex g_stage_mu;
+std::vector<StageBlk> *g_stage = new std::vector<StageBlk>();  // never destroyed
+size_t g_stage_held = 0;
+
+void stage_trim() {
+    std::lock_guard<std::mutex> g(g_stage_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (const StageBlk &b : *g_stage) {
+        (void)hipSetDevice(b.dev);
+        (void)hipFree(b.p);
+    }
+    (void)hipSetDevice(cur);
+    g_stage->clear();
+    g_stage_held = 0;
+}
 
 struct DBuf {
     void *p = nullptr;
@@ -229,13 +244,16 @@ struct DBuf {
         if (!p) return;
         if (staged) {
             (void)hipStreamSynchronize(user);
-            if (!t_stage) t_stage = new std::vector<StageBlk>();
-            if (t_stage_held + staged <= STAGE_HELD) {
-                t_stage->push_back(StageBlk{p, staged, dev});
-                t_stage_held += staged;
-            } else {
-                (void)hipFree(p);
+            bool kept = false;
+            {
+                std::lock_guard<std::mutex> g(g_stage_mu);
+                if (g_stage_held + staged <= STAGE_HELD) {
+                    g_stage->push_back(StageBlk{p, staged, dev});
+                    g_stage_held += staged;
+                    kept = true;
+                }
             }
+            if (!kept) (void)hipFree(p);
             p = nullptr;
             staged = 0;
             user = nullptr;
@@ -269,18 +287,18 @@ struct DBuf {
         (void)hipGetDevice(&d);
         size_t cap = 4096;
         while (cap < bytes) cap <<= 1;
-        if (t_stage) {  // the smallest cached block of this device that fits
-            size_t best = t_stage->size();
-            for (size_t k = 0; k < t_stage->size(); ++k) {
-                const StageBlk &b = (*t_stage)[k];
-                if (b.dev == d && b.cap >= bytes && (best == t_stage->size() || b.cap < (*t_stage)[best].cap))
+        {  // the smallest cached block of this device that fits
+            std::lock_guard<std::mutex> g(g_stage_mu);
+            std::vector<StageBlk> &c = *g_stage;
+            size_t best = c.size();
+            for (size_t k = 0; k < c.size(); ++k)
+                if (c[k].dev == d && c[k].cap >= bytes && (best == c.size() || c[k].cap < c[best].cap))
                     best = k;
-            }
-            if (best < t_stage->size()) {
-                p = (*t_stage)[best].p;
-                cap = (*t_stage)[best].cap;
-                t_stage->erase(t_stage->begin() + best);
-                t_stage_held -= cap;
+            if (best < c.size()) {
+                p = c[best].p;
+                cap = c[best].cap;
+                c.erase(c.begin() + best);
+                g_stage_held -= cap;
                 staged = cap;
                 dev = d;
                 user = stream;
@@ -2557,6 +2575,56 @@ int cxi_gather_probe_span(const cx_ring *ring, int lanes, int hops, uint64_t spa
     return CX_OK;
 }
 
+// Ring-sort timing (A/B, bench setup_s.ring_sort_roofline): the (ID, index)
+// sort of cx_ring_create over n device IDs, on a private stream with HIP
+// events around the sort alone.  variant 0 = radix_sort (MSD buckets, the
+// default), 1 = the 16-pass LSD sort.  *ms = the sort's time; *sorted = 1 if
+// the output is ascending by (key, tag) (checked on the device afterwards:
+// the MSD path's (key, tag) order).
+int cxi_sort_time(const cx_u128 *ids, size_t n, int device, int variant, double *ms, int *sorted) {
+    CX_CHECK(ids && ms && sorted && n >= 1 && n < ((size_t)1 << 31), CX_E_INVALID, "bad argument");
+    CX_CHECK(variant == 0 || variant == 1, CX_E_INVALID, "variant must be 0 or 1");
+    CX_HIP(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    CX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = [&]() -> int {
+        DBuf k0, k1, t0, t1, ws, flag;
+        CX_HIP(k0.alloc_pooled(n * sizeof(cell128), s));
+        CX_HIP(k1.alloc_pooled(n * sizeof(cell128), s));
+        CX_HIP(t0.alloc_pooled(n * sizeof(uint32_t), s));
+        CX_HIP(t1.alloc_pooled(n * sizeof(uint32_t), s));
+        CX_HIP(ws.alloc_pooled(cxk::sort_workspace_words(n) * sizeof(uint32_t), s));
+        CX_HIP(flag.alloc(sizeof(uint32_t)));
+        CX_HIP(hipMemcpyAsync(k0.p, ids, n * sizeof(cell128), hipMemcpyDeviceToDevice, s));
+        CX_HIP(cxk::iota(t0.as<uint32_t>(), n, 0, s));
+        CX_HIP(hipEventCreate(&e0));
+        CX_HIP(hipEventCreate(&e1));
+        CX_HIP(hipEventRecord(e0, s));
+        if (variant == 0)
+            CX_HIP(cxk::radix_sort(k0.as<cell128>(), t0.as<uint32_t>(), k1.as<cell128>(),
+                                   t1.as<uint32_t>(), n, ws.as<uint32_t>(), s));
+        else
+            CX_HIP(cxk::radix_sort_lsd(k0.as<cell128>(), t0.as<uint32_t>(), k1.as<cell128>(),
+                                       t1.as<uint32_t>(), n, ws.as<uint32_t>(), s));
+        CX_HIP(hipEventRecord(e1, s));
+        CX_HIP(cxk::check_sorted(k0.as<cell128>(), t0.as<uint32_t>(), n, flag.as<uint32_t>(), s));
+        uint32_t bad = 1;
+        CX_HIP(hipMemcpyAsync(&bad, flag.p, sizeof(bad), hipMemcpyDeviceToHost, s));
+        CX_HIP(hipStreamSynchronize(s));
+        float t = 0.f;
+        CX_HIP(hipEventElapsedTime(&t, e0, e1));
+        *ms = t;
+        *sorted = bad == 0;
+        return CX_OK;
+    }();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
 // Hash of the route table the ring built (the pattern-keyed window table, or
 // the arc planes when arc mode is on): A/B identity of two builds.
 int cxi_route_table_hash(const cx_ring *ring, int arc, uint64_t *out) {
@@ -2621,8 +2689,11 @@ int cxi_fingers_repair_info(const cx_ring *ring, int *repaired, uint64_t *search
 
 // Releases every pooled table (all devices).
 int cx_pool_trim(void) {
-    std::lock_guard<std::mutex> g(g_pool_mu);
-    pool_trim_locked(-1);
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        pool_trim_locked(-1);
+    }
+    stage_trim();  // the idle staging blocks of host-memory calls too
     return CX_OK;
 }
 int cxi_pool_trim(void) { return cx_pool_trim(); }

@@ -49,6 +49,51 @@ __device__ __forceinline__ void st128(cell128 *p, u128 x) {
     *reinterpret_cast<uint4 *>(p) = v;
 }
 
+// Variable shifts of 128-bit ring values, spelled in 64-bit halves.  Round 6
+// (profiles/r06/u128/): the compiled level-plane route-table
+// build with the round-5 gap code -- a u128 `>> gs` in a lane-divergent
+// branch -- wrote nondeterministic words, only in lanes 48-63 of a wave and
+// only in its slot-8 encode, with its inputs built on the host and no race
+// in the kernel; the same encode in the row-major build, standalone, and the
+// i128 shift itself (every amount, VGPR / SGPR amounts, divergent) were
+// exact.  Instruction padding cut the rate 8x without removing it.  No device
+// code shifts a u128 by a variable amount any more; these helpers take every
+// such shift (amounts in [0, 128); a uniform amount keeps them scalar).
+__host__ __device__ __forceinline__ u128 make128(uint64_t hi, uint64_t lo) {
+    return ((u128)hi << 64) | lo;
+}
+__host__ __device__ __forceinline__ uint64_t hi64(u128 v) { return (uint64_t)(v >> 64); }
+__host__ __device__ __forceinline__ uint64_t lo64(u128 v) { return (uint64_t)v; }
+// 2^s
+__host__ __device__ __forceinline__ u128 pow2_128(int s) {
+    const uint64_t b = 1ull << (s & 63);
+    return s < 64 ? make128(0, b) : make128(b, 0);
+}
+// v >> s
+__host__ __device__ __forceinline__ u128 shr128(u128 v, int s) {
+    const uint64_t hi = hi64(v), lo = lo64(v);
+    if (s == 0) return v;
+    if (s < 64) return make128(hi >> s, (lo >> s) | (hi << (64 - s)));
+    return make128(0, hi >> (s - 64));
+}
+// v << s
+__host__ __device__ __forceinline__ u128 shl128(u128 v, int s) {
+    const uint64_t hi = hi64(v), lo = lo64(v);
+    if (s == 0) return v;
+    if (s < 64) return make128((hi << s) | (lo >> (64 - s)), lo << s);
+    return make128(lo << (s - 64), 0);
+}
+// the 64 bits of v from bit s up: (uint64_t)(v >> s)
+__host__ __device__ __forceinline__ uint64_t bits64(u128 v, int s) { return lo64(shr128(v, s)); }
+// the top k bits, v >> (128 - k), for 0 <= k <= 64 (directory buckets)
+__host__ __device__ __forceinline__ uint64_t top_bits(u128 v, int k) {
+    return k >= 64 ? hi64(v) : (k <= 0 ? 0 : hi64(v) >> (64 - k));
+}
+// (uint64_t)(v >> (64 - k)) for 0 <= k <= 63: ID bits [64 - k, 128 - k)
+__host__ __device__ __forceinline__ uint64_t mid_bits(u128 v, int k) {
+    return k == 0 ? lo64(v) : (hi64(v) << k) | (lo64(v) >> (64 - k));
+}
+
 // floor(log2(d)) for d != 0: the finger index FingerTable::Lookup's first-match
 // scan selects (finger ranges [id+2^i, id+2^(i+1)-1] partition (id, id-1],
 // finger_table.h:177-188).
@@ -137,11 +182,11 @@ struct SearchView {
 // last ID).
 __device__ __forceinline__ uint32_t dir_lower_bound(const SearchView &sv, u128 x) {
     const int k = sv.k;
-    const uint4 e = sv.dir[(size_t)(uint64_t)(x >> (128 - k))];
+    const uint4 e = sv.dir[(size_t)top_bits(x, k)];
     const uint32_t lo = e.x, hi = e.y;
     if (lo == hi) return hi;
     const uint64_t frac = ((uint64_t)e.w << 32) | e.z;
-    const uint64_t xf = (uint64_t)(x >> (64 - k));  // ID bits [64-k, 128-k)
+    const uint64_t xf = mid_bits(x, k);  // ID bits [64-k, 128-k)
     if (xf < frac) return lo;
     if (xf > frac && hi - lo == 1) return hi;
     uint32_t a = (xf > frac) ? lo + 1 : lo, z = hi;
@@ -156,14 +201,14 @@ __device__ __forceinline__ uint32_t dir_lower_bound(const SearchView &sv, u128 x
 __device__ __forceinline__ uint32_t dir_successor(const SearchView &sv, u128 x) {
     const uint32_t n = sv.ev.n;
     const int k = sv.k;
-    const uint4 e = sv.dir[(size_t)(uint64_t)(x >> (128 - k))];
+    const uint4 e = sv.dir[(size_t)top_bits(x, k)];
     const uint32_t lo = e.x, hi = e.y;
     uint32_t ans;
     if (lo == hi) {
         ans = hi;
     } else {
         const uint64_t frac = ((uint64_t)e.w << 32) | e.z;
-        const uint64_t xf = (uint64_t)(x >> (64 - k));  // ID bits [64-k, 128-k)
+        const uint64_t xf = mid_bits(x, k);  // ID bits [64-k, 128-k)
         if (xf < frac) {
             ans = lo;
         } else if (xf > frac && hi - lo == 1) {

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_hist(const cell128 *keys, size_
     for (int j = 0; j < RS_ITEMS; ++j) {
         const size_t i = base + j * RS_BLOCK + threadIdx.x;
         if (i < n) {
-            const uint32_t d = (uint32_t)(ld128(keys + i) >> shift) & 0xFFu;
+            const uint32_t d = (uint32_t)bits64(ld128(keys + i), shift) & 0xFFu;
             atomicAdd(&h[d], 1u);
         }
     }
@@ -166,7 +166,8 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const cell128 *kin, con
         if (valid) {
             key = ld128(kin + i);
             tag = tin[i];
-            d = (uint32_t)(key >> shift) & 0xFFu;
+            // shift < 0: the tag's byte (-1 - shift) / 8 (the fallback's tag passes)
+            d = shift >= 0 ? (uint32_t)bits64(key, shift) & 0xFFu : (tag >> (-1 - shift)) & 0xFFu;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) wcnt[wave][lane + 64 * r] = 0;
@@ -197,31 +198,241 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_scatter(const cell128 *kin, con
     }
 }
 
-size_t sort_workspace_words(size_t n) {
-    const size_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-    return 256 * ntiles + scan_workspace_words(256 * ntiles);
+// Tag digits (the fallback's first four passes): the tag's byte `shift / 8`.
+__global__ __launch_bounds__(RS_BLOCK) void k_rs_hist_tag(const uint32_t *tags, size_t n,
+                                                          int shift, uint32_t *hist,
+                                                          uint32_t ntiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const size_t i = base + j * RS_BLOCK + threadIdx.x;
+        if (i < n) atomicAdd(&h[(tags[i] >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Sorts (keys, tags) by key, stable.  Ping-pongs between (k0,t0) and (k1,t1);
-// 16 passes leave the result in (k0, t0).
-hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
-                      uint32_t *ws, hipStream_t s) {
-    if (n <= 1) return hipSuccess;
+// ---------------------------------------------------------------------------
+// Ring sort, MSD first (round 6): the ring's IDs are hash outputs, so the top
+// kb = ceil(log2 n) - 8 bits split n keys into 2^kb buckets of ~256 keys.
+//   top passes  ceil(kb / 8) stable LSD passes over the top bytes (2 at
+//               2^24 keys): the keys grouped by bucket, in input order;
+//   bounds      each bucket's end from the sorted top bits (one pass);
+//   bucket      one block per bucket: its keys + tags in LDS, each element's
+//               rank = #elements ordered before it by (key, tag), the element
+//               written at its rank.
+// 2 + 2 passes over the keys instead of the LSD sort's 16 x (histogram +
+// scatter).  (key, tag) order is the LSD sort's stable order: every caller
+// hands in tags ascending in input order (iota, or survivors' old indices
+// then join tags).  A bucket above MS_CAP keys (clustered IDs) sets the
+// overflow word and the caller falls back to the LSD sort with the tag as
+// its lowest digits.  (A first version bucketed with one global atomic per
+// key for the count and one for the slot: 5.0 ms at 2^24 -- device-scope
+// atomics on 2^16 counters -- against 7.6 ms for the 16-pass LSD sort.)
+// ---------------------------------------------------------------------------
+constexpr uint32_t MS_CAP = 2048;
+constexpr int MS_BLOCK = 256;
+
+static int ms_bits(size_t n) {
+    int lg = 0;
+    while (((size_t)1 << lg) < n) ++lg;
+    const int kb = lg - 8;
+    return kb < 0 ? 0 : (kb > 24 ? 24 : kb);
+}
+
+__device__ __forceinline__ uint32_t ms_bucket(const cell128 *k, size_t i, int kb) {
+    return kb ? (uint32_t)(k[i].hi >> (64 - kb)) : 0u;
+}
+
+// keys grouped by bucket (ascending top kb bits): end[b] = one past bucket b's
+// last key, for every b in [0, nb) (empty buckets included).
+__global__ void k_ms_bounds(const cell128 *keys, size_t n, int kb, uint32_t nb, uint32_t *end) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t b = ms_bucket(keys, i, kb);
+        if (i == 0)
+            for (uint32_t c = 0; c < b; ++c) end[c] = 0;
+        const uint32_t nxt = i + 1 < n ? ms_bucket(keys, i + 1, kb) : nb;
+        for (uint32_t c = b; c < nxt; ++c) end[c] = (uint32_t)(i + 1);
+    }
+}
+
+
+// Block b sorts bucket b = [end[b-1], end[b]) of (kin, tin) into (kout, tout).
+// An element's rank is counted on a 32-bit prefix first -- the ID bits just
+// below the bucket's shared top kb bits, pre = bits [96 - kb, 128 - kb) --
+// in a branch-free pass over the bucket's prefixes in LDS (4 B each, eight per
+// step, every lane reading the same words: broadcasts); the few elements
+// whose prefix is not unique in the bucket (a 2^-32 event per pair on hashed
+// IDs; every pair of a clustered bucket) settle the tie by (key, tag) in a
+// second pass over the equal prefixes, reading those keys from global memory.
+// Only the prefixes live in LDS (8 KiB): 8 blocks per CU.  (Counting on the
+// full (key, tag) per element took 3.5 ms at 2^24 keys; prefixes with the
+// keys also in LDS, 3 blocks per CU, 0.94 ms.)
+__global__ __launch_bounds__(MS_BLOCK) void k_ms_bucket(const cell128 *kin, const uint32_t *tin,
+                                                        const uint32_t *end, uint32_t nb, int kb,
+                                                        cell128 *kout, uint32_t *tout,
+                                                        uint32_t *overflow) {
+    __shared__ alignas(16) uint32_t sp[MS_CAP];  // read as uint4
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t lo = b ? end[b - 1] : 0u, hi = end[b];
+        const uint32_t m = hi - lo;
+        if (m > MS_CAP) {
+            if (threadIdx.x == 0) atomicOr(overflow, 1u);
+            continue;
+        }
+        if (m <= 1) {
+            if (m == 1 && threadIdx.x == 0) {
+                st128(kout + lo, ld128(kin + lo));
+                tout[lo] = tin[lo];
+            }
+            continue;
+        }
+        for (uint32_t j = threadIdx.x; j < m; j += MS_BLOCK)
+            sp[j] = (uint32_t)bits64(ld128(kin + lo + j), 96 - kb);
+        for (uint32_t j = m + threadIdx.x; j < ((m + 7) & ~7u); j += MS_BLOCK)
+            sp[j] = 0xFFFFFFFFu;  // pad to a multiple of 8: never "less", counted as equal
+        __syncthreads();
+        const uint32_t m8 = (m + 7) & ~7u;
+        for (uint32_t j = threadIdx.x; j < m; j += MS_BLOCK) {
+            const u128 kj = ld128(kin + lo + j);
+            const uint32_t tj = tin[lo + j];
+            const uint32_t pj = sp[j];
+            uint32_t rank = 0, eq = 0;
+            for (uint32_t x = 0; x < m8; x += 8) {
+                const uint4 p = *reinterpret_cast<const uint4 *>(sp + x);
+                const uint4 r = *reinterpret_cast<const uint4 *>(sp + x + 4);
+                rank += (p.x < pj) + (p.y < pj) + (p.z < pj) + (p.w < pj) + (r.x < pj) +
+                        (r.y < pj) + (r.z < pj) + (r.w < pj);
+                eq += (p.x == pj) + (p.y == pj) + (p.z == pj) + (p.w == pj) + (r.x == pj) +
+                      (r.y == pj) + (r.z == pj) + (r.w == pj);
+            }
+            // the padding words (0xFFFFFFFF) count as equal when pj is all ones
+            if (eq > 1 + (pj == 0xFFFFFFFFu ? m8 - m : 0u)) {  // ties on the prefix: exact order
+                for (uint32_t x = 0; x < m; ++x)
+                    if (x != j && sp[x] == pj) {
+                        const u128 kx = ld128(kin + lo + x);
+                        rank += kx < kj || (kx == kj && tin[lo + x] < tj);
+                    }
+            }
+            st128(kout + lo + rank, kj);
+            tout[lo + rank] = tj;
+        }
+        __syncthreads();  // the LDS is refilled by the next bucket
+    }
+}
+
+size_t sort_workspace_words(size_t n) {
+    const size_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+    const size_t lsd = 256 * ntiles + scan_workspace_words(256 * ntiles);
+    // + the MSD path's bucket ends (after the passes' words) + its overflow word
+    return lsd + ((size_t)1 << ms_bits(n)) + 4;
+}
+
+// LSD passes over (k0, t0) <-> (k1, t1): `tag_passes` byte passes of the tag
+// first (then the order of equal keys is the tags' order, whatever the input
+// order), then the 16 key bytes; an even pass count leaves the result in
+// (k0, t0).
+static hipError_t lsd_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
+                           uint32_t *ws, int tag_passes, hipStream_t s) {
     const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
     uint32_t *hist = ws;
     uint32_t *scan_ws = ws + (size_t)256 * ntiles;
-    for (int pass = 0; pass < 16; ++pass) {
-        const int shift = 8 * pass;
+    for (int pass = 0; pass < 16 + tag_passes; ++pass) {
         cell128 *ki = (pass & 1) ? k1 : k0, *ko = (pass & 1) ? k0 : k1;
         uint32_t *ti = (pass & 1) ? t1 : t0, *to = (pass & 1) ? t0 : t1;
-        k_rs_hist<<<ntiles, RS_BLOCK, 0, s>>>(ki, n, shift, hist, ntiles);
+        const bool tagd = pass < tag_passes;
+        const int shift = tagd ? 8 * pass : 8 * (pass - tag_passes);
+        if (tagd)
+            k_rs_hist_tag<<<ntiles, RS_BLOCK, 0, s>>>(ti, n, shift, hist, ntiles);
+        else
+            k_rs_hist<<<ntiles, RS_BLOCK, 0, s>>>(ki, n, shift, hist, ntiles);
         hipError_t e = exclusive_scan(hist, (size_t)256 * ntiles, scan_ws, s);
         if (e != hipSuccess) return e;
-        k_rs_scatter<<<ntiles, RS_BLOCK, 0, s>>>(ki, ti, ko, to, n, shift, hist, ntiles);
+        k_rs_scatter<<<ntiles, RS_BLOCK, 0, s>>>(ki, ti, ko, to, n, tagd ? -1 - shift : shift,
+                                                 hist, ntiles);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t radix_sort_lsd(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
+                          uint32_t *ws, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    return lsd_sort(k0, t0, k1, t1, n, ws, 0, s);
+}
+
+// Sorts (keys, tags) by (key, tag) -- the stable key order for tags ascending
+// in input order -- into (k0, t0); (k1, t1) is scratch.  MSD bucket path
+// first; one host synchronisation reads its overflow word; a clustered input
+// then takes the LSD sort (4 tag + 16 key passes) over the partly sorted copy.
+hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
+                      uint32_t *ws, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    if (n >= (1ull << 31)) return hipErrorInvalidValue;
+    const int kb = ms_bits(n);
+    const size_t nb = (size_t)1 << kb;
+    const int tp = (kb + 7) / 8;  // top-byte passes
+    const size_t wsw = sort_workspace_words(n);
+    uint32_t *ovf = ws + wsw - 1;
+    uint32_t *end = ws + wsw - 2 - nb;  // beyond the passes' histogram and scan words
+    hipError_t e = hipMemsetAsync(ovf, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    uint32_t *hist = ws, *scan_ws = ws + (size_t)256 * ntiles;
+    cell128 *ka = k0, *kx = k1;
+    uint32_t *ta = t0, *tx = t1;
+    for (int p = 0; p < tp; ++p) {  // bytes 16 - tp ... 15, lowest first
+        const int shift = 8 * (16 - tp + p);
+        k_rs_hist<<<ntiles, RS_BLOCK, 0, s>>>(ka, n, shift, hist, ntiles);
+        if ((e = exclusive_scan(hist, (size_t)256 * ntiles, scan_ws, s)) != hipSuccess) return e;
+        k_rs_scatter<<<ntiles, RS_BLOCK, 0, s>>>(ka, ta, kx, tx, n, shift, hist, ntiles);
+        std::swap(ka, kx);
+        std::swap(ta, tx);
+    }
+    // (ka, ta): grouped by bucket; sorted into (kx, tx)
+    k_ms_bounds<<<cx_grid(n, 256), 256, 0, s>>>(ka, n, kb, (uint32_t)nb, end);
+    k_ms_bucket<<<(unsigned)(nb < 65535 * 8 ? nb : 65535 * 8), MS_BLOCK, 0, s>>>(
+        ka, ta, end, (uint32_t)nb, kb, kx, tx, ovf);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t o = 0;
+    if ((e = hipMemcpyAsync(&o, ovf, sizeof(o), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if (o) {
+        // clustered: (ka, ta) holds every key; sort it by (key, tag): 20
+        // passes leave the result in (ka, ta)
+        e = lsd_sort(ka, ta, kx, tx, n, ws, 4, s);
+        if (e != hipSuccess) return e;
+        std::swap(ka, kx);
+        std::swap(ta, tx);
+    }
+    if (kx != k0) {  // the result is in (kx, tx)
+        if ((e = hipMemcpyAsync(k0, kx, n * sizeof(cell128), hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return e;
+        e = hipMemcpyAsync(t0, tx, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
+    }
+    return e;
+}
+
+// *bad = 0 if (keys, tags) ascend by (key, tag), else nonzero (test / A/B).
+__global__ void k_check_sorted(const cell128 *k, const uint32_t *t, size_t n, uint32_t *bad) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i + 1 < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const u128 a = ld128(k + i), b = ld128(k + i + 1);
+        if (b < a || (a == b && t[i + 1] < t[i])) atomicOr(bad, 1u);
+    }
+}
+
+hipError_t check_sorted(const cell128 *k, const uint32_t *t, size_t n, uint32_t *bad,
+                        hipStream_t s) {
+    hipError_t e = hipMemsetAsync(bad, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n < 2) return e;
+    k_check_sorted<<<cx_grid(n, 256), 256, 0, s>>>(k, t, n, bad);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -719,8 +930,8 @@ __global__ void k_dir_lo(const cell128 *ring, uint32_t n, int k, uint32_t *lo) {
     const size_t nb = (size_t)1 << k;
     for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j <= n;
          j += (size_t)gridDim.x * blockDim.x) {
-        const long long pb = j == 0 ? -1 : (long long)(uint64_t)(ld128(ring + j - 1) >> (128 - k));
-        const long long cb = j == n ? (long long)nb : (long long)(uint64_t)(ld128(ring + j) >> (128 - k));
+        const long long pb = j == 0 ? -1 : (long long)top_bits(ld128(ring + j - 1), k);
+        const long long cb = j == n ? (long long)nb : (long long)top_bits(ld128(ring + j), k);
         for (long long b = pb + 1; b <= cb; ++b) lo[b] = (uint32_t)j;
     }
 }
@@ -732,7 +943,7 @@ __global__ void k_dir_pack(const cell128 *ring, uint32_t n, int k, const uint32_
          b += (size_t)gridDim.x * blockDim.x) {
         const uint32_t a = lo[b], z = lo[b + 1];
         uint64_t frac = 0;
-        if (a < z) frac = (uint64_t)(ld128(ring + a) >> (64 - k));
+        if (a < z) frac = mid_bits(ld128(ring + a), k);
         dir[b] = make_uint4(a, z, (uint32_t)frac, (uint32_t)(frac >> 32));
     }
 }
@@ -766,7 +977,7 @@ __global__ __launch_bounds__(SUCC_BLOCK) void k_fingers(SearchView sv, const cel
             const u128 idp = ld128(ring + p);
             const uint32_t nx = (p + 1 == n) ? 0u : p + 1;
             const u128 gap = ld128(ring + nx) - idp;  // clockwise distance to next peer
-            const u128 step = (u128)1 << i;
+            const u128 step = pow2_128(i);
             f = (step <= gap) ? nx : Searcher<DIR>::find(sv, lds, idp + step);
         }
         F[t] = f;
@@ -806,7 +1017,7 @@ constexpr int FT_ROW = FT_COLS + 1;  // padded row: conflict-free column writes
 __global__ void k_ring_slice(const cell128 *ring, size_t n, int kb, uint32_t *key) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x)
-        key[i] = (uint32_t)(ld128(ring + i) >> kb);
+        key[i] = (uint32_t)bits64(ld128(ring + i), kb);
 }
 
 __global__ __launch_bounds__(256) void k_fingers_plan(SearchView sv, const cell128 *ring,
@@ -837,7 +1048,7 @@ __global__ __launch_bounds__(256) void k_fingers_plan(SearchView sv, const cell1
     if (lane == 0) lvl0[b] = (uint8_t)(l0 > 128 ? 128 : l0);
     const int i = FT_L0 + lane;
     if (lane < FT_COLS && i >= l0)
-        S0[(size_t)b * FT_COLS + lane] = dir_successor(sv, ld128(ring + a) + ((u128)1 << i));
+        S0[(size_t)b * FT_COLS + lane] = dir_successor(sv, ld128(ring + a) + (pow2_128(i)));
 }
 
 // ROWS = false (F null, planes only): every search result goes straight to its
@@ -868,7 +1079,7 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
                                                              : 0u;
     if (threadIdx.x < rows) glog[threadIdx.x] = glog_g[a + threadIdx.x];
     const u128 ida = ld128(ring + a);
-    const uint32_t ka = (uint32_t)(ida >> kb);
+    const uint32_t ka = (uint32_t)bits64(ida, kb);
     // Window keys: for a level i >= kb the start t_p = id_p + 2^i carries
     // nothing into bits [kb, kb + 32) from below, so its slice is
     // slice(id_p) + 2^(i - kb) (mod 2^32) and the key of t_p relative to the
@@ -877,14 +1088,14 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
     // order correctly while offsets from t_a stay below 2^(kb + 32) (checked
     // on each window's exact last element and on each peer's offset); equal
     // keys are ties (exact search).
-    const u128 lim = (u128)1 << (kb + 32);
+    const u128 lim = pow2_128(kb + 32);
     u128 idp[2];
     uint32_t cp[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const uint32_t r = lane + 64 * k;
         idp[k] = r < rows ? ld128(ring + a + r) : ida;
-        cp[k] = (uint32_t)(idp[k] >> kb) - ka;
+        cp[k] = (uint32_t)bits64(idp[k], kb) - ka;
         if (idp[k] - ida >= lim) cp[k] = 0xFFFFFFFFu;  // off the key range: exact search
     }
     __syncthreads();
@@ -913,7 +1124,7 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
             const int lv = wave + 4 * lane;
             uint32_t e = s0[c0 + lv - FT_L0] + FT_W - 1;
             e = e >= n ? e - n : e;
-            arc = (ld128(ring + e) - (ida + ((u128)1 << (c0 + lv)))) < lim;
+            arc = (ld128(ring + e) - (ida + (pow2_128(c0 + lv)))) < lim;
         }
         const uint32_t arcbits = (uint32_t)__ballot(arc);
 #pragma unroll
@@ -968,7 +1179,7 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
                     f = e >= n ? e - n : e;
                 }
                 if (f == CX_NONE)  // tie on the key / past the window / no arc
-                    f = dir_successor(sv, idp[k] + ((u128)1 << i));
+                    f = dir_successor(sv, idp[k] + (pow2_128(i)));
                 if (ROWS)
                     tile[r * FT_ROW + (i - FT_L0)] = f;
                 else if (i >= Lft)
@@ -1008,7 +1219,7 @@ __global__ __launch_bounds__(256) void k_fingers_tile(SearchView sv, const cell1
                 else if (i >= FT_L0)
                     v[c] = tile[r * FT_ROW + (i - FT_L0)];
                 else  // a gap under 2^88 (clustered rings): exact search
-                    v[c] = dir_successor(sv, ld128(ring + p) + ((u128)1 << i));
+                    v[c] = dir_successor(sv, ld128(ring + p) + (pow2_128(i)));
             }
             o = make_uint4(v[0], v[1], v[2], v[3]);
         }
@@ -1092,7 +1303,7 @@ __global__ __launch_bounds__(256) void k_planes_repair(SearchView sv, const cell
         while (miss) {
             const int c = __builtin_ctzll(miss);
             miss &= miss - 1;
-            val[c][threadIdx.x] = dir_successor(sv, idp + ((u128)1 << (L + c)));
+            val[c][threadIdx.x] = dir_successor(sv, idp + (pow2_128(L + c)));
             ++searched;
         }
     }
@@ -1435,7 +1646,7 @@ __device__ __forceinline__ uint32_t finger_of(const SearchView &sv, const cell12
                                               uint32_t p, int i, u128 idp) {
     if (n == 1) return 0;
     const uint32_t nx = (p + 1 == n) ? 0u : p + 1;
-    const u128 step = (u128)1 << i;
+    const u128 step = pow2_128(i);
     return (step <= ld128(ring + nx) - idp) ? nx : dir_successor(sv, idp + step);
 }
 
@@ -1489,7 +1700,7 @@ __global__ void k_tree_build(const uint32_t *F, const cell128 *ring, uint32_t n,
 #pragma unroll
         for (int sl = 0; sl < 8; ++sl)
             e[sl] = f[sl] == CX_NONE ? ~0ull
-                                     : (((uint64_t)(ld128(ring + f[sl]) >> S) << ib) | f[sl]);
+                                     : ((bits64(ld128(ring + f[sl]), S) << ib) | f[sl]);
     }
 }
 
@@ -1518,7 +1729,7 @@ __device__ __forceinline__ int tree_plan(const PkCtx &c, u128 key, u128 &clo, bo
             cs = ch;
             const uint64_t f = ent[ch];
             const uint32_t nxt = (uint32_t)(f & c.imask);
-            const u128 nlo = (u128)(f >> c.ib) << c.S;
+            const u128 nlo = shl128((u128)(f >> c.ib), c.S);
             ++h;
             const int t = term_iv(key, clo, cw, nlo, c.W);
             if (t == 1) {
@@ -1780,7 +1991,7 @@ __global__ void k_ring_codes(const cell128 *ring, uint32_t n, int gs, uint32_t *
                              uint32_t *wide) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const u128 id = ld128(ring + p);
-        rs[p] = (uint32_t)(id >> (gs - 15));
+        rs[p] = (uint32_t)bits64(id, gs - 15);
         const u128 nx = ld128(ring + (p + 1 == n ? 0u : p + 1));
         if (n == 1 || msb128(nx - id) >= gs + 17) atomicOr(wide, 1u);
     }
@@ -2509,7 +2720,7 @@ hipError_t table_hash(const void *t, size_t bytes, unsigned long long *out, hipS
 // when d < u, the walk needs cur's exact ID (cex: clo = id_cur).
 __device__ __forceinline__ void cz_exact_d(const PkCtx &c, u128 key, u128 idc, uint64_t &dmin,
                                            uint64_t &dmax) {
-    dmin = dmax = (uint64_t)((key - idc) >> c.gs);
+    dmin = dmax = bits64(key - idc, c.gs);
 }
 
 // Exact hop from cur at level i through the finger table (below the table,
@@ -2526,7 +2737,7 @@ __device__ __forceinline__ int cz_exact(const PkCtx &c, u128 key, u128 &clo, uin
         // nh = id(cur + 1) from the memory round (A_EXACT): the finger is the
         // next peer unless the gap to it is below 2^i (then the directory)
         const uint32_t nx = cur + 1 == c.n ? 0u : cur + 1;
-        const u128 step = (u128)1 << i;
+        const u128 step = pow2_128(i);
         if (c.n == 1) {
             nxt = 0;
             idn = clo;
@@ -2705,7 +2916,7 @@ void k_route_tree(TreeIO io) {
     c.ib = ib;
     c.S = 64 + ib;
     c.imask = (1ull << ib) - 1;
-    c.W = ((u128)1 << c.S) - 1;
+    c.W = (pow2_128(c.S)) - 1;
     c.gs = cz_shift(ib);
     c.arc = ARC;
     c.Lh = io.Lh;
@@ -2888,7 +3099,7 @@ void k_route_tree(TreeIO io) {
             ri = lvl;
             cs = 0;
             const uint32_t nxt = (uint32_t)(m0 & c.imask);
-            const u128 nlo = (u128)(m0 >> ib) << c.S;
+            const u128 nlo = shl128((u128)(m0 >> ib), c.S);
             ++h;
             const int t = term_iv(key, clo, cex ? (u128)0 : c.W, nlo, c.W);
             if (t == 1) {
@@ -3897,7 +4108,7 @@ struct ChurnDir {
 
 // The key's 32-B bucket entry.
 __device__ __forceinline__ void cd_fetch(const ChurnDir &c, u128 key, uint4 &A, uint4 &B) {
-    const size_t b = (size_t)(uint64_t)(key >> (128 - c.kb));
+    const size_t b = (size_t)top_bits(key, c.kb);
     A = c.cd[2 * b];
     B = c.cd[2 * b + 1];
 }
@@ -3934,7 +4145,7 @@ __device__ __forceinline__ int cd_lookup(const ChurnDir &c, u128 key, const uint
                                          const uint4 B, uint32_t n_old, uint32_t n_new, int no,
                                          int nn, uint32_t &so, uint32_t &sn, uint32_t &has,
                                          uint32_t &mis) {
-    const uint64_t xf = (uint64_t)(key >> (64 - c.kb));
+    const uint64_t xf = mid_bits(key, c.kb);
     const uint64_t h0 = ((uint64_t)A.y << 32) | A.x;
     uint32_t O = B.x, N = B.y;  // bit k: merged entry m + k is old / new
     const uint64_t h1c = ((uint64_t)B.w << 32) | B.z;
@@ -4221,8 +4432,8 @@ __global__ void k_cd_lo(const cell128 *mid, uint32_t M, int kb, uint32_t *lo) {
     const size_t nb = (size_t)1 << kb;
     for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j <= M;
          j += (size_t)gridDim.x * blockDim.x) {
-        const long long pb = j == 0 ? -1 : (long long)(uint64_t)(ld128(mid + j - 1) >> (128 - kb));
-        const long long cb = j == M ? (long long)nb : (long long)(uint64_t)(ld128(mid + j) >> (128 - kb));
+        const long long pb = j == 0 ? -1 : (long long)top_bits(ld128(mid + j - 1), kb);
+        const long long cb = j == M ? (long long)nb : (long long)top_bits(ld128(mid + j), kb);
         for (long long b = pb + 1; b <= cb; ++b) lo[b] = (uint32_t)j;
     }
 }
@@ -4235,8 +4446,8 @@ __global__ void k_cd_pack(const cell128 *mid, const uint32_t *mso, const uint32_
         const uint32_t a = lo[b], z = lo[b + 1];
         const uint32_t cnt = z - a < 3 ? z - a : 3;
         const uint32_t m0 = a < M ? a : 0;
-        const uint64_t h0 = cnt >= 1 ? (uint64_t)(ld128(mid + a) >> (64 - kb)) : 0;
-        const uint64_t h1 = cnt >= 2 ? (uint64_t)(ld128(mid + a + 1) >> (64 - kb)) : 0;
+        const uint64_t h0 = cnt >= 1 ? mid_bits(ld128(mid + a), kb) : 0;
+        const uint64_t h1 = cnt >= 2 ? mid_bits(ld128(mid + a + 1), kb) : 0;
         uint32_t om = 0, nm = 0;  // old / new masks of the 32 merged entries
         uint32_t m = m0;
         for (int j = 0; j < 32; ++j) {
@@ -4522,7 +4733,7 @@ __global__ void k_hex_format(const cell128 *keys, size_t count, uint4 *out, uint
             for (int b = 0; b < 4; ++b) {
                 const int pos = 4 * j + b;
                 if (pos < nd) {
-                    const uint32_t d = (uint32_t)(v >> (4 * (nd - 1 - pos))) & 15u;
+                    const uint32_t d = (uint32_t)bits64(v, 4 * (nd - 1 - pos)) & 15u;
                     word |= (d < 10 ? '0' + d : 'a' + d - 10) << (8 * b);
                 }
             }

@@ -69,8 +69,17 @@ size_t sort_workspace_words(size_t n);
 size_t bucket_sort_workspace_words(size_t n);
 hipError_t bucket_sort(const cell128 *keys, size_t n, cell128 *out, uint32_t *ws,
                        uint32_t *overflow, hipStream_t s);
+// (keys, tags) by (key, tag) into (k0, t0) -- the stable key order when the
+// tags ascend in input order; MSD buckets + LDS bucket sort, LSD fallback for
+// clustered keys (one host synchronisation).  ws: sort_workspace_words(n).
 hipError_t radix_sort(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
                       uint32_t *ws, hipStream_t s);
+// *bad (device) = 0 iff (k, t) ascend by (key, tag).
+hipError_t check_sorted(const cell128 *k, const uint32_t *t, size_t n, uint32_t *bad,
+                        hipStream_t s);
+// The 16-pass LSD sort alone (stable by key), for A/B timing.
+hipError_t radix_sort_lsd(cell128 *k0, uint32_t *t0, cell128 *k1, uint32_t *t1, size_t n,
+                          uint32_t *ws, hipStream_t s);
 hipError_t unique_sorted(const cell128 *keys, const uint32_t *tags, size_t n, uint32_t *pos,
                          uint32_t *scan_ws, cell128 *out, uint32_t *old_to_new,
                          uint32_t *d_count, hipStream_t s);

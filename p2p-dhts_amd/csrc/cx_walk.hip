@@ -282,7 +282,7 @@ __global__ __launch_bounds__(WK_BLOCK) WK_ATTR void k_walk(WalkIO io) {
                 }
             } else {  // M_EXACT: the exact finger at level msb(d) = succ(id + 2^i)
                 const int i = msb128(d);
-                const u128 step = (u128)1 << i;
+                const u128 step = pow2_128(i);
                 uint32_t nxt;
                 u128 idn;
                 if (step <= xb - xa) {  // the next peer

@@ -59,6 +59,37 @@ def test_ring_build_equal_high_bits(cx, O):
     assert (cx.Ring(ids).ids() == O.ring_build(ids)).all()
 
 
+@pytest.mark.parametrize("kind", ["uniform", "cluster", "mixed", "dups"])
+def test_ring_build_sort_paths(cx, O, kind):
+    """Round 6 ring sort (cx_kernels.hip radix_sort): MSD buckets of ~256 keys
+    sorted in LDS by (key, tag), and the LSD fallback (4 tag + 16 key passes)
+    when a bucket passes 2048 keys.  uniform: the bucket path; cluster: one
+    bucket holds everything (fallback); mixed: uniform keys plus a dense run
+    in one bucket (fallback with most buckets already written); dups: many
+    equal keys (the kept duplicate is the first by input order)."""
+    rng = np.random.default_rng(0x50E7)
+    if kind == "uniform":
+        vals = O.ints_from_keys(O.splitmix_keys(0x50E8, 1 << 17))
+    elif kind == "cluster":
+        base = 0x3C3C_5A5A_0F0F_1234 << 64
+        vals = [base + int(x) * 7919 for x in rng.permutation(6000)]
+    elif kind == "mixed":
+        vals = O.ints_from_keys(O.splitmix_keys(0x50E9, 1 << 16))
+        vals += [(0x1234 << 112) + int(x) for x in rng.permutation(5000)]
+    else:
+        u = O.ints_from_keys(O.splitmix_keys(0x50EA, 3000))
+        vals = [u[int(i)] for i in rng.integers(0, 3000, size=40000)]
+    ids = O.keys_from_ints(vals)
+    ring = cx.Ring(ids)
+    assert (ring.ids() == O.ring_build(ids)).all()
+    import torch
+    from chordx.ring import sort_time
+    d = torch.from_numpy(ids.view(np.int64).copy()).cuda()
+    for variant in (0, 1):
+        _, ok = sort_time(d, variant)
+        assert ok, variant
+
+
 # ---------------------------------------------------------------- a5/a7 successor
 @pytest.mark.parametrize("search", [0, 1, 2, 3])
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 16, 17, 256, 257, 1000, 4095, 4096, 65537, 70000])
