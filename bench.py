@@ -1256,7 +1256,15 @@ def main():
             for k in (1, 8)}
         churn["epoch_amortized"]["note"] = (
             "a warm 1 %/1 % churn epoch's route-ready time (max over ranks) plus K timed batches "
-            "of the headline (2^25 lookups per GPU each), whole node")
+            "of the headline (2^25 lookups per GPU each), whole node; `overlapped`: epoch e "
+            "keeps serving while epoch e + 1 builds (churn_route_ready.overlapped), so under "
+            "back-to-back epochs the serving rate is the rate during a rebuild")
+        ov = churn.get("overlapped")
+        if ov:
+            during = dist.sum_over_ranks(int(ov["serving_lookups_per_s_during_rebuild"]), world, dev)
+            churn["epoch_amortized"]["overlapped"] = {
+                "lookups_per_s": during, "vs_headline": during / (world * Q * args.steps / dt_max),
+                "epoch_ms_under_load": dist.max_over_ranks(ov["rebuild_ms_under_load"], world, dev)}
         if "table_depth_ab" in churn:
             st = churn["table_depth_ab"]
             st["results_equal_default"] = dist.all_over_ranks(st["results_equal_default"], world, dev)

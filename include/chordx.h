@@ -88,8 +88,9 @@ int cx_device_count(int *count);
  * CX_POOL_CAP_GIB GiB (environment, default 96, 0 = off), for the next ring of
  * the same size -- a membership epoch reuses the previous epoch's HBM.  Any
  * allocation that fails releases the device's idle blocks and retries.
- * cx_pool_trim releases every idle block now (all devices); cx_pool_info
- * reports the idle blocks and their bytes. */
+ * cx_pool_trim releases every idle block now (all devices), and the idle
+ * device staging buffers of host-memory calls (one process-wide cache, at most
+ * 64 MiB idle); cx_pool_info reports the idle table blocks and their bytes. */
 int cx_pool_trim(void);
 int cx_pool_info(uint64_t *blocks, uint64_t *bytes);
 

@@ -50,7 +50,7 @@ __device__ __forceinline__ void st128(cell128 *p, u128 x) {
 }
 
 // Variable shifts of 128-bit ring values, spelled in 64-bit halves.  Round 6
-// (DESIGN §11, profiles/r06/u128/): the compiled level-plane route-table
+// (DESIGN §10, profiles/r06/u128/): the compiled level-plane route-table
 // build with the round-5 gap code -- a u128 `>> gs` in a lane-divergent
 // branch -- wrote nondeterministic words, only in lanes 48-63 of a wave and
 // only in its slot-8 encode, with its inputs built on the host and no race

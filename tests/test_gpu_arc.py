@@ -738,6 +738,61 @@ def test_arc_router_rccl_world1_general_path(cx, q, chunks):
     assert succ_ok == (True, 2, 0, True)  # one rank: every key is its own, none sent
 
 
+def _disagree_worker(rank, world, port, out, what):
+    import os
+    import sys
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "p2p-dhts_amd")]
+    import torch
+    import torch.distributed as tdist
+    import chordx
+    from chordx.arc import ArcRouter
+    tdist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    ids = torch.empty((20000, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(ids, 0xD15A)
+    ring = chordx.Ring(ids)
+    router = ArcRouter(ring, ring.n, rank, world, comm_device="cpu")
+    if what == "protocol":
+        router.exact = rank == 0  # rank 0: exact layout, rank 1: region layout
+    else:
+        router.self_exchange = rank == 0
+    q = 5000
+    keys = torch.empty((q, 2), dtype=torch.int64, device="cuda")
+    chordx.fill_splitmix(keys, 0xD15B, offset=rank * q)
+    src = (torch.arange(q, device="cuda") % ring.n).to(torch.int32)
+    owner = torch.empty(q, dtype=torch.int32, device="cuda")
+    hops = torch.empty(q, dtype=torch.uint8, device="cuda")
+    try:
+        router.route(src, keys, owner, hops)
+        out[rank] = "returned"
+    except RuntimeError as e:
+        out[rank] = "raised: " + str(e)[:80]
+    tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("what", ["protocol", "self_exchange"])
+def test_arc_router_ranks_disagree_raise_everywhere(cx, what):
+    """ranks that pick different protocols (exact layout vs
+    region layout) or different self_exchange settings gather rows of the
+    same length whose first word carries those choices; every rank sees the
+    disagreement and raises, none hangs in mismatched collectives."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_disagree_worker, args=(2, port, out, what), nprocs=2, join=True,
+                       start_method="spawn")
+    for r in range(2):
+        assert out[r].startswith("raised") and "disagree" in out[r], (r, out[r])
+
+
 # ---------------------------------------------------------------------------
 # Round 6 (VERDICT r05 item 1): the single-piece 2^25-key placement exchange on
 # a one-rank RCCL group.  Measured cause of the round-5 "half empty" return

@@ -1,5 +1,5 @@
 """No device code of libchordx shifts a 128-bit value by a variable amount
-(round 6, DESIGN §11): every such shift goes through cx_common.hpp's
+(round 6, DESIGN §10): every such shift goes through cx_common.hpp's
 64-bit-half helpers (pow2_128 / shr128 / shl128 / bits64).  The round-5
 level-plane route-table build wrote nondeterministic words in lanes 48-63
 around a compiled `u128 >> gs` (tests/test_gpu_u128.py, profiles/r06/u128/).
