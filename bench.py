@@ -91,6 +91,13 @@ C5_BYTES_STREAM = 210
 C5_BYTES_SURVEY = 139
 
 
+def progress(msg: str) -> None:
+    """One line on stderr per leg (the JSON line alone goes to stdout): long
+    multi-rank runs show they are alive."""
+    print(f"[bench r{os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}",
+          file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -344,6 +351,7 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
     # exchange self-test: the same protocol with every rank's own lookups sent
     # through the collectives too (self_exchange), so every lookup crosses
     # RCCL -- at N = 1 the exchange a one-GPU run can time and check
+    progress("arc: exchange self-test")
     router.self_exchange = True
     for t in (owner, hops, status):
         t.fill_(0xEE)
@@ -368,6 +376,7 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
     # DHash placement lists (n = 14) in the same layout (keys to
     # their owner's arc, windows read there from the arc + a 13-peer halo,
     # lists back): the same keys, K steps, equal to the replicated cx_nsucc
+    progress("arc: placement lists")
     lists = torch.empty((Q, 14), dtype=torch.int32, device=dev)
     cnt = torch.empty(Q, dtype=torch.uint8, device=dev)
     router.nsucc(keys, 14, lists, cnt)  # builds the halo ring once
@@ -378,6 +387,7 @@ def arc_leg(args, ring, src, keys, owner_ref, hops_ref, world, rank, dev, backen
     del lists, cnt, wl, wc
     # exact-successor mode: the same keys, their owners searched on
     # the owner's arc of the ring only
+    progress("arc: exact successors")
     own = torch.empty(Q, dtype=torch.int32, device=dev)
     router.successor(keys, own)  # builds the arc's ring once
     _, dt_sc = time_steps(lambda: router.successor(keys, own), args.steps, world, dev)
@@ -615,6 +625,7 @@ def churn_leg(ring, keys, src, dev, depth_ab=28):
     out["new_ring_peers"] = a1.n
     del k2, s2, o, h, st
     # epoch e (a1) keeps serving while epoch e + 1 builds
+    progress("churn: overlapped serving during rebuilds")
     out["overlapped"] = overlap_leg(a1, joins, leaves, keys, src, dev)
     # the same with the serving stream at high priority
     out["overlapped"]["high_priority_serving"] = overlap_leg(a1, joins, leaves, keys, src, dev,
@@ -624,6 +635,7 @@ def churn_leg(ring, keys, src, dev, depth_ab=28):
     r_def = out["warm"]["route_levels"]
 
     if depth_ab:
+        progress("churn: table depth ABBA")
         sub = {"route_levels": depth_ab, "route_levels_default": r_def}
         Q = keys.shape[0]
         srcw = (src.to(torch.int64) % a1.n).to(torch.int32)
@@ -1121,6 +1133,7 @@ def main():
     Q = 1 << args.keys_log2
 
     # ---- setup (untimed): replicated ring, converged finger + route tables ----
+    progress("setup: ring, fingers, route table")
     ring, t_gather, t_ring = setup_ring(args, world, rank, dev, backend)
     st0 = chordx.pool_stats()
     t0 = time.perf_counter()
@@ -1151,6 +1164,7 @@ def main():
         route_variant, f"route variant {route_variant}")
 
     # ---- warmup ----
+    progress("warmup")
     for _ in range(args.warmup):
         ring.route(src, keys, out=out)
     torch.cuda.synchronize(dev)
@@ -1172,6 +1186,7 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # one cx_route launch per step
 
     # ---- results (all reduced over ranks) ----
+    progress("timed steps done; checks")
     bad = dist.sum_over_ranks(int((status != 0).sum().item()), world, dev)
     sum_hops = dist.sum_over_ranks(int(hops.to(torch.int64).sum().item()), world, dev)
     # hop histogram (SURVEY 5 metrics), summed over ranks; hops <= 255 (hop cap)
@@ -1238,6 +1253,7 @@ def main():
         del so
 
     # ---- churn -> route-ready (f2), cold then warm ----
+    progress("churn -> route-ready leg")
     churn = None
     if not args.no_churn:
         churn = churn_leg(ring, keys, src, dev)
@@ -1272,11 +1288,13 @@ def main():
                 st["warm"]["route_ready_ms"], world, dev)
 
     # ---- arc-sharded C4 (all_to_all-v) on the same keys and steps ----
+    progress("arc leg")
     arc = None
     if not args.no_arc:
         arc = arc_leg(args, ring, src, keys, owner, hops, world, rank, dev, backend)
 
     # ---- CPU baseline: rank 0, every world size, after the timed region ----
+    progress("cpu baseline")
     cpu = None
     if rank == 0 and not args.no_cpu:
         F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
@@ -1289,6 +1307,7 @@ def main():
     dist.barrier(world)
 
     # ---- C5 (configs[4]) after the bench ring's tables are released ----
+    progress("c5 leg")
     c5 = None
     if not args.no_c5:
         ring.close()
@@ -1297,6 +1316,7 @@ def main():
         chordx.pool_trim()
 
     # ---- C2 / C3 (configs[1], configs[2]): small rings, after the bench ring ----
+    progress("c2 / c3 legs")
     c2 = c3 = None
     if not args.no_c2:
         c2 = c2_leg(args, world, rank, dev)

@@ -66,6 +66,17 @@ def main():
     outs = [(torch.full((Q,), -1, dtype=torch.int32, device=dev),
              torch.zeros(Q, dtype=torch.uint8, device=dev),
              torch.full((Q,), 9, dtype=torch.uint8, device=dev)) for _ in range(G)]
+    for rep in range(2):  # rep 0 warms every kernel and table (round 6: rank 0's
+        # first own walk ran 1.14 ms cold against 0.69-0.77 warm and set the max)
+        res = simulate(ring, G, Q, N, keys, srcs, outs, dev)
+    print(json.dumps(res))
+
+
+def simulate(ring, G, Q, N, keys, srcs, outs, dev):
+    for ow, hp, st in outs:  # every repetition writes every output afresh
+        ow.fill_(-1)
+        hp.fill_(0)
+        st.fill_(9)
     t = {k: [0.0] * G for k in ("count", "scatter", "own_walk", "recv_walk", "deliver")}
     parts, counts = [], []
     for g in range(G):  # ---- origin side
@@ -131,9 +142,10 @@ def main():
                "serial": Q / ((max(per) + max(xbytes) / (0.5 * 7 * XGMI_LINK) * 1e3) * 1e-3),
                "overlapped": Q / (max(max(per_overlap),
                                       max(xbytes) / (0.5 * 7 * XGMI_LINK) * 1e3) * 1e-3)},
-           "note": "one engine plays every rank (cx_arc_build per rank); exchange not measured: "
-                   "28 B out + 8 B back per remote lookup over 7 xGMI links at 50 % of 153 GB/s"}
-    print(json.dumps(res))
+           "note": "one engine plays every rank (cx_arc_build per rank), the whole simulation "
+                   "run twice and the second timed; exchange not measured: 28 B out + 8 B back "
+                   "per remote lookup over 7 xGMI links at 50 % of 153 GB/s"}
+    return res
 
 
 if __name__ == "__main__":

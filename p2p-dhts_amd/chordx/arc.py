@@ -581,13 +581,13 @@ class ArcRouter:
         # written (the count pass left each piece's indices piece-relative at
         # own_idx[cut[c]:])
         n_own = [0 if sx else cnt[c][me] for c in range(kg)]
+        walk_own = eng.arc_route_local
         if sum(n_own):
             if sum(1 for x in n_own if x) == 1:
                 c = next(c for c in range(kg) if n_own[c])
                 sl = slice(cut[c], cut[c + 1])
-                eng.arc_route_local(src[sl], keys[sl], own_idx[cut[c]: cut[c] + n_own[c]],
-                                    owner[sl], hops[sl],
-                                    status[sl] if status is not None else None)
+                walk_own(src[sl], keys[sl], own_idx[cut[c]: cut[c] + n_own[c]],
+                         owner[sl], hops[sl], status[sl] if status is not None else None)
             else:
                 idx_all = torch.empty(sum(n_own), dtype=torch.int32, device=dev)
                 at = 0
@@ -596,7 +596,7 @@ class ArcRouter:
                         torch.add(own_idx[cut[c]: cut[c] + n_own[c]], cut[c],
                                   out=idx_all[at: at + n_own[c]])
                         at += n_own[c]
-                eng.arc_route_local(src, keys, idx_all, owner, hops, status)
+                walk_own(src, keys, idx_all, owner, hops, status)
         backs = []
         for c in range(kg):
             got = inflight
