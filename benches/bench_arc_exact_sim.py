@@ -83,7 +83,10 @@ def simulate(ring, G, Q, N, keys, srcs, outs, dev):
         ring.arc_build(G, g)
         row = torch.zeros(G, dtype=torch.int64, device=dev)
         own_idx = torch.empty(Q, dtype=torch.int32, device=dev)
-        ws = torch.empty(ring.arc_own_ws_words(Q), dtype=torch.int32, device=dev)
+        # sized for either build of the count pass (the round-5 two-kernel pass
+        # took 2048 + Q / 4 words of scratch; ab/ A/B runs load that library)
+        ws = torch.empty(max(ring.arc_own_ws_words(Q), 2048 + (Q + 3) // 4), dtype=torch.int32,
+                         device=dev)
         _, t["count"][g] = timed(lambda: ring.arc_count_async(G, keys[g], row, g, own_idx, ws))
         cnt = row.tolist()
         cur = torch.empty(G, dtype=torch.int32, device=dev)

@@ -425,9 +425,10 @@ int cx_arc_partition_regions_async(const cx_ring *ring, int world, const uint32_
  * overflow, no host synchronisation): cx_arc_count_async writes the
  * per-destination counts of the lookups' keys into counts_dev (device,
  * world int64) and, with own_idx (device, q uint32) and own_ws (device
- * scratch of 2048 + ceil(q / 4) uint32), writes the indices of the lookups of
- * rank `me`'s own arc, ascending, into own_idx[0 .. counts[me]) for
- * cx_arc_route_local;
+ * scratch of one uint32), writes the indices of the lookups of rank `me`'s
+ * own arc into own_idx[0 .. counts[me]) for cx_arc_route_local (a permutation
+ * of them: ascending within each block of up to 16 384 lookups, the blocks'
+ * runs in completion order);
  * cx_arc_scatter_async, given those counts (still on the device), lays
  * destination d's lookups out at [sum_{j<d} counts[j], ...) of send_keys /
  * send_src / send_hint (q entries each; send_hint may be NULL) with perm[i] =

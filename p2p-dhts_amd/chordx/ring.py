@@ -601,8 +601,9 @@ class Ring:
 
     @staticmethod
     def arc_own_ws_words(q: int) -> int:
-        """int32 words of arc_count_async's own_ws scratch for q lookups."""
-        return 2048 + (int(q) + 3) // 4
+        """int32 words of arc_count_async's own_ws scratch for q lookups (the
+        own-run cursor: one word whatever q)."""
+        return 1
 
     def arc_count_async(self, world: int, keys, counts, me: int = -1, own_idx=None,
                         own_ws=None):
@@ -610,7 +611,8 @@ class Ring:
         `counts` (device int64, world elements), no host synchronisation; with
         own_idx (device int32, >= q elements) and own_ws (device int32 scratch,
         >= arc_own_ws_words(q) elements): the indices of rank `me`'s own
-        lookups, ascending, in own_idx[:counts[me]]."""
+        lookups in own_idx[:counts[me]] (a permutation of them, ascending
+        within each block's run)."""
         keys = self._prep_keys(keys)
         if not (_is_dev(keys) and _is_dev(counts)):
             raise TypeError("arc routing takes device tensors")

@@ -3649,111 +3649,141 @@ hipError_t arc_partition_regions(const uint32_t *src, const cell128 *keys, size_
     return hipGetLastError();
 }
 
-// Count pass of the exact-layout partition: counts[d] (int64, zeroed here) =
-// lookups whose key's arc is rank d's.  Keys only (16 B per lookup); block b
-// takes the contiguous lookups [b per, (b + 1) per) and folds them into its
-// LDS histogram, one global atomic per (block, destination) at the end.  With
-// own_idx: each lookup's destination byte (dest) and the block's count of
-// rank `me`'s lookups (blk_own[b]) are kept for k_arc_own_compact.
-constexpr uint32_t ARC_OWN_BLOCKS = 2048;
+// Count pass of the exact-layout partition, one kernel: counts[d] (int64) =
+// lookups whose key's arc is rank d's, and with own_idx the indices of rank
+// `me`'s lookups.  Keys only (16 B per lookup).  Block b takes the contiguous
+// lookups [b per, (b + 1) per), per <= 64 rounds of 256; lane j of each wave
+// accumulates the wave's count for rank j from one ballot per (round, rank),
+// so the histogram costs no LDS atomics per lookup, and each lane keeps one
+// bit per round for "rank me's".  At the end the block reserves its own
+// lookups' run with one atomic on *cursor and writes them there ascending
+// (runs in block completion order: own_idx is a permutation of the own
+// lookups, ascending within each block's run).  Round 5 wrote a destination
+// byte per lookup and compacted in a second kernel (132 + 70 us at 2^25).
+constexpr int ARC_CNT_ROUNDS = 64;  // rounds of 256 lookups per block at most
 
 __global__ __launch_bounds__(256) void k_arc_count_keys(const cell128 *keys, size_t q,
                                                         const ArcBound *bounds, int nb, int G,
                                                         unsigned long long *counts, int me,
-                                                        uint8_t *dest, uint32_t *blk_own,
+                                                        uint32_t *own_idx, uint32_t *cursor,
                                                         size_t per) {
     __shared__ uint32_t h[ARC_MAX_RANKS];
     __shared__ ArcBound sb[ARC_MAX_RANKS];
-    for (int j = threadIdx.x; j < G; j += blockDim.x) h[j] = 0;
-    for (int j = threadIdx.x; j < nb; j += blockDim.x) sb[j] = bounds[j];
+    __shared__ uint32_t wc[ARC_CNT_ROUNDS * 4];  // own lookups per (round, wave), then offsets
+    __shared__ uint32_t wsum[4], base_s;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int j = t; j < G; j += blockDim.x) h[j] = 0;
+    for (int j = t; j < nb; j += blockDim.x) sb[j] = bounds[j];
+    wc[t] = 0;  // blockDim.x == 256 == ARC_CNT_ROUNDS * 4
     __syncthreads();
     const size_t lo = blockIdx.x * per, hi = lo + per < q ? lo + per : q;
-    for (size_t b0 = lo; b0 < hi; b0 += (size_t)blockDim.x * ARC_SCAT_R) {  // uniform trips
+    const int rounds = (int)((hi - lo + 255) / 256);
+    uint32_t acc = 0;   // lane j < G: this wave's lookups bound for rank j
+    uint64_t mine = 0;  // bit r: this lane's lookup of round r is rank me's
+    // the next trip's keys are loaded before this trip's are classified, so a
+    // wave keeps its loads in flight through the compares and ballots
+    u128 kn[ARC_SCAT_R];
+#pragma unroll
+    for (int k = 0; k < ARC_SCAT_R; ++k) {
+        const size_t i = lo + (size_t)k * 256 + t;
+        kn[k] = i < hi ? ld128(keys + i) : (u128)0;
+    }
+    for (int r0 = 0; r0 < rounds; r0 += ARC_SCAT_R) {  // uniform trips
+        u128 kc[ARC_SCAT_R];
+#pragma unroll
+        for (int k = 0; k < ARC_SCAT_R; ++k) {
+            kc[k] = kn[k];
+            const size_t i = lo + (size_t)(r0 + ARC_SCAT_R + k) * 256 + t;
+            kn[k] = i < hi ? ld128(keys + i) : (u128)0;
+        }
         int d[ARC_SCAT_R];
 #pragma unroll
         for (int k = 0; k < ARC_SCAT_R; ++k) {
-            const size_t i = b0 + (size_t)k * blockDim.x + threadIdx.x;
+            const size_t i = lo + (size_t)(r0 + k) * 256 + t;
             d[k] = -1;
             if (i < hi) {
-                const u128 key = ld128(keys + i);
                 ArcRec r;
-                r.w0 = (uint64_t)key;
-                r.w1 = (uint64_t)(key >> 64);
+                r.w0 = (uint64_t)kc[k];
+                r.w1 = (uint64_t)(kc[k] >> 64);
                 r.hk = ARC_NEW << 8;
                 d[k] = arc_dest(r, sb, nb, G);
-                if (dest) dest[i] = (uint8_t)d[k];
             }
         }
+        for (int j = 0; j < G; ++j) {
+            uint32_t c = 0;
 #pragma unroll
-        for (int k = 0; k < ARC_SCAT_R; ++k) (void)arc_wave_slots(d[k], G, h);
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < G; j += blockDim.x)
-        if (h[j]) atomicAdd(&counts[j], (unsigned long long)h[j]);
-    if (blk_own && threadIdx.x == 0) blk_own[blockIdx.x] = h[me];
-}
-
-// The indices of rank `me`'s lookups in ascending order: block b (the same
-// lookups as in k_arc_count_keys) writes its own lookups at the sum of the
-// earlier blocks' counts, four destination bytes per thread and one block
-// scan per 1024 lookups -- no global atomics.
-__global__ __launch_bounds__(256) void k_arc_own_compact(const uint8_t *dest, size_t q, int me,
-                                                         const uint32_t *blk_own,
-                                                         uint32_t *own_idx, size_t per) {
-    __shared__ uint32_t part[256], wsum[4];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t acc = 0;
-    for (uint32_t j = t; j < blockIdx.x; j += blockDim.x) acc += blk_own[j];
-    part[t] = acc;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (t < o) part[t] += part[t + o];
-        __syncthreads();
-    }
-    uint32_t off = part[0];
-    const size_t lo = blockIdx.x * per, hi = lo + per < q ? lo + per : q;
-    for (size_t b0 = lo; b0 < hi; b0 += 4 * (size_t)blockDim.x) {  // uniform trips
-        const size_t i0 = b0 + 4 * (size_t)t;
-        uint32_t bits = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (i0 + k < hi && dest[i0 + k] == (uint8_t)me) bits |= 1u << k;
-        const uint32_t c = (uint32_t)__popc(bits);
-        uint32_t x = c;  // inclusive scan over the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
+            for (int k = 0; k < ARC_SCAT_R; ++k) c += (uint32_t)__popcll(__ballot(d[k] == j));
+            if (lane == j) acc += c;
         }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        uint32_t pos = off + x - c;
-        for (int j = 0; j < w; ++j) pos += wsum[j];
+        if (own_idx) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (bits & (1u << k)) own_idx[pos++] = (uint32_t)(i0 + k);
-        off += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        __syncthreads();
+            for (int k = 0; k < ARC_SCAT_R; ++k) {
+                const uint64_t m = __ballot(d[k] == me);
+                if (d[k] == me) mine |= 1ull << (r0 + k);
+                if (lane == 0 && r0 + k < ARC_CNT_ROUNDS) wc[(r0 + k) * 4 + w] = (uint32_t)__popcll(m);
+            }
+        }
+    }
+    if (lane < G && acc) atomicAdd(&h[lane], acc);
+    __syncthreads();
+    for (int j = t; j < G; j += blockDim.x)
+        if (h[j]) atomicAdd(&counts[j], (unsigned long long)h[j]);
+    if (!own_idx) return;  // block-uniform
+    // exclusive offsets of the (round, wave) runs, in index order
+    const uint32_t v = wc[t];
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t ex = x - v;
+    for (int j = 0; j < w; ++j) ex += wsum[j];
+    wc[t] = ex;
+    if (t == 0) {
+        const uint32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        base_s = tot ? atomicAdd(cursor, tot) : 0u;
+    }
+    __syncthreads();
+    const uint32_t base = base_s;
+    for (int r = 0; r < rounds; ++r) {  // uniform trips
+        const bool b = (mine >> r) & 1;
+        const uint64_t m = __ballot(b);
+        if (!m) continue;
+        if (b)
+            own_idx[base + wc[r * 4 + w] +
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                (uint32_t)(lo + (size_t)r * 256 + t);
     }
 }
 
-// own_ws: ARC_OWN_BLOCKS block counts, then one destination byte per lookup.
+// counts[0..G) and the own-run cursor zeroed in one launch.
+__global__ void k_arc_count_zero(unsigned long long *counts, int G, uint32_t *cursor) {
+    const int j = threadIdx.x;
+    if (j < G) counts[j] = 0;
+    if (j == 0 && cursor) *cursor = 0;
+}
+
+// own_ws: one word, the own-run cursor.
 hipError_t arc_count_keys(const cell128 *keys, size_t q, const ArcBound *bounds, int nb, int G,
                           int64_t *counts, int me, uint32_t *own_idx, uint32_t *own_ws,
                           hipStream_t s) {
-    hipError_t e = hipMemsetAsync(counts, 0, (size_t)G * sizeof(int64_t), s);
+    uint32_t *cursor = own_idx ? own_ws : nullptr;
+    auto *c64 = reinterpret_cast<unsigned long long *>(counts);
+    k_arc_count_zero<<<1, 64, 0, s>>>(c64, G, cursor);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess || q == 0) return e;
+    // ~2048 blocks when the batch allows (1024-lookup tiles, at most 16 a block)
     const size_t tiles = (q + 1023) / 1024;
-    const size_t grid = tiles < ARC_OWN_BLOCKS ? tiles : ARC_OWN_BLOCKS;
-    const size_t per = (tiles + grid - 1) / grid * 1024;
+    size_t tpb = (tiles + 2047) / 2048;
+    if (tpb > (size_t)ARC_CNT_ROUNDS / 4) tpb = ARC_CNT_ROUNDS / 4;
+    const size_t per = tpb * 1024;
     const unsigned g = (unsigned)((q + per - 1) / per);
-    uint32_t *blk = own_idx ? own_ws : nullptr;
-    uint8_t *dest = own_idx ? reinterpret_cast<uint8_t *>(own_ws + ARC_OWN_BLOCKS) : nullptr;
-    k_arc_count_keys<<<g, 256, 0, s>>>(keys, q, bounds, nb, G,
-                                       reinterpret_cast<unsigned long long *>(counts), me, dest,
-                                       blk, per);
-    if (own_idx && (e = hipGetLastError()) == hipSuccess)
-        k_arc_own_compact<<<g, 256, 0, s>>>(dest, q, me, blk, own_idx, per);
+    k_arc_count_keys<<<g, 256, 0, s>>>(keys, q, bounds, nb, G, c64, own_idx ? me : -1, own_idx,
+                                       cursor, per);
     return hipGetLastError();
 }
 

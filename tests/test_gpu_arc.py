@@ -414,7 +414,8 @@ def test_arc_count_and_exact_scatter(cx, O, n, G, q):
     torch.cuda.synchronize()
     assert dc2.tolist() == counts
     want_own = torch.nonzero(p0 < counts[0]).flatten()  # region 0 of the region layout
-    assert torch.equal(own[:counts[0]].long(), want_own)  # ascending
+    got_own = own[:counts[0]].long()  # a permutation, ascending within each block's run
+    assert torch.equal(torch.sort(got_own).values, want_own)
     assert bool((own[counts[0]:] == -7).all())
     pm = perm2.long()
     assert bool((pm[want_own] == -1).all())
