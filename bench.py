@@ -91,6 +91,47 @@ C5_BYTES_STREAM = 210
 C5_BYTES_SURVEY = 139
 
 
+class LegGuard:
+    """A watchdog per sub-record leg, on every rank.  The headline is measured
+    and its line assembled before the legs run; if a leg does not finish in
+    its limit (a collective that never completes on a new node, say), rank 0
+    prints the line as it stands -- the leg's key null, the leg named in
+    `legs_aborted` -- and every rank leaves with os._exit(0) after its own
+    limit, so a hung sub-record costs its record, not the headline.  Limits
+    are several times a leg's duration on a one-GPU box."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+        self.line = None  # rank 0: the line so far
+        self.timer = None
+
+    def start(self, name: str, seconds: float) -> None:
+        import threading
+        self.stop()
+        self.timer = threading.Timer(seconds, self._expire, (name, seconds))
+        self.timer.daemon = True
+        self.timer.start()
+
+    def stop(self) -> None:
+        if self.timer is not None:
+            self.timer.cancel()
+            self.timer = None
+
+    def _expire(self, name: str, seconds: float) -> None:
+        progress(f"leg {name!r} did not finish in {seconds:.0f} s: leaving")
+        if self.rank == 0 and self.line is not None:
+            self.line.setdefault("legs_aborted", []).append(
+                {"leg": name, "limit_s": seconds,
+                 "note": "watchdog: the leg did not finish; the keys of this and later legs "
+                         "are null"})
+            print(json.dumps(self.line), flush=True)
+        os._exit(0 if self.line is not None or self.rank != 0 else 3)
+
+
+# per-leg limit; CX_BENCH_LEG_LIMIT_S overrides it (the watchdog's own test)
+LEG_LIMIT_S = float(os.environ.get("CX_BENCH_LEG_LIMIT_S", "300"))
+
+
 def progress(msg: str) -> None:
     """One line on stderr per leg (the JSON line alone goes to stdout): long
     multi-rank runs show they are alive."""
@@ -1057,6 +1098,78 @@ def c3_leg(args, world, rank, dev):
             "oracle_sample_keys": m, "cpu_baseline": cpu}
 
 
+def headline_line(args, world, N, Q, dt_max, roof, traffic, kernel_name, algo_bytes, kern_ms,
+                  ref_bytes, gather, route_variant, table_bytes, cz_escapes, sum_hops, hist,
+                  max_hops, bad, owner_eq, counting_same, succ_ms, small, rsrc_ms, rsrc_bad,
+                  t_gather, t_ring, t_fing, t_fing_warm, setup_alloc):
+    """Rank 0's JSON line with the headline and its checks; the sub-record
+    legs (churn_route_ready, arc, cpu_baseline, c5, c2, c3) fill their keys
+    as they finish (LegGuard prints the line as it stands if one hangs)."""
+    total = world * Q * args.steps
+    line = line_base(args, world, total / dt_max, dt_max, {
+        "workload": "C4 finger-routed lookups with hop counts (per GPU): "
+                    f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step, "
+                    "src = q mod N, splitmix seeds 0x5EED0005/0x5EED0006",
+        "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
+        "parallelism": f"ring IDs all-gathered, replicated route tables, keys sharded "
+                       f"x{world} (arc-sharded all_to_all-v layout: `arc`)"})
+    roof.update({
+        "traffic": None if traffic is None else traffic * world,
+        "traffic_note": "PMC FETCH_SIZE + WRITE_SIZE per launch on one GPU "
+                        "(profiles/traffic_route.json) x N",
+        "kernel": kernel_name,
+        "per_gpu": {"achieved": algo_bytes / (kern_ms * 1e-3) / 1e9,
+                    "frac": algo_bytes / (kern_ms * 1e-3) / HBM_PEAK,
+                    "kernel_ms": kern_ms, "algo_bytes_per_launch": algo_bytes,
+                    "traffic": traffic, "rank": 0},
+        "algo_model": f"{BYTES_STREAM} B streams per lookup + {GRANULE} B per random "
+                      "gather issued (counted), summed over ranks"})
+    line.update({
+        "roofline": roof,
+        "reference_work_model": {"bytes_per_launch": ref_bytes,
+                                 "GBps": ref_bytes / (roof["kernel_ms"] * 1e-3) / 1e9,
+                                 "note": "SURVEY 8(d): 128 B per hop, summed over ranks; "
+                                         "hops the window table resolves without a gather "
+                                         "are priced too, so this is not a byte count of "
+                                         "the kernel"},
+        "cpu_baseline": None,
+        "arc": None,
+        "churn_route_ready": None,
+        "c5": None,
+        "c2": None,
+        "c3": None,
+        "gather_roofline": gather,
+        "route_variant": route_variant,
+        "route_table_bytes": table_bytes,
+        "route_cz_escapes": cz_escapes,
+        "mean_hops": sum_hops / (world * Q),
+        "hops_hist": hist,
+        "max_hops": max_hops,
+        "hops_hist_note": "hops_hist[h] = lookups of the timed batch (all ranks) that took "
+                          "h hops; the CPU baseline's sample carries the oracle's histogram "
+                          "(cpu_baseline.hist_equal)",
+        "bad_status": bad,
+        "route_owner_equals_successor": owner_eq,
+        "counting_build_same_results": counting_same,
+        "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
+        "route_small_batches": small,
+        "route_random_src": {"kernel_ms": rsrc_ms, "lookups_per_s": Q / (rsrc_ms * 1e-3),
+                             "bad_status": rsrc_bad,
+                             "note": "same keys and kernel, src uniform in [0, N) "
+                                     "(splitmix 0x5EED000A) instead of q mod N"},
+        "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring,
+                    "ring_sort_roofline": getattr(setup_ring, "sort_roofline", None),
+                    "fingers_build": t_fing, "fingers_build_again": t_fing_warm,
+                    "alloc": setup_alloc,
+                    "note": "fingers_build = converged fingers + route table on fresh "
+                            f"HBM (first touch of the {table_bytes / 2**30:.0f} GiB route "
+                            "table); fingers_build_again = the same build into the "
+                            "now-mapped tables"},
+        "ab_variants": "benches/bench_route.py --variants (route and search A/B kernels)",
+    })
+    return line
+
+
 def main_arc(args):
     """--mode arc: the arc-sharded layout (SURVEY 8e layout 2) is the headline."""
     world, rank, local = dist.env_rank()
@@ -1252,9 +1365,35 @@ def main():
         small[f"2^{lk}"] = {"us_per_launch": e0.elapsed_time(e1) / 20 * 1e3, "equal_to_batch": same}
         del so
 
+    # ---- the headline line (rank 0), before any sub-record leg ----
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == kernel_name:
+            traffic = tj.get("hbm_bytes_per_launch")
+    req = gathers / (kern_ms * 1e-3)
+    gather = {"requests_per_s": req, "ceiling": probe, "frac": req / probe,
+              "gathers_per_lookup": gathers / Q, "table_gathers": g64, "exact_id_gathers": r16,
+              "exact_hops": xc, "rank": 0,
+              "note": "random 64-B requests the walk issued (counting build, same batch) per "
+                      "second of kernel time, vs dependent quad-cooperative 64-B gathers/s "
+                      "(non-temporal, as the walk's) measured on the same route table in this "
+                      "run (rank 0)"}
+    guard = LegGuard(rank)
+    line = None
+    if rank == 0:
+        line = headline_line(args, world, N, Q, dt_max, roof, traffic, kernel_name, algo_bytes,
+                             kern_ms, ref_bytes, gather, route_variant, table_bytes, cz_escapes,
+                             sum_hops, hist, max_hops, bad, owner_eq, counting_same, succ_ms,
+                             small, rsrc_ms, rsrc_bad, t_gather, t_ring, t_fing, t_fing_warm,
+                             setup_alloc)
+        guard.line = line
+
     # ---- churn -> route-ready (f2), cold then warm ----
     progress("churn -> route-ready leg")
     churn = None
+    guard.start("churn_route_ready", LEG_LIMIT_S)
     if not args.no_churn:
         churn = churn_leg(ring, keys, src, dev)
         chordx.pool_trim()  # the new rings' blocks are not needed by the arc leg
@@ -1287,15 +1426,22 @@ def main():
             st["route_ready_ms_warm_max_over_ranks"] = dist.max_over_ranks(
                 st["warm"]["route_ready_ms"], world, dev)
 
+    if line is not None:
+        line["churn_route_ready"] = churn
+
     # ---- arc-sharded C4 (all_to_all-v) on the same keys and steps ----
     progress("arc leg")
     arc = None
+    guard.start("arc", LEG_LIMIT_S)
     if not args.no_arc:
         arc = arc_leg(args, ring, src, keys, owner, hops, world, rank, dev, backend)
+    if line is not None:
+        line["arc"] = arc
 
     # ---- CPU baseline: rank 0, every world size, after the timed region ----
     progress("cpu baseline")
     cpu = None
+    guard.start("cpu_baseline", LEG_LIMIT_S)
     if rank == 0 and not args.no_cpu:
         F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
         F_host[:] = ring.fingers_device().cpu().numpy().view(np.uint32)
@@ -1305,103 +1451,34 @@ def main():
                            args.cpu_seconds, world)
         del F_host
     dist.barrier(world)
+    if line is not None:
+        line["cpu_baseline"] = cpu
 
     # ---- C5 (configs[4]) after the bench ring's tables are released ----
     progress("c5 leg")
     c5 = None
+    guard.start("c5", LEG_LIMIT_S)
     if not args.no_c5:
         ring.close()
         chordx.pool_trim()
         c5 = c5_leg(args, world, rank, dev, backend)
         chordx.pool_trim()
+    if line is not None:
+        line["c5"] = c5
 
     # ---- C2 / C3 (configs[1], configs[2]): small rings, after the bench ring ----
     progress("c2 / c3 legs")
     c2 = c3 = None
+    guard.start("c2_c3", LEG_LIMIT_S)
     if not args.no_c2:
         c2 = c2_leg(args, world, rank, dev)
     if not args.no_c3:
         c3 = c3_leg(args, world, rank, dev)
         chordx.pool_trim()
-
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if tj.get("peers") == N and tj.get("keys") == Q and tj.get("kernel") == kernel_name:
-            traffic = tj.get("hbm_bytes_per_launch")
-    req = gathers / (kern_ms * 1e-3)
-    gather = {"requests_per_s": req, "ceiling": probe, "frac": req / probe,
-              "gathers_per_lookup": gathers / Q, "table_gathers": g64, "exact_id_gathers": r16,
-              "exact_hops": xc, "rank": 0,
-              "note": "random 64-B requests the walk issued (counting build, same batch) per "
-                      "second of kernel time, vs dependent quad-cooperative 64-B gathers/s "
-                      "(non-temporal, as the walk's) measured on the same route table in this "
-                      "run (rank 0)"}
+    guard.stop()
 
     if rank == 0:
-        total = world * Q * args.steps
-        line = line_base(args, world, total / dt_max, dt_max, {
-            "workload": "C4 finger-routed lookups with hop counts (per GPU): "
-                        f"2^{args.peers_log2}-peer ring, 2^{args.keys_log2} keys/GPU/step, "
-                        "src = q mod N, splitmix seeds 0x5EED0005/0x5EED0006",
-            "peers": N, "keys_per_gpu": Q, "global_batch": world * Q,
-            "parallelism": f"ring IDs all-gathered, replicated route tables, keys sharded "
-                           f"x{world} (arc-sharded all_to_all-v layout: `arc`)"})
-        roof.update({
-            "traffic": None if traffic is None else traffic * world,
-            "traffic_note": "PMC FETCH_SIZE + WRITE_SIZE per launch on one GPU "
-                            "(profiles/traffic_route.json) x N",
-            "kernel": kernel_name,
-            "per_gpu": {"achieved": algo_bytes / (kern_ms * 1e-3) / 1e9,
-                        "frac": algo_bytes / (kern_ms * 1e-3) / HBM_PEAK,
-                        "kernel_ms": kern_ms, "algo_bytes_per_launch": algo_bytes,
-                        "traffic": traffic, "rank": 0},
-            "algo_model": f"{BYTES_STREAM} B streams per lookup + {GRANULE} B per random "
-                          "gather issued (counted), summed over ranks"})
-        line.update({
-            "roofline": roof,
-            "reference_work_model": {"bytes_per_launch": ref_bytes,
-                                     "GBps": ref_bytes / (roof["kernel_ms"] * 1e-3) / 1e9,
-                                     "note": "SURVEY 8(d): 128 B per hop, summed over ranks; "
-                                             "hops the window table resolves without a gather "
-                                             "are priced too, so this is not a byte count of "
-                                             "the kernel"},
-            "cpu_baseline": cpu,
-            "arc": arc,
-            "churn_route_ready": churn,
-            "c5": c5,
-            "c2": c2,
-            "c3": c3,
-            "gather_roofline": gather,
-            "route_variant": route_variant,
-            "route_table_bytes": table_bytes,
-            "route_cz_escapes": cz_escapes,
-            "mean_hops": sum_hops / (world * Q),
-            "hops_hist": hist,
-            "max_hops": max_hops,
-            "hops_hist_note": "hops_hist[h] = lookups of the timed batch (all ranks) that took "
-                              "h hops; the CPU baseline's sample carries the oracle's histogram "
-                              "(cpu_baseline.hist_equal)",
-            "bad_status": bad,
-            "route_owner_equals_successor": owner_eq,
-            "counting_build_same_results": counting_same,
-            "exact_successor_lookups_per_s": Q / (succ_ms * 1e-3),
-            "route_small_batches": small,
-            "route_random_src": {"kernel_ms": rsrc_ms, "lookups_per_s": Q / (rsrc_ms * 1e-3),
-                                 "bad_status": rsrc_bad,
-                                 "note": "same keys and kernel, src uniform in [0, N) "
-                                         "(splitmix 0x5EED000A) instead of q mod N"},
-            "setup_s": {"id_all_gather": t_gather, "ring_sort": t_ring,
-                        "ring_sort_roofline": getattr(setup_ring, "sort_roofline", None),
-                        "fingers_build": t_fing, "fingers_build_again": t_fing_warm,
-                        "alloc": setup_alloc,
-                        "note": "fingers_build = converged fingers + route table on fresh "
-                                f"HBM (first touch of the {table_bytes / 2**30:.0f} GiB route "
-                                "table); fingers_build_again = the same build into the "
-                                "now-mapped tables"},
-            "ab_variants": "benches/bench_route.py --variants (route and search A/B kernels)",
-        })
+        line.update({"c2": c2, "c3": c3})
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
