@@ -352,10 +352,12 @@ class Ring:
 
     def set_search_variant(self, v: int):
         """Internal A/B switch: 0 = Eytzinger (LDS top levels), 1 = bucket directory
-        (default), 2 = wave-cooperative 16-ary tree (ballot/popcount), 3 =
-        wave-cooperative Eytzinger (16 lanes a query, four levels per ballot);
-        2 and 3 serve successor and predecessor only, the other searches keep
-        the directory."""
+        (default; successor / predecessor of >= 2^16 keys and >= 4 n on a ring
+        whose slice table fits LDS take the LDS slice table), 2 = wave-cooperative
+        16-ary tree (ballot/popcount), 3 = wave-cooperative Eytzinger (16 lanes a
+        query, four levels per ballot), 4 = the LDS slice table whenever the ring
+        fits (any batch), 5 = directory only; 2 to 5 serve successor and
+        predecessor only, the other searches keep the directory."""
         f = L.lib().cxi_set_search_variant
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.check(f(self._h, v))

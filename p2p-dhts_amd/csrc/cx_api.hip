@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <initializer_list>
+#include <algorithm>
 #include <atomic>
 #include <memory>
 #include <mutex>
@@ -450,8 +451,13 @@ struct cx_ring {
     uint4 *d_dir = nullptr;        // bucket directory [2^dir_k] (16 B entries)
     uint32_t *d_ring_key = nullptr; // ID slices [n] of the streaming finger build
     int dir_k = 1;
-    int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory,
-                                   // 2: wave-cooperative 16-ary tree (successor / predecessor)
+    int search_variant = 1;        // 0: Eytzinger (LDS top levels), 1: bucket directory
+                                   // (successor / predecessor of large batches on rings that
+                                   // fit LDS: the LDS slice table), 2: wave-cooperative 16-ary
+                                   // tree, 3: wave-cooperative Eytzinger, 4: LDS slice table
+                                   // whenever it fits, 5: directory only (1 without LDS)
+    void *d_sltab = nullptr;       // LDS slice table (variants 1 / 4, lazy; cxk::slice_tab_*)
+    int sl_b = 0, sl_steps = 0;
     cell128 *d_stree = nullptr;    // levels 1.. of the 16-ary tree (variant 2, lazy)
     uint32_t *d_eyt_rank = nullptr; // Eytzinger node -> sorted index (variant 3, lazy)
     int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
@@ -624,6 +630,7 @@ void free_ring(cx_ring *r) {
     table_free(r->device, r->d_cz, ent * 128);
     (void)hipFree(r->d_stree);
     (void)hipFree(r->d_eyt_rank);
+    (void)hipFree(r->d_sltab);
     table_free(r->device, r->d_ring_ext, (r->n + 1) * sizeof(cell128));
     (void)hipFree(r->d_min_keys);
     (void)hipFree(r->d_preds);
@@ -1041,6 +1048,50 @@ int eyt_rank_view(cx_ring *r, hipStream_t s) {
     return CX_OK;
 }
 
+// The LDS slice table (cxk::slice_tab_*) of a ring that fits LDS, built on
+// first use: b = ceil(log2 n) - 5 bucket bits (about 32 peers a bucket, 1 to
+// 12), the search rounds from its largest bucket.  *ok = false when the ring
+// does not fit (or has no HBM for it): the caller searches the directory.
+int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
+    *ok = false;
+    if (r->d_sltab) {
+        *ok = true;
+        return CX_OK;
+    }
+    int lg = 0;
+    while (((size_t)1 << lg) < r->n) ++lg;
+    const int b = lg - 5 < 1 ? 1 : (lg - 5 > 12 ? 12 : lg - 5);
+    const size_t bytes = cxk::slice_tab_bytes(r->n, b);
+    if (bytes > cxk::SLICE_TAB_MAX) return CX_OK;
+    void *tab = nullptr;
+    if (dev_malloc(&tab, bytes) != hipSuccess) return CX_OK;
+    const size_t nb = ((size_t)1 << b) + 1;
+    std::vector<uint32_t> off(nb);
+    hipError_t e = cxk::slice_tab_build(r->d_ring, r->n, b, tab, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(off.data(), tab, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        (void)hipFree(tab);
+        return fail(CX_E_HIP, hipGetErrorString(e));
+    }
+    uint32_t mx = 0;
+    for (size_t t = 0; t + 1 < nb; ++t) mx = std::max(mx, off[t + 1] - off[t]);
+    r->sl_steps = mx ? 32 - __builtin_clz(mx) : 0;
+    r->sl_b = b;
+    r->d_sltab = tab;
+    *ok = true;
+    return CX_OK;
+}
+
+// Variant 1 takes the LDS table for batches of >= 2^16 keys and >= 4 n (each
+// resident block stages the whole table once); variant 4 whenever it fits.
+bool slice_wanted(const cx_ring *r, size_t q) {
+    if (r->search_variant == 4) return true;
+    return r->search_variant == 1 && q >= ((size_t)1 << 16) && q >= 4 * r->n &&
+           cxk::slice_tab_bytes(r->n, 12) <= cxk::SLICE_TAB_MAX;
+}
+
 int stree_view(cx_ring *r, cxk::STreeView &st, hipStream_t s) {
     st = cxk::stree_plan(r->d_ring, r->n, r->d_stree);
     if (!r->d_stree && st.words) {
@@ -1075,7 +1126,15 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
         CX_HIP(cxk::successor_eyt16(ring->eyt(), ring->d_eyt_rank,
                                     reinterpret_cast<const cell128 *>(dk), q, dout, false, s));
     } else {
-        CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+        bool lds = false;
+        if (slice_wanted(ring, q) && (rc = slice_view(const_cast<cx_ring *>(ring), s, &lds)))
+            return rc;
+        if (lds)
+            CX_HIP(cxk::successor_lds(ring->d_sltab, ring->sl_b, ring->sl_steps, ring->d_ring,
+                                      ring->n, reinterpret_cast<const cell128 *>(dk), q, dout,
+                                      false, s));
+        else
+            CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     }
     return finish_out(owner, dout, q, memkind, s);
 }
@@ -1170,7 +1229,15 @@ int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t 
         CX_HIP(cxk::successor_eyt16(ring->eyt(), ring->d_eyt_rank,
                                     reinterpret_cast<const cell128 *>(dk), q, dout, true, s));
     } else {
-        CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
+        bool lds = false;
+        if (slice_wanted(ring, q) && (rc = slice_view(const_cast<cx_ring *>(ring), s, &lds)))
+            return rc;
+        if (lds)
+            CX_HIP(cxk::successor_lds(ring->d_sltab, ring->sl_b, ring->sl_steps, ring->d_ring,
+                                      ring->n, reinterpret_cast<const cell128 *>(dk), q, dout,
+                                      true, s));
+        else
+            CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     }
     return finish_out(pred, dout, q, memkind, s);
 }
@@ -2714,13 +2781,15 @@ int cxi_set_churn_variant(cx_ring *ring, int variant) {
     return CX_OK;
 }
 
-// 0 = Eytzinger search with LDS-staged top levels, 1 = bucket directory (default),
-// 2 = wave-cooperative 16-ary tree, 3 = wave-cooperative Eytzinger (16 lanes a
-// query, four levels per ballot) for cx_successor / cx_predecessor (variants
-// 2 and 3: the other searches keep the directory).
+// 0 = Eytzinger search with LDS-staged top levels, 1 = bucket directory (default;
+// large batches on rings that fit LDS: the LDS slice table), 2 = wave-cooperative
+// 16-ary tree, 3 = wave-cooperative Eytzinger (16 lanes a query, four levels per
+// ballot), 4 = LDS slice table whenever the ring fits, 5 = directory only, for
+// cx_successor / cx_predecessor (variants 2 to 5: the other searches keep the
+// directory).
 int cxi_set_search_variant(cx_ring *ring, int variant) {
     CX_CHECK(ring != nullptr, CX_E_INVALID, "null ring");
-    CX_CHECK(variant >= 0 && variant <= 3, CX_E_INVALID, "variant must be 0, 1, 2 or 3");
+    CX_CHECK(variant >= 0 && variant <= 5, CX_E_INVALID, "variant must be 0 to 5");
     if (variant == 0 || variant == 3) {
         int rc = use_device(ring);
         if (rc) return rc;

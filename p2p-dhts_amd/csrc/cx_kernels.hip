@@ -685,6 +685,179 @@ hipError_t predecessor(const SearchView &sv, const cell128 *keys, size_t q, uint
 }
 
 // ---------------------------------------------------------------------------
+// Rings that fit LDS (a7 / GetPredecessor, search variants 1 (automatic) and
+// 4): one table per ring, staged whole into every block -- the bucket
+// offsets off[t] = first index whose top b ID bits are >= t (t = 0 .. 2^b),
+// then the 16-bit slices s(p) = ID bits [128 - b - 16, 128 - b) of every
+// peer, each part padded to 16 B.  Within bucket t the slices are sorted, so
+// a key's successor is the lower bound of its own slice in [off[t],
+// off[t + 1]) -- exact unless that peer shares the key's top b + 16 bits
+// (probability n / 2^(b + 16), 2^-12 at C2), which reads the full IDs.  One
+// key line and LDS instead of a random directory line (and sometimes a ring
+// line) per key: the directory search of a 2^20-key batch is L2-request-bound
+// (profiles/r06/c2_pmc/).
+// ---------------------------------------------------------------------------
+__global__ void k_slice_tab_build(const cell128 *ring, uint32_t n, int b, uint32_t *off,
+                                  uint16_t *sl) {
+    const uint32_t nb = (1u << b) + 1u;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (size_t)n + nb;
+         i += (size_t)gridDim.x * blockDim.x) {
+        if (i < n) {
+            sl[i] = (uint16_t)(top_bits(ld128(ring + i), b + 16) & 0xFFFFu);
+        } else {  // off[t]: lower bound of t over the top b bits
+            const uint64_t t = i - n;
+            uint32_t a = 0, z = n;
+            while (a < z) {
+                const uint32_t m = a + (z - a) / 2;
+                if (top_bits(ld128(ring + m), b) < t) a = m + 1;
+                else z = m;
+            }
+            off[t] = a;
+        }
+    }
+}
+
+size_t slice_tab_bytes(size_t n, int b) {
+    const size_t nb = ((size_t)1 << b) + 1;
+    // whole 1-KiB runs (one LDS-DMA instruction per wave moves 1 KiB)
+    return ((nb * 4 + 15) / 16 * 16 + (n * 2 + 15) / 16 * 16 + 1023) / 1024 * 1024;
+}
+
+hipError_t slice_tab_build(const cell128 *ring, size_t n, int b, void *tab, hipStream_t s) {
+    const size_t nb = ((size_t)1 << b) + 1;
+    uint32_t *off = reinterpret_cast<uint32_t *>(tab);
+    uint16_t *sl = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(tab) + (nb * 4 + 15) / 16 * 16);
+    hipError_t e = hipMemsetAsync(tab, 0, slice_tab_bytes(n, b), s);  // the padding too
+    if (e != hipSuccess) return e;
+    k_slice_tab_build<<<cx_grid(n + nb, 256), 256, 0, s>>>(ring, (uint32_t)n, b, off, sl);
+    return hipGetLastError();
+}
+
+constexpr int SL_BLOCK = 1024;
+constexpr int SL_KEYS = 4;  // keys per lane per trip, their searches interleaved
+
+// steps: binary-search rounds that cover the largest bucket (ceil(log2(max + 1))).
+template <bool PRED>
+__global__ __launch_bounds__(SL_BLOCK) void k_successor_lds(const uint4 *tab, uint32_t tab_v4,
+                                                            int b, int steps, uint32_t n,
+                                                            const cell128 *ring,
+                                                            const cell128 *keys, size_t q,
+                                                            uint32_t *out) {
+    extern __shared__ uint4 lds4[];
+    const uint32_t *loff = reinterpret_cast<const uint32_t *>(lds4);
+    const uint16_t *lsl = reinterpret_cast<const uint16_t *>(
+        reinterpret_cast<const char *>(lds4) + ((((size_t)1 << b) + 1) * 4 + 15) / 16 * 16);
+    const size_t per = (size_t)SL_BLOCK * SL_KEYS;
+    size_t c0 = blockIdx.x * per;
+    // this block's first keys are in flight while the table lands in LDS
+    u128 x[SL_KEYS];
+#pragma unroll
+    for (int k = 0; k < SL_KEYS; ++k) {
+        const size_t i = c0 + (size_t)k * SL_BLOCK + threadIdx.x;
+        x[k] = i < q ? ld128(keys + i) : (u128)0;
+    }
+    // every 16-B piece of the table straight into LDS (LDS-DMA, no VGPRs),
+    // all issued before one wait: lane j of wave w moves piece it * SL_BLOCK +
+    // w * 64 + j to the same LDS offset (tab_v4: a multiple of 64 pieces)
+    const uint32_t wbase = threadIdx.x & ~63u;
+#pragma unroll
+    for (uint32_t it = 0; it < (uint32_t)((SLICE_TAB_MAX / 16 + SL_BLOCK - 1) / SL_BLOCK); ++it) {
+        const uint32_t v0 = it * SL_BLOCK + wbase;  // wave-uniform
+        if (v0 < tab_v4) {
+            const uint32_t v = v0 + (threadIdx.x & 63u);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(tab + v),
+                (__attribute__((address_space(3))) void *)(lds4 + v0), 16, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (; c0 < q; c0 += (size_t)gridDim.x * per) {
+        uint32_t a[SL_KEYS], z[SL_KEYS], e[SL_KEYS], xs[SL_KEYS];
+#pragma unroll
+        for (int k = 0; k < SL_KEYS; ++k) {
+            const uint32_t t = (uint32_t)top_bits(x[k], b);
+            a[k] = loff[t];
+            z[k] = e[k] = loff[t + 1];
+            xs[k] = (uint32_t)(top_bits(x[k], b + 16) & 0xFFFFu);
+        }
+        for (int it = 0; it < steps; ++it) {  // every lane the same rounds
+#pragma unroll
+            for (int k = 0; k < SL_KEYS; ++k) {
+                const uint32_t m = (a[k] + z[k]) >> 1;
+                const bool go = a[k] < z[k];
+                const uint32_t sv = lsl[go ? m : 0];
+                a[k] = go && sv < xs[k] ? m + 1 : a[k];
+                z[k] = go && !(sv < xs[k]) ? m : z[k];
+            }
+        }
+        u128 xn[SL_KEYS];
+        const size_t c1 = c0 + (size_t)gridDim.x * per;
+#pragma unroll
+        for (int k = 0; k < SL_KEYS; ++k) {
+            // peers sharing the key's top b + 16 bits (rare): their run of equal
+            // slices, then the full IDs, both by binary search (clustered rings
+            // put whole buckets in one run)
+            if (a[k] < e[k] && lsl[a[k]] == xs[k]) {
+                uint32_t u = a[k] + 1, w = e[k];
+                while (u < w) {
+                    const uint32_t m = (u + w) >> 1;
+                    if (lsl[m] <= xs[k]) u = m + 1;
+                    else w = m;
+                }
+                uint32_t lo = a[k];
+                while (lo < u) {
+                    const uint32_t m = (lo + u) >> 1;
+                    if (ld128(ring + m) < x[k]) lo = m + 1;
+                    else u = m;
+                }
+                a[k] = lo;
+            }
+            const size_t i = c0 + (size_t)k * SL_BLOCK + threadIdx.x;
+            const size_t i1 = c1 + (size_t)k * SL_BLOCK + threadIdx.x;
+            xn[k] = i1 < q ? ld128(keys + i1) : (u128)0;  // the next trip's keys
+            if (i < q) {
+                const uint32_t s = a[k] == n ? 0u : a[k];
+                out[i] = PRED ? (s == 0 ? n - 1 : s - 1) : s;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SL_KEYS; ++k) x[k] = xn[k];
+    }
+}
+
+hipError_t successor_lds(const void *tab, int b, int steps, const cell128 *ring, size_t n,
+                         const cell128 *keys, size_t q, uint32_t *out, bool pred,
+                         hipStream_t s) {
+    if (q == 0) return hipSuccess;
+    const size_t bytes = slice_tab_bytes(n, b);
+    if (bytes > SLICE_TAB_MAX || n == 0 || n > 0xFFFFFFFFull || b < 1 || b > 12 || steps < 0)
+        return hipErrorInvalidValue;
+    int dev = 0, cus = 256, per_cu = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    auto kern = pred ? k_successor_lds<true> : k_successor_lds<false>;
+    static const bool lds_ok = [] {  // dynamic LDS above 64 KiB, once per kernel
+        const int lim = (int)SLICE_TAB_MAX;
+        return hipFuncSetAttribute(reinterpret_cast<const void *>(k_successor_lds<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess &&
+               hipFuncSetAttribute(reinterpret_cast<const void *>(k_successor_lds<true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess;
+    }();
+    (void)lds_ok;  // a runtime without the attribute takes the launch as is
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SL_BLOCK, bytes) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    // one resident round of blocks (each stages the table once)
+    size_t g = (q + (size_t)SL_BLOCK * SL_KEYS - 1) / ((size_t)SL_BLOCK * SL_KEYS);
+    if (g > (size_t)cus * per_cu) g = (size_t)cus * per_cu;
+    kern<<<(unsigned)g, SL_BLOCK, bytes, s>>>(reinterpret_cast<const uint4 *>(tab),
+                                                (uint32_t)(bytes / 16), b, steps, (uint32_t)n,
+                                                ring, keys, q, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Search variant 2: wave-cooperative 16-ary search (static S+-tree over the
 // sorted ring).  Level 0 is the ring; level l >= 1 holds every 16^l-th ID,
 // S_l[j] = ring[j * 16^l], so block c of level l (16 consecutive entries) is

@@ -103,6 +103,15 @@ size_t fingers_workspace_bytes(size_t n);
 int finger_key_shift(size_t n);
 hipError_t predecessor(const SearchView &ev, const cell128 *keys, size_t q, uint32_t *pred,
                        hipStream_t s);
+// LDS slice tables of rings that fit LDS (search variants 1 and 4): the
+// table's bytes for n peers and b bucket bits, its build, and the search
+// (steps = binary-search rounds covering the largest bucket).
+constexpr size_t SLICE_TAB_MAX = 160 * 1024;
+size_t slice_tab_bytes(size_t n, int b);
+hipError_t slice_tab_build(const cell128 *ring, size_t n, int b, void *tab, hipStream_t s);
+hipError_t successor_lds(const void *tab, int b, int steps, const cell128 *ring, size_t n,
+                         const cell128 *keys, size_t q, uint32_t *out, bool pred,
+                         hipStream_t s);
 hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32_t *ring_key,
                          void *ws, uint32_t *F, hipStream_t s, uint32_t *FT = nullptr,
                          int Lft = 0, bool *planes_done = nullptr);

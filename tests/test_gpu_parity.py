@@ -91,8 +91,9 @@ def test_ring_build_sort_paths(cx, O, kind):
 
 
 # ---------------------------------------------------------------- a5/a7 successor
-@pytest.mark.parametrize("search", [0, 1, 2, 3])
-@pytest.mark.parametrize("n", [1, 2, 3, 8, 16, 17, 256, 257, 1000, 4095, 4096, 65537, 70000])
+@pytest.mark.parametrize("search", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 16, 17, 256, 257, 1000, 4095, 4096, 65537, 70000,
+                               100000])
 def test_successor(cx, O, n, search):
     ids = edge_ring(O, n, 77 + n)
     ring = cx.Ring(ids)
@@ -103,14 +104,51 @@ def test_successor(cx, O, n, search):
     assert (got == O.successor(want_ring, keys)).all()
 
 
-@pytest.mark.parametrize("search", [0, 1, 2, 3])
+@pytest.mark.parametrize("search", [0, 1, 2, 3, 4, 5])
 def test_successor_c2(cx, O, search):
-    """Config C2: 2^16-peer ring, 2^20 uniform keys (seeds of SURVEY 8d)."""
+    """Config C2: 2^16-peer ring, 2^20 uniform keys (seeds of SURVEY 8d).
+    Variant 1 takes the LDS slice table here (2^20 >= 4 n), 5 the directory."""
     ids = O.splitmix_keys(0x5EED0001, 1 << 16)
     keys = O.splitmix_keys(0x5EED0002, 1 << 20)
     ring = cx.Ring(ids)
     ring.set_search_variant(search)
     assert (ring.successor(keys) == O.successor(O.ring_build(ids), keys)).all()
+
+
+@pytest.mark.parametrize("pred", [False, True])
+@pytest.mark.parametrize("kind", ["cluster", "runs", "tiny_gaps"])
+def test_successor_lds_slice_table(cx, O, kind, pred):
+    """The LDS slice table (search variants 4 and 1) where its slices cannot
+    decide: a ring whose IDs share their top 40+ bits (one bucket, one run of
+    equal slices: the full-ID binary search), runs of IDs sharing the key's top
+    b + 16 bits beside uniform ones, and IDs 1 apart; keys at, next to and
+    between them.  Variant 1 at >= 4 n keys takes the same table."""
+    rng = np.random.default_rng(0x51CE)
+    if kind == "cluster":
+        base = 0x0123_4567_89AB << 80
+        vals = [base + (int(x) << 20) for x in rng.permutation(1 << 14)]
+    elif kind == "runs":
+        vals = O.ints_from_keys(O.splitmix_keys(0x51CF, 20000))
+        for j in range(40):
+            top = O.ints_from_keys(O.splitmix_keys(0x51D0 + j, 1))[0] >> 100 << 100
+            vals += [top + (int(x) << 40) for x in rng.permutation(300)]
+    else:
+        start = O.ints_from_keys(O.splitmix_keys(0x51D1, 1))[0]
+        vals = [(start + i) % (1 << 128) for i in range(5000)]
+        vals += O.ints_from_keys(O.splitmix_keys(0x51D2, 5000))
+    ids = O.keys_from_ints(vals)
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, 0x51D3, 1 << 16)
+    w = O.ints_from_keys(want_ring)
+    near = [(w[int(i)] + int(d)) % (1 << 128) for i, d in
+            zip(rng.integers(0, len(w), 4000), rng.integers(-3, 4, 4000))]
+    keys = np.concatenate([keys, O.keys_from_ints(near)])
+    want = (O.predecessor if pred else O.successor)(want_ring, keys)
+    for search in (4, 1, 5):
+        ring = cx.Ring(ids)
+        ring.set_search_variant(search)
+        got = ring.predecessor(keys) if pred else ring.successor(keys)
+        assert (got == want).all(), search
 
 
 # ---------------------------------------------------------------- a6 fingers
@@ -679,7 +717,7 @@ def test_misplaced_with_foreign_map_and_chained_churn(cx, O):
 
 
 
-@pytest.mark.parametrize("search", [1, 2, 3])
+@pytest.mark.parametrize("search", [1, 2, 3, 4, 5])
 def test_predecessor(cx, O, refvec, search):
     """Batched GetPredecessor vs the oracle: reference fixtures, edge rings and
     keys (IDs, +-1, 0, 2^128 - 1), N = 1, 2, 3."""
