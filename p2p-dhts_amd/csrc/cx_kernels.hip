@@ -795,10 +795,12 @@ __global__ __launch_bounds__(SL_BLOCK) void k_successor_lds(const uint4 *tab, ui
         const size_t c1 = c0 + (size_t)gridDim.x * per;
 #pragma unroll
         for (int k = 0; k < SL_KEYS; ++k) {
-            // peers sharing the key's top b + 16 bits (rare): their run of equal
-            // slices, then the full IDs, both by binary search (clustered rings
-            // put whole buckets in one run)
-            if (a[k] < e[k] && lsl[a[k]] == xs[k]) {
+            // peers sharing the key's top b + 16 bits (rare): the first one's
+            // ID decides unless it is below the key and the next peer shares
+            // them too; then the run of equal slices and the IDs in it by
+            // binary search (clustered rings put whole buckets in one run)
+            if (a[k] < e[k] && lsl[a[k]] == xs[k] &&
+                ld128(ring + a[k]) < x[k] && ++a[k] < e[k] && lsl[a[k]] == xs[k]) {
                 uint32_t u = a[k] + 1, w = e[k];
                 while (u < w) {
                     const uint32_t m = (u + w) >> 1;
