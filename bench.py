@@ -971,14 +971,15 @@ def c2_leg(args, world, rank, dev):
             "kernel_ms_per_step": ev_ms, "lookups_per_s_event_timed": world * Q / (ev_ms * 1e-3),
             "scaling": "weak",
             "config": {"workload": "C2: 2^16-peer ring (splitmix 0x5EED0001), 2^20 keys per GPU "
-                                   "(0x5EED0002), cx_successor (bucket directory search)",
+                                   "(0x5EED0002), cx_successor (round 6: LDS slice table, "
+                                   "k_successor_lds; the bucket directory for other shapes)",
                        "peers": N, "keys_per_gpu": Q},
             "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK * world / 1e9,
                          "achieved": world * algo / (ev_ms * 1e-3) / 1e9,
                          "frac": world * algo / (ev_ms * 1e-3) / (HBM_PEAK * world),
                          "model": "SURVEY 8(d): 20 B per query (16 key + 4 owner) + 16 B per peer "
                                   "once per batch, over the event-timed step (launch gaps "
-                                  "included; the kernel alone: profiles/r05)"},
+                                  "included; the kernel alone: profiles/r06/c2_lds)"},
             "parity_on_sample": parity, "oracle_sample_keys": Q, "cpu_baseline": cpu}
 
 
