@@ -115,6 +115,29 @@ def test_successor_c2(cx, O, search):
     assert (ring.successor(keys) == O.successor(O.ring_build(ids), keys)).all()
 
 
+def test_successor_lds_slice_table_churned_ring(cx, O):
+    """A ring from cx_churn builds its own slice table (lazily, from its own
+    IDs): successor / predecessor through the table on the parent and on two
+    chained churns equal the oracle on each ring, with the parent's table
+    built first (stale tables must not travel with the search variant)."""
+    ids = O.splitmix_keys(0x51D5, 30000)
+    keys = O.splitmix_keys(0x51D6, 1 << 17)
+    ring = cx.Ring(ids)
+    ring.set_search_variant(4)
+    want = O.ring_build(ids)
+    assert (ring.successor(keys) == O.successor(want, keys)).all()
+    for e in range(2):
+        joins = O.splitmix_keys(0x51D7 + e, 3000)
+        leaves = want[::7]
+        new, _ = ring.churn(joins, leaves)
+        want, _ = O.churn(want, joins, leaves)
+        assert (new.ids() == want).all()
+        new.set_search_variant(4)
+        assert (new.successor(keys) == O.successor(want, keys)).all()
+        assert (new.predecessor(keys) == O.predecessor(want, keys)).all()
+        ring = new
+
+
 @pytest.mark.parametrize("pred", [False, True])
 @pytest.mark.parametrize("kind", ["cluster", "runs", "tiny_gaps"])
 def test_successor_lds_slice_table(cx, O, kind, pred):
