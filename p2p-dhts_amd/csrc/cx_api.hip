@@ -458,6 +458,8 @@ struct cx_ring {
                                    // whenever it fits, 5: directory only (1 without LDS)
     void *d_sltab = nullptr;       // LDS slice table (variants 1 / 4, lazy; cxk::slice_tab_*)
     int sl_b = 0, sl_steps = 0;
+    std::mutex sl_mu;              // first searches build it (const queries on many threads)
+    std::atomic<bool> sl_ready{false};  // d_sltab / sl_b / sl_steps published
     cell128 *d_stree = nullptr;    // levels 1.. of the 16-ary tree (variant 2, lazy)
     uint32_t *d_eyt_rank = nullptr; // Eytzinger node -> sorted index (variant 3, lazy)
     int churn_variant = 1;         // 0: full re-sort, 1: merge of sorted joins (default)
@@ -1051,14 +1053,15 @@ int eyt_rank_view(cx_ring *r, hipStream_t s) {
 // The LDS slice table (cxk::slice_tab_*) of a ring that fits LDS, built on
 // first use: b = ceil(log2 n) - 4 bucket bits (about 16 peers a bucket, 1 to
 // 12, fewer when the table would not fit), the search rounds from its largest
-// bucket.  *ok = false when the ring
-// does not fit (or has no HBM for it): the caller searches the directory.
+// bucket.  *ok = false when the ring does not fit (or has no HBM for it): the
+// caller searches the directory.  Built once under the ring's sl_mu (const
+// queries may come from several threads) and published by sl_ready.
 int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
-    *ok = false;
-    if (r->d_sltab) {
-        *ok = true;
-        return CX_OK;
-    }
+    *ok = r->sl_ready.load(std::memory_order_acquire);
+    if (*ok) return CX_OK;
+    std::lock_guard<std::mutex> g(r->sl_mu);
+    *ok = r->sl_ready.load(std::memory_order_relaxed);
+    if (*ok) return CX_OK;
     int lg = 0;
     while (((size_t)1 << lg) < r->n) ++lg;
     int b = lg - 4 < 1 ? 1 : (lg - 4 > 12 ? 12 : lg - 4);
@@ -1082,6 +1085,7 @@ int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
     r->sl_steps = mx ? 32 - __builtin_clz(mx) : 0;
     r->sl_b = b;
     r->d_sltab = tab;
+    r->sl_ready.store(true, std::memory_order_release);
     *ok = true;
     return CX_OK;
 }
