@@ -115,6 +115,34 @@ def test_successor_c2(cx, O, search):
     assert (ring.successor(keys) == O.successor(O.ring_build(ids), keys)).all()
 
 
+def test_successor_lds_slice_table_concurrent_first_searches(cx, O):
+    """Four host threads make the first slice-table searches of a ring at once
+    (the table is built lazily by the first): every answer equals the oracle."""
+    import threading
+    ids = O.splitmix_keys(0x51D8, 50000)
+    want_ring = O.ring_build(ids)
+    keys = [O.splitmix_keys(0x51D9 + i, 1 << 16) for i in range(4)]
+    for rep in range(3):
+        ring = cx.Ring(ids)
+        ring.set_search_variant(4)
+        out, errs = [None] * 4, []
+
+        def run(i):
+            try:
+                out[i] = ring.successor(keys[i])
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs
+        for i in range(4):
+            assert (out[i] == O.successor(want_ring, keys[i])).all(), (rep, i)
+
+
 def test_successor_lds_slice_table_churned_ring(cx, O):
     """A ring from cx_churn builds its own slice table (lazily, from its own
     IDs): successor / predecessor through the table on the parent and on two
