@@ -117,6 +117,30 @@ class LegGuard:
             self.timer.cancel()
             self.timer = None
 
+    def run(self, name: str, fn):
+        """fn() under the watchdog; a leg that raises on this rank (an RCCL
+        error on a new node, say) ends the run like a hung one: rank 0 prints
+        the line as it stands with the leg and its error in `legs_failed`;
+        every rank leaves with status 0 at once (ranks waiting for it in a
+        collective leave when their own watchdog fires), so the launcher never
+        tears rank 0 down before its line is out."""
+        self.start(name, LEG_LIMIT_S)
+        try:
+            if os.environ.get("CX_BENCH_FAIL_LEG") == name:  # the failure path's own test
+                raise RuntimeError(f"injected failure in leg {name!r}")
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the line, then exit
+            self.stop()
+            progress(f"leg {name!r} failed: {type(e).__name__}: {e}")
+            if self.rank == 0 and self.line is not None:
+                self.line.setdefault("legs_failed", []).append(
+                    {"leg": name, "error": f"{type(e).__name__}: {e}"[:500],
+                     "note": "the keys of this and later legs are null"})
+                print(json.dumps(self.line), flush=True)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0 if self.line is not None or self.rank != 0 else 3)
+
     def _expire(self, name: str, seconds: float) -> None:
         progress(f"leg {name!r} did not finish in {seconds:.0f} s: leaving")
         if self.rank == 0 and self.line is not None:
@@ -1393,9 +1417,10 @@ def main():
 
     # ---- churn -> route-ready (f2), cold then warm ----
     progress("churn -> route-ready leg")
-    churn = None
-    guard.start("churn_route_ready", LEG_LIMIT_S)
-    if not args.no_churn:
+
+    def churn_block():
+        if args.no_churn:
+            return None
         churn = churn_leg(ring, keys, src, dev)
         chordx.pool_trim()  # the new rings' blocks are not needed by the arc leg
         churn["route_ready_ms_max_over_ranks"] = {
@@ -1426,56 +1451,67 @@ def main():
             st["results_equal_default"] = dist.all_over_ranks(st["results_equal_default"], world, dev)
             st["route_ready_ms_warm_max_over_ranks"] = dist.max_over_ranks(
                 st["warm"]["route_ready_ms"], world, dev)
+        return churn
 
+    churn = guard.run("churn_route_ready", churn_block)
     if line is not None:
         line["churn_route_ready"] = churn
 
     # ---- arc-sharded C4 (all_to_all-v) on the same keys and steps ----
     progress("arc leg")
-    arc = None
-    guard.start("arc", LEG_LIMIT_S)
-    if not args.no_arc:
-        arc = arc_leg(args, ring, src, keys, owner, hops, world, rank, dev, backend)
+    arc = guard.run("arc", lambda: None if args.no_arc else
+                    arc_leg(args, ring, src, keys, owner, hops, world, rank, dev, backend))
     if line is not None:
         line["arc"] = arc
 
     # ---- CPU baseline: rank 0, every world size, after the timed region ----
     progress("cpu baseline")
-    cpu = None
-    guard.start("cpu_baseline", LEG_LIMIT_S)
-    if rank == 0 and not args.no_cpu:
-        F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
-        F_host[:] = ring.fingers_device().cpu().numpy().view(np.uint32)
-        cpu = cpu_baseline(ring.ids(), F_host, keys.cpu().numpy().view(np.uint64),
-                           src.cpu().numpy().view(np.uint32),
-                           owner.cpu().numpy().view(np.uint32), hops.cpu().numpy(),
-                           args.cpu_seconds, world)
-        del F_host
-    dist.barrier(world)
+
+    def cpu_block():
+        cpu = None
+        if rank == 0 and not args.no_cpu:
+            F_host = np.empty((ring.n, chordx.CX_FINGERS), dtype=np.uint32)
+            F_host[:] = ring.fingers_device().cpu().numpy().view(np.uint32)
+            cpu = cpu_baseline(ring.ids(), F_host, keys.cpu().numpy().view(np.uint64),
+                               src.cpu().numpy().view(np.uint32),
+                               owner.cpu().numpy().view(np.uint32), hops.cpu().numpy(),
+                               args.cpu_seconds, world)
+            del F_host
+        dist.barrier(world)
+        return cpu
+
+    cpu = guard.run("cpu_baseline", cpu_block)
     if line is not None:
         line["cpu_baseline"] = cpu
 
     # ---- C5 (configs[4]) after the bench ring's tables are released ----
     progress("c5 leg")
-    c5 = None
-    guard.start("c5", LEG_LIMIT_S)
-    if not args.no_c5:
+
+    def c5_block():
+        if args.no_c5:
+            return None
         ring.close()
         chordx.pool_trim()
-        c5 = c5_leg(args, world, rank, dev, backend)
+        out = c5_leg(args, world, rank, dev, backend)
         chordx.pool_trim()
+        return out
+
+    c5 = guard.run("c5", c5_block)
     if line is not None:
         line["c5"] = c5
 
     # ---- C2 / C3 (configs[1], configs[2]): small rings, after the bench ring ----
     progress("c2 / c3 legs")
-    c2 = c3 = None
-    guard.start("c2_c3", LEG_LIMIT_S)
-    if not args.no_c2:
-        c2 = c2_leg(args, world, rank, dev)
-    if not args.no_c3:
-        c3 = c3_leg(args, world, rank, dev)
-        chordx.pool_trim()
+
+    def c23_block():
+        c2 = None if args.no_c2 else c2_leg(args, world, rank, dev)
+        c3 = None
+        if not args.no_c3:
+            c3 = c3_leg(args, world, rank, dev)
+            chordx.pool_trim()
+        return c2, c3
+
+    c2, c3 = guard.run("c2_c3", c23_block)
     guard.stop()
 
     if rank == 0:
