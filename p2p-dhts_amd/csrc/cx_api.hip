@@ -1052,8 +1052,8 @@ int eyt_rank_view(cx_ring *r, hipStream_t s) {
 
 // The LDS slice table (cxk::slice_tab_*) of a ring that fits LDS, built on
 // first use: b = ceil(log2 n) - 4 bucket bits (about 16 peers a bucket, 1 to
-// 12, fewer when the table would not fit), the search rounds from its largest
-// bucket.  *ok = false when the ring does not fit (or has no HBM for it): the
+// 12; down to ceil(log2 n) - 7 when the table would not fit, ~79 000 peers at
+// most), the search rounds from its largest bucket.  *ok = false when the ring does not fit (or has no HBM for it): the
 // caller searches the directory.  Built once under the ring's sl_mu (const
 // queries may come from several threads) and published by sl_ready.
 int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
@@ -1065,7 +1065,8 @@ int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
     int lg = 0;
     while (((size_t)1 << lg) < r->n) ++lg;
     int b = lg - 4 < 1 ? 1 : (lg - 4 > 12 ? 12 : lg - 4);
-    while (b > 1 && cxk::slice_tab_bytes(r->n, b) > cxk::SLICE_TAB_MAX) --b;
+    const int bmin = lg - 7 < 1 ? 1 : lg - 7;  // buckets of <= ~128 peers (<= 8 rounds)
+    while (b > bmin && cxk::slice_tab_bytes(r->n, b) > cxk::SLICE_TAB_MAX) --b;
     const size_t bytes = cxk::slice_tab_bytes(r->n, b);
     if (bytes > cxk::SLICE_TAB_MAX) return CX_OK;
     void *tab = nullptr;
@@ -1095,7 +1096,7 @@ int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
 bool slice_wanted(const cx_ring *r, size_t q) {
     if (r->search_variant == 4) return true;
     return r->search_variant == 1 && q >= ((size_t)1 << 16) && q >= 4 * r->n &&
-           cxk::slice_tab_bytes(r->n, 1) <= cxk::SLICE_TAB_MAX;
+           r->n * 2 < cxk::SLICE_TAB_MAX;
 }
 
 int stree_view(cx_ring *r, cxk::STreeView &st, hipStream_t s) {

@@ -115,6 +115,22 @@ def test_successor_c2(cx, O, search):
     assert (ring.successor(keys) == O.successor(O.ring_build(ids), keys)).all()
 
 
+@pytest.mark.parametrize("n", [75000, 79000, 81000])
+def test_successor_lds_slice_table_fit_boundary(cx, O, n):
+    """Rings at the LDS limit: 75 000 peers take b = 11, 79 000 b = 10 (the
+    smallest allowed), 81 000 do not fit and search the directory; variant 1
+    with >= 4 n keys and variant 4 give the oracle's answers either way."""
+    ids = edge_ring(O, n, 0x51DA + n)
+    want_ring = O.ring_build(ids)
+    keys = edge_keys(O, want_ring, 0x51DB, 4 * n + 10)
+    want = O.successor(want_ring, keys)
+    for search in (4, 1):
+        ring = cx.Ring(ids)
+        ring.set_search_variant(search)
+        assert (ring.successor(keys) == want).all(), search
+        assert (ring.predecessor(keys[:5000]) == O.predecessor(want_ring, keys[:5000])).all()
+
+
 def test_successor_lds_slice_table_concurrent_first_searches(cx, O):
     """Four host threads make the first slice-table searches of a ring at once
     (the table is built lazily by the first): every answer equals the oracle."""
