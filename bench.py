@@ -91,6 +91,97 @@ C5_BYTES_STREAM = 210
 C5_BYTES_SURVEY = 139
 
 
+def dir_search_requests(ids, keys, k, want_index=False):
+    """Random memory requests of the exact successor search over the bucket
+    directory (cx_common.hpp dir_successor, the kernel cx_successor runs on a
+    ring too large for the LDS slice table): one 16-B directory entry per key,
+    plus the ring IDs (16 B each) that the in-bucket binary search reads when
+    the entry alone does not decide -- replayed exactly on the host from the
+    sorted ring and the keys (uint64 (n, 2) / (q, 2) arrays {lo, hi}; k = the
+    directory's bucket bits, 0 < k < 64).  Returns (directory entries, ring
+    reads) and, with want_index, the successor index the replay reaches (the
+    test checks it against the oracle)."""
+    k = int(k)
+    sh, kk = np.uint64(64 - k), np.uint64(k)
+    hr, lr = ids[:, 1], ids[:, 0]
+    hk, lk = keys[:, 1], keys[:, 0]
+    bk = hk >> sh
+    br = hr >> sh
+    lo = np.searchsorted(br, bk, side="left")
+    hi = np.searchsorted(br, bk, side="right")
+    n = len(ids)
+    nonempty = lo < hi
+    loc = np.minimum(lo, n - 1)
+    frac = (hr[loc] << kk) | (lr[loc] >> sh)
+    xf = (hk << kk) | (lk >> sh)
+    search = nonempty & ~(xf < frac) & ~((xf > frac) & (hi - lo == 1))
+    a = np.where(xf > frac, lo + 1, lo).astype(np.int64)
+    z = hi.astype(np.int64)
+    ans = np.where(~nonempty | (xf < frac), lo, hi).astype(np.int64)
+    idx = np.nonzero(search)[0]
+    a, z = a[idx], z[idx]
+    xh, xl = hk[idx], lk[idx]
+    reads = 0
+    while True:
+        act = a < z
+        cnt = int(act.sum())
+        if cnt == 0:
+            break
+        reads += cnt
+        m = (a + z) // 2
+        mm = np.minimum(m, n - 1)
+        lt = (hr[mm] < xh) | ((hr[mm] == xh) & (lr[mm] < xl))
+        a = np.where(act & lt, m + 1, a)
+        z = np.where(act & ~lt, m, z)
+    ans[idx] = a
+    if want_index:
+        return len(keys), reads, np.where(ans == n, 0, ans)
+    return len(keys), reads
+
+
+def exact_successor_record(ring, keys, succ, ms, world, dev, sample=1 << 22):
+    """The exact successor search of the bench batch (north_star's
+    "exact successor lookups/sec"): its rate, and its roofline on a request
+    model -- 16 B key + 4 B owner per lookup and 64 B per random request (the
+    directory entry, and the ring IDs of the in-bucket binary search), the
+    requests per key replayed on the host over the first `sample` keys
+    (dir_search_requests; its answers must equal the GPU's, else no model)."""
+    q = keys.shape[0]
+    m = min(q, sample)
+    n = ring.n
+    k = 1
+    while (1 << k) < n:
+        k += 1
+    k = min(k + 1, 29)  # cx_api.hip build_search: ceil(log2 n) + 1 bucket bits
+    ks = keys[:m].cpu().numpy().view(np.uint64)
+    d, r, ans = dir_search_requests(ring.ids(), ks, k, want_index=True)
+    same = bool((ans.astype(np.uint32) == succ[:m].cpu().numpy().view(np.uint32)).all())
+    same = dist.all_over_ranks(same, world, dev)
+    per_key = (d + r) / m
+    algo = q * (20 + GRANULE * per_key)
+    achieved = dist.sum_over_ranks(int(algo), world, dev) / (dist.max_over_ranks(ms, world, dev) * 1e-3)
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic_successor.json")
+    if os.path.exists(tf) and n == 1 << 24 and q == 1 << 25:
+        with open(tf) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    return {"lookups_per_s": world * q / (dist.max_over_ranks(ms, world, dev) * 1e-3),
+            "kernel_ms": ms, "kernel": "k_successor<true, false> (bucket directory)",
+            "traffic": None if traffic is None else traffic * world,
+            "traffic_note": "PMC FETCH_SIZE + WRITE_SIZE per launch on one GPU "
+                            "(profiles/traffic_successor.json) x N",
+            "requests_per_key": per_key if same else None,
+            "ring_reads_per_key": r / m if same else None,
+            "model_replay_equals_gpu": same, "model_sample_keys": m,
+            "requests_per_s": world * q * per_key / (dist.max_over_ranks(ms, world, dev) * 1e-3),
+            "roofline": None if not same else {
+                "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK * world / 1e9,
+                "achieved": achieved / 1e9, "frac": achieved / (HBM_PEAK * world),
+                "model": "16 B key + 4 B owner per lookup + 64 B per random request (one "
+                         "directory entry per key, plus the ring IDs the in-bucket binary search "
+                         "reads, replayed on the host); whole node over the slowest rank"}}
+
+
 class LegGuard:
     """A watchdog per sub-record leg, on every rank.  The headline is measured
     and its line assembled before the legs run; if a leg does not finish in
@@ -1342,6 +1433,7 @@ def main():
     torch.cuda.synchronize(dev)
     succ_ms = e0.elapsed_time(e1) / 3
     owner_eq = dist.all_over_ranks(bool((succ == owner).all().item()), world, dev)
+    exact_rec = exact_successor_record(ring, keys, succ, succ_ms, world, dev)
     # gathers the walk issues on this batch: the counting build of the same
     # kernel, run once after the timed region (same inputs, same outputs)
     ref = (owner.clone(), hops.clone())
@@ -1413,6 +1505,7 @@ def main():
                              sum_hops, hist, max_hops, bad, owner_eq, counting_same, succ_ms,
                              small, rsrc_ms, rsrc_bad, t_gather, t_ring, t_fing, t_fing_warm,
                              setup_alloc)
+        line["exact_successor"] = exact_rec
         guard.line = line
 
     # ---- churn -> route-ready (f2), cold then warm ----
