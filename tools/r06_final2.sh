@@ -4,7 +4,7 @@
 #   GPU suite, C++ driver, smoke, default bench (N = 1, untraced), the same
 #   under a kernel trace (+ trace agreement), walk PMC groups, PMC FETCH /
 #   WRITE of the route-table build and the C5 kernel, C2 LDS-search PMC.
-TAG=${1:-r06/final2}
+TAG=${1:-r06/final3}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
 OUT=$R/gpurun_out/$TAG
