@@ -4468,7 +4468,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
     u128 key_n = 0;
     uint4 A_n = {0, 0, 0, 0}, B_n = {0, 0, 0, 0};
     if ((size_t)blockIdx.x * ROW_BLOCK + threadIdx.x < q) {
-        key_n = ld128(keys + (size_t)blockIdx.x * ROW_BLOCK + threadIdx.x);
+        key_n = ld128_nt(keys + (size_t)blockIdx.x * ROW_BLOCK + threadIdx.x);
         if (use_cd) cd_fetch(cd, key_n, A_n, B_n);
     }
     for (size_t base = (size_t)blockIdx.x * ROW_BLOCK; base < q; base += stride) {
@@ -4477,7 +4477,9 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_misplaced(SearchView sv_new, Sear
         const u128 key = key_n;
         const uint4 A = A_n, B = B_n;
         const bool more = i + stride < q;
-        if (more) key_n = ld128(keys + i + stride);
+        // keys stream (non-temporal): 3.376 vs 3.401 ms at C5, alternating
+        // processes (profiles/r06/c5_ntkeys/)
+        if (more) key_n = ld128_nt(keys + i + stride);
         if (i < q) {
             uint32_t sn = 0, so = 0, has = 0, m = 0;
             const bool settled =
