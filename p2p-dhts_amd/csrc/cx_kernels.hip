@@ -838,9 +838,8 @@ hipError_t successor_lds(const void *tab, int b, int steps, const cell128 *ring,
     const size_t bytes = slice_tab_bytes(n, b);
     if (bytes > SLICE_TAB_MAX || n == 0 || n > 0xFFFFFFFFull || b < 1 || b > 12 || steps < 0)
         return hipErrorInvalidValue;
-    int dev = 0, cus = 256, per_cu = 1;
+    int dev = 0;
     (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     auto kern = pred ? k_successor_lds<true> : k_successor_lds<false>;
     static const bool lds_ok = [] {  // dynamic LDS above 64 KiB, once per kernel
         const int lim = (int)SLICE_TAB_MAX;
@@ -850,12 +849,24 @@ hipError_t successor_lds(const void *tab, int b, int steps, const cell128 *ring,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess;
     }();
     (void)lds_ok;  // a runtime without the attribute takes the launch as is
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SL_BLOCK, bytes) != hipSuccess ||
-        per_cu < 1)
-        per_cu = 1;
+    // resident blocks for this table size, cached (the device and occupancy
+    // queries cost host time on every ~8-us launch): key = bytes | device | pred
+    static std::atomic<uint64_t> cached{0};
+    const uint64_t key = ((uint64_t)bytes << 7) | ((uint64_t)(dev & 63) << 1) | (pred ? 1u : 0u);
+    const uint64_t c = cached.load(std::memory_order_relaxed);
+    uint64_t resident = c >> 25 == 0 ? 0 : c & ((1ull << 25) - 1);
+    if (c >> 25 != key || resident == 0) {
+        int cus = 256, per_cu = 1;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, SL_BLOCK, bytes) !=
+                hipSuccess || per_cu < 1)
+            per_cu = 1;
+        resident = (uint64_t)cus * per_cu;
+        cached.store((key << 25) | resident, std::memory_order_relaxed);
+    }
     // one resident round of blocks (each stages the table once)
     size_t g = (q + (size_t)SL_BLOCK * SL_KEYS - 1) / ((size_t)SL_BLOCK * SL_KEYS);
-    if (g > (size_t)cus * per_cu) g = (size_t)cus * per_cu;
+    if (g > resident) g = resident;
     kern<<<(unsigned)g, SL_BLOCK, bytes, s>>>(reinterpret_cast<const uint4 *>(tab),
                                                 (uint32_t)(bytes / 16), b, steps, (uint32_t)n,
                                                 ring, keys, q, out);
