@@ -114,16 +114,23 @@ class Ring:
     def __len__(self):
         return self.n
 
+    def _torch_stream(self):
+        """Order the library's work on torch's current stream (one ABI call
+        only when that stream changed: small batches are host-bound)."""
+        cs = torch.cuda.current_stream(self.device).cuda_stream
+        if self.__dict__.get("_stream_set") != cs:
+            L.check(L.lib().cx_ring_set_stream(self._h, ctypes.c_void_p(cs)))
+            self._stream_set = cs
+
     def _mem(self, *arrays) -> int:
         dev = [_is_dev(a) for a in arrays if a is not None]
         if dev and all(dev):
-            # order the library's work on torch's current stream
-            L.check(L.lib().cx_ring_set_stream(
-                self._h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+            self._torch_stream()
             return L.CX_MEM_DEVICE
         if any(dev):
             raise TypeError("mix of device tensors and host arrays")
         L.check(L.lib().cx_ring_use_own_stream(self._h))
+        self._stream_set = None
         return L.CX_MEM_HOST
 
     def _empty(self, like, shape, np_dtype, th_dtype):
@@ -479,8 +486,7 @@ class Ring:
         return t.value, r.value, b.value
 
     def _arc_stream(self):
-        L.check(L.lib().cx_ring_set_stream(
-            self._h, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        self._torch_stream()
 
     def arc_seed(self, rank: int, src, keys):
         """(q, 4) int64 device tensor of NEW records (32 B each)."""
