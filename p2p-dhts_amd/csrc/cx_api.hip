@@ -1053,9 +1053,10 @@ int eyt_rank_view(cx_ring *r, hipStream_t s) {
 // The LDS slice table (cxk::slice_tab_*) of a ring that fits LDS, built on
 // first use: b = ceil(log2 n) - 4 bucket bits (about 16 peers a bucket, 1 to
 // 12; down to ceil(log2 n) - 7 when the table would not fit, ~79 000 peers at
-// most), the search rounds from its largest bucket.  *ok = false when the ring does not fit (or has no HBM for it): the
-// caller searches the directory.  Built once under the ring's sl_mu (const
-// queries may come from several threads) and published by sl_ready.
+// most), the search rounds from its largest bucket.  *ok = false when the ring
+// does not fit (or has no HBM for it): the caller searches the directory.
+// Built once under the ring's sl_mu (const queries may come from several
+// threads) and published by sl_ready.
 int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
     *ok = r->sl_ready.load(std::memory_order_acquire);
     if (*ok) return CX_OK;
