@@ -108,6 +108,42 @@ TEST(ChordGetSucc, FromPredecessor) {
     EXPECT_EQ(l.hops, 1);
 }
 
+// StoredLocally for a batch (abstract_chord_peer.cpp:720-725), through the
+// C++ mirror: a 4 096-peer ring and 2^16 + 3 x 512 keys (so the engine takes
+// its LDS slice table) against the first ID >= key with wrap, on the host.
+TEST(ChordStoredLocally, Batch) {
+    auto mix = [](uint64_t x) {
+        x += 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        return x ^ (x >> 31);
+    };
+    std::vector<Key> ids;
+    for (uint64_t i = 0; i < 4096; ++i) ids.push_back(Key(mix(2 * i), mix(2 * i + 1)));
+    Ring ring(ids);
+    const std::vector<Key> sorted = ring.Ids();
+    std::vector<Key> keys;
+    for (uint64_t i = 0; i < (1u << 16); ++i) keys.push_back(Key(mix(1000003 + 2 * i), mix(1000004 + 2 * i)));
+    for (size_t j = 0; j < 512; ++j) {  // an ID, its neighbours
+        const unsigned __int128 v = sorted[j * 8].value();
+        keys.push_back(Key(v));
+        keys.push_back(Key(v + 1));
+        keys.push_back(Key(v - 1));
+    }
+    const std::vector<uint32_t> got = ring.Successors(keys);
+    size_t bad = 0;
+    for (size_t i = 0; i < keys.size(); ++i) {
+        size_t a = 0, z = sorted.size();
+        while (a < z) {
+            const size_t m = (a + z) / 2;
+            if (sorted[m] < keys[i]) a = m + 1;
+            else z = m;
+        }
+        bad += got[i] != (a == sorted.size() ? 0u : (uint32_t)a);
+    }
+    EXPECT_EQ(bad, (size_t)0);
+}
+
 // GET_SUCC_FAILING (GetSuccTest.json): peer 127.0.0.1:7003 (constructed, its
 // server answers, min_key_ = id_, StartChord never called -> empty finger
 // table); its predecessor_ and only successor are a peer with ID
@@ -222,6 +258,7 @@ int main() {
     RUN(ChordGetSucc, Failing);
     RUN(ChordGetSucc, LivelockHitsHopCap);
     RUN(ChordGetPred, Fixtures);
+    RUN(ChordStoredLocally, Batch);
     RUN(DHashPeer, InsufficientSuccs);
     RUN(Wire, GetSuccJoinFixture);
     RUN(DataBlock, EncodeDecodeVal1);
