@@ -458,6 +458,7 @@ struct cx_ring {
                                    // whenever it fits, 5: directory only (1 without LDS)
     void *d_sltab = nullptr;       // LDS slice table (variants 1 / 4, lazy; cxk::slice_tab_*)
     int sl_b = 0, sl_steps = 0;
+    bool sl_dev16 = false;         // offsets as int16 deviations (one more bucket bit)
     std::mutex sl_mu;              // first searches build it (const queries on many threads)
     std::atomic<bool> sl_ready{false};  // d_sltab / sl_b / sl_steps published
     cell128 *d_stree = nullptr;    // levels 1.. of the 16-ary tree (variant 2, lazy)
@@ -1065,6 +1066,59 @@ int slice_view(cx_ring *r, hipStream_t s, bool *ok) {
     if (*ok) return CX_OK;
     int lg = 0;
     while (((size_t)1 << lg) < r->n) ++lg;
+    // first choice: b = ceil(log2 n) - 3 (~8 peers a bucket) with int16 offset
+    // deviations, when they fit 16 bits (uniform rings) and the table fits LDS
+    {
+        const int b16 = lg - 3 < 1 ? 1 : (lg - 3 > 14 ? 14 : lg - 3);
+        const size_t bytes16 = cxk::slice_tab_bytes(r->n, b16, true);
+        const size_t tmp_bytes = cxk::slice_tab_bytes(r->n, b16);
+        void *tmp = nullptr, *tab = nullptr;
+        if (bytes16 <= cxk::SLICE_TAB_MAX && dev_malloc(&tmp, tmp_bytes) == hipSuccess) {
+            const size_t nb = ((size_t)1 << b16) + 1;
+            std::vector<uint32_t> off(nb);
+            hipError_t e = cxk::slice_tab_build(r->d_ring, r->n, b16, tmp, s);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(off.data(), tmp, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) {
+                (void)hipFree(tmp);
+                return fail(CX_E_HIP, hipGetErrorString(e));
+            }
+            std::vector<int16_t> dev(nb);
+            bool fits = true;
+            uint32_t mx = 0;
+            for (size_t t = 0; t < nb && fits; ++t) {
+                const long long d = (long long)off[t] - (long long)((uint64_t)t * r->n >> b16);
+                fits = d >= -32768 && d <= 32767;
+                dev[t] = (int16_t)d;
+                if (t + 1 < nb) mx = std::max(mx, off[t + 1] - off[t]);
+            }
+            const size_t off16 = (nb * 2 + 15) / 16 * 16, off32 = (nb * 4 + 15) / 16 * 16;
+            if (fits && dev_malloc(&tab, bytes16) == hipSuccess) {
+                e = hipMemsetAsync(tab, 0, bytes16, s);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(tab, dev.data(), nb * 2, hipMemcpyHostToDevice, s);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(static_cast<char *>(tab) + off16,
+                                       static_cast<char *>(tmp) + off32, r->n * 2,
+                                       hipMemcpyDeviceToDevice, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                (void)hipFree(tmp);
+                if (e != hipSuccess) {
+                    (void)hipFree(tab);
+                    return fail(CX_E_HIP, hipGetErrorString(e));
+                }
+                r->sl_steps = mx ? 32 - __builtin_clz(mx) : 0;
+                r->sl_b = b16;
+                r->sl_dev16 = true;
+                r->d_sltab = tab;
+                r->sl_ready.store(true, std::memory_order_release);
+                *ok = true;
+                return CX_OK;
+            }
+            (void)hipFree(tmp);
+        }
+    }
     int b = lg - 4 < 1 ? 1 : (lg - 4 > 12 ? 12 : lg - 4);
     const int bmin = lg - 7 < 1 ? 1 : lg - 7;  // buckets of <= ~128 peers (<= 8 rounds)
     while (b > bmin && cxk::slice_tab_bytes(r->n, b) > cxk::SLICE_TAB_MAX) --b;
@@ -1138,9 +1192,9 @@ int cx_successor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t *o
         if (slice_wanted(ring, q) && (rc = slice_view(const_cast<cx_ring *>(ring), s, &lds)))
             return rc;
         if (lds)
-            CX_HIP(cxk::successor_lds(ring->d_sltab, ring->sl_b, ring->sl_steps, ring->d_ring,
-                                      ring->n, reinterpret_cast<const cell128 *>(dk), q, dout,
-                                      false, s));
+            CX_HIP(cxk::successor_lds(ring->d_sltab, ring->sl_b, ring->sl_dev16, ring->sl_steps,
+                                      ring->d_ring, ring->n,
+                                      reinterpret_cast<const cell128 *>(dk), q, dout, false, s));
         else
             CX_HIP(cxk::successor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     }
@@ -1241,9 +1295,9 @@ int cx_predecessor(const cx_ring *ring, const cx_u128 *keys, size_t q, uint32_t 
         if (slice_wanted(ring, q) && (rc = slice_view(const_cast<cx_ring *>(ring), s, &lds)))
             return rc;
         if (lds)
-            CX_HIP(cxk::successor_lds(ring->d_sltab, ring->sl_b, ring->sl_steps, ring->d_ring,
-                                      ring->n, reinterpret_cast<const cell128 *>(dk), q, dout,
-                                      true, s));
+            CX_HIP(cxk::successor_lds(ring->d_sltab, ring->sl_b, ring->sl_dev16, ring->sl_steps,
+                                      ring->d_ring, ring->n,
+                                      reinterpret_cast<const cell128 *>(dk), q, dout, true, s));
         else
             CX_HIP(cxk::predecessor(ring->sv(), reinterpret_cast<const cell128 *>(dk), q, dout, s));
     }

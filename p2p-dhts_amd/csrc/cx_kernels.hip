@@ -4,6 +4,7 @@
 // in HBM: ring IDs as 16-B cells (AoS, one dwordx4 per ID), finger table as
 // row-major uint32 [peer][128], Eytzinger copy of the ring for searches.
 #include <atomic>
+#include <initializer_list>
 #include <cmath>
 #include <type_traits>
 
@@ -720,10 +721,12 @@ __global__ void k_slice_tab_build(const cell128 *ring, uint32_t n, int b, uint32
     }
 }
 
-size_t slice_tab_bytes(size_t n, int b) {
+// dev16: the offsets as int16 deviations from (t n) >> b (uniform rings: half
+// the bytes, so one more bucket bit fits LDS)
+size_t slice_tab_bytes(size_t n, int b, bool dev16) {
     const size_t nb = ((size_t)1 << b) + 1;
     // whole 1-KiB runs (one LDS-DMA instruction per wave moves 1 KiB)
-    return ((nb * 4 + 15) / 16 * 16 + (n * 2 + 15) / 16 * 16 + 1023) / 1024 * 1024;
+    return ((nb * (dev16 ? 2 : 4) + 15) / 16 * 16 + (n * 2 + 15) / 16 * 16 + 1023) / 1024 * 1024;
 }
 
 hipError_t slice_tab_build(const cell128 *ring, size_t n, int b, void *tab, hipStream_t s) {
@@ -740,7 +743,7 @@ constexpr int SL_BLOCK = 1024;
 constexpr int SL_KEYS = 4;  // keys per lane per trip, their searches interleaved
 
 // steps: binary-search rounds that cover the largest bucket (ceil(log2(max + 1))).
-template <bool PRED>
+template <bool PRED, bool D16>
 __global__ __launch_bounds__(SL_BLOCK) void k_successor_lds(const uint4 *tab, uint32_t tab_v4,
                                                             int b, int steps, uint32_t n,
                                                             const cell128 *ring,
@@ -748,8 +751,10 @@ __global__ __launch_bounds__(SL_BLOCK) void k_successor_lds(const uint4 *tab, ui
                                                             uint32_t *out) {
     extern __shared__ uint4 lds4[];
     const uint32_t *loff = reinterpret_cast<const uint32_t *>(lds4);
+    const int16_t *ldev = reinterpret_cast<const int16_t *>(lds4);
     const uint16_t *lsl = reinterpret_cast<const uint16_t *>(
-        reinterpret_cast<const char *>(lds4) + ((((size_t)1 << b) + 1) * 4 + 15) / 16 * 16);
+        reinterpret_cast<const char *>(lds4) +
+        ((((size_t)1 << b) + 1) * (D16 ? 2 : 4) + 15) / 16 * 16);
     const size_t per = (size_t)SL_BLOCK * SL_KEYS;
     size_t c0 = blockIdx.x * per;
     // this block's first keys are in flight while the table lands in LDS
@@ -780,8 +785,13 @@ __global__ __launch_bounds__(SL_BLOCK) void k_successor_lds(const uint4 *tab, ui
 #pragma unroll
         for (int k = 0; k < SL_KEYS; ++k) {
             const uint32_t t = (uint32_t)top_bits(x[k], b);
-            a[k] = loff[t];
-            z[k] = e[k] = loff[t + 1];
+            if (D16) {
+                a[k] = (uint32_t)(((uint64_t)t * n >> b) + ldev[t]);
+                z[k] = e[k] = (uint32_t)(((uint64_t)(t + 1) * n >> b) + ldev[t + 1]);
+            } else {
+                a[k] = loff[t];
+                z[k] = e[k] = loff[t + 1];
+            }
             xs[k] = (uint32_t)(top_bits(x[k], b + 16) & 0xFFFFu);
         }
         for (int it = 0; it < steps; ++it) {  // every lane the same rounds
@@ -831,28 +841,34 @@ __global__ __launch_bounds__(SL_BLOCK) void k_successor_lds(const uint4 *tab, ui
     }
 }
 
-hipError_t successor_lds(const void *tab, int b, int steps, const cell128 *ring, size_t n,
-                         const cell128 *keys, size_t q, uint32_t *out, bool pred,
+hipError_t successor_lds(const void *tab, int b, bool dev16, int steps, const cell128 *ring,
+                         size_t n, const cell128 *keys, size_t q, uint32_t *out, bool pred,
                          hipStream_t s) {
     if (q == 0) return hipSuccess;
-    const size_t bytes = slice_tab_bytes(n, b);
-    if (bytes > SLICE_TAB_MAX || n == 0 || n > 0xFFFFFFFFull || b < 1 || b > 12 || steps < 0)
+    const size_t bytes = slice_tab_bytes(n, b, dev16);
+    if (bytes > SLICE_TAB_MAX || n == 0 || n > 0xFFFFFFFFull || b < 1 || b > 14 || steps < 0)
         return hipErrorInvalidValue;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    auto kern = pred ? k_successor_lds<true> : k_successor_lds<false>;
+    auto kern = pred ? (dev16 ? k_successor_lds<true, true> : k_successor_lds<true, false>)
+                     : (dev16 ? k_successor_lds<false, true> : k_successor_lds<false, false>);
     static const bool lds_ok = [] {  // dynamic LDS above 64 KiB, once per kernel
         const int lim = (int)SLICE_TAB_MAX;
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(k_successor_lds<false>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess &&
-               hipFuncSetAttribute(reinterpret_cast<const void *>(k_successor_lds<true>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, lim) == hipSuccess;
+        bool ok = true;
+        for (const void *k : {reinterpret_cast<const void *>(k_successor_lds<false, false>),
+                              reinterpret_cast<const void *>(k_successor_lds<true, false>),
+                              reinterpret_cast<const void *>(k_successor_lds<false, true>),
+                              reinterpret_cast<const void *>(k_successor_lds<true, true>)})
+            ok = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lim) ==
+                     hipSuccess && ok;
+        return ok;
     }();
     (void)lds_ok;  // a runtime without the attribute takes the launch as is
     // resident blocks for this table size, cached (the device and occupancy
     // queries cost host time on every ~8-us launch): key = bytes | device | pred
     static std::atomic<uint64_t> cached{0};
-    const uint64_t key = ((uint64_t)bytes << 7) | ((uint64_t)(dev & 63) << 1) | (pred ? 1u : 0u);
+    const uint64_t key = ((uint64_t)bytes << 7) | ((uint64_t)(dev & 31) << 2) |
+                         (dev16 ? 2u : 0u) | (pred ? 1u : 0u);
     const uint64_t c = cached.load(std::memory_order_relaxed);
     uint64_t resident = c >> 25 == 0 ? 0 : c & ((1ull << 25) - 1);
     if (c >> 25 != key || resident == 0) {

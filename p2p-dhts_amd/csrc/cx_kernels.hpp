@@ -107,10 +107,10 @@ hipError_t predecessor(const SearchView &ev, const cell128 *keys, size_t q, uint
 // table's bytes for n peers and b bucket bits, its build, and the search
 // (steps = binary-search rounds covering the largest bucket).
 constexpr size_t SLICE_TAB_MAX = 160 * 1024;
-size_t slice_tab_bytes(size_t n, int b);
+size_t slice_tab_bytes(size_t n, int b, bool dev16 = false);
 hipError_t slice_tab_build(const cell128 *ring, size_t n, int b, void *tab, hipStream_t s);
-hipError_t successor_lds(const void *tab, int b, int steps, const cell128 *ring, size_t n,
-                         const cell128 *keys, size_t q, uint32_t *out, bool pred,
+hipError_t successor_lds(const void *tab, int b, bool dev16, int steps, const cell128 *ring,
+                         size_t n, const cell128 *keys, size_t q, uint32_t *out, bool pred,
                          hipStream_t s);
 hipError_t fingers_build(const SearchView &sv, const cell128 *ring, const uint32_t *ring_key,
                          void *ws, uint32_t *F, hipStream_t s, uint32_t *FT = nullptr,

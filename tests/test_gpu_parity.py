@@ -183,17 +183,21 @@ def test_successor_lds_slice_table_churned_ring(cx, O):
 
 
 @pytest.mark.parametrize("pred", [False, True])
-@pytest.mark.parametrize("kind", ["cluster", "runs", "tiny_gaps"])
+@pytest.mark.parametrize("kind", ["cluster", "cluster_big", "runs", "tiny_gaps"])
 def test_successor_lds_slice_table(cx, O, kind, pred):
     """The LDS slice table (search variants 4 and 1) where its slices cannot
     decide: a ring whose IDs share their top 40+ bits (one bucket, one run of
-    equal slices: the full-ID binary search), runs of IDs sharing the key's top
+    equal slices: the full-ID binary search; with 40 000 such IDs the int16
+    offset deviations overflow and the uint32 table is used), runs of IDs sharing the key's top
     b + 16 bits beside uniform ones, and IDs 1 apart; keys at, next to and
     between them.  Variant 1 at >= 4 n keys takes the same table."""
     rng = np.random.default_rng(0x51CE)
     if kind == "cluster":
         base = 0x0123_4567_89AB << 80
         vals = [base + (int(x) << 20) for x in rng.permutation(1 << 14)]
+    elif kind == "cluster_big":  # offsets past int16 deviations: the uint32 table
+        base = 0x0123_4567_89AB << 80
+        vals = [base + (int(x) << 20) for x in rng.permutation(40000)]
     elif kind == "runs":
         vals = O.ints_from_keys(O.splitmix_keys(0x51CF, 20000))
         for j in range(40):
