@@ -691,9 +691,10 @@ hipError_t predecessor(const SearchView &sv, const cell128 *keys, size_t q, uint
 // ---------------------------------------------------------------------------
 // Rings that fit LDS (a7 / GetPredecessor, search variants 1 (automatic) and
 // 4): one table per ring, staged whole into every block -- the bucket
-// offsets off[t] = first index whose top b ID bits are >= t (t = 0 .. 2^b),
-// then the 16-bit slices s(p) = ID bits [128 - b - 16, 128 - b) of every
-// peer, each part padded to 16 B.  Within bucket t the slices are sorted, so
+// offsets off[t] = first index whose top b ID bits are >= t (t = 0 .. 2^b;
+// as int16 deviations from (t n) >> b when they fit, D16, which leaves room
+// for one more bucket bit), then the 16-bit slices s(p) = ID bits
+// [128 - b - 16, 128 - b) of every peer, each part padded to 16 B.  Within bucket t the slices are sorted, so
 // a key's successor is the lower bound of its own slice in [off[t],
 // off[t + 1]) -- exact unless that peer shares the key's top b + 16 bits
 // (probability n / 2^(b + 16), 2^-12 at C2), which reads the full IDs.  One
